@@ -1,0 +1,527 @@
+// Flash attention for gfx950 (MFMA 16x16x32 bf16, 64-key tiles, online softmax).
+//
+// Layout trick ("swapped" products, so no P transpose is ever needed):
+//   S^T = K . Q^T   A = K rows from LDS (ds_read_b128, XOR swizzled), B = Q^T
+//                   fragments held in VGPRs. C-layout: col = query (lane&15),
+//                   row = key (4*(lane>>4)+r)  -> the softmax over keys of one
+//                   query is lane-local + 2 shuffles (xor 16, 32).
+//   O^T = V^T . P^T A = V^T read with ds_read_b64_tr_b16 (hardware transpose) from
+//                   a row-major LDS V tile, B = P^T taken directly from the S^T
+//                   accumulators of the same lane (k-slot order permuted to match).
+//
+// Kernels
+//  * attn_prefill<D, GB, CAUSAL, PAGED>: varlen packed queries. PAGED reads K/V
+//    from the paged cache [nblocks][Hkv][64][D] through block tables (prefill with
+//    any prior context: chunked prefill / prefix reuse); !PAGED reads K/V straight
+//    from a packed qkv buffer (bidirectional encoders). One block = 4 waves =
+//    GB query heads sharing one KV head x (4/GB) groups of 32 query rows.
+//  * attn_decode<D, G>: one query token per sequence, split-K over the context
+//    (flash-decoding). Each wave streams its own 64-key tiles (K straight to
+//    VGPRs, V through a wave-private LDS tile for the transposed read); 4 waves
+//    combine in LDS; partitions merged by attn_decode_reduce.
+//
+// Replaces reference ops K5/K6 (causal GQA attention in transformers' Llama SDPA path,
+// [dep] modeling_llama.py:191-215) and E3 (XLM-R/BERT bidirectional attention).
+#include "common.h"
+using namespace ragk;
+
+namespace {
+
+constexpr int KT = 64;  // keys per tile == KV-cache page size
+
+template <int D>
+struct Cfg {
+  static constexpr int NC = D / 8;               // 16-B chunks per row
+  static constexpr int ROWB = D * 2;             // bytes per row
+  static constexpr int TILEB = KT * D * 2;       // bytes per K or V tile
+  static constexpr int PIECES = TILEB / 1024;    // 1-KiB glds pieces per tile
+  static constexpr int RPP = 1024 / ROWB;        // rows per piece
+  static constexpr int KS = D / 32;              // k-steps of QK^T
+  static constexpr int DT = D / 16;              // 16-wide d tiles of O
+  static constexpr int GR = D / 16;              // 32-B granules per row
+  static constexpr int RB = 8 / GR;              // rows per 256-B bank row
+};
+
+// K tile: swizzle for row reads (ds_read_b128)
+template <int D>
+__device__ __forceinline__ int kswz(int row) {
+  constexpr int NC = Cfg<D>::NC;
+  return (row / (16 / NC)) & (NC - 1);
+}
+// V tile: swizzle for transposed reads (keeps 32-B granules intact)
+template <int D>
+__device__ __forceinline__ int vswz(int row) {
+  return 2 * ((row / Cfg<D>::RB) & (Cfg<D>::GR - 1));
+}
+
+__device__ __forceinline__ bf16x4 tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) bf16x4*)(p));
+}
+
+// Stage one 64-row tile (K or V) into LDS with glds; `pieces_per_wave` pieces per wave.
+// row_src(row) returns the global row pointer for tile row `row`.
+template <int D, bool IS_V, typename RowSrc>
+__device__ __forceinline__ void stage_kv(char* lds_tile, int wid, int nwaves, int lane, RowSrc row_src) {
+  constexpr int NC = Cfg<D>::NC, PIECES = Cfg<D>::PIECES, RPP = Cfg<D>::RPP;
+  for (int p = wid; p < PIECES; p += nwaves) {
+    const int row = p * RPP + lane / NC;
+    const int ph = lane % NC;
+    const int c = ph ^ (IS_V ? vswz<D>(row) : kswz<D>(row));
+    glds16(row_src(row) + c * 8, lds_tile + p * 1024);
+  }
+}
+
+// V^T A-fragment for d-tile dt and key k-step ks (32 keys) from a V tile in LDS.
+template <int D>
+__device__ __forceinline__ bf16x8 load_vt(const char* sV, int dt, int ks, int lane) {
+  const int h = lane >> 4, i = lane & 15;
+  const int chunk = 2 * dt + ((i >> 1) & 1);
+  const int r0 = 32 * ks + 4 * h + (i >> 2);
+  const int r1 = r0 + 16;
+  const bf16x4 a = tr_read(sV + r0 * Cfg<D>::ROWB + 16 * (chunk ^ vswz<D>(r0)) + 8 * (i & 1));
+  const bf16x4 b = tr_read(sV + r1 * Cfg<D>::ROWB + 16 * (chunk ^ vswz<D>(r1)) + 8 * (i & 1));
+  return (bf16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+template <int D>
+__device__ __forceinline__ bf16x8 load_k(const char* sK, int t, int s, int lane) {
+  const int R = 16 * t + (lane & 15);
+  const int c = 4 * s + (lane >> 4);
+  return *reinterpret_cast<const bf16x8*>(sK + R * Cfg<D>::ROWB + 16 * (c ^ kswz<D>(R)));
+}
+
+__device__ __forceinline__ bf16x8 pack_p(const f32x4& a, const f32x4& b) {
+  return (bf16x8){f2bf_s(a[0]), f2bf_s(a[1]), f2bf_s(a[2]), f2bf_s(a[3]),
+                  f2bf_s(b[0]), f2bf_s(b[1]), f2bf_s(b[2]), f2bf_s(b[3])};
+}
+
+// ------------------------------------------------------------------------------------
+// Prefill / encoder attention
+// ------------------------------------------------------------------------------------
+struct PrefillArgs {
+  const bf16_t* q;  int q_stride;          // token row stride (elements); head h at +h*D
+  const bf16_t* k;  const bf16_t* v;       // PAGED: caches; else packed K/V base pointers
+  int kv_stride;                           // !PAGED: token row stride of k/v
+  const int* block_tables; int bt_stride;  // PAGED
+  const int* cu_q;                         // [S+1] query token offsets
+  const int* cu_kv;                        // [S+1] kv token offsets (!PAGED)
+  const int* kv_lens;                      // [S] total context length per sequence
+  const int* tiles;                        // [n][2] = (seq, q_start)
+  bf16_t* out; int out_stride;
+  int Hq, Hkv;
+  float scale_log2;
+};
+
+template <int D, int GB, bool CAUSAL, bool PAGED>
+__global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
+  using C = Cfg<D>;
+  constexpr int QT = 32 * (4 / GB);  // query positions per block
+  __shared__ __attribute__((aligned(16))) char smem[4 * C::TILEB];  // [buf][K|V]
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  const int seq = a.tiles[2 * blockIdx.x], q_start = a.tiles[2 * blockIdx.x + 1];
+  const int G = a.Hq / a.Hkv;
+  const int groups_per_kv = G / GB;
+  const int kvh = blockIdx.y / groups_per_kv;
+  const int gsub = blockIdx.y % groups_per_kv;
+  const int hq = kvh * G + gsub * GB + (wid % GB);
+  const int pbase = q_start + (wid / GB) * 32;
+
+  const int q_off = a.cu_q[seq];
+  const int q_len = a.cu_q[seq + 1] - q_off;
+  const int kv_len = a.kv_lens[seq];
+  const int ctx0 = kv_len - q_len;  // absolute position of query 0
+
+  const int blk_qmax = min(q_start + QT, q_len) - 1;
+  const int n_keys = CAUSAL ? min(kv_len, ctx0 + blk_qmax + 1) : kv_len;
+  const int n_kt = (n_keys + KT - 1) / KT;
+  const int wave_qmax = min(pbase + 31, q_len - 1);
+  const int wave_pmax = ctx0 + wave_qmax;
+
+  const int fr = lane & 15, fh = lane >> 4;
+
+  // Q^T fragments (B operand), 2 query sub-tiles of 16
+  bf16x8 qf[2][C::KS];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    int qi = pbase + 16 * qt + fr;
+    qi = qi < q_len ? qi : q_len - 1;
+    const bf16_t* qp = a.q + (size_t)(q_off + qi) * a.q_stride + hq * D + 8 * fh;
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) qf[qt][s] = *reinterpret_cast<const bf16x8*>(qp + 32 * s);
+  }
+
+  f32x4 o[C::DT][2];
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) o[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m_i[2] = {-INFINITY, -INFINITY}, l_i[2] = {0.f, 0.f};
+
+  const int kv_off = PAGED ? 0 : a.cu_kv[seq];
+  const int* bt = PAGED ? a.block_tables + (size_t)seq * a.bt_stride : nullptr;
+
+  auto stage = [&](int kt, int buf) {
+    char* sK = smem + buf * 2 * C::TILEB;
+    char* sV = sK + C::TILEB;
+    if constexpr (PAGED) {
+      const size_t base = ((size_t)bt[kt] * a.Hkv + kvh) * KT * D;
+      const bf16_t* kb = a.k + base;
+      const bf16_t* vb = a.v + base;
+      stage_kv<D, false>(sK, wid_u, 4, lane, [&](int r) { return kb + (size_t)r * D; });
+      stage_kv<D, true>(sV, wid_u, 4, lane, [&](int r) { return vb + (size_t)r * D; });
+    } else {
+      const int k0 = kt * KT;
+      auto rowp = [&](const bf16_t* base, int r) {
+        int tok = k0 + r;
+        tok = tok < kv_len ? tok : kv_len - 1;
+        return base + (size_t)(kv_off + tok) * a.kv_stride + kvh * D;
+      };
+      stage_kv<D, false>(sK, wid_u, 4, lane, [&](int r) { return rowp(a.k, r); });
+      stage_kv<D, true>(sV, wid_u, 4, lane, [&](int r) { return rowp(a.v, r); });
+    }
+  };
+
+  if (n_kt > 0) stage(0, 0);
+  wait_vmcnt0();
+  __syncthreads();
+
+  for (int kt = 0; kt < n_kt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < n_kt) stage(kt + 1, cur ^ 1);
+    const char* sK = smem + cur * 2 * C::TILEB;
+    const char* sV = sK + C::TILEB;
+    const int k0 = kt * KT;
+    if (!CAUSAL || k0 <= wave_pmax) {
+      // ---- S^T = K Q^T ----
+      f32x4 s[4][2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s[t][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
+        s[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < C::KS; ++ks) {
+          const bf16x8 kf = load_k<D>(sK, t, ks, lane);
+          s[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][ks], s[t][0], 0, 0, 0);
+          s[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][ks], s[t][1], 0, 0, 0);
+        }
+      }
+      // ---- online softmax (per query column, lane-local + xor 16/32) ----
+      const bool need_mask = CAUSAL ? (k0 + KT - 1 > ctx0 + pbase) || (k0 + KT > kv_len) : (k0 + KT > kv_len);
+      float alpha[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int qpos = ctx0 + pbase + 16 * qt + fr;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = s[t][qt][r] * a.scale_log2;
+            if (need_mask) {
+              const int kj = k0 + 16 * t + 4 * fh + r;
+              const bool ok = kj < kv_len && (!CAUSAL || kj <= qpos);
+              x = ok ? x : -INFINITY;
+            }
+            s[t][qt][r] = x;
+            mx = fmaxf(mx, x);
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_i[qt], mx);
+        const float m_use = m_new == -INFINITY ? 0.f : m_new;
+        alpha[qt] = exp2f(m_i[qt] - m_use);
+        float ls = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float p = exp2f(s[t][qt][r] - m_use);
+            s[t][qt][r] = p;
+            ls += p;
+          }
+        l_i[qt] = l_i[qt] * alpha[qt] + ls;
+        m_i[qt] = m_new;
+      }
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) o[dt][qt] *= alpha[qt];
+      // ---- O^T += V^T P^T ----
+      bf16x8 pb[2][2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) pb[ks][qt] = pack_p(s[2 * ks][qt], s[2 * ks + 1][qt]);
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 vf = load_vt<D>(sV, dt, ks, lane);
+          o[dt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[ks][0], o[dt][0], 0, 0, 0);
+          o[dt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[ks][1], o[dt][1], 0, 0, 0);
+        }
+    }
+    wait_vmcnt0();
+    __syncthreads();
+  }
+
+  // ---- finalize: O = O^T / l, store 4 consecutive d (8 B) per (dt, qt) ----
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    float l = l_i[qt];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int qi = pbase + 16 * qt + fr;
+    if (qi < q_len) {
+      bf16_t* op = a.out + (size_t)(q_off + qi) * a.out_stride + hq * D + 4 * fh;
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+        const f32x4 v = o[dt][qt] * inv;
+        const unsigned lo = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+        const unsigned hi = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(op + 16 * dt) = make_uint2(lo, hi);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Decode attention (one query token per sequence), split-K over context partitions.
+// ------------------------------------------------------------------------------------
+struct DecodeArgs {
+  const bf16_t* q; int q_stride;           // [B] rows, head h at +h*D
+  const bf16_t* kc; const bf16_t* vc;      // paged caches
+  const int* block_tables; int bt_stride;
+  const int* kv_lens;                      // [B]
+  float* part_o;                           // [B][Hq][max_parts][D]
+  float* part_ml;                          // [B][Hq][max_parts][2]
+  bf16_t* out; int out_stride;
+  int Hq, Hkv, part_tiles, max_parts;
+  float scale_log2;
+};
+
+template <int D, int G>
+__global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a) {
+  using C = Cfg<D>;
+  static_assert(G <= 16, "at most 16 query heads per KV head");
+  __shared__ __attribute__((aligned(16))) char smem[4 * C::TILEB];  // one V tile per wave
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int kv_len = a.kv_lens[b];
+  const int n_kt = (kv_len + KT - 1) / KT;
+  const int kt0 = part * a.part_tiles;
+  if (kt0 >= n_kt) return;  // block-uniform early exit (before any barrier)
+  const int kt1 = min(kt0 + a.part_tiles, n_kt);
+  const int nparts = (n_kt + a.part_tiles - 1) / a.part_tiles;
+  const int fr = lane & 15, fh = lane >> 4;
+  const int* bt = a.block_tables + (size_t)b * a.bt_stride;
+
+  bf16x8 qf[C::KS];
+  {
+    const int g = fr < G ? fr : 0;
+    const bf16_t* qp = a.q + (size_t)b * a.q_stride + (kvh * G + g) * D + 8 * fh;
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(qp + 32 * s);
+      qf[s] = fr < G ? v : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  f32x4 o[C::DT];
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m_i = -INFINITY, l_i = 0.f;
+  char* sV = smem + wid * C::TILEB;
+
+  for (int kt = kt0 + wid_u; kt < kt1; kt += 4) {
+    const size_t base = ((size_t)bt[kt] * a.Hkv + kvh) * KT * D;
+    const bf16_t* kb = a.kc + base;
+    const bf16_t* vb = a.vc + base;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous tile's V reads retired
+    // V tile -> wave-private LDS (transposed reads later)
+    stage_kv<D, true>(sV, 0, 1, lane, [&](int r) { return vb + (size_t)r * D; });
+    // K fragments straight to VGPRs
+    bf16x8 kf[4][C::KS];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s)
+        kf[t][s] = *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
+    f32x4 s4[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s4[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) s4[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t][s], qf[s], s4[t], 0, 0, 0);
+    }
+    const int k0 = kt * KT;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kj = k0 + 16 * t + 4 * fh + r;
+        const float x = kj < kv_len ? s4[t][r] * a.scale_log2 : -INFINITY;
+        s4[t][r] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_i, mx);
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;
+    const float alpha = exp2f(m_i - m_use);
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s4[t][r] - m_use);
+        s4[t][r] = p;
+        ls += p;
+      }
+    l_i = l_i * alpha + ls;
+    m_i = m_new;
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) o[dt] *= alpha;
+    const bf16x8 pb0 = pack_p(s4[0], s4[1]);
+    const bf16x8 pb1 = pack_p(s4[2], s4[3]);
+    wait_vmcnt0();  // V tile landed in this wave's LDS
+#pragma unroll
+    for (int dt = 0; dt < C::DT; ++dt) {
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(load_vt<D>(sV, dt, 0, lane), pb0, o[dt], 0, 0, 0);
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(load_vt<D>(sV, dt, 1, lane), pb1, o[dt], 0, 0, 0);
+    }
+  }
+
+  // ---- combine the 4 waves in LDS ----
+  __syncthreads();
+  float* sm = reinterpret_cast<float*>(smem);    // [4][16] max
+  float* sl = sm + 4 * 16;                       // [4][64] partial l (per lane)
+  float* so = sl + 4 * 64;                       // [4][16][D] O
+  if (fh == 0) sm[wid * 16 + fr] = m_i;
+  sl[wid * 64 + lane] = l_i;
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) so[(wid * 16 + fr) * D + 16 * dt + 4 * fh + r] = o[dt][r];
+  __syncthreads();
+  // thread -> (g, d) pairs
+  for (int e = threadIdx.x; e < G * D; e += 256) {
+    const int g = e / D, d = e % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[w * 16 + g]);
+    const float Mu = M == -INFINITY ? 0.f : M;
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float sc = exp2f(sm[w * 16 + g] - Mu);
+      L += (sl[w * 64 + g] + sl[w * 64 + g + 16] + sl[w * 64 + g + 32] + sl[w * 64 + g + 48]) * sc;
+      O += so[(w * 16 + g) * D + d] * sc;
+    }
+    const int hq = kvh * G + g;
+    if (nparts == 1) {
+      a.out[(size_t)b * a.out_stride + hq * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+    } else {
+      const size_t pi = ((size_t)b * a.Hq + hq) * a.max_parts + part;
+      a.part_o[pi * D + d] = O;
+      if (d == 0) {
+        a.part_ml[pi * 2] = M;
+        a.part_ml[pi * 2 + 1] = L;
+      }
+    }
+  }
+}
+
+// merge split-K partitions: grid (Hq, B), block D threads
+__global__ void attn_decode_reduce_kernel(DecodeArgs a, int D) {
+  const int hq = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+  const int n_kt = (a.kv_lens[b] + KT - 1) / KT;
+  const int nparts = (n_kt + a.part_tiles - 1) / a.part_tiles;
+  if (nparts <= 1 || d >= D) return;
+  const size_t p0 = ((size_t)b * a.Hq + hq) * a.max_parts;
+  float M = -INFINITY;
+  for (int p = 0; p < nparts; ++p) M = fmaxf(M, a.part_ml[(p0 + p) * 2]);
+  const float Mu = M == -INFINITY ? 0.f : M;
+  float L = 0.f, O = 0.f;
+  for (int p = 0; p < nparts; ++p) {
+    const float sc = exp2f(a.part_ml[(p0 + p) * 2] - Mu);
+    L += a.part_ml[(p0 + p) * 2 + 1] * sc;
+    O += a.part_o[(p0 + p) * D + d] * sc;
+  }
+  a.out[(size_t)b * a.out_stride + hq * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+}
+
+template <int D, int GB, bool CAUSAL, bool PAGED>
+hipError_t launch_prefill(const PrefillArgs& a, int n_tiles, hipStream_t st) {
+  const int G = a.Hq / a.Hkv;
+  dim3 grid(n_tiles, a.Hkv * (G / GB));
+  hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+// Returns the query positions per block (the host builds `tiles` with this step).
+RAGK_API int ragk_attn_prefill_qtile(int Hq, int Hkv) {
+  const int G = Hq / Hkv;
+  const int GB = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
+  return 32 * (4 / GB);
+}
+
+RAGK_API int ragk_attn_prefill(const void* q, int q_stride, const void* k, const void* v, int kv_stride,
+                               const int* block_tables, int bt_stride, const int* cu_q, const int* cu_kv,
+                               const int* kv_lens, const int* tiles, int n_tiles, void* out, int out_stride,
+                               int Hq, int Hkv, int D, int causal, int paged, float scale, hipStream_t st) {
+  if (n_tiles <= 0) return 0;
+  if (Hq % Hkv) return (int)hipErrorInvalidValue;
+  PrefillArgs a{(const bf16_t*)q, q_stride, (const bf16_t*)k, (const bf16_t*)v, kv_stride, block_tables, bt_stride,
+                cu_q, cu_kv, kv_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, scale * 1.4426950408889634f};
+  const int G = Hq / Hkv;
+  const int GB = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
+#define RAGK_PF(DD, GG, CC, PP)                                                          \
+  if (D == DD && GB == GG && (bool)causal == CC && (bool)paged == PP)                      \
+    return (int)launch_prefill<DD, GG, CC, PP>(a, n_tiles, st);
+  RAGK_PF(128, 4, true, true)
+  RAGK_PF(128, 1, true, true)
+  RAGK_PF(64, 1, true, true)
+  RAGK_PF(64, 4, true, true)
+  RAGK_PF(128, 4, true, false)
+  RAGK_PF(64, 1, false, false)
+  RAGK_PF(32, 1, false, false)
+  RAGK_PF(128, 1, false, false)
+  RAGK_PF(64, 1, true, false)
+#undef RAGK_PF
+  return (int)hipErrorInvalidValue;
+}
+
+RAGK_API int ragk_attn_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
+                              int bt_stride, const int* kv_lens, float* part_o, float* part_ml, void* out,
+                              int out_stride, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
+                              float scale, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (Hq % Hkv || part_tiles < 1 || max_parts < 1) return (int)hipErrorInvalidValue;
+  DecodeArgs a{(const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, bt_stride, kv_lens,
+               part_o, part_ml, (bf16_t*)out, out_stride, Hq, Hkv, part_tiles, max_parts,
+               scale * 1.4426950408889634f};
+  const int G = Hq / Hkv;
+  dim3 grid(max_parts, Hkv, B);
+#define RAGK_DC(DD, GG)                                                            \
+  if (D == DD && G == GG) {                                                          \
+    hipLaunchKernelGGL((attn_decode_kernel<DD, GG>), grid, dim3(256), 0, st, a);     \
+    if (max_parts > 1)                                                               \
+      hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(Hq, B), dim3(DD), 0, st, a, DD); \
+    return (int)hipGetLastError();                                                   \
+  }
+  RAGK_DC(128, 4)
+  RAGK_DC(128, 8)
+  RAGK_DC(128, 1)
+  RAGK_DC(64, 1)
+  RAGK_DC(64, 4)
+  RAGK_DC(128, 2)
+#undef RAGK_DC
+  return (int)hipErrorInvalidValue;
+}

@@ -1,0 +1,114 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernel library.
+//
+// Every kernel in csrc/kernels/*.hip is written for 64-lane wavefronts, MFMA
+// matrix cores and the 160 KiB LDS of gfx950. No CUDA / dual-path code: this
+// library only targets --offload-arch=gfx950.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RAGK_API extern "C" __attribute__((visibility("default")))
+
+typedef unsigned short bf16_t;  // raw bf16 bits in memory
+typedef __attribute__((ext_vector_type(8))) short bf16x8;  // MFMA A/B fragment (4 VGPRs)
+typedef __attribute__((ext_vector_type(4))) short bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;    // 16x16 MFMA accumulator
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
+namespace ragk {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ float bf2f(bf16_t x) {
+  return __uint_as_float(((unsigned)x) << 16);
+}
+__device__ __forceinline__ float bf2f_s(short x) {
+  return __uint_as_float(((unsigned)(unsigned short)x) << 16);
+}
+// Round-to-nearest-even f32 -> bf16; hipcc lowers the __bf16 cast to
+// v_cvt_pk_bf16_f32 on gfx950 (keeps NaNs NaN).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, h);
+}
+__device__ __forceinline__ short f2bf_s(float f) { return (short)f2bf(f); }
+
+// 16-byte vector of 8 bf16 <-> 8 floats
+__device__ __forceinline__ void unpack8(const u32x4 v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  u32x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    v[i] = (unsigned)f2bf(f[2 * i]) | ((unsigned)f2bf(f[2 * i + 1]) << 16);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x a multiple of 64 (<= 1024). `red` needs
+// blockDim.x/64 floats of LDS. Result is broadcast to every thread.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+// Bijective XCD-aware block remap (MI355X: 8 XCDs, blocks dealt round-robin).
+// Blocks b, b+8, b+16... share an XCD; remap so each XCD gets a contiguous range
+// of logical tile ids (neighbouring tiles share operand panels in its L2).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+// async global -> LDS copy, 16 B per lane; LDS destination = wave-uniform base + lane*16.
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base,
+                                   16, 0, 0);
+}
+__device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+}  // namespace ragk
+
+// Epilogue selector shared by the GEMM family.
+enum RagkEpilogue : int {
+  EPI_NONE = 0,      // C = acc
+  EPI_BIAS = 1,      // C = acc + bias[n]
+  EPI_RESID = 2,     // C = resid + acc            (resid may alias C)
+  EPI_BIAS_RESID = 3,// C = resid + acc + bias[n]
+  EPI_BIAS_GELU = 4, // C = gelu_erf(acc + bias[n])
+  EPI_SILU_MUL = 5,  // paired columns: C[:, j] = silu(gate_j) * up_j
+  EPI_GELU = 6,      // C = gelu_erf(acc)
+  EPI_BIAS_GELU_TANH = 7,  // GPT-2 MLP
+};

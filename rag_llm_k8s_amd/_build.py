@@ -1,0 +1,112 @@
+"""In-tree native build for the framework.
+
+Two artefacts, both written into ``rag_llm_k8s_amd/_lib/`` so they travel with the
+repository snapshot to the GPU box:
+
+* ``libragk_hip.so``  -- every gfx950 HIP kernel in ``csrc/kernels/*.hip``
+  (hipcc --offload-arch=gfx950), C ABI, loaded with ctypes after ``import torch``
+  so it binds to torch's HIP runtime (same ``libamdhip64.so.7`` SONAME).
+* ``_ragk_rt*.so``    -- the C++ host runtime in ``csrc/runtime/*.cpp`` (pybind11):
+  safetensors mmap reader, faiss-format index I/O, tokenizers, KV block manager.
+
+Incremental: an object is rebuilt only when its source or a header is newer.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(ROOT, "rag_llm_k8s_amd", "_lib")
+OBJ_DIR = os.path.join(ROOT, "build", "obj")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+HIP_LIB = os.path.join(LIB_DIR, "libragk_hip.so")
+
+
+def _newer(src_files, target):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in src_files)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed: %s\n%s" % (" ".join(cmd), r.stdout))
+    return r.stdout
+
+
+def build_hip(verbose=False, jobs=None):
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    os.makedirs(LIB_DIR, exist_ok=True)
+    kdir = os.path.join(ROOT, "csrc", "kernels")
+    srcs = sorted(glob.glob(os.path.join(kdir, "*.hip")))
+    headers = glob.glob(os.path.join(kdir, "*.h"))
+    flags = ["-O3", "--offload-arch=" + ARCH, "-fPIC", "-std=c++17", "-I" + kdir,
+             "-Wno-unused-result", "-munsafe-fp-atomics"]
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
+        objs.append(o)
+        if _newer([s] + headers, o):
+            todo.append((s, o))
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        futs = [ex.submit(_run, [HIPCC] + flags + ["-c", s, "-o", o]) for s, o in todo]
+        for f in futs:
+            out = f.result()
+            if verbose and out.strip():
+                print(out)
+    if todo or _newer(objs, HIP_LIB):
+        _run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", HIP_LIB])
+    return HIP_LIB
+
+
+def runtime_ext_path():
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(LIB_DIR, "_ragk_rt" + suffix)
+
+
+def build_runtime(verbose=False):
+    import pybind11
+
+    os.makedirs(LIB_DIR, exist_ok=True)
+    rdir = os.path.join(ROOT, "csrc", "runtime")
+    srcs = sorted(glob.glob(os.path.join(rdir, "*.cpp")))
+    if not srcs:
+        return None
+    headers = glob.glob(os.path.join(rdir, "*.h"))
+    target = runtime_ext_path()
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    inc = ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"], "-I" + rdir]
+    flags = ["-O2", "-fPIC", "-std=c++17", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"]
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(OBJ_DIR, "rt_" + os.path.basename(s) + ".o")
+        objs.append(o)
+        if _newer([s] + headers, o):
+            todo.append((s, o))
+    with cf.ThreadPoolExecutor(min(8, os.cpu_count() or 4)) as ex:
+        for f in [ex.submit(_run, ["g++"] + flags + inc + ["-c", s, "-o", o]) for s, o in todo]:
+            out = f.result()
+            if verbose and out.strip():
+                print(out)
+    if todo or _newer(objs, target):
+        _run(["g++", "-shared", "-fPIC"] + objs + ["-o", target])
+    return target
+
+
+def build_all(verbose=False):
+    paths = [build_hip(verbose=verbose), build_runtime(verbose=verbose)]
+    return [p for p in paths if p]
+
+
+if __name__ == "__main__":
+    for p in build_all(verbose="-v" in sys.argv):
+        print(p)

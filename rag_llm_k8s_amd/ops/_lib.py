@@ -1,0 +1,96 @@
+"""ctypes binding of the gfx950 kernel library (``_lib/libragk_hip.so``).
+
+Dispatch policy of the whole ``ops`` package: tensors on a GPU go to the native HIP
+kernels -- if the library is missing or fails to load on a GPU box, we raise
+(no silent eager fallback); tensors on the CPU go to the pure-torch reference
+implementations in :mod:`rag_llm_k8s_amd.ops.reference` (the CPU plumbing
+configuration of BASELINE.json config 1).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib", "libragk_hip.so")
+
+P, I, F, S, U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_uint64
+
+_SIGS = {
+    "ragk_gemm": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
+    "ragk_gemm_path": [I, P, I, P, I, P, I, P, P, I, I, I, I, I, S],
+    "ragk_rmsnorm": [P, I, P, I, P, P, I, I, I, F, S],
+    "ragk_layernorm": [P, I, P, I, P, P, P, I, I, I, F, S],
+    "ragk_embed": [P, P, P, I, I, I, S],
+    "ragk_embed_ln": [P, P, P, P, P, P, P, P, I, I, F, I, S],
+    "ragk_rope_kv": [P, I, P, P, P, P, P, P, I, I, I, I, I, I, S],
+    "ragk_pool_l2norm": [P, I, P, P, I, I, I, I, S],
+    "ragk_silu_mul": [P, I, P, I, I, I, S],
+    "ragk_gather_rows": [P, I, P, P, I, I, I, S],
+    "ragk_attn_prefill_qtile": [I, I],
+    "ragk_attn_prefill": [P, I, P, P, I, P, I, P, P, P, P, I, P, I, I, I, I, I, I, F, S],
+    "ragk_attn_decode": [P, I, P, P, P, I, P, P, P, P, I, I, I, I, I, I, I, F, S],
+    "ragk_topk_candidates": [P, I, I, I, I, I, P, P, S],
+    "ragk_sample_candidates": [P, P, I, I, P, P, P, P, P, P, P, S],
+    "ragk_l2_partial": [P, I, I, I, I, P, I, I, P, P, P, P, S],
+    "ragk_topk_merge": [P, P, I, I, I, P, P, S],
+    "ragk_l2_append": [P, I, I, I, P, I, S],
+    "ragk_l2_gather": [P, I, I, P, I, P, S],
+}
+_OPTIONAL = {"ragk_allreduce_oneshot", "ragk_ipc_get_handle", "ragk_ipc_open_handle", "ragk_ipc_close_handle",
+             "ragk_allreduce_ipc", "ragk_ivf_scan", "ragk_quant_fp8", "ragk_gemm_fp8"}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def available() -> bool:
+    return os.path.exists(LIB_PATH)
+
+
+def lib():
+    """Load (once) and return the kernel library. Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryError(
+                "gfx950 kernel library not built (%s). Run `python -m rag_llm_k8s_amd._build` "
+                "or __graft_entry__.build()." % LIB_PATH)
+        h = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, args in _SIGS.items():
+            fn = getattr(h, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        _lib = h
+        return h
+
+
+def has_symbol(name: str) -> bool:
+    try:
+        return hasattr(lib(), name)
+    except NativeLibraryError:
+        return False
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise NativeLibraryError("%s failed with hipError %d" % (what, rc))
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()

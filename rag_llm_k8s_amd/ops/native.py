@@ -1,0 +1,281 @@
+"""Shape-checked Python entry points of the gfx950 kernels (GPU tensors only).
+
+Every function validates dtype / contiguity / shapes on the host *before* the launch
+(a mis-shaped launch could fault the GPU), then calls the C ABI with the current
+HIP stream, so everything here is capturable in a hipGraph (torch.cuda.CUDAGraph).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+from ._lib import check, ptr, stream_ptr
+from .reference import EPI
+
+
+def _req(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _bf16_2d(t, name):
+    _req(t.is_cuda and t.dtype == torch.bfloat16 and t.dim() == 2, "%s must be a 2-D bf16 GPU tensor" % name)
+    _req(t.stride(1) == 1, "%s must be row-contiguous" % name)
+
+
+# ----------------------------------------------------------------------------- GEMM
+def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=None):
+    """out[M,N] = epi(x[M,K] @ w[N,K]^T). For epi='silu_mul', w is the packed
+    gate/up weight [2N, K] (see reference.pack_gate_up) and out has N columns."""
+    _bf16_2d(x, "x")
+    _bf16_2d(w, "w")
+    M, K = x.shape
+    e = EPI[epi]
+    N = w.shape[0] // 2 if epi == "silu_mul" else w.shape[0]
+    _req(w.shape[1] == K, "K mismatch %s vs %s" % (tuple(x.shape), tuple(w.shape)))
+    _req(K % 128 == 0, "K must be a multiple of 128 (got %d)" % K)
+    if epi == "silu_mul":
+        _req(N % 64 == 0, "silu_mul needs N % 64 == 0")
+    if "bias" in epi:
+        _req(bias is not None and bias.is_cuda and bias.dtype == torch.bfloat16 and bias.numel() == N
+             and bias.is_contiguous(), "bias must be bf16[N]")
+    if "resid" in epi:
+        _bf16_2d(resid, "resid")
+        _req(resid.shape == (M, N), "resid shape")
+    odt = torch.float32 if out_f32 else torch.bfloat16
+    if out is None:
+        out = torch.empty((M, N), dtype=odt, device=x.device)
+    _req(out.dtype == odt and out.shape == (M, N) and out.stride(1) == 1, "out shape/dtype")
+    if M > 64 and N % 8 != 0 and epi != "silu_mul":
+        raise ValueError("tile GEMM needs N % 8 == 0")
+    if M == 0:
+        return out
+    L = _lib.lib()
+    ldr = resid.stride(0) if resid is not None else 0
+    if path is None:
+        rc = L.ragk_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
+                         ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), stream_ptr())
+    else:
+        rc = L.ragk_gemm_path(path, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(),
+                              out.stride(0), ptr(bias), ptr(resid), ldr, M, N, K, e, stream_ptr())
+    check(rc, "ragk_gemm")
+    return out
+
+
+# ----------------------------------------------------------------------------- norms
+def rmsnorm(x, w, eps, out=None, resid=None):
+    _bf16_2d(x, "x")
+    T, H = x.shape
+    _req(w.numel() == H and w.dtype == torch.bfloat16, "weight")
+    _req(H % 8 == 0 and H <= 8192, "H must be a multiple of 8, <= 8192")
+    if resid is not None:
+        _bf16_2d(resid, "resid")
+        _req(resid.shape == x.shape, "resid shape")
+    out = torch.empty_like(x) if out is None else out
+    check(_lib.lib().ragk_rmsnorm(x.data_ptr(), x.stride(0), ptr(resid), resid.stride(0) if resid is not None else 0,
+                                  w.data_ptr(), out.data_ptr(), out.stride(0), T, H, float(eps), stream_ptr()),
+          "ragk_rmsnorm")
+    return out
+
+
+def layernorm(x, g, b, eps, out=None, resid=None):
+    _bf16_2d(x, "x")
+    T, H = x.shape
+    _req(H % 8 == 0 and H <= 8192, "H")
+    out = torch.empty_like(x) if out is None else out
+    check(_lib.lib().ragk_layernorm(x.data_ptr(), x.stride(0), ptr(resid), resid.stride(0) if resid is not None else 0,
+                                    g.data_ptr(), b.data_ptr(), out.data_ptr(), out.stride(0), T, H, float(eps),
+                                    stream_ptr()), "ragk_layernorm")
+    return out
+
+
+def embed(ids, table, out=None):
+    _req(ids.dtype == torch.int32 and ids.is_cuda and ids.is_contiguous(), "ids int32")
+    V, H = table.shape
+    out = torch.empty((ids.numel(), H), dtype=table.dtype, device=table.device) if out is None else out
+    check(_lib.lib().ragk_embed(ids.data_ptr(), table.data_ptr(), out.data_ptr(), ids.numel(), H, V, stream_ptr()),
+          "ragk_embed")
+    return out
+
+
+def embed_ln(ids, pos_ids, word, pos, type_row, g, b, eps, do_ln=True, out=None):
+    _req(ids.dtype == torch.int32 and pos_ids.dtype == torch.int32, "int32 ids")
+    _req(int(ids.numel()) == int(pos_ids.numel()), "ids/pos_ids")
+    H = word.shape[1]
+    out = torch.empty((ids.numel(), H), dtype=word.dtype, device=word.device) if out is None else out
+    check(_lib.lib().ragk_embed_ln(ids.data_ptr(), pos_ids.data_ptr(), word.data_ptr(), pos.data_ptr(),
+                                   ptr(type_row), ptr(g), ptr(b), out.data_ptr(), ids.numel(), H, float(eps),
+                                   int(do_ln), stream_ptr()), "ragk_embed_ln")
+    return out
+
+
+def rope_kv(qkv, positions, cos_t, sin_t, slots, k_cache, v_cache, Hq, Hkv, D, apply_rope=True):
+    """In-place RoPE on q and k (inside qkv [T, (Hq+2Hkv)*D]) + paged cache write."""
+    _bf16_2d(qkv, "qkv")
+    T = qkv.shape[0]
+    _req(qkv.shape[1] >= (Hq + 2 * Hkv) * D, "qkv width")
+    _req(positions.dtype == torch.int32 and positions.numel() == T, "positions")
+    if slots is not None:
+        _req(slots.dtype == torch.int32 and slots.numel() == T, "slots")
+        _req(k_cache.dim() == 4 and k_cache.shape[1] == Hkv and k_cache.shape[3] == D, "cache layout")
+    BS = k_cache.shape[2] if k_cache is not None else 64
+    check(_lib.lib().ragk_rope_kv(qkv.data_ptr(), qkv.stride(0), positions.data_ptr(), ptr(cos_t), ptr(sin_t),
+                                  ptr(slots), ptr(k_cache), ptr(v_cache), T, Hq, Hkv, D, BS, int(apply_rope),
+                                  stream_ptr()), "ragk_rope_kv")
+
+
+def pool_l2norm(hidden, cu, mode="cls", normalize=True, out=None):
+    _bf16_2d(hidden, "hidden")
+    B = cu.numel() - 1
+    H = hidden.shape[1]
+    _req(H <= 2048, "H <= 2048")
+    m = {"cls": 0, "mean": 1, "last": 2}[mode]
+    out = torch.empty((B, H), dtype=torch.float32, device=hidden.device) if out is None else out
+    check(_lib.lib().ragk_pool_l2norm(hidden.data_ptr(), hidden.stride(0), cu.data_ptr(), out.data_ptr(), B, H, m,
+                                      int(normalize), stream_ptr()), "ragk_pool_l2norm")
+    return out
+
+
+def silu_mul(x, out=None):
+    _bf16_2d(x, "x")
+    T, I2 = x.shape
+    I = I2 // 2
+    out = torch.empty((T, I), dtype=x.dtype, device=x.device) if out is None else out
+    check(_lib.lib().ragk_silu_mul(x.data_ptr(), x.stride(0), out.data_ptr(), out.stride(0), T, I, stream_ptr()),
+          "ragk_silu_mul")
+    return out
+
+
+def gather_rows(x, idx, out=None):
+    _bf16_2d(x, "x")
+    _req(idx.dtype == torch.int32 and idx.is_cuda, "idx int32")
+    n = idx.numel()
+    out = torch.empty((n, x.shape[1]), dtype=x.dtype, device=x.device) if out is None else out
+    check(_lib.lib().ragk_gather_rows(x.data_ptr(), x.stride(0), idx.data_ptr(), out.data_ptr(), out.stride(0), n,
+                                      x.shape[1], stream_ptr()), "ragk_gather_rows")
+    return out
+
+
+# ----------------------------------------------------------------------------- attention
+def prefill_qtile(Hq, Hkv):
+    G = Hq // Hkv
+    GB = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
+    return 32 * (4 // GB)
+
+
+def build_prefill_tiles(q_lens, Hq, Hkv):
+    """(seq, q_start) work list, heaviest (latest query positions) first."""
+    qt = prefill_qtile(Hq, Hkv)
+    tiles = []
+    for s, ql in enumerate(q_lens):
+        for q0 in range(0, int(ql), qt):
+            tiles.append((s, q0))
+    tiles.sort(key=lambda t: -t[1])
+    return torch.tensor(tiles, dtype=torch.int32).reshape(-1, 2)
+
+
+def attn_prefill(q, k, v, cu_q, kv_lens, tiles, out, Hq, Hkv, D, causal=True, paged=True, block_tables=None,
+                 cu_kv=None, kv_stride=0, scale=None):
+    """q: [T, >=Hq*D] bf16 (row stride arbitrary). paged: k/v caches [nb, Hkv, 64, D];
+    else packed k/v row pointers with `kv_stride` (element stride per token)."""
+    _req(q.dtype == torch.bfloat16 and q.stride(-1) == 1, "q")
+    _req(tiles.dtype == torch.int32 and tiles.is_cuda and tiles.is_contiguous(), "tiles int32 on GPU")
+    _req(D in (32, 64, 128), "head_dim must be 32/64/128")
+    if paged:
+        _req(k.dim() == 4 and k.shape[2] == 64 and k.shape[1] == Hkv and k.shape[3] == D, "paged cache [nb,Hkv,64,D]")
+        _req(block_tables is not None and block_tables.dtype == torch.int32, "block_tables int32")
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    n_tiles = tiles.shape[0]
+    check(_lib.lib().ragk_attn_prefill(
+        q.data_ptr(), q.stride(0), k.data_ptr(), v.data_ptr(), kv_stride, ptr(block_tables),
+        block_tables.stride(0) if block_tables is not None else 0, cu_q.data_ptr(), ptr(cu_kv), kv_lens.data_ptr(),
+        tiles.data_ptr(), n_tiles, out.data_ptr(), out.stride(0), Hq, Hkv, D, int(causal), int(paged), float(scale),
+        stream_ptr()), "ragk_attn_prefill")
+    return out
+
+
+def decode_partitions(max_kv_len, batch, Hkv, target_blocks=1024):
+    """(part_tiles, max_parts) for split-K decode sized for >= target_blocks blocks."""
+    max_kt = max(1, (max_kv_len + 63) // 64)
+    pt = max(4, -(-max_kt * batch * Hkv // target_blocks))
+    pt = -(-pt // 4) * 4
+    return pt, -(-max_kt // pt)
+
+
+def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, part_tiles, max_parts, ws_o=None,
+                ws_ml=None, scale=None):
+    B = kv_lens.numel()
+    _req(k_cache.dim() == 4 and k_cache.shape[2] == 64 and k_cache.shape[3] == D, "paged cache")
+    _req(block_tables.dtype == torch.int32 and block_tables.shape[0] >= B, "block_tables")
+    _req(kv_lens.dtype == torch.int32, "kv_lens int32")
+    G = Hq // Hkv
+    _req(G <= 16, "G <= 16")
+    if max_parts > 1:
+        if ws_o is None:
+            ws_o = torch.empty((B, Hq, max_parts, D), dtype=torch.float32, device=q.device)
+            ws_ml = torch.empty((B, Hq, max_parts, 2), dtype=torch.float32, device=q.device)
+        _req(ws_o.numel() >= B * Hq * max_parts * D and ws_ml.numel() >= B * Hq * max_parts * 2, "workspace")
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    check(_lib.lib().ragk_attn_decode(
+        q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
+        block_tables.stride(0), kv_lens.data_ptr(), ptr(ws_o), ptr(ws_ml), out.data_ptr(), out.stride(0), B, Hq, Hkv,
+        D, part_tiles, max_parts, float(scale), stream_ptr()), "ragk_attn_decode")
+    return out
+
+
+# ----------------------------------------------------------------------------- sampling
+def topk_candidates(logits, K, vocab_offset=0, cand_v=None, cand_i=None):
+    _req(logits.dtype == torch.float32 and logits.is_cuda and logits.stride(1) == 1, "logits fp32")
+    B, V = logits.shape
+    _req(1 <= K <= 256, "1 <= K <= 256")
+    if cand_v is None:
+        cand_v = torch.empty((B, K), dtype=torch.float32, device=logits.device)
+        cand_i = torch.empty((B, K), dtype=torch.int32, device=logits.device)
+    check(_lib.lib().ragk_topk_candidates(logits.data_ptr(), logits.stride(0), B, V, K, vocab_offset,
+                                          cand_v.data_ptr(), cand_i.data_ptr(), stream_ptr()), "ragk_topk_candidates")
+    return cand_v, cand_i
+
+
+def sample_candidates(cand_v, cand_i, temps, top_ks, top_ps, seeds, steps, out_tok=None, out_lp=None):
+    B, n = cand_v.shape
+    _req(n <= 2048, "<= 2048 candidates")
+    _req(temps.dtype == torch.float32 and top_ks.dtype == torch.int32 and top_ps.dtype == torch.float32, "param dtypes")
+    _req(seeds.dtype == torch.int64 and steps.dtype == torch.int32, "seeds int64 / steps int32")
+    out_tok = torch.empty(B, dtype=torch.int32, device=cand_v.device) if out_tok is None else out_tok
+    check(_lib.lib().ragk_sample_candidates(cand_v.data_ptr(), cand_i.data_ptr(), B, n, temps.data_ptr(),
+                                            top_ks.data_ptr(), top_ps.data_ptr(), seeds.data_ptr(), steps.data_ptr(),
+                                            out_tok.data_ptr(), ptr(out_lp), stream_ptr()), "ragk_sample_candidates")
+    return out_tok
+
+
+# ----------------------------------------------------------------------------- search
+def l2_search(xt, cap, n, q, k, row_begin=0, ids_map=None):
+    """Exact squared-L2 top-k over rows [row_begin, n) of a column-major store xt[d][cap].
+    Returns (D fp32 [nq,k], I int64 [nq,k]) with faiss padding semantics."""
+    _req(xt.dtype == torch.float32 and q.dtype == torch.float32 and q.is_contiguous(), "fp32")
+    d = xt.shape[0]
+    nq = q.shape[0]
+    _req(q.shape[1] == d, "dim mismatch")
+    _req(1 <= k <= 64, "1 <= k <= 64")
+    L = _lib.lib()
+    G = max(1, -(-(n - row_begin) // 1024))
+    pd = torch.empty((nq, G, k), dtype=torch.float32, device=q.device)
+    pi = torch.empty((nq, G, k), dtype=torch.int32, device=q.device)
+    check(L.ragk_l2_partial(xt.data_ptr(), cap, d, row_begin, n, q.data_ptr(), nq, k, pd.data_ptr(), pi.data_ptr(),
+                            ptr(ids_map), None, stream_ptr()), "ragk_l2_partial")
+    while G > 1:
+        Go = -(-G // 64)
+        od = torch.empty((nq, Go, k), dtype=torch.float32, device=q.device)
+        oi = torch.empty((nq, Go, k), dtype=torch.int32, device=q.device)
+        check(L.ragk_topk_merge(pd.data_ptr(), pi.data_ptr(), nq, G, k, od.data_ptr(), oi.data_ptr(), stream_ptr()),
+              "ragk_topk_merge")
+        pd, pi, G = od, oi, Go
+    return pd.reshape(nq, k), pi.reshape(nq, k).long()
+
+
+def l2_append(xt, cap, n0, x):
+    _req(x.dtype == torch.float32 and x.is_contiguous() and x.shape[1] == xt.shape[0], "x fp32 [n,d]")
+    check(_lib.lib().ragk_l2_append(xt.data_ptr(), cap, xt.shape[0], n0, x.data_ptr(), x.shape[0], stream_ptr()),
+          "ragk_l2_append")

@@ -1,0 +1,315 @@
+"""T1 kernel tier: every gfx950 HIP kernel vs a plain PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+from rag_llm_k8s_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 256, 256), (7, 4096, 512), (64, 512, 1024), (100, 384, 384), (256, 512, 512),
+                                   (300, 1024, 768), (1111, 6144, 4096)])
+def test_gemm_plain(native, M, N, K):
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    y = native.gemm(x, w)
+    ref = x.float() @ w.float().t()
+    assert rel_err(y, ref) < 1e-2
+
+
+@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("M", [1, 16, 33, 64])
+def test_gemm_paths_agree(native, path, M):
+    torch.manual_seed(1)
+    K, N = 1024, 768
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / 32).bfloat16()
+    y = native.gemm(x, w, path=path)
+    assert rel_err(y, x.float() @ w.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 5, 64, 200])
+def test_gemm_epilogues(native, M):
+    torch.manual_seed(2)
+    K, N = 512, 640
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / 16).bfloat16()
+    b = torch.randn(N, device=DEV).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    for epi in ["bias", "resid", "bias_resid", "bias_gelu", "gelu", "bias_gelu_tanh"]:
+        y = native.gemm(x, w, bias=b, resid=r, epi=epi)
+        ref = R.linear(x.cpu(), w.cpu(), b.cpu(), r.cpu(), epi=epi)
+        assert rel_err(y.cpu(), ref) < 1e-2, epi
+    yf = native.gemm(x, w, out_f32=True)
+    assert yf.dtype == torch.float32 and rel_err(yf, x.float() @ w.float().t()) < 1e-3
+
+
+@pytest.mark.parametrize("M", [1, 3, 64, 129])
+def test_gemm_silu_mul(native, M):
+    torch.manual_seed(3)
+    K, I = 512, 384
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    g = (torch.randn(I, K, device=DEV) / 16).bfloat16()
+    u = (torch.randn(I, K, device=DEV) / 16).bfloat16()
+    wp = R.pack_gate_up(g, u)
+    y = native.gemm(x, wp, epi="silu_mul")
+    ref = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
+    assert y.shape == (M, I)
+    assert rel_err(y, ref) < 1e-2
+
+
+def test_gemm_inplace_residual(native):
+    torch.manual_seed(4)
+    M, K, N = 80, 256, 256
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / 16).bfloat16()
+    h = torch.randn(M, N, device=DEV).bfloat16()
+    ref = h.float() + x.float() @ w.float().t()
+    native.gemm(x, w, resid=h, epi="resid", out=h)
+    assert rel_err(h, ref) < 1e-2
+
+
+@pytest.mark.parametrize("T,H", [(1, 4096), (37, 4096), (5, 384), (8, 1024)])
+def test_rmsnorm(native, T, H):
+    torch.manual_seed(5)
+    x = torch.randn(T, H, device=DEV).bfloat16()
+    w = torch.randn(H, device=DEV).bfloat16()
+    y = native.rmsnorm(x, w, 1e-5)
+    ref = R.rmsnorm(x.cpu(), w.cpu(), 1e-5)
+    assert (y.cpu().float() - ref.float()).abs().max().item() <= 0.0625
+    assert rel_err(y.cpu(), ref) < 4e-3
+    # fused residual
+    r = torch.randn(T, H, device=DEV).bfloat16()
+    r_ref = r.cpu().clone()
+    y2 = native.rmsnorm(x, w, 1e-5, resid=r)
+    ref2 = R.rmsnorm(x.cpu(), w.cpu(), 1e-5, resid=r_ref)
+    assert torch.equal(r.cpu(), r_ref)
+    assert rel_err(y2.cpu(), ref2) < 4e-3
+
+
+@pytest.mark.parametrize("T,H", [(3, 384), (17, 1024)])
+def test_layernorm(native, T, H):
+    torch.manual_seed(6)
+    x = torch.randn(T, H, device=DEV).bfloat16()
+    r = torch.randn(T, H, device=DEV).bfloat16()
+    g = torch.randn(H, device=DEV).bfloat16()
+    b = torch.randn(H, device=DEV).bfloat16()
+    y = native.layernorm(x, g, b, 1e-12, resid=r)
+    assert rel_err(y.cpu(), R.layernorm(x.cpu(), g.cpu(), b.cpu(), 1e-12, resid=r.cpu())) < 1e-2
+
+
+def test_embed_and_gather(native):
+    V, H = 1000, 256
+    table = torch.randn(V, H, device=DEV).bfloat16()
+    ids = torch.randint(0, V, (33,), device=DEV, dtype=torch.int32)
+    assert torch.equal(native.embed(ids, table), table[ids.long()])
+    idx = torch.tensor([3, 0, 32], dtype=torch.int32, device=DEV)
+    e = native.embed(ids, table)
+    assert torch.equal(native.gather_rows(e, idx), e[idx.long()])
+
+
+def test_embed_ln(native):
+    torch.manual_seed(7)
+    V, P, H = 500, 64, 384
+    word = torch.randn(V, H, device=DEV).bfloat16()
+    pos = torch.randn(P, H, device=DEV).bfloat16()
+    typ = torch.randn(1, H, device=DEV).bfloat16()
+    g = torch.randn(H, device=DEV).bfloat16()
+    b = torch.randn(H, device=DEV).bfloat16()
+    ids = torch.randint(0, V, (20,), device=DEV, dtype=torch.int32)
+    pids = torch.randint(0, P, (20,), device=DEV, dtype=torch.int32)
+    y = native.embed_ln(ids, pids, word, pos, typ, g, b, 1e-12)
+    h = word[ids.long()].float() + pos[pids.long()].float() + typ.float()
+    ref = torch.nn.functional.layer_norm(h, (H,), g.float(), b.float(), 1e-12)
+    assert rel_err(y, ref) < 1e-2
+
+
+def test_rope_kv_write(native):
+    torch.manual_seed(8)
+    T, Hq, Hkv, D, BS = 70, 8, 2, 128, 64
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).bfloat16()
+    pos = torch.arange(T, dtype=torch.int32, device=DEV) + 5
+    cos, sin = R.rope_tables(D, 1024, theta=500000.0,
+                             scaling={"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                      "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    kc = torch.zeros(4, Hkv, BS, D, device=DEV).bfloat16()
+    vc = torch.zeros_like(kc)
+    slots = torch.arange(T, dtype=torch.int32, device=DEV) + 64  # blocks 1..2
+    orig = qkv.clone()
+    native.rope_kv(qkv, pos, cos.to(DEV), sin.to(DEV), slots, kc, vc, Hq, Hkv, D)
+    q = orig[:, :Hq * D].reshape(T, Hq, D).cpu()
+    k = orig[:, Hq * D:(Hq + Hkv) * D].reshape(T, Hkv, D).cpu()
+    v = orig[:, (Hq + Hkv) * D:].reshape(T, Hkv, D).cpu()
+    q_ref = R.apply_rope(q, pos.long().cpu(), cos, sin)
+    k_ref = R.apply_rope(k, pos.long().cpu(), cos, sin)
+    assert torch.equal(qkv[:, :Hq * D].reshape(T, Hq, D).cpu(), q_ref)
+    kc_c = kc.cpu()
+    vc_c = vc.cpu()
+    for t in range(T):
+        s = t + 64
+        assert torch.equal(kc_c[s // BS, :, s % BS], k_ref[t])
+        assert torch.equal(vc_c[s // BS, :, s % BS], v[t])
+
+
+def _paged_setup(lens, Hkv, D, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    nb_per = [(L + 63) // 64 for L in lens]
+    total = sum(nb_per) + 3
+    kc = torch.zeros(total, Hkv, 64, D).bfloat16()
+    vc = torch.zeros_like(kc)
+    perm = torch.randperm(total, generator=g)
+    bts, i = [], 0
+    maxb = max(nb_per)
+    for L, nb in zip(lens, nb_per):
+        blocks = perm[i:i + nb]
+        i += nb
+        bt = torch.zeros(maxb, dtype=torch.int32)
+        bt[:nb] = blocks.int()
+        bts.append(bt)
+        kk = torch.randn(nb * 64, Hkv, D, generator=g)
+        vv = torch.randn(nb * 64, Hkv, D, generator=g)
+        kc[blocks] = kk.reshape(nb, 64, Hkv, D).permute(0, 2, 1, 3).bfloat16()
+        vc[blocks] = vv.reshape(nb, 64, Hkv, D).permute(0, 2, 1, 3).bfloat16()
+    return kc, vc, torch.stack(bts)
+
+
+@pytest.mark.parametrize("q_lens,kv_lens,Hq,Hkv", [([37], [37], 8, 2), ([100, 64, 1], [100, 300, 129], 32, 8),
+                                                   ([200], [200], 4, 4), ([5, 70], [513, 70], 8, 1)])
+def test_attn_prefill_paged(native, q_lens, kv_lens, Hq, Hkv):
+    D = 128
+    torch.manual_seed(9)
+    kc, vc, bt = _paged_setup(kv_lens, Hkv, D)
+    T = sum(q_lens)
+    q = torch.randn(T, Hq * D).bfloat16()
+    cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(q_lens), 0)), dtype=torch.int32)
+    kvl = torch.tensor(kv_lens, dtype=torch.int32)
+    tiles = native.build_prefill_tiles(q_lens, Hq, Hkv)
+    out = torch.empty(T, Hq * D, device=DEV).bfloat16()
+    native.attn_prefill(q.to(DEV), kc.to(DEV), vc.to(DEV), cu.to(DEV), kvl.to(DEV), tiles.to(DEV), out, Hq, Hkv, D,
+                        causal=True, paged=True, block_tables=bt.to(DEV))
+    ref = R.attention_varlen(q.reshape(T, Hq, D), None, None, cu, kvl, True, 1 / math.sqrt(D),
+                             k_full=lambda s: R.paged_kv_view(kc, bt[s], kv_lens[s], 64),
+                             v_full=lambda s: R.paged_kv_view(vc, bt[s], kv_lens[s], 64))
+    assert rel_err(out.cpu().reshape(T, Hq, D), ref) < 2e-2
+
+
+@pytest.mark.parametrize("D,H", [(32, 12), (64, 16)])
+def test_attn_encoder_contig(native, D, H):
+    torch.manual_seed(10)
+    lens = [7, 130, 64]
+    T = sum(lens)
+    qkv = torch.randn(T, 3 * H * D).bfloat16()
+    cu = torch.tensor([0, 7, 137, 201], dtype=torch.int32)
+    kvl = torch.tensor(lens, dtype=torch.int32)
+    tiles = native.build_prefill_tiles(lens, H, H)
+    out = torch.empty(T, H * D, device=DEV).bfloat16()
+    g = qkv.to(DEV)
+    native.attn_prefill(g, g[:, H * D:], g[:, 2 * H * D:], cu.to(DEV), kvl.to(DEV), tiles.to(DEV), out, H, H, D,
+                        causal=False, paged=False, cu_kv=cu.to(DEV), kv_stride=3 * H * D)
+    q = qkv[:, :H * D].reshape(T, H, D)
+    k = qkv[:, H * D:2 * H * D].reshape(T, H, D)
+    v = qkv[:, 2 * H * D:].reshape(T, H, D)
+    ref = R.attention_varlen(q, k, v, cu, kvl, False, 1 / math.sqrt(D), cu_kv=cu)
+    assert rel_err(out.cpu().reshape(T, H, D), ref) < 2e-2
+
+
+@pytest.mark.parametrize("kv_lens,Hq,Hkv,target", [([1], 32, 8, 1024), ([65, 300, 4100], 32, 8, 1024),
+                                                   ([777, 5], 32, 8, 8), ([200], 8, 8, 64)])
+def test_attn_decode(native, kv_lens, Hq, Hkv, target):
+    D = 128
+    torch.manual_seed(11)
+    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=3)
+    B = len(kv_lens)
+    q = torch.randn(B, Hq * D).bfloat16()
+    kvl = torch.tensor(kv_lens, dtype=torch.int32)
+    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv, target_blocks=target)
+    out = torch.empty(B, Hq * D, device=DEV).bfloat16()
+    native.attn_decode(q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), kvl.to(DEV), out, Hq, Hkv, D, pt, mp)
+    cu = torch.arange(B + 1, dtype=torch.int32)
+    ref = R.attention_varlen(q.reshape(B, Hq, D), None, None, cu, kvl, True, 1 / math.sqrt(D),
+                             k_full=lambda s: R.paged_kv_view(kc, bt[s], kv_lens[s], 64),
+                             v_full=lambda s: R.paged_kv_view(vc, bt[s], kv_lens[s], 64))
+    assert rel_err(out.cpu().reshape(B, Hq, D), ref) < 2e-2
+
+
+def test_pool_l2norm(native):
+    torch.manual_seed(12)
+    h = torch.randn(50, 384, device=DEV).bfloat16()
+    cu = torch.tensor([0, 10, 11, 50], dtype=torch.int32, device=DEV)
+    for mode in ["cls", "mean", "last"]:
+        y = native.pool_l2norm(h, cu, mode=mode)
+        ref = R.pool_l2norm(h.cpu(), cu.cpu(), mode=mode)
+        assert rel_err(y.cpu(), ref) < 1e-3, mode
+        assert torch.allclose(y.norm(dim=-1).cpu(), torch.ones(3), atol=1e-4)
+
+
+def test_silu_mul(native):
+    x = torch.randn(9, 2 * 512, device=DEV).bfloat16()
+    y = native.silu_mul(x)
+    ref = torch.nn.functional.silu(x[:, :512].float()) * x[:, 512:].float()
+    assert rel_err(y, ref) < 1e-2
+
+
+def test_topk_and_greedy(native):
+    torch.manual_seed(13)
+    B, V = 4, 128256
+    logits = torch.randn(B, V, device=DEV) * 3
+    cv, ci = native.topk_candidates(logits, 50)
+    ref_v, ref_i = torch.topk(logits, 50, dim=-1)
+    assert torch.allclose(cv, ref_v)
+    assert torch.equal(ci.long(), ref_i)
+    temps = torch.zeros(B, device=DEV)
+    ks = torch.full((B,), 50, dtype=torch.int32, device=DEV)
+    ps = torch.full((B,), 0.9, device=DEV)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV)
+    steps = torch.zeros(B, dtype=torch.int32, device=DEV)
+    tok = native.sample_candidates(cv, ci, temps, ks, ps, seeds, steps)
+    assert torch.equal(tok.long(), logits.argmax(-1))
+
+
+def test_sampling_support_matches_hf_rules(native):
+    """Sampled tokens always lie in the HF temperature->top-k->top-p kept set, and the
+    empirical distribution matches the renormalised kept probabilities."""
+    torch.manual_seed(14)
+    V = 1000
+    logits = torch.randn(1, V) * 4
+    kept, probs, _ = R.sample_from_logits(logits[0], 0.7, 50, 0.9)
+    n = 4000
+    L = logits.to(DEV).expand(n, V).contiguous()
+    cv, ci = native.topk_candidates(L, 50)
+    tok = native.sample_candidates(cv, ci, torch.full((n,), 0.7, device=DEV),
+                                   torch.full((n,), 50, dtype=torch.int32, device=DEV),
+                                   torch.full((n,), 0.9, device=DEV),
+                                   torch.arange(n, dtype=torch.int64, device=DEV) * 7919 + 1,
+                                   torch.zeros(n, dtype=torch.int32, device=DEV)).cpu().long()
+    kept_set = set(kept.tolist())
+    assert set(tok.tolist()) <= kept_set
+    counts = torch.zeros(V)
+    counts.index_add_(0, tok, torch.ones(n))
+    emp = counts[kept] / n
+    assert (emp - probs).abs().max().item() < 0.05
+
+
+@pytest.mark.parametrize("N,d,nq,k", [(0, 64, 2, 5), (3, 64, 1, 5), (10000, 384, 32, 4), (5000, 1024, 3, 10),
+                                      (70000, 128, 9, 8)])
+def test_l2_search(native, N, d, nq, k):
+    torch.manual_seed(15)
+    xb = torch.randn(N, d)
+    q = torch.randn(nq, d)
+    cap = max(N, 1) + 17
+    xt = torch.zeros(d, cap, device=DEV)
+    if N:
+        native.l2_append(xt, cap, 0, xb.to(DEV))
+    D, I = native.l2_search(xt, cap, N, q.to(DEV), k)
+    Dr, Ir = R.l2_knn(xb, q, k)
+    assert torch.equal(I.cpu(), Ir)
+    assert torch.allclose(D.cpu(), Dr, rtol=1e-4, atol=1e-3)
