@@ -102,6 +102,59 @@ __global__ __launch_bounds__(ST) void l2_block_topk_kernel(const float* __restri
   }
 }
 
+// IVF-Flat scan: block (probe p, chunk c) x query q scans rows [start, end) of list
+// probes[q][p] in the list-ordered column-major store -> partial top-k at [q][p*chunks+c].
+constexpr int IVF_DMAX = 2048;
+__global__ __launch_bounds__(ST) void ivf_scan_kernel(const float* __restrict__ xt, int cap, int d,
+                                                      const float* __restrict__ q, const int* __restrict__ probes,
+                                                      int nprobe, int chunks, const int* __restrict__ offsets,
+                                                      const int* __restrict__ ids_map, int k, float* out_d,
+                                                      int* out_i) {
+  __shared__ float qs[IVF_DMAX];
+  __shared__ float sd[RPB];
+  __shared__ int sidx[RPB];
+  const int qi = blockIdx.y;
+  const int p = blockIdx.x / chunks, c = blockIdx.x % chunks;
+  const int list = probes[(size_t)qi * nprobe + p];
+  const int lend = offsets[list + 1];
+  const int r0 = offsets[list] + c * RPB;
+  const int r1 = min(lend, r0 + RPB);
+  for (int t = threadIdx.x; t < d; t += ST) qs[t] = q[(size_t)qi * d + t];
+  __syncthreads();
+  float acc[RPT];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
+  if (r0 < r1) {
+    for (int t = 0; t < d; ++t) {
+      const float* col = xt + (size_t)t * cap;
+      const float qv = qs[t];
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        const int row = r0 + r * ST + threadIdx.x;
+        const float x = row < r1 ? col[row] : 0.f;
+        const float df = x - qv;
+        acc[r] = fmaf(df, df, acc[r]);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int slot = r * ST + threadIdx.x;
+    const int row = r0 + slot;
+    const bool ok = row < r1;
+    sd[slot] = ok ? acc[r] : FLT_MAX;
+    sidx[slot] = ok ? ids_map[row] : -1;
+  }
+  __syncthreads();
+  bitonic_asc(sd, sidx, RPB);
+  const int G = gridDim.x;
+  for (int i = threadIdx.x; i < k; i += ST) {
+    const size_t o = ((size_t)qi * G + blockIdx.x) * k + i;
+    out_d[o] = sd[i];
+    out_i[o] = sidx[i];
+  }
+}
+
 // in: [nq][G][k] -> out: [nq][ceil(G/64)][k]
 constexpr int MG = 64;
 __global__ __launch_bounds__(ST) void topk_merge_kernel(const float* __restrict__ in_d, const int* __restrict__ in_i,
@@ -161,6 +214,17 @@ RAGK_API int ragk_l2_partial(const float* xt, int cap, int d, int row_begin, int
   dim3 grid(G, (nq + QC - 1) / QC);
   hipLaunchKernelGGL(l2_block_topk_kernel, grid, dim3(ST), 0, st, xt, cap, d, row_begin, n > 0 ? row_end : row_begin,
                      q, nq, k, out_d, out_i, ids_map);
+  return (int)hipGetLastError();
+}
+
+// out buffers: nq * nprobe * chunks * k entries; chunks = ceil(max_list_len / 1024)
+RAGK_API int ragk_ivf_scan(const float* xt, int cap, int d, const float* q, int nq, const int* probes, int nprobe,
+                           int chunks, const int* offsets, const int* ids_map, int k, float* out_d, int* out_i,
+                           hipStream_t st) {
+  if (nq <= 0) return 0;
+  if (d > IVF_DMAX || k > RPB || chunks < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ivf_scan_kernel, dim3(nprobe * chunks, nq), dim3(ST), 0, st, xt, cap, d, q, probes, nprobe,
+                     chunks, offsets, ids_map, k, out_d, out_i);
   return (int)hipGetLastError();
 }
 

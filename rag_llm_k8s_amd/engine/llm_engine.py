@@ -1,0 +1,418 @@
+"""Continuous-batching generation engine (replaces transformers' generate loop, D2).
+
+Reference loop ([dep] generation/utils.py _sample, driven from /root/reference/llm/rag.py:172):
+one prompt at a time, DynamicCache, temperature -> top-k(50) -> top-p -> multinomial, stop on
+EOS or max_new_tokens. The reference runs concurrent Flask requests as independent
+generate() calls with no batching.
+
+Here:
+  * requests join a waiting queue; each engine step is either a PREFILL step (new prompts,
+    packed varlen, chunked to `max_prefill_tokens`) or a DECODE step over every running
+    sequence (continuous batching: sequences enter/leave between steps);
+  * KV lives in a paged cache (64-token blocks, block manager); admission reserves the
+    blocks for prompt + max_new_tokens, so a running sequence is never preempted;
+  * decode steps replay a hipGraph per batch-size bucket (static input buffers, one H2D
+    copy of a packed metadata block, sampling inside the graph); the host only reads back
+    the sampled token ids;
+  * tensor parallel: every TP rank runs the same deterministic schedule on the same inputs
+    (rank 0 broadcasts new requests), so no per-step metadata broadcast is needed.
+"""
+from __future__ import annotations
+
+import itertools
+import logging
+import threading
+import time
+from collections import deque
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+from ..models.llama import StepInput
+from ..ops.backend import AttnMeta
+from .kv_manager import BLOCK, make_block_manager
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class SamplingParams:
+    max_new_tokens: int = 150
+    temperature: float = 0.7
+    top_p: float = 0.9
+    top_k: int = 50
+    do_sample: bool = True
+    seed: Optional[int] = None
+    stop_token_ids: tuple = ()
+    ignore_eos: bool = False  # benchmark mode: always generate max_new_tokens
+
+
+WAITING, RUNNING, FINISHED = 0, 1, 2
+
+
+class Sequence:
+    _ids = itertools.count()
+
+    def __init__(self, prompt_ids, params: SamplingParams, seed: int):
+        self.id = next(Sequence._ids)
+        self.prompt = list(prompt_ids)
+        self.out: List[int] = []
+        self.params = params
+        self.seed = seed
+        self.computed = 0  # tokens whose K/V is in the cache
+        self.status = WAITING
+        self.t_arrive = time.perf_counter()
+        self.t_first = None
+        self.t_done = None
+        self.finish_reason = None
+        self.done = threading.Event()
+        self.user = None  # opaque payload for the caller
+
+    @property
+    def length(self):
+        return len(self.prompt) + len(self.out)
+
+    def token_at(self, i):
+        n = len(self.prompt)
+        return self.prompt[i] if i < n else self.out[i - n]
+
+
+class LLMEngine:
+    def __init__(self, model, num_blocks: int, max_batch: int = 64, max_prefill_tokens: int = 32768,
+                 max_model_len: int = 16384, eos_ids=(), use_graphs: bool = True, tp_group=None, top_k_cap: int = 64,
+                 graph_buckets=None):
+        self.model = model
+        self.device = model.device
+        self.max_batch = max_batch
+        self.max_prefill_tokens = max_prefill_tokens
+        self.max_model_len = max_model_len
+        self.eos = set(int(e) for e in eos_ids)
+        self.bm = make_block_manager(num_blocks)
+        self.max_blocks = -(-max_model_len // BLOCK)
+        model.allocate_kv_cache(num_blocks)
+        self.waiting = deque()
+        self.running: List[Sequence] = []
+        self.lock = threading.Lock()
+        self.tp_group = tp_group
+        self.tp_size = 1 if tp_group is None else torch.distributed.get_world_size(tp_group)
+        self.K = top_k_cap
+        self.is_cuda = self.device.type == "cuda"
+        self.use_graphs = use_graphs and self.is_cuda
+        self.buckets = sorted(set(graph_buckets or [b for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
+                                                    if b <= max_batch] + [max_batch]))
+        self.graphs = {}
+        self.stats = dict(prefill_steps=0, decode_steps=0, prefill_tokens=0, decode_tokens=0, prefill_s=0.0,
+                          decode_s=0.0)
+        self._pin = torch.empty(1 << 20 if self.is_cuda else 0, dtype=torch.int32, pin_memory=self.is_cuda)
+        self._pin_off = 0
+
+    # ------------------------------------------------------------------ requests
+    def add_request(self, prompt_ids, params: SamplingParams, seed: Optional[int] = None) -> Sequence:
+        if len(prompt_ids) == 0:
+            raise ValueError("empty prompt")
+        if len(prompt_ids) + params.max_new_tokens > self.max_model_len:
+            raise ValueError("prompt (%d) + max_new_tokens (%d) exceeds max_model_len %d"
+                             % (len(prompt_ids), params.max_new_tokens, self.max_model_len))
+        s = Sequence(prompt_ids, params, seed if seed is not None else (params.seed if params.seed is not None
+                                                                        else int(time.time_ns() & 0xFFFFFFFF)))
+        with self.lock:
+            self.waiting.append(s)
+        return s
+
+    def has_work(self):
+        return bool(self.waiting) or bool(self.running)
+
+    # ------------------------------------------------------------------ scheduling
+    def _admit(self):
+        """Pick (seq, start, n) prefill chunks for this step."""
+        chunks = []
+        budget = self.max_prefill_tokens
+        # continue partially-prefilled running sequences first
+        for s in self.running:
+            if s.computed < len(s.prompt) and budget > 0:
+                n = min(len(s.prompt) - s.computed, budget)
+                chunks.append((s, s.computed, n))
+                budget -= n
+        with self.lock:
+            while self.waiting and budget > 0 and len(self.running) < self.max_batch:
+                s = self.waiting[0]
+                need = len(s.prompt) + s.params.max_new_tokens
+                if not self.bm.can_allocate(s.id, need):
+                    break
+                self.waiting.popleft()
+                self.bm.ensure(s.id, need)
+                s.status = RUNNING
+                self.running.append(s)
+                n = min(len(s.prompt), budget)
+                chunks.append((s, 0, n))
+                budget -= n
+        return chunks
+
+    def step(self):
+        """One engine step. Returns the sequences that finished in it."""
+        self._pin_off = 0
+        chunks = self._admit()
+        if chunks:
+            return self._prefill(chunks)
+        ready = [s for s in self.running if s.computed >= len(s.prompt)]
+        if ready:
+            return self._decode(ready)
+        return []
+
+    def run_until_done(self, callback=None):
+        finished = []
+        while self.has_work():
+            f = self.step()
+            finished.extend(f)
+            if callback:
+                for s in f:
+                    callback(s)
+        return finished
+
+    def generate(self, prompts, params: SamplingParams, seeds=None):
+        seqs = [self.add_request(p, params, seed=None if seeds is None else seeds[i]) for i, p in enumerate(prompts)]
+        self.run_until_done()
+        return [s.out for s in seqs]
+
+    # ------------------------------------------------------------------ helpers
+    def _h2d_i32(self, host_list):
+        """Stage a host int list through a reusable pinned buffer (reset every step; every
+        step ends with a device->host sync, so the buffer is free again by then)."""
+        t = torch.tensor(host_list, dtype=torch.int32)
+        if not self.is_cuda:
+            return t
+        n = t.numel()
+        if self._pin_off + n > self._pin.numel():
+            cap = max(1 << 20, 2 * (self._pin_off + n))
+            torch.cuda.current_stream(self.device).synchronize()
+            self._pin = torch.empty(cap, dtype=torch.int32, pin_memory=True)
+            self._pin_off = 0
+        buf = self._pin[self._pin_off:self._pin_off + n]
+        self._pin_off += n
+        buf.copy_(t.reshape(-1))
+        return buf.to(self.device, non_blocking=True).reshape(t.shape)
+
+    def _finish(self, s, reason):
+        s.status = FINISHED
+        s.finish_reason = reason
+        s.t_done = time.perf_counter()
+        self.bm.free(s.id)
+        self.running.remove(s)
+        s.done.set()
+
+    def _accept(self, s, tok):
+        if s.t_first is None:
+            s.t_first = time.perf_counter()
+        s.out.append(int(tok))
+        p = s.params
+        if not p.ignore_eos and (int(tok) in self.eos or int(tok) in p.stop_token_ids):
+            return "stop"
+        if len(s.out) >= p.max_new_tokens:
+            return "length"
+        if s.length >= self.max_model_len:
+            return "length"
+        return None
+
+    def _sampling_tensors(self, seqs, pad_to=None):
+        n = pad_to or len(seqs)
+        temps, ks, ps, seeds, steps = [], [], [], [], []
+        for s in seqs:
+            p = s.params
+            t = p.temperature if p.do_sample else 0.0
+            temps.append(float(t))
+            ks.append(int(min(p.top_k, self.K) if p.top_k > 0 else self.K))
+            ps.append(float(p.top_p))
+            seeds.append(int(s.seed) & 0x7FFFFFFFFFFFFFFF)
+            steps.append(len(s.out))
+        for _ in range(n - len(seqs)):
+            temps.append(0.0); ks.append(1); ps.append(1.0); seeds.append(0); steps.append(0)
+        dev = self.device
+        return (torch.tensor(temps, dtype=torch.float32).to(dev), torch.tensor(ks, dtype=torch.int32).to(dev),
+                torch.tensor(ps, dtype=torch.float32).to(dev), torch.tensor(seeds, dtype=torch.int64).to(dev),
+                torch.tensor(steps, dtype=torch.int32).to(dev))
+
+    def _sample_rows(self, logits, temps, ks, ps, seeds, steps, out=None):
+        be = self.model.be
+        w = self.model.w
+        lg = logits[:, :w.vocab_valid] if w.vocab_valid < logits.shape[1] else logits
+        cv, ci = be.topk_candidates(lg.contiguous() if not lg.is_contiguous() else lg, self.K,
+                                    vocab_offset=w.vocab_offset)
+        if self.tp_size > 1:
+            cv, ci = self._gather_candidates(cv, ci)
+        tok = be.sample_candidates(cv, ci, temps, ks, ps, seeds, steps)
+        if out is not None:
+            out.copy_(tok)
+            return out
+        return tok
+
+    def _gather_candidates(self, cv, ci):
+        import torch.distributed as dist
+
+        B, K = cv.shape
+        gv = torch.empty((self.tp_size, B, K), dtype=cv.dtype, device=cv.device)
+        gi = torch.empty((self.tp_size, B, K), dtype=ci.dtype, device=ci.device)
+        dist.all_gather_into_tensor(gv, cv.contiguous(), group=self.tp_group)
+        dist.all_gather_into_tensor(gi, ci.contiguous(), group=self.tp_group)
+        return gv.permute(1, 0, 2).reshape(B, self.tp_size * K).contiguous(), \
+            gi.permute(1, 0, 2).reshape(B, self.tp_size * K).contiguous()
+
+    # ------------------------------------------------------------------ prefill
+    def _prefill(self, chunks):
+        t0 = time.perf_counter()
+        ids, pos, slots, cu, kvl, bts, qlens, out_rows, out_seqs = [], [], [], [0], [], [], [], [], []
+        for s, start, n in chunks:
+            table = self.bm.table(s.id)
+            for p in range(start, start + n):
+                ids.append(s.token_at(p))
+                pos.append(p)
+                slots.append(table[p // BLOCK] * BLOCK + p % BLOCK)
+            cu.append(cu[-1] + n)
+            kvl.append(start + n)
+            qlens.append(n)
+            row = list(table[:self.max_blocks]) + [0] * (self.max_blocks - len(table))
+            bts.append(row)
+            if start + n == len(s.prompt):
+                out_rows.append(cu[-1] - 1)
+                out_seqs.append(s)
+        from ..ops.native import build_prefill_tiles
+
+        m = self.model
+        tiles = build_prefill_tiles(qlens, m.Hq, m.Hkv)
+        meta = AttnMeta("prefill", self._h2d_i32(kvl), self._h2d_i32(bts).reshape(len(chunks), self.max_blocks),
+                        cu_q=self._h2d_i32(cu), tiles=tiles.to(self.device), host_kv_lens=kvl, host_q_lens=qlens)
+        inp = StepInput(self._h2d_i32(ids), self._h2d_i32(pos), self._h2d_i32(slots), meta,
+                        self._h2d_i32(out_rows) if out_rows else None)
+        finished = []
+        if out_rows:
+            logits = m.forward(inp)
+            tok = self._sample_rows(logits, *self._sampling_tensors(out_seqs)).cpu().tolist()
+        else:
+            m.hidden_states(StepInput(inp.ids, inp.positions, inp.slots, meta, self._h2d_i32([0])))
+            tok = []
+            if self.is_cuda:
+                torch.cuda.current_stream(self.device).synchronize()
+        for s, start, n in chunks:
+            s.computed = start + n
+        for s, t in zip(out_seqs, tok):
+            r = self._accept(s, t)
+            if r:
+                self._finish(s, r)
+                finished.append(s)
+        self.stats["prefill_steps"] += 1
+        self.stats["prefill_tokens"] += len(ids)
+        self.stats["prefill_s"] += time.perf_counter() - t0
+        return finished
+
+    # ------------------------------------------------------------------ decode
+    def _bucket(self, n):
+        for b in self.buckets:
+            if b >= n:
+                return b
+        return n
+
+    def _decode_inputs_host(self, seqs, B):
+        """Packed int32 metadata: ids[B] pos[B] slots[B] kv_lens[B] bt[B*maxb]."""
+        mb = self.max_blocks
+        ids, pos, slots, kvl, bt = [], [], [], [], []
+        for s in seqs:
+            p = s.length - 1
+            table = self.bm.table(s.id)
+            ids.append(s.token_at(p))
+            pos.append(p)
+            slots.append(table[p // BLOCK] * BLOCK + p % BLOCK)
+            kvl.append(p + 1)
+            bt.extend(table[:mb])
+            bt.extend([0] * (mb - min(len(table), mb)))
+        for _ in range(B - len(seqs)):  # padded rows -> scratch block 0
+            ids.append(0); pos.append(0); slots.append(0); kvl.append(1)
+            bt.extend([0] * mb)
+        return ids + pos + slots + kvl + bt
+
+    def _decode_graph(self, B):
+        if B in self.graphs:
+            return self.graphs[B]
+        from ..ops.native import decode_partitions
+
+        m = self.model
+        dev = self.device
+        mb = self.max_blocks
+        packed = torch.zeros(4 * B + B * mb, dtype=torch.int32, device=dev)
+        ids, pos, slots, kvl = (packed[i * B:(i + 1) * B] for i in range(4))
+        bt = packed[4 * B:].view(B, mb)
+        pt, mp = decode_partitions(self.max_model_len, B, m.Hkv)
+        ws_o = torch.empty((B, m.Hq, mp, m.D), dtype=torch.float32, device=dev) if mp > 1 else None
+        ws_ml = torch.empty((B, m.Hq, mp, 2), dtype=torch.float32, device=dev) if mp > 1 else None
+        meta = AttnMeta("decode", kvl, bt, part_tiles=pt, max_parts=mp, ws_o=ws_o, ws_ml=ws_ml)
+        samp = dict(temps=torch.zeros(B, dtype=torch.float32, device=dev),
+                    ks=torch.ones(B, dtype=torch.int32, device=dev),
+                    ps=torch.ones(B, dtype=torch.float32, device=dev),
+                    seeds=torch.zeros(B, dtype=torch.int64, device=dev),
+                    steps=torch.zeros(B, dtype=torch.int32, device=dev))
+        out_tok = torch.zeros(B, dtype=torch.int32, device=dev)
+        inp = StepInput(ids, pos, slots, meta, None)
+
+        def run():
+            logits = m.forward(inp)
+            self._sample_rows(logits, samp["temps"], samp["ks"], samp["ps"], samp["seeds"], samp["steps"],
+                              out=out_tok)
+
+        entry = dict(packed=packed, samp=samp, out=out_tok, run=run, graph=None, meta=meta)
+        if self.use_graphs:
+            kvl.fill_(1)  # scratch-only rows while capturing
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    run()
+            torch.cuda.current_stream(dev).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                run()
+            entry["graph"] = g
+        self.graphs[B] = entry
+        return entry
+
+    def warmup_graphs(self, sizes=None):
+        for b in sizes or self.buckets:
+            self._decode_graph(b)
+
+    def _decode(self, seqs):
+        t0 = time.perf_counter()
+        n = len(seqs)
+        finished = []
+        if self.is_cuda:
+            B = self._bucket(n)
+            e = self._decode_graph(B)
+            e["packed"].copy_(self._h2d_i32(self._decode_inputs_host(seqs, B)))
+            temps, ks, ps, seeds, steps = self._sampling_tensors(seqs, pad_to=B)
+            e["samp"]["temps"].copy_(temps)
+            e["samp"]["ks"].copy_(ks)
+            e["samp"]["ps"].copy_(ps)
+            e["samp"]["seeds"].copy_(seeds)
+            e["samp"]["steps"].copy_(steps)
+            if e["graph"] is not None:
+                e["graph"].replay()
+            else:
+                e["run"]()
+            tok = e["out"][:n].cpu().tolist()
+        else:
+            host = self._decode_inputs_host(seqs, n)
+            mb = self.max_blocks
+            t = torch.tensor(host, dtype=torch.int32)
+            kvl = t[3 * n:4 * n]
+            meta = AttnMeta("decode", kvl, t[4 * n:].view(n, mb), host_kv_lens=kvl.tolist())
+            inp = StepInput(t[:n], t[n:2 * n], t[2 * n:3 * n], meta, None)
+            logits = self.model.forward(inp)
+            tok = self._sample_rows(logits, *self._sampling_tensors(seqs)).tolist()
+        for s in seqs:
+            s.computed = s.length
+        for s, t in zip(seqs, tok):
+            r = self._accept(s, t)
+            if r:
+                self._finish(s, r)
+                finished.append(s)
+        self.stats["decode_steps"] += 1
+        self.stats["decode_tokens"] += n
+        self.stats["decode_s"] += time.perf_counter() - t0
+        return finished

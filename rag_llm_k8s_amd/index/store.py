@@ -1,0 +1,134 @@
+"""Document store = vector index + chunk metadata, with the reference's on-disk layout.
+
+Reference behaviour and its fixes:
+  ensure_index_exists / update_index / search_documents   /root/reference/llm/rag.py:57-86,114-120
+  * index + metadata re-read from disk on every request    -> kept resident (HBM), reloaded
+    only if the files on disk change (mtime check);
+  * unlocked read-modify-write of both files               -> single writer lock + atomic
+    os.replace snapshots, so readers never see torn files;
+  * faiss label -1 mapped to metadata[-1] (last chunk)     -> -1 results are dropped, making the
+    "No relevant information found" branch reachable;
+  * startup re-ingest duplicates chunks                    -> idempotent by (filename, chunk_id)
+    unless reingest_append=True (legacy behaviour).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+
+import numpy as np
+
+from .faiss_io import load_metadata, read_index, save_metadata
+from .flat import FlatL2Index
+
+log = logging.getLogger(__name__)
+
+
+class DocumentStore:
+    def __init__(self, index_path, dim, device="cpu", index_type="flat", ivf_nlist=1024, ivf_nprobe=32):
+        self.index_path = index_path
+        self.meta_path = index_path + ".metadata"
+        self.dim = dim
+        self.device = device
+        self.index_type = index_type
+        self.ivf_nlist, self.ivf_nprobe = ivf_nlist, ivf_nprobe
+        self.index = self._new_index()
+        self.metadata = []
+        self._keys = set()
+        self._wlock = threading.Lock()
+        self._mtimes = None
+
+    def _new_index(self):
+        if self.index_type == "ivf":
+            from .ivf import IVFFlatIndex
+
+            return IVFFlatIndex(self.dim, device=self.device, nlist=self.ivf_nlist, nprobe=self.ivf_nprobe)
+        return FlatL2Index(self.dim, device=self.device)
+
+    # ------------------------------------------------------------------ lifecycle
+    def ensure_exists(self):
+        """Reference ensure_index_exists(): create an empty index + [] metadata if missing."""
+        if not os.path.exists(self.index_path):
+            log.info("Faiss index not found. Creating a new one.")
+            self.persist()
+        else:
+            log.info("Faiss index found.")
+            self.load()
+
+    def _disk_mtimes(self):
+        try:
+            return (os.path.getmtime(self.index_path), os.path.getmtime(self.meta_path))
+        except OSError:
+            return None
+
+    def load(self):
+        r = read_index(self.index_path)
+        meta = load_metadata(self.meta_path) if os.path.exists(self.meta_path) else []
+        if r["d"] != self.dim:
+            raise ValueError("index dimension %d != embedder dimension %d" % (r["d"], self.dim))
+        idx = self._new_index()
+        if r["type"] == "flat":
+            if r["ntotal"]:
+                if self.index_type == "ivf":
+                    idx.train(r["xb"])
+                idx.add(r["xb"])
+        else:
+            from .ivf import IVFFlatIndex
+
+            idx = IVFFlatIndex.from_lists(r, device=self.device)
+        self.index = idx
+        self.metadata = list(meta)
+        self._keys = {(m.get("filename"), m.get("chunk_id")) for m in self.metadata if isinstance(m, dict)}
+        self._mtimes = self._disk_mtimes()
+
+    def maybe_reload(self):
+        """Pick up index files replaced on disk by another writer (e.g. an offline ingest job)."""
+        m = self._disk_mtimes()
+        if m is not None and self._mtimes is not None and m != self._mtimes:
+            with self._wlock:
+                self.load()
+
+    def persist(self):
+        self.index.write(self.index_path)
+        save_metadata(self.meta_path, self.metadata)
+        self._mtimes = self._disk_mtimes()
+
+    # ------------------------------------------------------------------ writes
+    def add(self, vectors, metadata, dedupe=True, persist=True):
+        """Append vectors + metadata (reference update_index). Returns number added."""
+        vecs = np.asarray(vectors.cpu() if hasattr(vectors, "cpu") else vectors, dtype=np.float32)
+        if vecs.ndim == 1:
+            vecs = vecs.reshape(1, -1)
+        with self._wlock:
+            keep = list(range(len(metadata)))
+            if dedupe:
+                keep = [i for i, m in enumerate(metadata) if (m["filename"], m["chunk_id"]) not in self._keys]
+            if keep:
+                if self.index_type == "ivf" and not self.index.is_trained:
+                    self.index.train(vecs[keep])
+                self.index.add(vecs[keep])
+                for i in keep:
+                    self.metadata.append(metadata[i])
+                    self._keys.add((metadata[i]["filename"], metadata[i]["chunk_id"]))
+                if persist:
+                    self.persist()
+            log.info("Index updated. Total vectors: %d, Dimension: %d", self.index.ntotal, self.dim)
+            return len(keep)
+
+    # ------------------------------------------------------------------ reads
+    def search(self, qvecs, k):
+        """Batched search -> list (per query) of [(metadata, squared_l2)] ascending, -1 dropped."""
+        D, I = self.index.search(qvecs, k)
+        out = []
+        for drow, irow in zip(D.tolist(), I.tolist()):
+            res = []
+            for d, i in zip(drow, irow):
+                if 0 <= i < len(self.metadata):
+                    res.append((self.metadata[i], float(d)))
+            out.append(res)
+        return out
+
+    def info(self):
+        return {"total_vectors": int(self.index.ntotal), "dimension": int(self.dim),
+                "total_chunks": len(self.metadata), "sample_chunks": self.metadata[:5] if self.metadata else []}

@@ -1,0 +1,279 @@
+"""Llama-3.x decoder (8B / 70B / tiny) for the serving engine.
+
+Reference: transformers' LlamaForCausalLM as loaded by /root/reference/llm/rag.py:24 and
+driven by model.generate at :172 (per-layer structure [dep] modeling_llama.py:284-323).
+
+MI355X-first design:
+  * q/k/v fused into one [ (Hq+2Hkv)*D, H ] weight; gate/up packed into the
+    [64 gate | 64 up]-row tile layout so SiLU(gate)*up is the GEMM epilogue;
+  * residual adds are GEMM epilogues (o_proj, down_proj write h += x @ W^T in place);
+  * RoPE + paged-KV write is one kernel; attention reads K/V only from the paged cache;
+  * Megatron tensor parallelism: qkv / gate-up column-parallel, o / down row-parallel
+    (2 all-reduces per layer over RCCL/xGMI), lm_head vocab-parallel (the sampler
+    all-gathers only the per-rank top-k candidates -- exact because top-k precedes top-p).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+from ..ops.backend import AttnMeta, get_backend
+from ..ops.reference import pack_gate_up, rope_tables
+
+
+@dataclass
+class LlamaConfig:
+    vocab_size: int = 128256
+    hidden_size: int = 4096
+    intermediate_size: int = 14336
+    num_hidden_layers: int = 32
+    num_attention_heads: int = 32
+    num_key_value_heads: int = 8
+    head_dim: int = 128
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 500000.0
+    rope_scaling: Optional[dict] = field(default_factory=lambda: {
+        "rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+        "original_max_position_embeddings": 8192})
+    max_position_embeddings: int = 131072
+    tie_word_embeddings: bool = False
+    bos_token_id: int = 128000
+    eos_token_id: List[int] = field(default_factory=lambda: [128001, 128008, 128009])
+    model_type: str = "llama"
+
+    @classmethod
+    def from_dict(cls, d):
+        c = cls()
+        for k in ("vocab_size", "hidden_size", "intermediate_size", "num_hidden_layers", "num_attention_heads",
+                  "rms_norm_eps", "rope_theta", "max_position_embeddings", "tie_word_embeddings", "bos_token_id",
+                  "model_type"):
+            if k in d and d[k] is not None:
+                setattr(c, k, d[k])
+        c.num_key_value_heads = d.get("num_key_value_heads") or c.num_attention_heads
+        c.head_dim = d.get("head_dim") or c.hidden_size // c.num_attention_heads
+        c.rope_scaling = d.get("rope_scaling")
+        eos = d.get("eos_token_id")
+        if eos is not None:
+            c.eos_token_id = eos if isinstance(eos, list) else [eos]
+        return c
+
+    @classmethod
+    def from_json(cls, path):
+        with open(path) as f:
+            return cls.from_dict(json.load(f))
+
+    def to_hf_dict(self):
+        return {
+            "architectures": ["LlamaForCausalLM"], "model_type": "llama", "vocab_size": self.vocab_size,
+            "hidden_size": self.hidden_size, "intermediate_size": self.intermediate_size,
+            "num_hidden_layers": self.num_hidden_layers, "num_attention_heads": self.num_attention_heads,
+            "num_key_value_heads": self.num_key_value_heads, "head_dim": self.head_dim,
+            "rms_norm_eps": self.rms_norm_eps, "rope_theta": self.rope_theta, "rope_scaling": self.rope_scaling,
+            "max_position_embeddings": self.max_position_embeddings,
+            "tie_word_embeddings": self.tie_word_embeddings, "bos_token_id": self.bos_token_id,
+            "eos_token_id": self.eos_token_id, "hidden_act": "silu", "attention_bias": False, "mlp_bias": False,
+            "torch_dtype": "bfloat16",
+        }
+
+
+def llama31_8b():
+    return LlamaConfig()
+
+
+def llama31_70b():
+    return LlamaConfig(hidden_size=8192, intermediate_size=28672, num_hidden_layers=80, num_attention_heads=64,
+                       num_key_value_heads=8)
+
+
+def llama_tiny(vocab=512, layers=2, hidden=256, heads=4, kv_heads=2, inter=512):
+    return LlamaConfig(vocab_size=vocab, hidden_size=hidden, intermediate_size=inter, num_hidden_layers=layers,
+                       num_attention_heads=heads, num_key_value_heads=kv_heads, head_dim=hidden // heads,
+                       max_position_embeddings=4096, bos_token_id=1, eos_token_id=[2])
+
+
+# ------------------------------------------------------------------------------------- weights
+class LlamaWeights:
+    """Rank-local (TP-sharded) device tensors in kernel layouts."""
+
+    def __init__(self, cfg: LlamaConfig, tp_rank=0, tp_size=1):
+        self.cfg, self.tp_rank, self.tp_size = cfg, tp_rank, tp_size
+        self.layers = []
+        self.embed = self.norm = self.lm_head = None
+
+    # ---- shard geometry
+    def geom(self):
+        c, tp = self.cfg, self.tp_size
+        assert c.num_attention_heads % tp == 0 and c.num_key_value_heads % tp == 0, "heads % tp"
+        assert c.intermediate_size % tp == 0 and (c.intermediate_size // tp) % 64 == 0, "intermediate % (64*tp)"
+        return dict(Hq=c.num_attention_heads // tp, Hkv=c.num_key_value_heads // tp, D=c.head_dim,
+                    I=c.intermediate_size // tp, V=-(-c.vocab_size // tp))
+
+    @classmethod
+    def from_hf(cls, cfg, get, device, tp_rank=0, tp_size=1, dtype=torch.bfloat16):
+        """`get(name, rows=None, cols=None)` returns (a slice of) an HF-named tensor."""
+        w = cls(cfg, tp_rank, tp_size)
+        g = w.geom()
+        r = tp_rank
+        D, Hq, Hkv, I, Vl = g["D"], g["Hq"], g["Hkv"], g["I"], g["V"]
+
+        def dev(t):
+            return t.to(device=device, dtype=dtype, non_blocking=False).contiguous()
+
+        w.embed = dev(get("model.embed_tokens.weight"))
+        for i in range(cfg.num_hidden_layers):
+            p = "model.layers.%d." % i
+            q = get(p + "self_attn.q_proj.weight", rows=(r * Hq * D, (r + 1) * Hq * D))
+            k = get(p + "self_attn.k_proj.weight", rows=(r * Hkv * D, (r + 1) * Hkv * D))
+            v = get(p + "self_attn.v_proj.weight", rows=(r * Hkv * D, (r + 1) * Hkv * D))
+            o = get(p + "self_attn.o_proj.weight", cols=(r * Hq * D, (r + 1) * Hq * D))
+            gt = get(p + "mlp.gate_proj.weight", rows=(r * I, (r + 1) * I))
+            up = get(p + "mlp.up_proj.weight", rows=(r * I, (r + 1) * I))
+            dn = get(p + "mlp.down_proj.weight", cols=(r * I, (r + 1) * I))
+            w.layers.append(dict(
+                ln_in=dev(get(p + "input_layernorm.weight")), ln_post=dev(get(p + "post_attention_layernorm.weight")),
+                wqkv=dev(torch.cat([q, k, v], 0)), wo=dev(o), wgu=dev(pack_gate_up(gt, up)), wdown=dev(dn)))
+        w.norm = dev(get("model.norm.weight"))
+        V = cfg.vocab_size
+        lo, hi = r * Vl, min(V, (r + 1) * Vl)
+        name = "model.embed_tokens.weight" if cfg.tie_word_embeddings else "lm_head.weight"
+        lm = get(name, rows=(lo, hi))
+        if lm.shape[0] < Vl:  # pad the last vocab shard
+            lm = torch.cat([lm, torch.zeros(Vl - lm.shape[0], lm.shape[1], dtype=lm.dtype)], 0)
+        w.lm_head = dev(lm)
+        w.vocab_offset = lo
+        w.vocab_valid = hi - lo
+        return w
+
+    @classmethod
+    def from_checkpoint(cls, path, cfg, device, tp_rank=0, tp_size=1):
+        from ..runtime.safetensors_io import CheckpointReader
+
+        rd = CheckpointReader(path)
+        try:
+            return cls.from_hf(cfg, rd.get, device, tp_rank, tp_size)
+        finally:
+            rd.close()
+
+    @classmethod
+    def from_state_dict(cls, cfg, sd, device, tp_rank=0, tp_size=1):
+        def get(name, rows=None, cols=None):
+            t = sd[name]
+            if rows is not None:
+                t = t[rows[0]:rows[1]]
+            if cols is not None:
+                t = t[:, cols[0]:cols[1]]
+            return t
+
+        return cls.from_hf(cfg, get, device, tp_rank, tp_size)
+
+    @classmethod
+    def random(cls, cfg, device, tp_rank=0, tp_size=1, seed=0, dtype=torch.bfloat16):
+        """Random-init weights of the architecture, generated directly on `device` in the
+        rank-local shard shapes (no host round trip: 16 GB for 8B in well under a second)."""
+        w = cls(cfg, tp_rank, tp_size)
+        g = w.geom()
+        D, Hq, Hkv, I, Vl = g["D"], g["Hq"], g["Hkv"], g["I"], g["V"]
+        H = cfg.hidden_size
+        gen = torch.Generator(device=device).manual_seed(seed * 1000 + tp_rank)
+
+        def rnd(*shape, std=0.02):
+            return (torch.randn(*shape, device=device, generator=gen, dtype=torch.float32) * std).to(dtype)
+
+        def ones(n):
+            return (1.0 + 0.1 * torch.randn(n, device=device, generator=gen)).to(dtype)
+
+        w.embed = rnd(cfg.vocab_size, H)
+        for _ in range(cfg.num_hidden_layers):
+            w.layers.append(dict(ln_in=ones(H), ln_post=ones(H), wqkv=rnd((Hq + 2 * Hkv) * D, H),
+                                 wo=rnd(H, Hq * D), wgu=rnd(2 * I, H), wdown=rnd(H, I)))
+        w.norm = ones(H)
+        w.lm_head = rnd(Vl, H)
+        w.vocab_offset = tp_rank * Vl
+        w.vocab_valid = min(cfg.vocab_size - tp_rank * Vl, Vl)
+        return w
+
+    def nbytes(self):
+        t = [self.embed, self.norm, self.lm_head] + [v for l in self.layers for v in l.values()]
+        return sum(x.numel() * x.element_size() for x in t)
+
+
+# ------------------------------------------------------------------------------------- model
+@dataclass
+class StepInput:
+    ids: torch.Tensor  # int32 [T]
+    positions: torch.Tensor  # int32 [T]
+    slots: torch.Tensor  # int32 [T]
+    meta: AttnMeta
+    logits_idx: Optional[torch.Tensor] = None  # int32 [n] rows that need logits (None = all)
+
+
+class LlamaModel:
+    def __init__(self, cfg: LlamaConfig, weights: LlamaWeights, device, comm=None, max_positions=None):
+        self.cfg, self.w, self.device = cfg, weights, torch.device(device)
+        self.be = get_backend(self.device)
+        g = weights.geom()
+        self.Hq, self.Hkv, self.D, self.I, self.Vl = g["Hq"], g["Hkv"], g["D"], g["I"], g["V"]
+        self.comm = comm  # tensor-parallel communicator (None at TP=1)
+        self.tp_rank = weights.tp_rank
+        mp = max_positions or cfg.max_position_embeddings
+        cos, sin = rope_tables(self.D, mp, cfg.rope_theta, cfg.rope_scaling)
+        self.cos, self.sin = cos.to(self.device), sin.to(self.device)
+        self.kv_cache = None  # list of (k, v) per layer: [nblocks, Hkv, 64, D]
+
+    def allocate_kv_cache(self, num_blocks, dtype=torch.bfloat16):
+        self.kv_cache = [(torch.zeros(num_blocks, self.Hkv, 64, self.D, dtype=dtype, device=self.device),
+                          torch.zeros(num_blocks, self.Hkv, 64, self.D, dtype=dtype, device=self.device))
+                         for _ in range(self.cfg.num_hidden_layers)]
+        return self.kv_cache
+
+    def kv_bytes_per_block(self, dtype=torch.bfloat16):
+        return 2 * self.cfg.num_hidden_layers * self.Hkv * 64 * self.D * torch.tensor([], dtype=dtype).element_size()
+
+    def _allreduce(self, x):
+        if self.comm is not None:
+            self.comm.all_reduce(x)
+
+    def hidden_states(self, inp: StepInput):
+        """Run the decoder stack; returns the final-norm'ed rows selected by logits_idx."""
+        be, w, c = self.be, self.w, self.cfg
+        Hq, Hkv, D = self.Hq, self.Hkv, self.D
+        first = self.tp_rank == 0
+        h = be.embed(inp.ids, w.embed)
+        T = h.shape[0]
+        attn = torch.empty((T, Hq * D), dtype=h.dtype, device=h.device)
+        for li, L in enumerate(w.layers):
+            kc, vc = self.kv_cache[li]
+            xn = be.rmsnorm(h, L["ln_in"], c.rms_norm_eps)
+            qkv = be.gemm(xn, L["wqkv"])
+            be.rope_kv(qkv, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
+            if inp.meta.kind == "decode":
+                be.attn_decode(qkv, kc, vc, inp.meta, attn, Hq, Hkv, D)
+            else:
+                be.attn_prefill(qkv, kc, vc, inp.meta, attn, Hq, Hkv, D)
+            if first:
+                be.gemm(attn, L["wo"], resid=h, epi="resid", out=h)
+            else:
+                be.gemm(attn, L["wo"], out=h)
+            self._allreduce(h)
+            xn = be.rmsnorm(h, L["ln_post"], c.rms_norm_eps)
+            a = be.gemm(xn, L["wgu"], epi="silu_mul")
+            if first:
+                be.gemm(a, L["wdown"], resid=h, epi="resid", out=h)
+            else:
+                be.gemm(a, L["wdown"], out=h)
+            self._allreduce(h)
+        if inp.logits_idx is not None:
+            h = be.gather_rows(h, inp.logits_idx)
+        return be.rmsnorm(h, w.norm, c.rms_norm_eps)
+
+    def logits(self, hs):
+        """Rank-local vocab-shard logits (fp32)."""
+        return self.be.gemm(hs, self.w.lm_head, out_f32=True)
+
+    def forward(self, inp: StepInput):
+        return self.logits(self.hidden_states(inp))

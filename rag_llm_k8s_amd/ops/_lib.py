@@ -37,6 +37,7 @@ _SIGS = {
     "ragk_sample_candidates": [P, P, I, I, P, P, P, P, P, P, P, S],
     "ragk_l2_partial": [P, I, I, I, I, P, I, I, P, P, P, P, S],
     "ragk_topk_merge": [P, P, I, I, I, P, P, S],
+    "ragk_ivf_scan": [P, I, I, P, I, P, I, I, P, P, I, P, P, S],
     "ragk_l2_append": [P, I, I, I, P, I, S],
     "ragk_l2_gather": [P, I, I, P, I, P, S],
 }

@@ -1,0 +1,226 @@
+"""Compute backends used by the model code.
+
+``NativeBackend``  -- GPU: every op is a gfx950 HIP kernel from ``libragk_hip.so``
+                      (no eager/torch fallback: a missing library raises).
+``TorchBackend``   -- CPU: the fp32-accumulating torch reference ops (BASELINE config 1,
+                      CPU plumbing), also used as the oracle in tests.
+
+Both expose the same methods with the same tensor layouts (paged KV cache
+[nblocks, Hkv, 64, D], packed gate/up weights, fused qkv rows), so the Llama /
+encoder / GPT-2 model code and the serving engine are device-agnostic.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+from . import reference as R
+
+KV_BLOCK = 64
+
+
+@dataclass
+class AttnMeta:
+    """Attention metadata for one forward step (device tensors + host mirrors)."""
+    kind: str  # "prefill" | "decode"
+    kv_lens: torch.Tensor  # int32 [S]
+    block_tables: torch.Tensor  # int32 [S, maxb]
+    cu_q: Optional[torch.Tensor] = None  # int32 [S+1] (prefill)
+    tiles: Optional[torch.Tensor] = None  # int32 [n,2] (prefill)
+    part_tiles: int = 4  # decode split-K
+    max_parts: int = 1
+    ws_o: Optional[torch.Tensor] = None
+    ws_ml: Optional[torch.Tensor] = None
+    host_kv_lens: List[int] = field(default_factory=list)
+    host_q_lens: List[int] = field(default_factory=list)
+
+
+class TorchBackend:
+    name = "torch"
+
+    def __init__(self, device="cpu"):
+        self.device = torch.device(device)
+
+    # GEMM family ---------------------------------------------------------------
+    def gemm(self, x, w, bias=None, resid=None, epi="none", out=None, out_f32=False):
+        y = R.linear(x, w, bias, resid, epi=epi, out_f32=out_f32)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+
+    def rmsnorm(self, x, w, eps, out=None):
+        y = R.rmsnorm(x, w, eps)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+
+    def layernorm(self, x, g, b, eps, out=None, resid=None):
+        y = R.layernorm(x, g, b, eps, resid=resid)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+
+    def embed(self, ids, table, out=None):
+        y = table[ids.long()]
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+
+    def embed_ln(self, ids, pos_ids, word, pos, type_row, g, b, eps, do_ln=True):
+        h = word[ids.long()].float() + pos[pos_ids.long()].float()
+        if type_row is not None:
+            h = h + type_row.float().reshape(1, -1)
+        if do_ln:
+            h = torch.nn.functional.layer_norm(h, (h.shape[-1],), g.float(), b.float(), eps)
+        return h.to(word.dtype)
+
+    def gather_rows(self, x, idx):
+        return x[idx.long()]
+
+    def silu_mul(self, x):
+        I = x.shape[1] // 2
+        return (torch.nn.functional.silu(x[:, :I].float()) * x[:, I:].float()).to(x.dtype)
+
+    def rope_kv(self, qkv, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D, apply_rope=True):
+        T = qkv.shape[0]
+        q = qkv[:, :Hq * D].reshape(T, Hq, D)
+        k = qkv[:, Hq * D:(Hq + Hkv) * D].reshape(T, Hkv, D)
+        v = qkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].reshape(T, Hkv, D)
+        if apply_rope:
+            p = positions.long()
+            q.copy_(R.apply_rope(q, p, cos_t, sin_t))
+            k.copy_(R.apply_rope(k, p, cos_t, sin_t))
+        if slots is not None and kc is not None:
+            s = slots.long()
+            ok = s >= 0
+            s = s[ok]
+            kc[s // KV_BLOCK, :, s % KV_BLOCK] = k[ok]
+            vc[s // KV_BLOCK, :, s % KV_BLOCK] = v[ok]
+
+    def attn_prefill(self, q, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
+        T = q.shape[0]
+        qq = q[:, :Hq * D].reshape(T, Hq, D)
+        bt = meta.block_tables.cpu()
+        lens = meta.host_kv_lens
+        o = R.attention_varlen(qq, None, None, meta.cu_q.cpu(), lens, True, 1.0 / math.sqrt(D),
+                               k_full=lambda s: R.paged_kv_view(kc, bt[s], lens[s], KV_BLOCK),
+                               v_full=lambda s: R.paged_kv_view(vc, bt[s], lens[s], KV_BLOCK))
+        out.copy_(o.reshape(T, Hq * D))
+        return out
+
+    def attn_decode(self, q, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
+        B = q.shape[0]
+        cu = torch.arange(B + 1, dtype=torch.int32)
+        m = AttnMeta("prefill", meta.kv_lens, meta.block_tables, cu_q=cu, host_kv_lens=meta.host_kv_lens)
+        return self.attn_prefill(q, kc, vc, m, out, Hq, Hkv, D)
+
+    def attn_encoder(self, qkv, cu, lens_host, tiles, out, H, D):
+        T = qkv.shape[0]
+        q = qkv[:, :H * D].reshape(T, H, D)
+        k = qkv[:, H * D:2 * H * D].reshape(T, H, D)
+        v = qkv[:, 2 * H * D:3 * H * D].reshape(T, H, D)
+        o = R.attention_varlen(q, k, v, cu.cpu(), lens_host, False, 1.0 / math.sqrt(D), cu_kv=cu.cpu())
+        out.copy_(o.reshape(T, H * D))
+        return out
+
+    def pool_l2norm(self, hidden, cu, mode="cls", normalize=True):
+        return R.pool_l2norm(hidden, cu.cpu(), mode=mode, normalize=normalize)
+
+    # sampling -----------------------------------------------------------------
+    def topk_candidates(self, logits, K, vocab_offset=0):
+        k = min(K, logits.shape[1])
+        v, i = torch.topk(logits.float(), k, dim=-1)
+        if k < K:
+            v = torch.cat([v, torch.full((v.shape[0], K - k), float("-inf"))], 1)
+            i = torch.cat([i, torch.full((i.shape[0], K - k), -1)], 1)
+        return v, (i + vocab_offset).int()
+
+    def sample_candidates(self, cand_v, cand_i, temps, top_ks, top_ps, seeds, steps):
+        out = torch.empty(cand_v.shape[0], dtype=torch.int32)
+        for b in range(cand_v.shape[0]):
+            order = torch.argsort(cand_v[b], descending=True, stable=True)
+            v, i = cand_v[b][order], cand_i[b][order]
+            k = int(top_ks[b])
+            k = len(v) if k <= 0 or k > len(v) else k
+            v, i = v[:k], i[:k]
+            t = float(temps[b])
+            if t <= 0:
+                out[b] = int(i[0])
+                continue
+            g = torch.Generator().manual_seed((int(seeds[b]) * 1000003 + int(steps[b])) & 0x7FFFFFFFFFFFFFFF)
+            u = float(torch.rand(1, generator=g))
+            _, _, pick = R.sample_from_logits_candidates(v, i, t, float(top_ps[b]), u)
+            out[b] = pick
+        return out
+
+
+class NativeBackend(TorchBackend):
+    name = "native"
+
+    def __init__(self, device="cuda"):
+        super().__init__(device)
+        from . import native
+
+        self.n = native
+        native._lib.lib()  # fail loudly now if the gfx950 library is missing
+
+    def gemm(self, x, w, bias=None, resid=None, epi="none", out=None, out_f32=False):
+        return self.n.gemm(x, w, bias=bias, resid=resid, epi=epi, out=out, out_f32=out_f32)
+
+    def rmsnorm(self, x, w, eps, out=None):
+        return self.n.rmsnorm(x, w, eps, out=out)
+
+    def layernorm(self, x, g, b, eps, out=None, resid=None):
+        return self.n.layernorm(x, g, b, eps, out=out, resid=resid)
+
+    def embed(self, ids, table, out=None):
+        return self.n.embed(ids, table, out=out)
+
+    def embed_ln(self, ids, pos_ids, word, pos, type_row, g, b, eps, do_ln=True):
+        return self.n.embed_ln(ids, pos_ids, word, pos, type_row, g, b, eps, do_ln=do_ln)
+
+    def gather_rows(self, x, idx):
+        return self.n.gather_rows(x, idx)
+
+    def silu_mul(self, x):
+        return self.n.silu_mul(x)
+
+    def rope_kv(self, qkv, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D, apply_rope=True):
+        self.n.rope_kv(qkv, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D, apply_rope=apply_rope)
+
+    def attn_prefill(self, q, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
+        return self.n.attn_prefill(q, kc, vc, meta.cu_q, meta.kv_lens, meta.tiles, out, Hq, Hkv, D, causal=True,
+                                   paged=True, block_tables=meta.block_tables)
+
+    def attn_decode(self, q, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
+        return self.n.attn_decode(q, kc, vc, meta.block_tables, meta.kv_lens, out, Hq, Hkv, D, meta.part_tiles,
+                                  meta.max_parts, meta.ws_o, meta.ws_ml)
+
+    def attn_encoder(self, qkv, cu, lens_host, tiles, out, H, D):
+        return self.n.attn_prefill(qkv, qkv[:, H * D:], qkv[:, 2 * H * D:], cu, _lens_dev(cu), tiles, out, H, H, D,
+                                   causal=False, paged=False, cu_kv=cu, kv_stride=qkv.stride(0))
+
+    def pool_l2norm(self, hidden, cu, mode="cls", normalize=True):
+        return self.n.pool_l2norm(hidden, cu, mode=mode, normalize=normalize)
+
+    def topk_candidates(self, logits, K, vocab_offset=0):
+        return self.n.topk_candidates(logits, K, vocab_offset=vocab_offset)
+
+    def sample_candidates(self, cand_v, cand_i, temps, top_ks, top_ps, seeds, steps):
+        return self.n.sample_candidates(cand_v, cand_i, temps, top_ks, top_ps, seeds, steps)
+
+
+def _lens_dev(cu):
+    return (cu[1:] - cu[:-1]).contiguous()
+
+
+def get_backend(device) -> TorchBackend:
+    dev = torch.device(device)
+    return NativeBackend(dev) if dev.type == "cuda" else TorchBackend(dev)

@@ -275,6 +275,38 @@ def l2_search(xt, cap, n, q, k, row_begin=0, ids_map=None):
     return pd.reshape(nq, k), pi.reshape(nq, k).long()
 
 
+def _merge_all(pd, pi, nq, G, k):
+    L = _lib.lib()
+    while G > 1:
+        Go = -(-G // 64)
+        od = torch.empty((nq, Go, k), dtype=torch.float32, device=pd.device)
+        oi = torch.empty((nq, Go, k), dtype=torch.int32, device=pd.device)
+        check(L.ragk_topk_merge(pd.data_ptr(), pi.data_ptr(), nq, G, k, od.data_ptr(), oi.data_ptr(), stream_ptr()),
+              "ragk_topk_merge")
+        pd, pi, G = od, oi, Go
+    return pd.reshape(nq, k), pi.reshape(nq, k).long()
+
+
+def ivf_search(xt, cap, q, probes, offsets, ids_map, k, max_list=None):
+    """IVF-Flat scan of the probed lists. probes int32 [nq, nprobe] (device), offsets int32
+    [nlist+1] (device, list-ordered store), ids_map int32 [ntotal] original ids."""
+    _req(xt.dtype == torch.float32 and q.dtype == torch.float32 and q.is_contiguous(), "fp32")
+    _req(probes.dtype == torch.int32 and offsets.dtype == torch.int32 and ids_map.dtype == torch.int32, "int32")
+    d = xt.shape[0]
+    nq, nprobe = probes.shape
+    _req(1 <= k <= 64 and d <= 2048, "k <= 64, d <= 2048")
+    if max_list is None:
+        max_list = int((offsets[1:] - offsets[:-1]).max().item())
+    chunks = max(1, -(-max_list // 1024))
+    G = nprobe * chunks
+    pd = torch.empty((nq, G, k), dtype=torch.float32, device=q.device)
+    pi = torch.empty((nq, G, k), dtype=torch.int32, device=q.device)
+    check(_lib.lib().ragk_ivf_scan(xt.data_ptr(), cap, d, q.data_ptr(), nq, probes.data_ptr(), nprobe, chunks,
+                                   offsets.data_ptr(), ids_map.data_ptr(), k, pd.data_ptr(), pi.data_ptr(),
+                                   stream_ptr()), "ragk_ivf_scan")
+    return _merge_all(pd, pi, nq, G, k)
+
+
 def l2_append(xt, cap, n0, x):
     _req(x.dtype == torch.float32 and x.is_contiguous() and x.shape[1] == xt.shape[0], "x fp32 [n,d]")
     check(_lib.lib().ragk_l2_append(xt.data_ptr(), cap, xt.shape[0], n0, x.data_ptr(), x.shape[0], stream_ptr()),

@@ -181,6 +181,21 @@ def sample_from_logits(logits, temperature, top_k, top_p, u=None):
     return ki, p, pick
 
 
+def sample_from_logits_candidates(vals, idx, temperature, top_p, u):
+    """vals/idx: top-k candidates sorted descending. Applies temperature and top-p, then
+    draws with uniform `u` (inverse CDF). Returns (kept ids, probs, picked id)."""
+    x = vals.float() / temperature
+    probs = torch.softmax(x, -1)
+    cum_before = torch.cumsum(probs, 0) - probs
+    keep = cum_before < top_p
+    keep[0] = True
+    ki = idx[keep]
+    p = torch.softmax(x[keep], -1)
+    c = torch.cumsum(p, 0)
+    j = int(torch.searchsorted(c, torch.tensor([u * float(c[-1])]), right=True)[0])
+    return ki, p, int(ki[min(j, len(ki) - 1)])
+
+
 def l2_knn(xb, q, k):
     """faiss IndexFlatL2.search: squared L2, ascending; pad (-1, FLT_MAX)."""
     n = xb.shape[0]

@@ -1,0 +1,107 @@
+"""Tokenizer front-end (replaces the reference's AutoTokenizer, D5).
+
+Reference use: tokenizer.encode(full_prompt) -> ids with BOS, no chat template
+(/root/reference/llm/rag.py:170) and tokenizer.decode(output[0], skip_special_tokens=True)
+(:173); the embedder tokenises with truncation at max_seq_length (sentence-transformers).
+
+Backends, in order of preference:
+  1. the native C++ tokenizer in ``_ragk_rt`` (byte-level BPE for Llama-3 / GPT-2,
+     WordPiece for BERT, Unigram for XLM-R) reading the same ``tokenizer.json``;
+  2. HF ``tokenizers`` (Rust), which the reference itself uses -- also the parity oracle.
+Set RAGK_TOKENIZER=hf|native to force one.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+
+class Tokenizer:
+    def __init__(self, path_or_dir, backend=None):
+        p = path_or_dir
+        if os.path.isdir(p):
+            p = os.path.join(p, "tokenizer.json")
+        self.path = p
+        with open(p, encoding="utf-8") as f:
+            self.spec = json.load(f)
+        self.cfg = {}
+        tc = os.path.join(os.path.dirname(p), "tokenizer_config.json")
+        if os.path.exists(tc):
+            with open(tc) as f:
+                self.cfg = json.load(f)
+        backend = backend or os.environ.get("RAGK_TOKENIZER", "auto")
+        self.impl = None
+        self.backend = None
+        if backend in ("auto", "native"):
+            try:
+                from . import native_rt
+
+                rt = native_rt()
+                if rt is not None and hasattr(rt, "Tokenizer"):
+                    self.impl = rt.Tokenizer(p)
+                    self.backend = "native"
+            except Exception:
+                if backend == "native":
+                    raise
+                self.impl = None
+        if self.impl is None:
+            from tokenizers import Tokenizer as HFTok
+
+            self.impl = HFTok.from_file(p)
+            self.impl.no_truncation()
+            self.impl.no_padding()
+            self.backend = "hf"
+        self.special_ids = set()
+        for t in self.spec.get("added_tokens", []):
+            if t.get("special"):
+                self.special_ids.add(t["id"])
+        self.vocab_size = self._vocab_size()
+        self.bos_id = self._tok_id(self.cfg.get("bos_token"))
+        self.eos_id = self._tok_id(self.cfg.get("eos_token"))
+
+    def _tok_id(self, t):
+        if isinstance(t, dict):
+            t = t.get("content")
+        if not t:
+            return None
+        return self.token_to_id(t)
+
+    def _vocab_size(self):
+        if self.backend == "hf":
+            return self.impl.get_vocab_size(with_added_tokens=True)
+        return self.impl.vocab_size()
+
+    def token_to_id(self, t):
+        return self.impl.token_to_id(t)
+
+    def encode(self, text, add_special_tokens=True, max_length=None):
+        if self.backend == "hf":
+            ids = self.impl.encode(text, add_special_tokens=add_special_tokens).ids
+        else:
+            ids = self.impl.encode(text, add_special_tokens)
+        if max_length is not None and len(ids) > max_length:
+            ids = self._truncate(ids, max_length, add_special_tokens)
+        return list(ids)
+
+    def _truncate(self, ids, max_length, add_special):
+        """Right truncation that keeps the trailing special token (e.g. [SEP] / </s>)."""
+        if add_special and ids and ids[-1] in self.special_ids:
+            return ids[:max_length - 1] + [ids[-1]]
+        return ids[:max_length]
+
+    def encode_batch(self, texts, add_special_tokens=True, max_length=None):
+        if self.backend == "hf":
+            encs = self.impl.encode_batch(list(texts), add_special_tokens=add_special_tokens)
+            out = [e.ids for e in encs]
+        else:
+            out = [self.impl.encode(t, add_special_tokens) for t in texts]
+        if max_length is not None:
+            out = [self._truncate(list(x), max_length, add_special_tokens) if len(x) > max_length else list(x)
+                   for x in out]
+        return out
+
+    def decode(self, ids, skip_special_tokens=True):
+        ids = [int(i) for i in ids if 0 <= int(i) < self.vocab_size]
+        if self.backend == "hf":
+            return self.impl.decode(ids, skip_special_tokens=skip_special_tokens)
+        return self.impl.decode(ids, skip_special_tokens)

@@ -1,0 +1,275 @@
+"""RAG orchestration (reference L6, /root/reference/llm/rag.py:88-181).
+
+Query path (reference generate_text, :146-181), per request:
+  embed query -> search k -> top context_k into the prompt template -> tokenize (BOS, no chat
+  template) -> generate(max_new_tokens, temperature, top_p) -> decode full sequence ->
+  split("Chatbot:")[-1].strip() -> {"generated_text", "context"}.
+
+Differences by design: concurrent requests are micro-batched through the embedder and the
+index (one encoder forward + one search kernel per batch), and all generations share one
+continuous-batching engine driven by a dedicated loop thread (the reference runs
+independent model.generate calls per Flask thread). Ingest embeds every chunk of a PDF in
+packed batches instead of one chunk at a time.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import queue
+import threading
+import time
+
+import torch
+
+from ..engine.llm_engine import SamplingParams
+from ..ingest import pdf as pdfmod
+from ..ingest.text import NO_RESULTS, build_context, build_prompt, chunk_metadata, postprocess, split_text
+from ..utils import metrics
+from ..utils.metrics import Trace
+
+log = logging.getLogger(__name__)
+
+
+class EngineLoop(threading.Thread):
+    """Drives LLMEngine.step() on one thread; wakes when requests arrive."""
+
+    def __init__(self, engine, control=None):
+        super().__init__(daemon=True, name="llm-engine-loop")
+        self.engine = engine
+        self.cv = threading.Condition()
+        self.stop_flag = False
+        self.control = control  # TP control channel (rank 0 side), see parallel/tp.py
+        self.error = None
+
+    def submit(self, prompt_ids, params, seed=None):
+        s = self.engine.add_request(prompt_ids, params, seed=seed)
+        with self.cv:
+            self.cv.notify()
+        return s
+
+    def run(self):
+        eng = self.engine
+        try:
+            while not self.stop_flag:
+                with self.cv:
+                    while not eng.has_work() and not self.stop_flag:
+                        self.cv.wait(timeout=0.5)
+                if self.stop_flag:
+                    break
+                if self.control is not None:
+                    self.control.publish_step(eng)
+                fin = eng.step()
+                metrics.set_gauge("kv_free", eng.bm.free_blocks())
+                for s in fin:
+                    metrics.inc("tokens", len(s.out))
+        except Exception as e:  # surface engine failure to every waiter
+            log.exception("engine loop failed")
+            self.error = e
+            for s in list(eng.running) + list(eng.waiting):
+                s.finish_reason = "error"
+                s.done.set()
+        finally:
+            if self.control is not None:
+                self.control.publish_shutdown()
+
+    def stop(self):
+        self.stop_flag = True
+        with self.cv:
+            self.cv.notify_all()
+
+
+class MicroBatcher(threading.Thread):
+    """Collects concurrent retrieval requests for `window_s`, then embeds + searches them together."""
+
+    def __init__(self, fn, window_s=0.002, max_batch=256):
+        super().__init__(daemon=True, name="embed-batcher")
+        self.fn, self.window_s, self.max_batch = fn, window_s, max_batch
+        self.q = queue.Queue()
+
+    def submit(self, item):
+        ev = threading.Event()
+        box = {}
+        self.q.put((item, ev, box))
+        ev.wait()
+        if "error" in box:
+            raise box["error"]
+        return box["result"]
+
+    def run(self):
+        while True:
+            first = self.q.get()
+            batch = [first]
+            deadline = time.perf_counter() + self.window_s
+            while len(batch) < self.max_batch:
+                t = deadline - time.perf_counter()
+                if t <= 0:
+                    break
+                try:
+                    batch.append(self.q.get(timeout=t))
+                except queue.Empty:
+                    break
+            try:
+                res = self.fn([b[0] for b in batch])
+                for (item, ev, box), r in zip(batch, res):
+                    box["result"] = r
+                    ev.set()
+            except Exception as e:
+                for item, ev, box in batch:
+                    box["error"] = e
+                    ev.set()
+
+
+class RagService:
+    def __init__(self, cfg, llm_engine, llm_tokenizer, embedder, store, gen_config=None, start_threads=True,
+                 control=None):
+        self.cfg = cfg
+        self.engine = llm_engine
+        self.tok = llm_tokenizer
+        self.embedder = embedder
+        self.store = store
+        gen = gen_config or {}
+        do_sample = cfg.do_sample if cfg.do_sample is not None else bool(gen.get("do_sample", True))
+        eos = gen.get("eos_token_id")
+        stop = tuple(eos) if isinstance(eos, list) else ((eos,) if eos is not None else ())
+        self.params = SamplingParams(max_new_tokens=cfg.max_new_tokens, temperature=cfg.temperature,
+                                     top_p=cfg.top_p, top_k=cfg.top_k, do_sample=do_sample, stop_token_ids=stop)
+        self.loop = EngineLoop(llm_engine, control=control)
+        self.batcher = MicroBatcher(self._retrieve_batch)
+        self._seed = cfg.seed
+        self._seed_lock = threading.Lock()
+        self.ready = False
+        if start_threads:
+            self.loop.start()
+            self.batcher.start()
+
+    # ------------------------------------------------------------------ retrieval
+    def _retrieve_batch(self, prompts):
+        tr = Trace("retrieve")
+        with tr.span("embed"):
+            q = self.embedder.embed(list(prompts))
+        with tr.span("search"):
+            self.store.maybe_reload()
+            res = self.store.search(q, self.cfg.retrieve_k)
+        return [(r, tr.spans) for r in res]
+
+    def retrieve(self, prompt):
+        return self.batcher.submit(prompt)
+
+    # ------------------------------------------------------------------ generation
+    def _next_seed(self):
+        with self._seed_lock:
+            self._seed += 1
+            return self._seed
+
+    def _prompt_ids(self, full_prompt):
+        ids = self.tok.encode(full_prompt, add_special_tokens=True)
+        limit = self.engine.max_model_len - self.params.max_new_tokens
+        if len(ids) > limit:
+            if self.cfg.truncate_prompt != "left":
+                raise ValueError("prompt of %d tokens exceeds the model limit %d" % (len(ids), limit))
+            ids = ids[len(ids) - limit:]  # keep the question and "Chatbot:" suffix
+        return ids
+
+    def generate(self, user_prompt, params=None, debug=False):
+        """Synchronous /generate (thread-safe)."""
+        tr = Trace("generate")
+        results, rspans = self.retrieve(user_prompt)
+        for k, v in rspans.items():
+            tr.spans[k] = v
+        log.debug("User query: %s", user_prompt)
+        log.debug("Search results: %s", [(m.get("filename"), m.get("chunk_id"), d) for m, d in results])
+        if not results:
+            return {"generated_text": NO_RESULTS}
+        context = build_context(results, self.cfg.context_k)
+        log.debug("Context: %s...", context[:500])
+        with tr.span("tokenize"):
+            ids = self._prompt_ids(build_prompt(context, user_prompt))
+        metrics.inc("prompt_tokens", len(ids))
+        s = self.loop.submit(ids, params or self.params, seed=self._next_seed())
+        s.done.wait()
+        if s.finish_reason == "error":
+            raise RuntimeError("generation engine failed: %r" % (self.loop.error,))
+        tr.add("queue+prefill", (s.t_first or s.t_done) - s.t_arrive)
+        tr.add("decode", s.t_done - (s.t_first or s.t_done))
+        metrics.observe("ttft", (s.t_first or s.t_done) - s.t_arrive)
+        with tr.span("detokenize"):
+            text = postprocess(self.tok.decode(s.prompt + s.out, skip_special_tokens=True))
+        metrics.observe("request", tr.total())
+        log.debug("Generated response: %s...", text[:200])
+        out = {"generated_text": text, "context": context}
+        if debug:
+            out["timings_ms"] = tr.summary_ms()
+            out["prompt_tokens"] = len(ids)
+            out["generated_tokens"] = len(s.out)
+        return out
+
+    def generate_batch(self, prompts, params=None, seeds=None):
+        """Many queries at once (benchmark / offline): one embed + one search + one engine run.
+        Must not be mixed with the background loop (call with start_threads=False)."""
+        t0 = time.perf_counter()
+        q = self.embedder.embed(list(prompts))
+        res = self.store.search(q, self.cfg.retrieve_k)
+        seqs, ctxs = [], []
+        for i, (p, r) in enumerate(zip(prompts, res)):
+            if not r:
+                seqs.append(None)
+                ctxs.append(None)
+                continue
+            ctx = build_context(r, self.cfg.context_k)
+            ids = self._prompt_ids(build_prompt(ctx, p))
+            seqs.append(self.engine.add_request(ids, params or self.params,
+                                                seed=(seeds[i] if seeds is not None else self._next_seed())))
+            ctxs.append(ctx)
+        self.engine.run_until_done()
+        outs = []
+        for s, ctx in zip(seqs, ctxs):
+            if s is None:
+                outs.append({"generated_text": NO_RESULTS})
+                continue
+            text = postprocess(self.tok.decode(s.prompt + s.out, skip_special_tokens=True))
+            outs.append({"generated_text": text, "context": ctx, "_latency_s": s.t_done - t0,
+                         "_ttft_s": (s.t_first or s.t_done) - t0, "_prompt_tokens": len(s.prompt),
+                         "_gen_tokens": len(s.out)})
+        return outs
+
+    # ------------------------------------------------------------------ ingest
+    def ingest_pdf_bytes(self, filename, data, persist=True):
+        """Reference upload_pdf/process_pdf: extract -> chunk -> embed -> update_index."""
+        text = pdfmod.extract_text(data)
+        chunks = split_text(text, self.cfg.chunk_words, self.cfg.chunk_overlap)
+        if chunks:
+            vecs = self.embedder.embed(chunks)
+            self.store.add(vecs, chunk_metadata(filename, chunks), dedupe=not self.cfg.reingest_append,
+                           persist=persist)
+            metrics.set_gauge("index", self.store.index.ntotal)
+        return len(chunks)
+
+    def ingest_directory(self):
+        """Reference process_pdf_directory(): every *.pdf in PDF_DIR (idempotent by default)."""
+        d = self.cfg.pdf_dir
+        if not os.path.isdir(d):
+            log.warning("No PDF files found in %s", d)
+            return 0
+        files = sorted(f for f in os.listdir(d) if f.endswith(".pdf"))
+        if not files:
+            log.warning("No PDF files found in %s", d)
+            return 0
+        total = 0
+        for fn in files:
+            with open(os.path.join(d, fn), "rb") as f:
+                total += self.ingest_pdf_bytes(fn, f.read(), persist=False)
+        self.store.persist()
+        log.info("Processed %d PDFs into %d chunks", len(files), total)
+        return len(files)
+
+    def index_info(self):
+        self.store.maybe_reload()
+        return self.store.info()
+
+    def health(self):
+        return {"engine_alive": self.loop.is_alive() and self.loop.error is None, "ready": self.ready,
+                "kv_free_blocks": self.engine.bm.free_blocks(), "index_vectors": int(self.store.index.ntotal),
+                "hbm_bytes": torch.cuda.memory_allocated() if torch.cuda.is_available() else 0}
+
+    def shutdown(self):
+        self.loop.stop()

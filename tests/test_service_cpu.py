@@ -1,0 +1,141 @@
+"""T4 service tier on CPU (BASELINE config 1 plumbing): GPT-2 generator + MiniLM-shaped encoder,
+synthetic PDFs, faiss-format FlatL2 -- full Flask contract of /root/reference/llm/rag.py:122-197."""
+import io
+import os
+
+import pytest
+
+from rag_llm_k8s_amd.config import RagConfig
+from rag_llm_k8s_amd.ingest.text import NO_RESULTS
+from rag_llm_k8s_amd.models import encoder as E
+from rag_llm_k8s_amd.models import gpt2 as G2
+from rag_llm_k8s_amd.utils import synthetic as S
+
+
+@pytest.fixture(scope="module")
+def assets(tmp_path_factory):
+    root = tmp_path_factory.mktemp("models")
+    G2.write_gpt2_checkpoint(str(root), G2.gpt2_tiny(1024), seed=0)
+    ecfg = E.EncoderConfig(vocab_size=1024, hidden_size=128, num_hidden_layers=2, num_attention_heads=4,
+                           intermediate_size=256, max_seq_length=128)
+    S.write_encoder_checkpoint(str(root / "minilm"), ecfg, seed=0)
+    pdfs = tmp_path_factory.mktemp("pdfs")
+    S.write_pdf_corpus(str(pdfs), 3, pages=2, words_per_page=900)
+    return root, pdfs
+
+
+def make_cfg(root, pdfs, index_dir):
+    return RagConfig(model_path=str(root), index_path=str(index_dir / "faiss_index"), pdf_dir=str(pdfs),
+                     embed_model=str(root / "minilm"), device="cpu", max_new_tokens=6, max_model_len=1024,
+                     max_batch=4, use_cuda_graphs=False, kv_cache_blocks=64, seed=1)
+
+
+def make_service(cfg):
+    from rag_llm_k8s_amd.server.builder import build_service
+
+    svc = build_service(cfg)
+    svc.store.ensure_exists()
+    return svc
+
+
+@pytest.fixture(scope="module")
+def client(assets, tmp_path_factory):
+    from rag_llm_k8s_amd.server.app import create_app
+
+    root, pdfs = assets
+    idx = tmp_path_factory.mktemp("index")
+    svc = make_service(make_cfg(root, pdfs, idx))
+    assert svc.ingest_directory() == 3
+    svc.ready = True
+    app = create_app(svc)
+    yield app.test_client(), svc, idx
+    svc.shutdown()
+
+
+def test_index_info(client):
+    c, svc, _ = client
+    r = c.get("/index_info")
+    assert r.status_code == 200
+    j = r.get_json()
+    assert j["dimension"] == 128
+    assert j["total_vectors"] == j["total_chunks"] >= 3
+    assert len(j["sample_chunks"]) == min(5, j["total_chunks"])
+    assert set(j["sample_chunks"][0]) == {"filename", "chunk_id", "text"}
+
+
+@pytest.mark.parametrize("route", ["/generate", "/query"])
+def test_generate(client, route):
+    c, svc, _ = client
+    r = c.post(route, json={"prompt": "Pleabra tisho quar?"})
+    assert r.status_code == 200, r.get_json()
+    j = r.get_json()
+    assert set(j) == {"generated_text", "context"}
+    assert isinstance(j["generated_text"], str)
+    assert j["context"].startswith("Document 'doc_0000")
+    assert j["context"].count("(chunk ") == 3  # context_k = 3 of retrieve_k = 5
+
+
+def test_generate_debug_timings(client):
+    c, svc, _ = client
+    j = c.post("/generate", json={"prompt": "x", "debug": True}).get_json()
+    assert "timings_ms" in j and j["generated_tokens"] >= 1
+    for k in ("embed", "search", "tokenize", "decode"):
+        assert k in j["timings_ms"]
+
+
+def test_generate_missing_body_is_500(client):
+    c, _, _ = client
+    r = c.post("/generate", data="not json", content_type="text/plain")
+    assert r.status_code in (400, 415, 500)
+
+
+def test_upload_errors_and_success(client):
+    c, svc, _ = client
+    r = c.post("/upload_pdf", data={}, content_type="multipart/form-data")
+    assert r.status_code == 400 and r.get_json() == {"error": "No file part"}
+    r = c.post("/upload_pdf", data={"file": (io.BytesIO(b""), "")}, content_type="multipart/form-data")
+    assert r.status_code == 400 and r.get_json() == {"error": "No selected file"}
+    r = c.post("/upload_pdf", data={"file": (io.BytesIO(b"abc"), "notes.txt")}, content_type="multipart/form-data")
+    assert r.status_code == 400 and r.get_json() == {"error": "Invalid file format"}
+    from rag_llm_k8s_amd.ingest.pdf import write_pdf
+
+    words = " ".join("w%d" % i for i in range(1700))
+    data = write_pdf([[words]])
+    before = svc.store.index.ntotal
+    r = c.post("/upload_pdf", data={"file": (io.BytesIO(data), "new.pdf")}, content_type="multipart/form-data")
+    assert r.status_code == 200
+    assert r.get_json() == {"message": "PDF processed and indexed successfully. 3 chunks created."}
+    assert svc.store.index.ntotal == before + 3
+
+
+def test_health_and_metrics(client):
+    c, _, _ = client
+    assert c.get("/healthz").status_code == 200
+    assert c.get("/readyz").status_code == 200
+    m = c.get("/metrics")
+    assert m.status_code == 200 and b"rag_stage_seconds" in m.data
+
+
+def test_restart_is_idempotent(client, assets):
+    _, svc, idx = client
+    root, pdfs = assets
+    n = svc.store.index.ntotal
+    svc2 = make_service(make_cfg(root, pdfs, idx))
+    try:
+        assert svc2.store.index.ntotal == n
+        svc2.ingest_directory()
+        assert svc2.store.index.ntotal == n  # reference would duplicate every chunk here
+        assert os.path.exists(str(idx / "faiss_index.metadata"))
+    finally:
+        svc2.shutdown()
+
+
+def test_empty_index_reply(assets, tmp_path):
+    root, _ = assets
+    cfg = make_cfg(root, tmp_path / "nopdfs", tmp_path)
+    svc = make_service(cfg)
+    try:
+        assert svc.ingest_directory() == 0
+        assert svc.generate("anything") == {"generated_text": NO_RESULTS}
+    finally:
+        svc.shutdown()
