@@ -1,0 +1,166 @@
+#!/usr/bin/env python
+"""Headline benchmark (BASELINE.json): end-to-end RAG query p50 latency + generation tokens/s,
+Llama-3.1-8B (random init, bf16), all-MiniLM-L6-v2-shaped embedder, 10k-chunk FlatL2 index
+resident in HBM, retrieve top-k = 4 (all 4 go into the prompt), 150 new tokens per query.
+
+One "step" = one wave of `--concurrency` concurrent /query requests per data-parallel replica
+served end to end: batched query embedding -> HBM L2 top-k -> prompt build (reference template) ->
+tokenize -> continuous-batching prefill + hipGraph decode (temperature 0.7, top-p 0.9, top-k 50,
+150 tokens, EOS ignored so every request produces exactly 150 tokens) -> detokenize ->
+"Chatbot:" post-processing.
+
+Multi-GPU: one process per GPU (torchrun). Default parallelism is data-parallel replicas
+(weak scaling: per-GPU work fixed, like k8s replicas behind the Service); --tp T groups T GPUs
+into one tensor-parallel engine over RCCL/xGMI.
+
+value = total generated tokens of all ranks / max-over-ranks wall time of the K timed steps.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "end-to-end RAG query p50 latency + gen tokens/sec, Llama-3.1-8B top-k=4"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--concurrency", type=int, default=32, help="concurrent queries per replica per step")
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--model", default="8b", choices=["8b", "70b", "tiny"])
+    ap.add_argument("--embedder", default="minilm", choices=["minilm", "bge-large", "bge-m3", "tiny"])
+    ap.add_argument("--chunks", type=int, default=10000)
+    ap.add_argument("--retrieve-k", type=int, default=4)
+    ap.add_argument("--context-k", type=int, default=4)
+    ap.add_argument("--max-new-tokens", type=int, default=150)
+    ap.add_argument("--index", default="flat", choices=["flat", "ivf"])
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def pct(xs, p):
+    xs = sorted(xs)
+    if not xs:
+        return None
+    k = (len(xs) - 1) * p / 100.0
+    f = int(k)
+    c = min(f + 1, len(xs) - 1)
+    return xs[f] + (xs[c] - xs[f]) * (k - f)
+
+
+def main():
+    a = parse()
+    import torch
+
+    from rag_llm_k8s_amd import _build
+    from rag_llm_k8s_amd.engine.llm_engine import SamplingParams
+    from rag_llm_k8s_amd.parallel import dist as D
+    from rag_llm_k8s_amd.parallel.comm import TPComm
+    from rag_llm_k8s_amd.utils.workload import build_workload, make_queries
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
+    if int(os.environ.get("LOCAL_RANK", "0")) == 0:
+        _build.build_all()
+    ctx = D.init_distributed(tp=a.tp)
+    D.barrier(ctx)
+    dev = ctx.device
+    comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, dev, ctx.tp_cpu_group) if ctx.tp > 1 else None
+    t_setup = time.time()
+    wl = build_workload(model=a.model, embedder=a.embedder, n_chunks=a.chunks, retrieve_k=a.retrieve_k,
+                        context_k=a.context_k, max_new_tokens=a.max_new_tokens, max_batch=a.concurrency,
+                        device=dev, ctx=ctx, tp_comm=comm, seed=0, use_graphs=not a.no_graphs, index_type=a.index)
+    svc = wl.svc
+    svc.engine.warmup_graphs()
+    params = SamplingParams(max_new_tokens=a.max_new_tokens, temperature=0.7, top_p=0.9, top_k=50, do_sample=True,
+                            ignore_eos=True)
+    setup_s = time.time() - t_setup
+
+    def run_step(step_id):
+        # identical queries/seeds inside a TP group, different across DP replicas and steps
+        qs = make_queries(wl.wm, a.concurrency, seed=100000 * ctx.dp_rank + 1000 + step_id)
+        seeds = [1000 * (step_id + 1000) + i for i in range(len(qs))]
+        return svc.generate_batch(qs, params=params, seeds=seeds)
+
+    for w in range(a.warmup):
+        run_step(-1 - w)
+    D.barrier(ctx)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lat, ttft, ptoks, gtoks, step_ms = [], [], [], [], []
+    for s in range(a.steps):
+        ts = time.perf_counter()
+        outs = run_step(s)
+        step_ms.append((time.perf_counter() - ts) * 1e3)
+        for o in outs:
+            if "_latency_s" in o:
+                lat.append(o["_latency_s"] * 1e3)
+                ttft.append(o["_ttft_s"] * 1e3)
+                ptoks.append(o["_prompt_tokens"])
+                gtoks.append(o["_gen_tokens"])
+    torch.cuda.synchronize()
+    D.barrier(ctx)
+    elapsed = time.perf_counter() - t0
+    elapsed_max = D.all_reduce_max(ctx, elapsed)
+    my_tokens = sum(gtoks) if ctx.tp_rank == 0 else 0
+    total_tokens = D.all_reduce_sum(ctx, float(my_tokens))
+    allstats = D.all_gather_object(ctx, dict(lat=lat, ttft=ttft, ptoks=ptoks, eng=svc.engine.stats,
+                                             setup=wl.timings, step_ms=step_ms))
+    if ctx.rank == 0:
+        L = [x for s in allstats for x in s["lat"]]
+        T = [x for s in allstats for x in s["ttft"]]
+        P = [x for s in allstats for x in s["ptoks"]]
+        value = total_tokens / elapsed_max
+        par = "dp%d" % ctx.dp if ctx.tp == 1 else ("tp%d" % ctx.tp if ctx.dp == 1 else "tp%d_dp%d" % (ctx.tp, ctx.dp))
+        eng = allstats[0]["eng"]
+        res = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "generated tokens/s (aggregate over all GPUs)",
+            "n_gpus": ctx.world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed_max / a.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init weights of the named architectures; Zipfian pseudo-English corpus "
+                    "of %d x 1000-word chunks; trained 128k BPE + WordPiece tokenizers)" % a.chunks,
+            "config": {
+                "model": {"8b": "Llama-3.1-8B-Instruct", "70b": "Llama-3.1-70B-Instruct", "tiny": "llama-tiny"}[a.model],
+                "embedder": {"minilm": "all-MiniLM-L6-v2", "bge-large": "bge-large-en-v1.5", "bge-m3": "bge-m3",
+                             "tiny": "tiny"}[a.embedder],
+                "index": "%s %d chunks (HBM-resident)" % ("FlatL2" if a.index == "flat" else "IVF-Flat", a.chunks),
+                "retrieve_k": a.retrieve_k, "context_k": a.context_k,
+                "global_batch": a.concurrency * ctx.dp,
+                "seq_len": int(round(sum(P) / max(1, len(P)))),
+                "max_new_tokens": a.max_new_tokens,
+                "parallelism": par,
+            },
+            "p50_latency_ms": round(pct(L, 50), 1) if L else None,
+            "p90_latency_ms": round(pct(L, 90), 1) if L else None,
+            "ttft_p50_ms": round(pct(T, 50), 1) if T else None,
+            "per_gpu_tokens_per_s": round(value / ctx.world, 2),
+            "engine": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in eng.items()},
+            "setup_s": round(setup_s, 1),
+        }
+        line = json.dumps(res)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    D.shutdown(ctx)
+
+
+if __name__ == "__main__":
+    main()

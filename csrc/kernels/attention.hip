@@ -487,6 +487,7 @@ RAGK_API int ragk_attn_prefill(const void* q, int q_stride, const void* k, const
     return (int)launch_prefill<DD, GG, CC, PP>(a, n_tiles, st);
   RAGK_PF(128, 4, true, true)
   RAGK_PF(128, 1, true, true)
+  RAGK_PF(128, 2, true, true)
   RAGK_PF(64, 1, true, true)
   RAGK_PF(64, 4, true, true)
   RAGK_PF(128, 4, true, false)

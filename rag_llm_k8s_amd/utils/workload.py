@@ -1,0 +1,155 @@
+"""Synthetic RAG serving workload (shared by bench.py, smoke() and the GPU e2e tests).
+
+Builds, fully offline and on the target device:
+  * a Llama-3-style 128,256-token BPE tokenizer and a BERT WordPiece tokenizer trained on a
+    Zipfian pseudo-English corpus (same word model as the documents);
+  * random-init Llama weights of the requested architecture generated directly in HBM;
+  * a random-init sentence encoder (MiniLM-L6 / bge-large / bge-m3 shaped);
+  * a corpus of N chunks of `chunk_words` words (the reference chunker's 1000-word windows),
+    embedded by the encoder into the HBM-resident index;
+  * a RagService wired exactly like the server (retrieve_k / context_k / prompt template).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+from ..config import RagConfig
+from .synthetic import WordModel, train_llama3_tokenizer, train_small_bpe, train_wordpiece_tokenizer
+
+
+def asset_dir(tag):
+    d = os.path.join(os.environ.get("RAGK_ASSET_DIR", "/tmp/ragk_assets"), tag)
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def _once(path, build, ctx=None):
+    """Build an asset once per node: rank 0 builds, others wait on the file."""
+    from ..parallel.dist import barrier
+
+    done = path + ".done"
+    is_builder = ctx is None or ctx.local_rank == 0
+    if is_builder and not os.path.exists(done):
+        build()
+        with open(done, "w") as f:
+            f.write("ok")
+    if ctx is not None and ctx.initialized:
+        barrier(ctx)
+    t0 = time.time()
+    while not os.path.exists(done):
+        time.sleep(0.2)
+        if time.time() - t0 > 600:
+            raise TimeoutError("asset %s never appeared" % path)
+
+
+def make_tokenizers(wm, llm_vocab, enc_vocab, ctx=None):
+    from ..runtime.tokenizer import Tokenizer
+
+    tag = "tok_%d_%d" % (llm_vocab, enc_vocab)
+    d = asset_dir(tag)
+    llm_d, enc_d = os.path.join(d, "llm"), os.path.join(d, "enc")
+
+    def build():
+        if llm_vocab >= 128256:
+            train_llama3_tokenizer(llm_d, wm)
+        else:
+            train_small_bpe(llm_d, llm_vocab, wm)
+        train_wordpiece_tokenizer(enc_d, wm, corpus_words=600_000, vocab=enc_vocab)
+
+    _once(os.path.join(d, "tok"), build, ctx)
+    return Tokenizer(llm_d), Tokenizer(enc_d)
+
+
+def make_chunks(wm, n_chunks, chunk_words, seed=0):
+    rng = np.random.default_rng(seed + 123)
+    idx = np.searchsorted(wm.cdf, rng.random(n_chunks * chunk_words), side="right")
+    idx = np.minimum(idx, len(wm.words) - 1)
+    words = wm.words[idx]
+    out = []
+    for i in range(n_chunks):
+        w = words[i * chunk_words:(i + 1) * chunk_words]
+        out.append(" ".join(w))
+    return out
+
+
+def make_queries(wm, n, seed, words=12):
+    rng = np.random.default_rng(seed)
+    qs = []
+    for _ in range(n):
+        w = list(wm.sample(words, rng))
+        qs.append(" ".join(w).capitalize() + "?")
+    return qs
+
+
+class Workload:
+    def __init__(self, svc, wm, llm_tok, timings, n_chunks):
+        self.svc, self.wm, self.llm_tok, self.timings, self.n_chunks = svc, wm, llm_tok, timings, n_chunks
+
+
+def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=1000, retrieve_k=4, context_k=4,
+                   max_new_tokens=150, max_batch=32, max_model_len=8192, max_prefill_tokens=32768, device="cuda",
+                   ctx=None, tp_comm=None, seed=0, use_graphs=True, index_type="flat", kv_blocks=None,
+                   word_vocab=400000):
+    from ..engine.encoder_engine import EmbeddingEngine
+    from ..engine.llm_engine import LLMEngine
+    from ..index.store import DocumentStore
+    from ..models import encoder as E
+    from ..models import llama as L
+    from ..server.rag_service import RagService
+
+    t = {}
+    t0 = time.time()
+    wm = WordModel(n_words=word_vocab, seed=seed)
+    lcfg = {"8b": L.llama31_8b, "70b": L.llama31_70b,
+            "tiny": lambda: L.llama_tiny(vocab=1024, layers=2, hidden=512, heads=4, kv_heads=1, inter=512)}[model]()
+    ecfg = {"minilm": E.minilm_l6, "bge-large": E.bge_large_en, "bge-m3": E.bge_m3,
+            "tiny": lambda: E.EncoderConfig(vocab_size=2048, hidden_size=128, num_hidden_layers=2,
+                                            num_attention_heads=4, intermediate_size=256, max_seq_length=128)}[embedder]()
+    enc_vocab = ecfg.vocab_size if ecfg.model_type == "bert" else 30522
+    llm_tok, enc_tok = make_tokenizers(wm, lcfg.vocab_size, enc_vocab, ctx)
+    if ecfg.model_type != "bert":  # XLM-R shaped: reuse the WordPiece ids (random weights, vocab 250002)
+        ecfg.model_type = "bert"
+    t["tokenizers_s"] = time.time() - t0
+
+    t0 = time.time()
+    tp_rank = ctx.tp_rank if ctx is not None else 0
+    tp_size = ctx.tp if ctx is not None else 1
+    w = L.LlamaWeights.random(lcfg, device, tp_rank, tp_size, seed=seed)
+    m = L.LlamaModel(lcfg, w, device, comm=tp_comm, max_positions=max_model_len)
+    blocks = kv_blocks or (max_batch * (-(-max_model_len // 64)) + 16)
+    engine = LLMEngine(m, num_blocks=blocks, max_batch=max_batch, max_prefill_tokens=max_prefill_tokens,
+                       max_model_len=max_model_len, eos_ids=lcfg.eos_token_id, use_graphs=use_graphs,
+                       tp_group=ctx.tp_group if (ctx is not None and tp_size > 1) else None)
+    ew = E.EncoderWeights.random(ecfg, device, seed=seed + 1)
+    emb = EmbeddingEngine(E.EncoderModel(ecfg, ew, device), enc_tok)
+    t["weights_s"] = time.time() - t0
+
+    t0 = time.time()
+    chunks = make_chunks(wm, n_chunks, chunk_words, seed)
+    t["corpus_s"] = time.time() - t0
+    t0 = time.time()
+    cfg = RagConfig(device=device, retrieve_k=retrieve_k, context_k=context_k, max_new_tokens=max_new_tokens,
+                    max_batch=max_batch, max_model_len=max_model_len, index_path="/tmp/ragk_bench_index",
+                    index_type=index_type, seed=seed)
+    store = DocumentStore(cfg.index_path, emb.dim, device=device, index_type=index_type)
+    vecs = emb.embed(chunks)
+    meta = [{"filename": "synthetic_%05d.pdf" % (i // 20), "chunk_id": i % 20, "text": c}
+            for i, c in enumerate(chunks)]
+    store.add(vecs, meta, dedupe=False, persist=False)
+    if device.startswith("cuda"):
+        torch.cuda.synchronize()
+    t["ingest_s"] = time.time() - t0
+    svc = RagService(cfg, engine, llm_tok, emb, store, gen_config={"do_sample": True,
+                                                                   "eos_token_id": lcfg.eos_token_id},
+                     start_threads=False)
+    return Workload(svc, wm, llm_tok, t, n_chunks)
+
+
+def config_hash(d):
+    return hashlib.sha1(json.dumps(d, sort_keys=True).encode()).hexdigest()[:8]
