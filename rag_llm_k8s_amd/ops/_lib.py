@@ -22,6 +22,7 @@ P, I, F, S, U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p
 _SIGS = {
     "ragk_gemm": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_path": [I, P, I, P, I, P, I, P, P, I, I, I, I, I, S],
+    "ragk_gemm_pp": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_rmsnorm": [P, I, P, I, P, P, I, I, I, F, S],
     "ragk_layernorm": [P, I, P, I, P, P, P, I, I, I, F, S],
     "ragk_embed": [P, P, P, I, I, I, S],

@@ -26,6 +26,16 @@ def _bf16_2d(t, name):
 
 
 # ----------------------------------------------------------------------------- GEMM
+PP_MIN_M = int(__import__("os").environ.get("RAGK_PP_MIN_M", "1024"))
+
+
+def use_pp(M, N, K, epi):
+    """Large-M GEMMs go to the 256x256 8-wave ping-pong kernel (gemm_pp.hip)."""
+    if M < PP_MIN_M or K % 64:
+        return False
+    return N % 128 == 0 if epi == "silu_mul" else N % 8 == 0
+
+
 def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=None):
     """out[M,N] = epi(x[M,K] @ w[N,K]^T). For epi='silu_mul', w is the packed
     gate/up weight [2N, K] (see reference.pack_gate_up) and out has N columns."""
@@ -54,7 +64,12 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
         return out
     L = _lib.lib()
     ldr = resid.stride(0) if resid is not None else 0
-    if path is None:
+    if path is None and use_pp(M, N, K, epi):
+        path = 2
+    if path == 2:
+        rc = L.ragk_gemm_pp(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
+                            ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), stream_ptr())
+    elif path is None:
         rc = L.ragk_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
                          ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), stream_ptr())
     else:

@@ -26,6 +26,28 @@ def test_gemm_plain(native, M, N, K):
     assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 256, 128), (300, 1024, 768), (1111, 6144, 4096), (256, 256, 128),
+                                   (2049, 512, 1024), (513, 4104, 256)])
+def test_gemm_pingpong(native, M, N, K):
+    torch.manual_seed(20)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    b = torch.randn(N, device=DEV).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    y = native.gemm(x, w, path=2)
+    assert rel_err(y, x.float() @ w.float().t()) < 1e-2
+    for epi in ["bias", "resid", "bias_resid", "bias_gelu"]:
+        y = native.gemm(x, w, bias=b, resid=r, epi=epi, path=2)
+        assert rel_err(y.cpu(), R.linear(x.cpu(), w.cpu(), b.cpu(), r.cpu(), epi=epi)) < 1e-2, epi
+    yf = native.gemm(x, w, out_f32=True, path=2)
+    assert rel_err(yf, x.float() @ w.float().t()) < 1e-3
+    if N % 256 == 0:
+        g, u = w[: N // 2], w[N // 2:]
+        y = native.gemm(x, R.pack_gate_up(g, u), epi="silu_mul", path=2)
+        ref = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
+        assert rel_err(y, ref) < 1e-2
+
+
 @pytest.mark.parametrize("path", [0, 1])
 @pytest.mark.parametrize("M", [1, 16, 33, 64])
 def test_gemm_paths_agree(native, path, M):

@@ -47,11 +47,12 @@ def main():
             w = (torch.randn(wn, K, device=dev) / math.sqrt(K)).bfloat16()
             r = torch.randn(M, N_, device=dev).bfloat16() if epi == "resid" else None
             out = torch.empty(M, N_, device=dev).bfloat16()
-            t = timeit(lambda: N.gemm(x, w, resid=r, epi=epi, out=out))
+            t = timeit(lambda: N.gemm(x, w, resid=r, epi=epi, out=out, path=2))
+            t0 = timeit(lambda: N.gemm(x, w, resid=r, epi=epi, out=out, path=0))
             flops = 2 * M * wn * K
             tt = timeit(lambda: torch.matmul(x, w.t()))
-            rows.append(dict(kind="gemm_prefill", name=name, M=M, N=wn, K=K, ours_us=t * 1e6, ours_tflops=flops / t / 1e12,
-                             torch_us=tt * 1e6, torch_tflops=flops / tt / 1e12))
+            rows.append(dict(kind="gemm_prefill", name=name, M=M, N=wn, K=K, pp_us=t * 1e6, pp_tflops=flops / t / 1e12,
+                             tile128_tflops=flops / t0 / 1e12, torch_us=tt * 1e6, torch_tflops=flops / tt / 1e12))
             print(rows[-1], flush=True)
 
     # ---------------- decode GEMMs (weight streaming)
