@@ -295,6 +295,161 @@ __global__ __launch_bounds__(SK_WAVES * 64) void gemm_skinny_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Pipelined weight-streaming GEMV/GEMM for decode (M <= 64), v2.
+//  * software pipeline: the next 128-deep K block's weights + activations are loaded into a
+//    second register set while the MFMAs of the current one run (the v1 loop was latency-bound:
+//    load -> wait -> 4 MFMAs, ~4 iterations per wave);
+//  * weights are streamed with non-temporal loads (read exactly once);
+//  * NT n-tiles per wave reuse each activation fragment NT times (cuts the L2 activation
+//    traffic that dominated at M = 32..64);
+//  * rows >= M read a clamped (valid) row: their outputs are garbage but never stored, so no
+//    per-element select sits between a load and its MFMA.
+// ------------------------------------------------------------------------------------
+template <int MT, int NT, int NACC>
+struct GemvFrags {
+  bf16x8 w[NACC][NT][4];
+  bf16x8 x[MT][4];
+};
+
+template <int MT, int NT, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(SK_WAVES * 64) void gemm_gemv_kernel(
+    const bf16_t* __restrict__ X, int ldx, const bf16_t* __restrict__ W, int ldw, void* C, int ldc,
+    const bf16_t* __restrict__ bias, const bf16_t* resid, int ldr, int M, int N, int K) {
+  constexpr bool PAIR = (EPI == EPI_SILU_MUL);
+  constexpr int NACC = PAIR ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) f32x4 red[SK_WAVES][NACC * NT * MT][64];
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int fr = lane & 15, fh = lane >> 4;
+  const int nbase = blockIdx.x * 16 * NT;
+  const bf16_t* wp[NACC][NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = nbase + 16 * j + fr;
+    if constexpr (PAIR) {
+      const int r0 = (col >> 6) * 128 + (col & 63);
+      wp[0][j] = W + (size_t)r0 * ldw + fh * 8;
+      wp[1][j] = W + (size_t)(r0 + 64) * ldw + fh * 8;
+    } else {
+      wp[0][j] = W + (size_t)min(col, N - 1) * ldw + fh * 8;
+    }
+  }
+  const bf16_t* xp[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) xp[t] = X + (size_t)min(t * 16 + fr, M - 1) * ldx + fh * 8;
+
+  f32x4 acc[NACC][NT][MT];
+#pragma unroll
+  for (int a = 0; a < NACC; ++a)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) acc[a][j][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto load = [&](GemvFrags<MT, NT, NACC>& f, int kb) {
+    const int k = kb * 128;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int a = 0; a < NACC; ++a)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          f.w[a][j][s] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp[a][j] + k + 32 * s));
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) f.x[t][s] = *reinterpret_cast<const bf16x8*>(xp[t] + k + 32 * s);
+  };
+  auto compute = [&](const GemvFrags<MT, NT, NACC>& f) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int a = 0; a < NACC; ++a)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            acc[a][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.x[t][s], f.w[a][j][s], acc[a][j][t], 0, 0, 0);
+  };
+
+  const int nkb = K >> 7;
+  GemvFrags<MT, NT, NACC> fa, fb;
+  int kb = wid;
+  if (kb < nkb) load(fa, kb);
+  for (; kb < nkb; kb += 2 * SK_WAVES) {
+    const int kb2 = kb + SK_WAVES;
+    if (kb2 < nkb) load(fb, kb2);
+    compute(fa);
+    const int kb3 = kb2 + SK_WAVES;
+    if (kb3 < nkb) load(fa, kb3);
+    if (kb2 < nkb) compute(fb);
+  }
+
+#pragma unroll
+  for (int a = 0; a < NACC; ++a)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) red[wid][(a * NT + j) * MT + t][lane] = acc[a][j][t];
+  __syncthreads();
+
+  // element e = (j, t, lane, r): row = 16t + 4*(lane>>4) + r, col = nbase + 16j + (lane&15)
+  for (int e = threadIdx.x; e < NT * MT * 64 * 4; e += SK_WAVES * 64) {
+    const int j = e / (MT * 256), rem = e % (MT * 256);
+    const int t = rem >> 8, ln = (rem >> 2) & 63, r = rem & 3;
+    const int row = t * 16 + 4 * (ln >> 4) + r;
+    const int col = nbase + 16 * j + (ln & 15);
+    if (row >= M || col >= N) continue;
+    float v = 0.f, u = 0.f;
+#pragma unroll
+    for (int w = 0; w < SK_WAVES; ++w) {
+      v += red[w][j * MT + t][ln][r];
+      if constexpr (PAIR) u += red[w][(NT + j) * MT + t][ln][r];
+    }
+    if constexpr (PAIR) v = silu(v) * u;
+    if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH)
+      v += bf2f(bias[col]);
+    if constexpr (EPI == EPI_RESID || EPI == EPI_BIAS_RESID) v += bf2f(resid[(size_t)row * ldr + col]);
+    if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_GELU) v = gelu_erf(v);
+    if constexpr (EPI == EPI_BIAS_GELU_TANH) v = gelu_tanh(v);
+    if constexpr (OUT_F32)
+      reinterpret_cast<float*>(C)[(size_t)row * ldc + col] = v;
+    else
+      reinterpret_cast<bf16_t*>(C)[(size_t)row * ldc + col] = f2bf(v);
+  }
+}
+
+template <int MT, int NT, int EPI, bool F32>
+hipError_t launch_gemv(const void* X, int ldx, const void* W, int ldw, void* C, int ldc, const void* bias,
+                       const void* resid, int ldr, int M, int N, int K, hipStream_t st) {
+  hipLaunchKernelGGL((gemm_gemv_kernel<MT, NT, EPI, F32>), dim3((N + 16 * NT - 1) / (16 * NT)), dim3(SK_WAVES * 64),
+                     0, st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
+                     (const bf16_t*)resid, ldr, M, N, K);
+  return hipGetLastError();
+}
+
+// NT=2 when it still leaves >= 2 blocks per CU (and PAIR needs N % 32 for whole tiles)
+template <int EPI, bool F32>
+hipError_t dispatch_gemv(const void* X, int ldx, const void* W, int ldw, void* C, int ldc, const void* bias,
+                         const void* resid, int ldr, int M, int N, int K, hipStream_t st) {
+  const int mt = (M + 15) / 16;
+  const bool nt2 = M > 16 && N >= 32 * 512 && (EPI != EPI_SILU_MUL || N % 32 == 0);
+#define RAGK_GV(MTV)                                                                                         \
+  case MTV:                                                                                                  \
+    if (nt2 && MTV <= 2)                                                                                     \
+      return launch_gemv<MTV, (MTV <= 2 ? 2 : 1), EPI, F32>(X, ldx, W, ldw, C, ldc, bias, resid, ldr, M, N, K, st); \
+    return launch_gemv<MTV, 1, EPI, F32>(X, ldx, W, ldw, C, ldc, bias, resid, ldr, M, N, K, st);
+  switch (mt) {
+    RAGK_GV(1)
+    RAGK_GV(2)
+    RAGK_GV(3)
+    RAGK_GV(4)
+    default: return hipErrorInvalidValue;
+  }
+#undef RAGK_GV
+}
+
 template <int EPI, bool F32>
 hipError_t launch_tile(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
                        const void* resid, int ldr, int M, int N, int K, hipStream_t st) {
@@ -362,13 +517,19 @@ RAGK_API int ragk_gemm(const void* A, int lda, const void* B, int ldb, void* C, 
 #undef RAGK_GEMM_CASE
 }
 
-// Force a specific path (tests / benchmarks): path 0 = tile, 1 = skinny.
+// Force a specific path (tests / benchmarks): path 0 = tile, 1 = skinny v1, 3 = pipelined gemv v2.
 RAGK_API int ragk_gemm_path(int path, const void* A, int lda, const void* B, int ldb, void* C, int ldc,
                             const void* bias, const void* resid, int ldr, int M, int N, int K, int epi,
                             hipStream_t st) {
   if (K % 128 != 0) return (int)hipErrorInvalidValue;
-  if (path == 1) {
+  if (path == 1 || path == 3) {
     if (M > 64) return (int)hipErrorInvalidValue;
+    if (path == 3) {
+      if (epi == EPI_SILU_MUL) return (int)dispatch_gemv<EPI_SILU_MUL, false>(A, lda, B, ldb, C, ldc, bias, resid, ldr, M, N, K, st);
+      if (epi == EPI_NONE) return (int)dispatch_gemv<EPI_NONE, false>(A, lda, B, ldb, C, ldc, bias, resid, ldr, M, N, K, st);
+      if (epi == EPI_RESID) return (int)dispatch_gemv<EPI_RESID, false>(A, lda, B, ldb, C, ldc, bias, resid, ldr, M, N, K, st);
+      return (int)hipErrorInvalidValue;
+    }
     if (epi == EPI_SILU_MUL) return (int)dispatch_skinny<EPI_SILU_MUL, false>(A, lda, B, ldb, C, ldc, bias, resid, ldr, M, N, K, st);
     if (epi == EPI_NONE) return (int)dispatch_skinny<EPI_NONE, false>(A, lda, B, ldb, C, ldc, bias, resid, ldr, M, N, K, st);
     if (epi == EPI_RESID) return (int)dispatch_skinny<EPI_RESID, false>(A, lda, B, ldb, C, ldc, bias, resid, ldr, M, N, K, st);

@@ -65,11 +65,12 @@ def main():
             w = (torch.randn(wn, K, device=dev) / math.sqrt(K)).bfloat16()
             r = torch.randn(M, N_, device=dev).bfloat16() if epi == "resid" else None
             out = torch.empty(M, N_, device=dev).bfloat16()
-            t = timeit(lambda: N.gemm(x, w, resid=r, epi=epi, out=out), iters=50)
+            t = timeit(lambda: N.gemm(x, w, resid=r, epi=epi, out=out, path=1), iters=50)
+            t1 = timeit(lambda: N.gemm(x, w, resid=r, epi=epi, out=out, path=3), iters=50)
             tt = timeit(lambda: torch.matmul(x, w.t()), iters=50)
             byts = wn * K * 2
-            rows.append(dict(kind="gemm_decode", name=name, M=M, N=wn, K=K, ours_us=t * 1e6, ours_TBps=byts / t / 1e12,
-                             torch_us=tt * 1e6, torch_TBps=byts / tt / 1e12))
+            rows.append(dict(kind="gemm_decode", name=name, M=M, N=wn, K=K, v2_us=t * 1e6, v2_TBps=byts / t / 1e12,
+                             v1_TBps=byts / t1 / 1e12, torch_us=tt * 1e6, torch_TBps=byts / tt / 1e12))
             print(rows[-1], flush=True)
 
     # ---------------- prefill attention (causal, GQA 32/8, D=128)
