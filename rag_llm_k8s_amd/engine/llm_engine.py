@@ -120,6 +120,19 @@ class LLMEngine:
             self.waiting.append(s)
         return s
 
+    def make_sequence(self, prompt_ids, params: SamplingParams, seed: int) -> Sequence:
+        if len(prompt_ids) == 0:
+            raise ValueError("empty prompt")
+        if len(prompt_ids) + params.max_new_tokens > self.max_model_len:
+            raise ValueError("prompt (%d) + max_new_tokens (%d) exceeds max_model_len %d"
+                             % (len(prompt_ids), params.max_new_tokens, self.max_model_len))
+        return Sequence(prompt_ids, params, seed)
+
+    def add_sequence(self, s: Sequence):
+        with self.lock:
+            self.waiting.append(s)
+        return s
+
     def has_work(self):
         return bool(self.waiting) or bool(self.running)
 
@@ -250,10 +263,17 @@ class LLMEngine:
         import torch.distributed as dist
 
         B, K = cv.shape
-        gv = torch.empty((self.tp_size, B, K), dtype=cv.dtype, device=cv.device)
-        gi = torch.empty((self.tp_size, B, K), dtype=ci.dtype, device=ci.device)
-        dist.all_gather_into_tensor(gv, cv.contiguous(), group=self.tp_group)
-        dist.all_gather_into_tensor(gi, ci.contiguous(), group=self.tp_group)
+        if cv.is_cuda:
+            gv = torch.empty((self.tp_size, B, K), dtype=cv.dtype, device=cv.device)
+            gi = torch.empty((self.tp_size, B, K), dtype=ci.dtype, device=ci.device)
+            dist.all_gather_into_tensor(gv, cv.contiguous(), group=self.tp_group)
+            dist.all_gather_into_tensor(gi, ci.contiguous(), group=self.tp_group)
+        else:  # gloo (CPU plumbing / tests)
+            lv = [torch.empty_like(cv) for _ in range(self.tp_size)]
+            li = [torch.empty_like(ci) for _ in range(self.tp_size)]
+            dist.all_gather(lv, cv.contiguous(), group=self.tp_group)
+            dist.all_gather(li, ci.contiguous(), group=self.tp_group)
+            gv, gi = torch.stack(lv), torch.stack(li)
         return gv.permute(1, 0, 2).reshape(B, self.tp_size * K).contiguous(), \
             gi.permute(1, 0, 2).reshape(B, self.tp_size * K).contiguous()
 

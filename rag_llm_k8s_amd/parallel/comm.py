@@ -38,6 +38,11 @@ class TPComm:
             return x
         if self.ipc is not None and self.ipc.fits(x):
             return self.ipc.all_reduce(x)
+        if not x.is_cuda and x.dtype == torch.bfloat16:  # gloo: reduce in fp32, round once
+            y = x.float()
+            dist.all_reduce(y, group=self.group)
+            x.copy_(y)
+            return x
         dist.all_reduce(x, group=self.group)
         return x
 

@@ -42,18 +42,31 @@ class EngineLoop(threading.Thread):
         self.error = None
 
     def submit(self, prompt_ids, params, seed=None):
-        s = self.engine.add_request(prompt_ids, params, seed=seed)
+        if self.control is not None:  # TP: admission is broadcast to the follower ranks first
+            s = self.engine.make_sequence(prompt_ids, params, seed if seed is not None else 0)
+            self.control.enqueue(s)
+        else:
+            s = self.engine.add_request(prompt_ids, params, seed=seed)
         with self.cv:
             self.cv.notify()
         return s
 
+    def _idle(self):
+        eng = self.engine
+        pending = self.control.has_pending() if self.control is not None else False
+        return not eng.has_work() and not pending
+
     def run(self):
+        from ..parallel.tp import HEARTBEAT_S
+
         eng = self.engine
         try:
             while not self.stop_flag:
                 with self.cv:
-                    while not eng.has_work() and not self.stop_flag:
+                    while self._idle() and not self.stop_flag:
                         self.cv.wait(timeout=0.5)
+                        if self.control is not None and time.time() - self.control.last_publish > HEARTBEAT_S:
+                            self.control.publish_heartbeat()
                 if self.stop_flag:
                     break
                 if self.control is not None:

@@ -1,0 +1,162 @@
+"""T3' distributed tier on CPU: 2-process gloo groups exercising the same code paths the GPUs
+use over RCCL (TP sharded Llama, TP request broadcast, DP embedding all-gather, sharded index)."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from rag_llm_k8s_amd.models.llama import llama_tiny
+from rag_llm_k8s_amd.utils.synthetic import llama_state_dict
+
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(fn, *args):
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_entry, args=(fn, port, d, args), nprocs=WORLD, join=True)
+        out = {}
+        for r in range(WORLD):
+            p = os.path.join(d, "r%d.pt" % r)
+            if os.path.exists(p):
+                out[r] = torch.load(p, weights_only=False)
+        return out
+
+
+def _entry(rank, fn, port, d, args):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from rag_llm_k8s_amd.parallel.dist import init_distributed
+
+    ctx = init_distributed(tp=args[0] if args else 1, backend="gloo")
+    try:
+        res = fn(ctx, *args[1:])
+        torch.save(res, os.path.join(d, "r%d.pt" % rank))
+    finally:
+        dist.destroy_process_group()
+
+
+CFG = llama_tiny(vocab=320, layers=2, hidden=256, heads=4, kv_heads=2, inter=512)
+
+
+def _prefill_logits(model, ids):
+    from rag_llm_k8s_amd.models.llama import StepInput
+    from rag_llm_k8s_amd.ops.backend import AttnMeta
+
+    n = len(ids)
+    model.allocate_kv_cache(8)
+    slots = torch.arange(64, 64 + n, dtype=torch.int32)
+    bt = torch.tensor([[1, 2, 3, 4]], dtype=torch.int32)
+    meta = AttnMeta("prefill", torch.tensor([n], dtype=torch.int32), bt, cu_q=torch.tensor([0, n], dtype=torch.int32),
+                    host_kv_lens=[n])
+    return model.forward(StepInput(torch.tensor(ids, dtype=torch.int32), torch.arange(n, dtype=torch.int32), slots,
+                                   meta, torch.tensor([n - 1], dtype=torch.int32)))
+
+
+def _tp_worker(ctx, sd, ids):
+    from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights
+    from rag_llm_k8s_amd.parallel.comm import TPComm
+
+    w = LlamaWeights.from_state_dict(CFG, sd, "cpu", ctx.tp_rank, ctx.tp)
+    comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, "cpu")
+    m = LlamaModel(CFG, w, "cpu", comm=comm, max_positions=512)
+    local = _prefill_logits(m, ids)  # vocab shard
+    parts = [torch.empty_like(local) for _ in range(ctx.tp)]
+    dist.all_gather(parts, local, group=ctx.tp_group)
+    return torch.cat(parts, 1)[:, :CFG.vocab_size]
+
+
+def test_tp2_logits_match_tp1():
+    from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights
+
+    sd = llama_state_dict(CFG, seed=4, std=0.05)
+    ids = torch.randint(3, CFG.vocab_size, (40,)).tolist()
+    ref = _prefill_logits(LlamaModel(CFG, LlamaWeights.from_state_dict(CFG, sd, "cpu"), "cpu", max_positions=512), ids)
+    out = _run(_tp_worker, 2, sd, ids)
+    for r in range(WORLD):
+        rel = ((out[r] - ref).norm() / ref.norm()).item()
+        assert rel < 2e-2, rel
+    assert torch.equal(out[0], out[1])
+
+
+def _tp_control_worker(ctx, sd, prompts):
+    import threading
+
+    from rag_llm_k8s_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights
+    from rag_llm_k8s_amd.parallel.comm import TPComm
+    from rag_llm_k8s_amd.parallel.tp import TPControl, follow
+    from rag_llm_k8s_amd.server.rag_service import EngineLoop
+
+    w = LlamaWeights.from_state_dict(CFG, sd, "cpu", ctx.tp_rank, ctx.tp)
+    m = LlamaModel(CFG, w, "cpu", comm=TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, "cpu"), max_positions=512)
+    eng = LLMEngine(m, num_blocks=32, max_batch=4, max_model_len=512, use_graphs=False, tp_group=ctx.tp_group)
+    p = SamplingParams(max_new_tokens=5, temperature=0.8, top_p=0.9, top_k=20, ignore_eos=True)
+    if ctx.rank == 0:
+        loop = EngineLoop(eng, control=TPControl(ctx.tp_cpu_group))
+        loop.start()
+        seqs = [loop.submit(pr, p, seed=i + 7) for i, pr in enumerate(prompts)]
+        for s in seqs:
+            s.done.wait(60)
+        loop.stop()
+        loop.join(30)
+        return [s.out for s in seqs]
+    follow(eng, ctx.tp_cpu_group)
+    return "followed"
+
+
+def test_tp_control_broadcast_keeps_ranks_in_lockstep():
+    sd = llama_state_dict(CFG, seed=5, std=0.05)
+    prompts = [[5, 6, 7, 8, 9], list(range(10, 60)), [100, 101]]
+    out = _run(_tp_control_worker, 2, sd, prompts)
+    assert out[1] == "followed"
+    assert [len(o) for o in out[0]] == [5, 5, 5]
+
+
+def _dp_worker(ctx, texts):
+    from rag_llm_k8s_amd.engine.encoder_engine import EmbeddingEngine
+    from rag_llm_k8s_amd.models import encoder as E
+    from rag_llm_k8s_amd.parallel.dp import ShardedFlatIndex, embed_distributed
+    from rag_llm_k8s_amd.utils.synthetic import encoder_state_dict
+
+    class Tok:  # deterministic toy tokenizer
+        def encode_batch(self, ts, add_special_tokens=True, max_length=None):
+            return [[(ord(c) * 7 + i) % 500 for i, c in enumerate(t[:60])] or [1] for t in ts]
+
+    cfg = E.EncoderConfig(vocab_size=500, hidden_size=128, num_hidden_layers=1, num_attention_heads=4,
+                          intermediate_size=256, max_seq_length=64)
+    weights = E.EncoderWeights.from_state_dict(cfg, encoder_state_dict(cfg, seed=1), "cpu")
+    enc = EmbeddingEngine(E.EncoderModel(cfg, weights, "cpu"), Tok())
+    full = embed_distributed(enc, texts, group=None)
+    idx = ShardedFlatIndex(128, device="cpu")
+    idx.add(full)
+    q = full[ctx.rank::2] + 0.01
+    D, I = idx.search(q, 4)
+    return dict(full=full, D=D, I=I, q=q)
+
+
+def test_dp_embedding_and_sharded_search():
+    from rag_llm_k8s_amd.index.flat import FlatL2Index
+
+    texts = ["doc %d %s" % (i, "abc" * (i % 7)) for i in range(23)]
+    out = _run(_dp_worker, 1, texts)
+    assert torch.allclose(out[0]["full"], out[1]["full"])
+    ref = FlatL2Index(128)
+    ref.add(out[0]["full"])
+    for r in range(WORLD):
+        D, I = ref.search(out[r]["q"], 4)
+        assert torch.equal(out[r]["I"], I)
+        assert torch.allclose(out[r]["D"], D, atol=1e-5)
