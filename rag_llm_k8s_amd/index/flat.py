@@ -112,10 +112,15 @@ class FlatL2Index:
 
     # ---------------------------------------------------------------- persistence
     def write(self, path):
+        from ..runtime import native_rt
         from .faiss_io import atomic_write, write_flat_l2
 
         xb = self.reconstruct_all()
-        atomic_write(path, lambda f: write_flat_l2(f, xb))
+        rt = native_rt()
+        if rt is not None:  # C++ writer: temp file + fsync + rename
+            rt.write_flat_index(path, xb.reshape(-1, self.d))
+        else:
+            atomic_write(path, lambda f: write_flat_l2(f, xb))
 
     @classmethod
     def read(cls, path, device="cpu"):

@@ -33,6 +33,15 @@ _REV = {torch.bfloat16: "BF16", torch.float16: "F16", torch.float32: "F32", torc
 class SafeFile:
     def __init__(self, path):
         self.path = path
+        self._native = None
+        try:
+            from . import native_rt
+
+            rt = native_rt()
+            if rt is not None:
+                self._native = rt.SafeTensors(path)
+        except Exception:
+            self._native = None
         self._f = open(path, "rb")
         self._mm = mmap.mmap(self._f.fileno(), 0, access=mmap.ACCESS_READ)
         (n,) = struct.unpack("<Q", self._mm[:8])
@@ -52,6 +61,14 @@ class SafeFile:
         slices of the first / second dimension for TP sharding."""
         dt, shape, (a, b) = self.info(name)
         npdt, tdt, _ = _DT[dt]
+        if self._native is not None and (rows is not None or cols is not None):
+            # C++ row/col slice copy (GIL released): each TP rank touches only its shard's bytes
+            r0, r1 = rows if rows is not None else (-1, -1)
+            c0, c1 = cols if cols is not None else (-1, -1)
+            t = torch.from_numpy(self._native.slice(name, r0, r1, c0, c1))
+            if tdt in (torch.bfloat16, torch.float8_e4m3fn):
+                t = t.view(tdt)
+            return t
         arr = np.frombuffer(self._mm, dtype=npdt, count=(b - a) // np.dtype(npdt).itemsize, offset=self.base + a)
         arr = arr.reshape(shape) if shape else arr.reshape(())
         if rows is not None:

@@ -1,0 +1,200 @@
+"""C++ host runtime (_ragk_rt): tokenizers vs HF `tokenizers` (oracle), safetensors mmap reader
+vs the `safetensors` package, faiss IxF2 I/O vs the Python writer, KV block manager vs PyBlockManager."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from rag_llm_k8s_amd.utils.synthetic import WordModel
+
+LLAMA3_PAT = (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}{1,3}| ?[^\s\p{L}\p{N}]+[\r\n]*|"
+              r"\s*[\r\n]+|\s+(?!\S)|\s+")
+
+TEXTS = [
+    "Hello world! It's a test: don't STOP, we'll see.  Double  spaces\tand\ttabs.\n\nNew paragraph 12345 678.",
+    "Ünïcödé café naïve résumé — “quotes” ‘single’ … 漢字テスト 한국어 текст ١٢٣ 𝔘𝔫𝔦",
+    "   leading spaces and trailing   ",
+    "line1\r\nline2\n  \n\tindented\n",
+    "a1b2c3 x=y+z (paren) [brack] {brace} <tag> #hash @at $5.00 50% 3.14159e-10",
+    "I'M YOU'RE THEY'VE WE'D SHE'LL IT'S",
+    "",
+    "emoji 😀🚀 mixed👍text",
+]
+
+
+@pytest.fixture(scope="module")
+def rt():
+    from rag_llm_k8s_amd import _build
+    from rag_llm_k8s_amd.runtime import native_rt
+
+    _build.build_runtime()
+    import rag_llm_k8s_amd.runtime as R
+
+    R._tried = False
+    m = native_rt()
+    assert m is not None
+    return m
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    wm = WordModel(n_words=30000, seed=3)
+    lines = wm.corpus_lines(200000)
+    return wm, lines + TEXTS * 50
+
+
+def _check(rt, tok, path, texts, add_special=True):
+    n = rt.Tokenizer(path)
+    for t in texts:
+        ref = tok.encode(t, add_special_tokens=add_special).ids
+        got = n.encode(t, add_special)
+        assert got == ref, (t[:80], got[:20], ref[:20])
+        assert n.decode(got, True) == tok.decode(ref, skip_special_tokens=True), t[:80]
+    assert n.vocab_size() == tok.get_vocab_size(with_added_tokens=True)
+
+
+def test_bpe_gpt2_regex(rt, corpus, tmp_path):
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+
+    wm, lines = corpus
+    tok = Tokenizer(models.BPE())
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    tok.train_from_iterator(lines, trainers.BpeTrainer(vocab_size=4000, show_progress=False,
+                                                       initial_alphabet=pre_tokenizers.ByteLevel.alphabet()))
+    p = str(tmp_path / "gpt2.json")
+    tok.save(p)
+    _check(rt, tok, p, TEXTS + [wm.text(300) for _ in range(20)])
+
+
+def test_bpe_llama3_split_regex_with_specials(rt, corpus, tmp_path):
+    from tokenizers import AddedToken, Regex, Tokenizer, decoders, models, pre_tokenizers, processors, trainers
+
+    wm, lines = corpus
+    tok = Tokenizer(models.BPE(ignore_merges=True))
+    tok.pre_tokenizer = pre_tokenizers.Sequence([
+        pre_tokenizers.Split(Regex(LLAMA3_PAT), behavior="isolated", invert=False),
+        pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=False)])
+    tok.decoder = decoders.ByteLevel()
+    tok.train_from_iterator(lines, trainers.BpeTrainer(vocab_size=6000, show_progress=False,
+                                                       initial_alphabet=pre_tokenizers.ByteLevel.alphabet()))
+    tok.add_special_tokens([AddedToken("<|begin_of_text|>", special=True), AddedToken("<|eot_id|>", special=True)])
+    bos = tok.token_to_id("<|begin_of_text|>")
+    tok.post_processor = processors.TemplateProcessing(single="<|begin_of_text|> $A",
+                                                       special_tokens=[("<|begin_of_text|>", bos)])
+    p = str(tmp_path / "llama3.json")
+    tok.save(p)
+    texts = TEXTS + [wm.text(200) + " <|eot_id|> tail" for _ in range(10)] + ["<|begin_of_text|>x<|eot_id|>"]
+    _check(rt, tok, p, texts)
+    _check(rt, tok, p, texts, add_special=False)
+
+
+def test_wordpiece_bert(rt, corpus, tmp_path):
+    from rag_llm_k8s_amd.utils.synthetic import train_wordpiece_tokenizer
+
+    wm, lines = corpus
+    d = str(tmp_path / "wp")
+    tok = train_wordpiece_tokenizer(d, wm, corpus_words=100000, vocab=3000)
+    _check(rt, tok, os.path.join(d, "tokenizer.json"), TEXTS + [wm.text(150) for _ in range(10)])
+
+
+def test_unigram_metaspace(rt, corpus, tmp_path):
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+
+    wm, lines = corpus
+    tok = Tokenizer(models.Unigram())
+    tok.pre_tokenizer = pre_tokenizers.Metaspace()
+    tok.decoder = decoders.Metaspace()
+    tok.train_from_iterator(lines[:3000], trainers.UnigramTrainer(vocab_size=2000, show_progress=False,
+                                                                 special_tokens=["<unk>"], unk_token="<unk>"))
+    p = str(tmp_path / "uni.json")
+    tok.save(p)
+    texts = [wm.text(60) for _ in range(20)] + ["hello world", "zzqqxx unknownchars"]
+    n = rt.Tokenizer(p)
+    agree = 0
+    for t in texts:
+        ref = tok.encode(t).ids
+        got = n.encode(t, True)
+        agree += int(got == ref)
+        assert n.decode(got, True) == tok.decode(ref)
+    assert agree >= len(texts) - 2  # Viterbi ties may break differently
+
+
+def test_native_wrapper_used_by_default(rt, corpus, tmp_path):
+    from rag_llm_k8s_amd.runtime.tokenizer import Tokenizer as W
+    from rag_llm_k8s_amd.utils.synthetic import train_small_bpe
+
+    wm, _ = corpus
+    d = str(tmp_path / "small")
+    train_small_bpe(d, 600, wm)
+    a, b = W(d, backend="native"), W(d, backend="hf")
+    assert a.backend == "native" and b.backend == "hf"
+    for t in TEXTS:
+        assert a.encode(t) == b.encode(t)
+        assert a.decode(a.encode(t)) == b.decode(b.encode(t))
+    assert a.bos_id == b.bos_id
+
+
+def test_safetensors_reader(rt, tmp_path):
+    from safetensors.torch import save_file
+
+    t = {"a": torch.randn(5, 7).bfloat16(), "b": torch.arange(12, dtype=torch.int64).reshape(3, 4),
+         "c": torch.randn(3)}
+    p = str(tmp_path / "x.safetensors")
+    save_file(t, p, metadata={"format": "pt"})
+    st = rt.SafeTensors(p)
+    assert sorted(st.keys()) == ["a", "b", "c"] and st.metadata()["format"] == "pt"
+    a = torch.from_numpy(st.view("a").copy()).view(torch.bfloat16)
+    assert torch.equal(a, t["a"])
+    assert torch.equal(torch.from_numpy(st.view("b").copy()), t["b"])
+    sl = torch.from_numpy(st.slice("a", 1, 4, 2, 6)).view(torch.bfloat16)
+    assert torch.equal(sl, t["a"][1:4, 2:6])
+    assert torch.equal(torch.from_numpy(st.slice("b", 1, 3)), t["b"][1:3])
+    # the Python reader prefers / matches the native one
+    from rag_llm_k8s_amd.runtime.safetensors_io import SafeFile
+
+    sf = SafeFile(p)
+    assert torch.equal(sf.get("a", rows=(1, 4), cols=(2, 6)), t["a"][1:4, 2:6])
+
+
+def test_faiss_io_native_vs_python(rt, tmp_path):
+    from rag_llm_k8s_amd.index import faiss_io
+
+    xb = np.random.default_rng(0).standard_normal((11, 6)).astype(np.float32)
+    p1, p2 = str(tmp_path / "a"), str(tmp_path / "b")
+    rt.write_flat_index(p1, xb)
+    faiss_io.atomic_write(p2, lambda f: faiss_io.write_flat_l2(f, xb))
+    assert open(p1, "rb").read() == open(p2, "rb").read()
+    d, n, metric, x = rt.read_flat_index(p2)
+    assert (d, n, metric) == (6, 11, 1) and np.array_equal(x, xb)
+    with open(p1, "r+b") as f:
+        f.truncate(40)
+    with pytest.raises(RuntimeError):
+        rt.read_flat_index(p1)
+
+
+def test_block_manager_native_matches_python(rt):
+    from rag_llm_k8s_amd.engine.kv_manager import PyBlockManager
+
+    a, b = rt.BlockManager(20, True), PyBlockManager(20)
+    rng = np.random.default_rng(1)
+    live = set()
+    for step in range(300):
+        if live and rng.random() < 0.4:
+            s = int(rng.choice(sorted(live)))
+            a.free(s)
+            b.free(s)
+            live.discard(s)
+        else:
+            s = int(rng.integers(0, 8))
+            n = int(rng.integers(1, 300))
+            assert a.can_allocate(s, n) == b.can_allocate(s, n)
+            if b.can_allocate(s, n):
+                assert a.ensure(s, n) == b.ensure(s, n)
+                live.add(s)
+        assert a.free_blocks() == b.free_blocks()
+        for s in live:
+            assert a.table(s) == b.table(s)
+    with pytest.raises(RuntimeError):
+        a.ensure(99, 10 ** 6)
