@@ -48,16 +48,22 @@ __device__ void bitonic_desc(float* v, int* ix, int n) {
   }
 }
 
-__global__ __launch_bounds__(TK_THREADS) void topk_candidates_kernel(const float* __restrict__ logits, int ld, int V,
-                                                                     int K, int vocab_offset, float* cand_v,
-                                                                     int* cand_i) {
+// Block (row b, vocab chunk c): top-K of logits[b, c*Vc : min((c+1)*Vc, V)] -> candidates
+// [b][c*K + i]; chunking spreads one row over `chunks` workgroups (128k vocab: 16 x 8k).
+__global__ __launch_bounds__(TK_THREADS) void topk_candidates_kernel(const float* __restrict__ logits, int ld, int Vtot,
+                                                                     int K, int vocab_offset, int chunks,
+                                                                     float* cand_v, int* cand_i) {
   __shared__ unsigned hist[256];
   __shared__ unsigned s_prefix, s_krem, s_cnt_gt, s_cnt_eq;
   __shared__ float sv[MAXK];
   __shared__ int si[MAXK];
-  const int b = blockIdx.x;
-  const float* row = logits + (size_t)b * ld;
-  unsigned prefix = 0, mask = 0, krem = (unsigned)min(K, V);
+  const int b = blockIdx.x / chunks, chunk = blockIdx.x % chunks;
+  const int Vc = ((Vtot + chunks - 1) / chunks + 7) & ~7;
+  const int c0 = min(chunk * Vc, Vtot);
+  const int V = min(Vtot - c0, Vc);
+  const float* row = logits + (size_t)b * ld + c0;
+  vocab_offset += c0;
+  unsigned prefix = 0, mask = 0, krem = (unsigned)min(K, max(V, 1));
   for (int shift = 24; shift >= 0; shift -= 8) {
     for (int i = threadIdx.x; i < 256; i += TK_THREADS) hist[i] = 0;
     __syncthreads();
@@ -86,8 +92,8 @@ __global__ __launch_bounds__(TK_THREADS) void topk_candidates_kernel(const float
   if (threadIdx.x == 0) { s_cnt_gt = 0; s_cnt_eq = 0; }
   for (int i = threadIdx.x; i < MAXK; i += TK_THREADS) { sv[i] = -INFINITY; si[i] = 0x7fffffff; }
   __syncthreads();
-  const int kk = min(K, V);
-  const unsigned n_gt = (unsigned)kk - krem;
+  const int kk = max(0, min(K, V));
+  const unsigned n_gt = (unsigned)kk - min(krem, (unsigned)kk);
   for (int i = threadIdx.x; i < V; i += TK_THREADS) {
     const float x = row[i];
     const unsigned k = fkey(x);
@@ -106,9 +112,10 @@ __global__ __launch_bounds__(TK_THREADS) void topk_candidates_kernel(const float
   int n = 1;
   while (n < kk) n <<= 1;
   bitonic_desc(sv, si, n);
+  const size_t obase = ((size_t)b * chunks + chunk) * K;  // row b, slots [chunk*K, chunk*K + K)
   for (int i = threadIdx.x; i < K; i += TK_THREADS) {
-    cand_v[(size_t)b * K + i] = i < kk ? sv[i] : -INFINITY;
-    cand_i[(size_t)b * K + i] = i < kk ? si[i] : -1;
+    cand_v[obase + i] = i < kk ? sv[i] : -INFINITY;
+    cand_i[obase + i] = i < kk ? si[i] : -1;
   }
 }
 
@@ -181,12 +188,13 @@ __global__ __launch_bounds__(SC_THREADS) void sample_candidates_kernel(
 
 }  // namespace
 
-RAGK_API int ragk_topk_candidates(const float* logits, int ld, int B, int V, int K, int vocab_offset, float* cand_v,
-                                  int* cand_i, hipStream_t st) {
+// cand_v / cand_i: [B][chunks*K]
+RAGK_API int ragk_topk_candidates(const float* logits, int ld, int B, int V, int K, int vocab_offset, int chunks,
+                                  float* cand_v, int* cand_i, hipStream_t st) {
   if (B <= 0) return 0;
-  if (K < 1 || K > MAXK) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(topk_candidates_kernel, dim3(B), dim3(TK_THREADS), 0, st, logits, ld, V, K, vocab_offset, cand_v,
-                     cand_i);
+  if (K < 1 || K > MAXK || chunks < 1 || chunks > 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(topk_candidates_kernel, dim3(B * chunks), dim3(TK_THREADS), 0, st, logits, ld, V, K, vocab_offset,
+                     chunks, cand_v, cand_i);
   return (int)hipGetLastError();
 }
 

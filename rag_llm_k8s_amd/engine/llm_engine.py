@@ -249,8 +249,12 @@ class LLMEngine:
         be = self.model.be
         w = self.model.w
         lg = logits[:, :w.vocab_valid] if w.vocab_valid < logits.shape[1] else logits
+        # chunk count from the padded shard width so every TP rank gathers equal-sized lists,
+        # and all ranks' candidates together fit the sampler's 2048-entry merge
+        from ..ops.native import topk_chunks
+        chunks = topk_chunks(logits.shape[1], self.K, min(512, 2048 // self.tp_size))
         cv, ci = be.topk_candidates(lg.contiguous() if not lg.is_contiguous() else lg, self.K,
-                                    vocab_offset=w.vocab_offset)
+                                    vocab_offset=w.vocab_offset, chunks=chunks)
         if self.tp_size > 1:
             cv, ci = self._gather_candidates(cv, ci)
         tok = be.sample_candidates(cv, ci, temps, ks, ps, seeds, steps)

@@ -23,6 +23,8 @@ _SIGS = {
     "ragk_gemm": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_path": [I, P, I, P, I, P, I, P, P, I, I, I, I, I, S],
     "ragk_gemm_pp": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
+    "ragk_gemm_dec": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, I, P, P, S],
+    "ragk_gemm_dec_splits": [I, I, I],
     "ragk_rmsnorm": [P, I, P, I, P, P, I, I, I, F, S],
     "ragk_layernorm": [P, I, P, I, P, P, P, I, I, I, F, S],
     "ragk_embed": [P, P, P, I, I, I, S],
@@ -34,7 +36,7 @@ _SIGS = {
     "ragk_attn_prefill_qtile": [I, I],
     "ragk_attn_prefill": [P, I, P, P, I, P, I, P, P, P, P, I, P, I, I, I, I, I, I, F, S],
     "ragk_attn_decode": [P, I, P, P, P, I, P, P, P, P, I, I, I, I, I, I, I, F, S],
-    "ragk_topk_candidates": [P, I, I, I, I, I, P, P, S],
+    "ragk_topk_candidates": [P, I, I, I, I, I, I, P, P, S],
     "ragk_sample_candidates": [P, P, I, I, P, P, P, P, P, P, P, S],
     "ragk_l2_partial": [P, I, I, I, I, P, I, I, P, P, P, P, S],
     "ragk_topk_merge": [P, P, I, I, I, P, P, S],

@@ -134,7 +134,7 @@ class TorchBackend:
         return R.pool_l2norm(hidden, cu.cpu(), mode=mode, normalize=normalize)
 
     # sampling -----------------------------------------------------------------
-    def topk_candidates(self, logits, K, vocab_offset=0):
+    def topk_candidates(self, logits, K, vocab_offset=0, max_cand=512, chunks=None):
         k = min(K, logits.shape[1])
         v, i = torch.topk(logits.float(), k, dim=-1)
         if k < K:
@@ -210,8 +210,8 @@ class NativeBackend(TorchBackend):
     def pool_l2norm(self, hidden, cu, mode="cls", normalize=True):
         return self.n.pool_l2norm(hidden, cu, mode=mode, normalize=normalize)
 
-    def topk_candidates(self, logits, K, vocab_offset=0):
-        return self.n.topk_candidates(logits, K, vocab_offset=vocab_offset)
+    def topk_candidates(self, logits, K, vocab_offset=0, max_cand=512, chunks=None):
+        return self.n.topk_candidates(logits, K, vocab_offset=vocab_offset, max_cand=max_cand, chunks=chunks)
 
     def sample_candidates(self, cand_v, cand_i, temps, top_ks, top_ps, seeds, steps):
         return self.n.sample_candidates(cand_v, cand_i, temps, top_ks, top_ps, seeds, steps)

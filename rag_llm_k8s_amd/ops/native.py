@@ -29,6 +29,27 @@ def _bf16_2d(t, name):
 PP_MIN_M = int(__import__("os").environ.get("RAGK_PP_MIN_M", "1024"))
 
 
+DEC_DEFAULT = __import__("os").environ.get("RAGK_DEC_GEMM", "1") == "1"
+DEC_WS_BYTES = int(__import__("os").environ.get("RAGK_DEC_WS_MB", "96")) << 20
+_dec_ws = {}
+
+
+def dec_workspace(device):
+    """Per-device split-K workspace for the decode GEMM: fp32 slabs + ticket counters (zeroed once;
+    the last-arriving block resets its counter). Allocated eagerly, before any graph capture."""
+    key = str(device)
+    if key not in _dec_ws:
+        _dec_ws[key] = (torch.empty(DEC_WS_BYTES // 4, dtype=torch.float32, device=device),
+                        torch.zeros(65536, dtype=torch.int32, device=device))
+    return _dec_ws[key]
+
+
+def use_dec(M, N, K, epi):
+    """v3 (LDS-shared activations) wins over v1 only on vocab-sized N at M > 16 (lm_head: 5.1 vs
+    3.1 TB/s at M=32, cache-cold); v1 stays the default elsewhere (profiles/kernels_r1_decode.json)."""
+    return 16 < M <= 64 and N >= 32768 and K % 256 == 0 and epi != "silu_mul"
+
+
 def use_pp(M, N, K, epi):
     """Large-M GEMMs go to the 256x256 8-wave ping-pong kernel (gemm_pp.hip)."""
     if M < PP_MIN_M or K % 64:
@@ -66,7 +87,18 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
     ldr = resid.stride(0) if resid is not None else 0
     if path is None and use_pp(M, N, K, epi):
         path = 2
-    if path == 2:
+    if path is None and DEC_DEFAULT and use_dec(M, N, K, epi):
+        path = 4
+    if path == 4:
+        ws, cnt = dec_workspace(x.device)
+        S = L.ragk_gemm_dec_splits(N, K, e)
+        need = S * (2 if epi == "silu_mul" else 1) * M * N
+        _req(S == 1 or need <= ws.numel(), "decode GEMM workspace too small (%d > %d floats)" % (need, ws.numel()))
+        _req(-(-N // 128) <= cnt.numel(), "too many n-tiles for the counter buffer")
+        rc = L.ragk_gemm_dec(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
+                             ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), S, ws.data_ptr(), cnt.data_ptr(),
+                             stream_ptr())
+    elif path == 2:
         rc = L.ragk_gemm_pp(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
                             ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), stream_ptr())
     elif path is None:
@@ -241,14 +273,28 @@ def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, par
 
 
 # ----------------------------------------------------------------------------- sampling
-def topk_candidates(logits, K, vocab_offset=0, cand_v=None, cand_i=None):
+TOPK_CHUNK = 16384  # vocab entries per top-k workgroup (128k vocab -> 7 workgroups per row)
+
+
+def topk_chunks(V, K, max_cand=512):
+    """Workgroups per row for the candidate top-k: enough to fill the chip at decode batch
+    sizes, few enough that chunks*K candidates (x TP ranks) stay cheap to merge."""
+    return max(1, min(V // TOPK_CHUNK, max_cand // K, 64))
+
+
+def topk_candidates(logits, K, vocab_offset=0, max_cand=512, chunks=None, cand_v=None, cand_i=None):
+    """Per-row top-K of a (vocab-shard of) fp32 logits -> (values, global ids) [B, chunks*K]:
+    `chunks` sorted-descending lists of K, one per vocab chunk; the sampler merges them."""
     _req(logits.dtype == torch.float32 and logits.is_cuda and logits.stride(1) == 1, "logits fp32")
     B, V = logits.shape
     _req(1 <= K <= 256, "1 <= K <= 256")
+    chunks = topk_chunks(V, K, max_cand) if chunks is None else int(chunks)
+    _req(1 <= chunks <= 64, "1 <= chunks <= 64")
     if cand_v is None:
-        cand_v = torch.empty((B, K), dtype=torch.float32, device=logits.device)
-        cand_i = torch.empty((B, K), dtype=torch.int32, device=logits.device)
-    check(_lib.lib().ragk_topk_candidates(logits.data_ptr(), logits.stride(0), B, V, K, vocab_offset,
+        cand_v = torch.empty((B, chunks * K), dtype=torch.float32, device=logits.device)
+        cand_i = torch.empty((B, chunks * K), dtype=torch.int32, device=logits.device)
+    _req(cand_v.shape == (B, chunks * K) and cand_i.shape == (B, chunks * K), "candidate buffers [B, chunks*K]")
+    check(_lib.lib().ragk_topk_candidates(logits.data_ptr(), logits.stride(0), B, V, K, vocab_offset, chunks,
                                           cand_v.data_ptr(), cand_i.data_ptr(), stream_ptr()), "ragk_topk_candidates")
     return cand_v, cand_i
 

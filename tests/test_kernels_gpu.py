@@ -48,6 +48,28 @@ def test_gemm_pingpong(native, M, N, K):
         assert rel_err(y, ref) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1, 7, 16, 32, 33, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (384, 512), (1000, 768)])
+def test_gemm_decode_v3(native, M, N, K):
+    torch.manual_seed(21)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    ref = x.float() @ w.float().t()
+    for _ in range(2):  # second call checks the split-K counters were reset
+        y = native.gemm(x, w, path=4)
+        assert rel_err(y, ref) < 1e-2
+    y = native.gemm(x, w, resid=r, epi="resid", path=4)
+    assert rel_err(y, ref + r.float()) < 1e-2
+    yf = native.gemm(x, w, out_f32=True, path=4)
+    assert rel_err(yf, ref) < 1e-3
+    if N % 128 == 0:
+        g, u = w[: N // 2], w[N // 2:]
+        y = native.gemm(x, R.pack_gate_up(g, u), epi="silu_mul", path=4)
+        ref2 = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
+        assert rel_err(y, ref2) < 1e-2
+
+
 @pytest.mark.parametrize("path", [0, 1])
 @pytest.mark.parametrize("M", [1, 16, 33, 64])
 def test_gemm_paths_agree(native, path, M):
@@ -286,9 +308,29 @@ def test_topk_and_greedy(native):
     B, V = 4, 128256
     logits = torch.randn(B, V, device=DEV) * 3
     cv, ci = native.topk_candidates(logits, 50)
+    chunks = native.topk_chunks(V, 50)
+    assert chunks > 1 and cv.shape == (B, chunks * 50)
+    # each chunk's list is the exact sorted top-50 of its vocab slice
+    Vc = ((V + chunks - 1) // chunks + 7) & ~7
+    for c in range(chunks):
+        sl = logits[:, c * Vc: min((c + 1) * Vc, V)]
+        rv, ri = torch.topk(sl, 50, dim=-1)
+        assert torch.allclose(cv[:, c * 50:(c + 1) * 50], rv)
+        assert torch.equal(ci[:, c * 50:(c + 1) * 50].long(), ri + c * Vc)
+    # merged, they contain the global top-50
     ref_v, ref_i = torch.topk(logits, 50, dim=-1)
-    assert torch.allclose(cv, ref_v)
-    assert torch.equal(ci.long(), ref_i)
+    mv, order = torch.sort(cv, dim=-1, descending=True)
+    assert torch.allclose(mv[:, :50], ref_v)
+    assert torch.equal(torch.gather(ci, 1, order)[:, :50].long(), ref_i)
+    # single-chunk path, vocab offset (TP shard) and short rows
+    cv1, ci1 = native.topk_candidates(logits, 50, vocab_offset=1000, chunks=1)
+    assert torch.allclose(cv1, ref_v) and torch.equal(ci1.long(), ref_i + 1000)
+    short = logits[:, :37].contiguous()
+    cvs, cis = native.topk_candidates(short, 50, chunks=3)
+    assert cvs.shape == (B, 150)
+    valid = cis >= 0
+    assert int(valid.sum()) == B * 37
+    assert torch.isinf(cvs[~valid]).all()
     temps = torch.zeros(B, device=DEV)
     ks = torch.full((B,), 50, dtype=torch.int32, device=DEV)
     ps = torch.full((B,), 0.9, device=DEV)
