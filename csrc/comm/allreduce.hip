@@ -1,0 +1,252 @@
+// Single-node all-reduce over xGMI peer mappings (gfx950 / MI355X).
+//
+// The reference has no collectives at all; this is the latency path for
+// tensor-parallel decode, where each layer all-reduces a [B, 4096] bf16 residual
+// (8 KB x B). RCCL's ring is per-link bound on the point-to-point xGMI mesh (7 links per
+// GPU) and pays launch + protocol latency per call; here every rank maps every peer's
+// staging buffer once (hipIpc handles exchanged over the gloo control group) and one
+// kernel does the whole collective with direct xGMI loads:
+//
+//   one-shot  (small messages): every rank copies its input into its staging buffer,
+//             signals all peers, waits for all peers, then reads ALL ranks' copies of its
+//             output slice and sums them in rank order (bit-identical on every rank).
+//   two-shot  (medium messages): reduce-scatter (rank r reduces sub-slice r from all
+//             peers into its result buffer) -> signal -> all-gather (read every peer's
+//             reduced sub-slice).  Each byte crosses xGMI ~2x instead of world x.
+//
+// Synchronisation is per workgroup: block b of every rank owns the same element range, so
+// block b only waits for block b of its peers (no grid-wide barrier). Flags are
+// monotonically increasing epochs kept on the device (graph-capturable: no host-side
+// counter). Staging/result buffers are double-buffered by epoch parity. The grid size is
+// fixed per communicator, so every block takes part in every call and all blocks share
+// the epoch = call index: when block b passes the start barrier of call e, every peer has
+// finished call e-1 (stream order), so no peer still reads the half of call e-2 that the
+// next call overwrites, whatever element range any block owns.
+//
+// The whole region is allocated uncached (hipDeviceMallocUncached): payload stores and
+// peer loads bypass the per-XCD L2s; flag stores/polls are system-scope atomics and the
+// reader issues a system-scope acquire after its poll. Every spin is bounded: a peer
+// that never arrives sets an error word (ragk_ar_error) instead of hanging the GPU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../kernels/common.h"
+using namespace ragk;
+
+namespace {
+
+constexpr int AR_MAX_RANKS = 8;
+constexpr int AR_MAX_BLOCKS = 80;
+constexpr int AR_THREADS = 512;
+constexpr unsigned AR_SPIN_LIMIT = 1u << 24;  // x ~100 ns sleep ≈ 2 s, then give up
+
+struct ArFlags {
+  unsigned start[AR_MAX_BLOCKS][AR_MAX_RANKS];  // written by peers: "rank p reached epoch e (phase 1)"
+  unsigned mid[AR_MAX_BLOCKS][AR_MAX_RANKS];    // two-shot phase 2
+  unsigned epoch[AR_MAX_BLOCKS];                // local per-block epoch counter
+  unsigned error;                               // set when a bounded spin gives up
+};
+
+constexpr size_t FLAG_BYTES = (sizeof(ArFlags) + 4095) & ~size_t(4095);
+
+struct ArPeers {
+  char* base[AR_MAX_RANKS];  // every rank's region (own one included), mapped in this process
+};
+
+__device__ __forceinline__ unsigned ld_sys(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Block-level barrier with the same block of every peer: release my writes, publish `ep` into
+// slot [b][rank] of every peer's `which` array, wait until all peers published `ep` into mine.
+__device__ void peer_barrier(const ArPeers& P, int rank, int world, int which, unsigned ep) {
+  __syncthreads();
+  const int b = blockIdx.x;
+  if (threadIdx.x < world) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: payload visible before the flag
+    ArFlags* pf = reinterpret_cast<ArFlags*>(P.base[threadIdx.x]);
+    st_sys(which ? &pf->mid[b][rank] : &pf->start[b][rank], ep);
+    ArFlags* mf = reinterpret_cast<ArFlags*>(P.base[rank]);
+    const unsigned* slot = which ? &mf->mid[b][threadIdx.x] : &mf->start[b][threadIdx.x];
+    unsigned n = 0;
+    while (ld_sys(slot) < ep) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++n > AR_SPIN_LIMIT) {
+        st_sys(&mf->error, 1u);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ u32x4 ld16(const void* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+}
+
+// n8 = elements / 8 (16-byte vectors). data_bytes = capacity of one staging half.
+template <bool TWO_SHOT>
+__global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPeers P, int rank, int world, const bf16_t* in,
+                                                               bf16_t* out, long n8, size_t data_bytes) {
+  const int b = blockIdx.x;
+  ArFlags* mine = reinterpret_cast<ArFlags*>(P.base[rank]);
+  __shared__ unsigned s_ep;
+  if (threadIdx.x == 0) s_ep = mine->epoch[b] + 1;
+  __syncthreads();
+  const unsigned ep = s_ep;
+  // staging half h (input copies), result half h (two-shot reduced slices)
+  const size_t stage_off = FLAG_BYTES + (size_t)(ep & 1) * data_bytes;
+  const size_t result_off = FLAG_BYTES + 2 * data_bytes + (size_t)(ep & 1) * data_bytes;
+  const long per = (n8 + gridDim.x - 1) / gridDim.x;
+  const long v0 = min((long)b * per, n8), v1 = min(v0 + per, n8);
+
+  // 1. copy my slice of the input into my staging buffer
+  u32x4* my_stage = reinterpret_cast<u32x4*>(P.base[rank] + stage_off);
+  const u32x4* in4 = reinterpret_cast<const u32x4*>(in);
+  for (long v = v0 + threadIdx.x; v < v1; v += AR_THREADS) my_stage[v] = in4[v];
+  peer_barrier(P, rank, world, 0, ep);
+
+  u32x4* out4 = reinterpret_cast<u32x4*>(out);
+  if (!TWO_SHOT) {
+    for (long v = v0 + threadIdx.x; v < v1; v += AR_THREADS) {
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int p = 0; p < world; ++p) {
+        float f[8];
+        unpack8(ld16(P.base[p] + stage_off + v * 16), f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += f[i];
+      }
+      out4[v] = pack8(acc);
+    }
+  } else {
+    // sub-slice r of this block's range is reduced by rank r
+    const long sub = (v1 - v0 + world - 1) / world;
+    const long s0 = min(v0 + rank * sub, v1), s1 = min(s0 + sub, v1);
+    u32x4* my_res = reinterpret_cast<u32x4*>(P.base[rank] + result_off);
+    for (long v = s0 + threadIdx.x; v < s1; v += AR_THREADS) {
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int p = 0; p < world; ++p) {
+        float f[8];
+        unpack8(ld16(P.base[p] + stage_off + v * 16), f);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] += f[i];
+      }
+      my_res[v] = pack8(acc);
+    }
+    peer_barrier(P, rank, world, 1, ep);
+    for (int p = 0; p < world; ++p) {
+      const long t0 = min(v0 + p * sub, v1), t1 = min(t0 + sub, v1);
+      for (long v = t0 + threadIdx.x; v < t1; v += AR_THREADS) out4[v] = ld16(P.base[p] + result_off + v * 16);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) mine->epoch[b] = ep;
+}
+
+struct ArHandle {
+  int rank, world, blocks;
+  size_t data_bytes;  // capacity of one staging half (= max message bytes)
+  char* local;
+  ArPeers peers;
+  bool opened[AR_MAX_RANKS];
+};
+
+}  // namespace
+
+// Region layout: [flags | stage0 | stage1 | result0 | result1], each stage/result = max_bytes.
+// `blocks` (1..80) is the fixed grid of every call on this communicator (same on all ranks).
+RAGK_API void* ragk_ar_create(int rank, int world, long max_bytes, int blocks) {
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || max_bytes <= 0) return nullptr;
+  if (blocks < 1 || blocks > AR_MAX_BLOCKS) return nullptr;
+  ArHandle* h = new ArHandle();
+  memset(h, 0, sizeof(*h));
+  h->rank = rank;
+  h->world = world;
+  h->blocks = blocks;
+  h->data_bytes = ((size_t)max_bytes + 4095) & ~size_t(4095);
+  const size_t total = FLAG_BYTES + 4 * h->data_bytes;
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, total, hipDeviceMallocUncached) != hipSuccess) {
+    delete h;
+    return nullptr;
+  }
+  if (hipMemset(p, 0, total) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    (void)hipFree(p);
+    delete h;
+    return nullptr;
+  }
+  h->local = (char*)p;
+  h->peers.base[rank] = h->local;
+  return h;
+}
+
+RAGK_API int ragk_ar_ipc_handle(void* hp, void* out64) {
+  ArHandle* h = (ArHandle*)hp;
+  hipIpcMemHandle_t mh;
+  hipError_t e = hipIpcGetMemHandle(&mh, h->local);
+  if (e != hipSuccess) return (int)e;
+  memcpy(out64, &mh, sizeof(mh));
+  return 0;
+}
+
+RAGK_API int ragk_ar_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// handles: world x ragk_ar_handle_size() bytes (own entry ignored)
+RAGK_API int ragk_ar_open_peers(void* hp, const void* handles) {
+  ArHandle* h = (ArHandle*)hp;
+  const size_t hs = sizeof(hipIpcMemHandle_t);
+  for (int p = 0; p < h->world; ++p) {
+    if (p == h->rank) continue;
+    hipIpcMemHandle_t mh;
+    memcpy(&mh, (const char*)handles + p * hs, hs);
+    void* ptr = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&ptr, mh, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return (int)e;
+    h->peers.base[p] = (char*)ptr;
+    h->opened[p] = true;
+  }
+  return 0;
+}
+
+RAGK_API long ragk_ar_max_bytes(void* hp) { return (long)((ArHandle*)hp)->data_bytes; }
+
+// in/out: bf16[n] (n % 8 == 0, 16-byte aligned; in == out allowed). mode 0 = one-shot, 1 = two-shot.
+RAGK_API int ragk_ar_allreduce(void* hp, const void* in, void* out, long n, int mode, hipStream_t st) {
+  ArHandle* h = (ArHandle*)hp;
+  if (!h || n <= 0) return n == 0 ? 0 : (int)hipErrorInvalidValue;
+  if (n % 8 || (size_t)n * 2 > h->data_bytes || ((uintptr_t)in & 15) || ((uintptr_t)out & 15))
+    return (int)hipErrorInvalidValue;
+  for (int p = 0; p < h->world; ++p)
+    if (!h->peers.base[p]) return (int)hipErrorInvalidValue;  // peers not opened
+  const long n8 = n / 8;
+  const int blocks = h->blocks;
+  if (mode == 1)
+    hipLaunchKernelGGL(allreduce_kernel<true>, dim3(blocks), dim3(AR_THREADS), 0, st, h->peers, h->rank, h->world,
+                       (const bf16_t*)in, (bf16_t*)out, n8, h->data_bytes);
+  else
+    hipLaunchKernelGGL(allreduce_kernel<false>, dim3(blocks), dim3(AR_THREADS), 0, st, h->peers, h->rank, h->world,
+                       (const bf16_t*)in, (bf16_t*)out, n8, h->data_bytes);
+  return (int)hipGetLastError();
+}
+
+// 1 if any bounded spin gave up since creation (a peer never arrived), else 0; < 0 on error.
+RAGK_API int ragk_ar_error(void* hp) {
+  ArHandle* h = (ArHandle*)hp;
+  unsigned v = 0;
+  if (hipMemcpy(&v, h->local + offsetof(ArFlags, error), 4, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return (int)v;
+}
+
+RAGK_API void ragk_ar_destroy(void* hp) {
+  ArHandle* h = (ArHandle*)hp;
+  if (!h) return;
+  for (int p = 0; p < h->world; ++p)
+    if (h->opened[p]) (void)hipIpcCloseMemHandle(h->peers.base[p]);
+  (void)hipFree(h->local);
+  delete h;
+}

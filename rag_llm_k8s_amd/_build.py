@@ -46,8 +46,9 @@ def build_hip(verbose=False, jobs=None):
     os.makedirs(OBJ_DIR, exist_ok=True)
     os.makedirs(LIB_DIR, exist_ok=True)
     kdir = os.path.join(ROOT, "csrc", "kernels")
-    srcs = sorted(glob.glob(os.path.join(kdir, "*.hip")))
-    headers = glob.glob(os.path.join(kdir, "*.h"))
+    cdir = os.path.join(ROOT, "csrc", "comm")
+    srcs = sorted(glob.glob(os.path.join(kdir, "*.hip")) + glob.glob(os.path.join(cdir, "*.hip")))
+    headers = glob.glob(os.path.join(kdir, "*.h")) + glob.glob(os.path.join(cdir, "*.h"))
     flags = ["-O3", "--offload-arch=" + ARCH, "-fPIC", "-std=c++17", "-I" + kdir,
              "-Wno-unused-result", "-munsafe-fp-atomics"]
     objs, todo = [], []

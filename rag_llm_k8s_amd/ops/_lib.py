@@ -43,9 +43,17 @@ _SIGS = {
     "ragk_ivf_scan": [P, I, I, P, I, P, I, I, P, P, I, P, P, S],
     "ragk_l2_append": [P, I, I, I, P, I, S],
     "ragk_l2_gather": [P, I, I, P, I, P, S],
+    # csrc/comm/allreduce.hip (xGMI peer-mapped all-reduce)
+    "ragk_ar_create": [I, I, ctypes.c_long, I],
+    "ragk_ar_ipc_handle": [P, P],
+    "ragk_ar_handle_size": [],
+    "ragk_ar_open_peers": [P, P],
+    "ragk_ar_max_bytes": [P],
+    "ragk_ar_allreduce": [P, P, P, ctypes.c_long, I, S],
+    "ragk_ar_error": [P],
+    "ragk_ar_destroy": [P],
 }
-_OPTIONAL = {"ragk_allreduce_oneshot", "ragk_ipc_get_handle", "ragk_ipc_open_handle", "ragk_ipc_close_handle",
-             "ragk_allreduce_ipc", "ragk_ivf_scan", "ragk_quant_fp8", "ragk_gemm_fp8"}
+_RESTYPES = {"ragk_ar_create": ctypes.c_void_p, "ragk_ar_max_bytes": ctypes.c_long, "ragk_ar_destroy": None}
 
 _lib = None
 _lock = threading.Lock()
@@ -75,7 +83,7 @@ def lib():
         for name, args in _SIGS.items():
             fn = getattr(h, name)
             fn.argtypes = args
-            fn.restype = ctypes.c_int
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
         _lib = h
         return h
 

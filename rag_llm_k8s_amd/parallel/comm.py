@@ -3,11 +3,13 @@
 Llama TP (Megatron layout) needs two all-reduces of the [T, hidden] residual per layer.
 * Default: RCCL all_reduce through torch.distributed on the TP group (ring/tree over xGMI;
   capturable in the decode hipGraph).
-* Small messages (decode: 8 KB x batch) are latency-bound on a ring over 7 point-to-point
-  xGMI links; the IPC one-shot path (``ragk_allreduce_ipc``) maps every peer's staging
-  buffer into each rank (hipIpc handles exchanged over the gloo group) and reduces all 8
-  slices with direct xGMI loads in one kernel -- enabled with RAGK_IPC_ALLREDUCE=1 once
-  validated on the node (it needs all peers on one host).
+* Small / medium messages (decode: 8 KB x batch) are latency-bound on a ring over 7
+  point-to-point xGMI links; the peer-mapped path (parallel/ipc_allreduce.py, kernel in
+  csrc/comm/allreduce.hip) maps every peer's staging buffer into each rank (hipIpc handles
+  exchanged over the gloo group) and does the collective in one kernel with direct xGMI
+  loads: one-shot <= 512 KB, two-shot <= 8 MB, RCCL above. On by default on GPUs
+  (RAGK_IPC_ALLREDUCE=0 disables); it is cross-checked against RCCL at start-up and
+  disabled, loudly, if the check fails.
 """
 from __future__ import annotations
 
@@ -22,15 +24,24 @@ class TPComm:
         self.group, self.size, self.rank, self.device = group, size, rank, device
         self.cpu_group = cpu_group
         self.ipc = None
-        if os.environ.get("RAGK_IPC_ALLREDUCE", "0") == "1":
+        want = os.environ.get("RAGK_IPC_ALLREDUCE", "1") == "1"
+        if want and size > 1 and str(device).startswith("cuda") and cpu_group is not None:
+            import logging
+
+            log = logging.getLogger(__name__)
             try:
                 from .ipc_allreduce import IPCAllReduce
 
-                self.ipc = IPCAllReduce(group, cpu_group, size, rank, device)
+                ipc = IPCAllReduce(group, cpu_group, size, rank, device)
+                ok = torch.tensor([1 if ipc.self_test(group) else 0], device=device)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)  # all ranks agree
+                if int(ok.item()) == 1:
+                    self.ipc = ipc
+                else:
+                    log.warning("IPC all-reduce self-test failed; using RCCL")
+                    ipc.close()
             except Exception as e:  # fall back to RCCL, loudly
-                import logging
-
-                logging.getLogger(__name__).warning("IPC all-reduce unavailable (%s); using RCCL", e)
+                log.warning("IPC all-reduce unavailable (%s); using RCCL", e)
                 self.ipc = None
 
     def all_reduce(self, x: torch.Tensor):
