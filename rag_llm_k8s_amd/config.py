@@ -61,6 +61,10 @@ class RagConfig:
     use_cuda_graphs: bool = True
     log_level: str = "INFO"
     truncate_prompt: str = "left"  # left | none (GPT-2 has 1024 positions; the reference prompt is ~4.3k tokens)
+    request_timeout_s: float = 600.0  # /generate waits at most this long, then aborts the sequence -> 500
+    step_timeout_s: float = 300.0  # watchdog: an engine step (incl. its collectives) longer than this = hung
+    watchdog_exit: bool = True  # hung engine -> dump stacks and exit so k8s restarts the pod
+    index_recovery: str = "rebuild"  # rebuild (quarantine unreadable index, re-ingest PDF_DIR) | fail
     extra: dict = field(default_factory=dict)
 
     @classmethod
@@ -78,7 +82,9 @@ class RagConfig:
             "MAX_MODEL_LEN": ("max_model_len", int), "MAX_PREFILL_TOKENS": ("max_prefill_tokens", int),
             "KV_CACHE_FRACTION": ("kv_cache_fraction", float), "KV_CACHE_BLOCKS": ("kv_cache_blocks", int),
             "USE_CUDA_GRAPHS": ("use_cuda_graphs", bool), "LOG_LEVEL": ("log_level", str),
-            "TRUNCATE_PROMPT": ("truncate_prompt", str),
+            "TRUNCATE_PROMPT": ("truncate_prompt", str), "REQUEST_TIMEOUT_S": ("request_timeout_s", float),
+            "STEP_TIMEOUT_S": ("step_timeout_s", float), "WATCHDOG_EXIT": ("watchdog_exit", bool),
+            "INDEX_RECOVERY": ("index_recovery", str),
         }
         for env, (attr, cast) in m.items():
             setattr(c, attr, _env(env, getattr(c, attr), cast))

@@ -31,6 +31,7 @@ import torch
 
 from ..models.llama import StepInput
 from ..ops.backend import AttnMeta
+from ..utils import faults
 from .kv_manager import BLOCK, make_block_manager
 
 log = logging.getLogger(__name__)
@@ -94,6 +95,7 @@ class LLMEngine:
         self.waiting = deque()
         self.running: List[Sequence] = []
         self.lock = threading.Lock()
+        self._aborts = []
         self.tp_group = tp_group
         self.tp_size = 1 if tp_group is None else torch.distributed.get_world_size(tp_group)
         self.K = top_k_cap
@@ -162,9 +164,38 @@ class LLMEngine:
                 budget -= n
         return chunks
 
+    def abort(self, s: Sequence):
+        """Cancel a sequence (request timeout / client gone); applied at the next step boundary."""
+        with self.lock:
+            self._aborts.append(s)
+
+    def _apply_aborts(self):
+        with self.lock:
+            ab, self._aborts = self._aborts, []
+            for s in ab:
+                if s in self.waiting:
+                    self.waiting.remove(s)
+                    s.status, s.finish_reason, s.t_done = FINISHED, "abort", time.perf_counter()
+                    s.done.set()
+        for s in ab:
+            if s in self.running:
+                self._finish(s, "abort")
+
+    def _fault_hooks(self):
+        f = faults.faults()
+        if not f:
+            return
+        if "engine_crash_at_step" in f and faults.tick("engine_crash_at_step") >= int(f["engine_crash_at_step"]):
+            raise faults.FaultInjected("injected engine failure")
+        if "step_delay_ms" in f:
+            time.sleep(float(f["step_delay_ms"]) / 1000.0)
+
     def step(self):
         """One engine step. Returns the sequences that finished in it."""
         self._pin_off = 0
+        if self._aborts:
+            self._apply_aborts()
+        self._fault_hooks()
         chunks = self._admit()
         if chunks:
             return self._prefill(chunks)

@@ -16,9 +16,11 @@ from __future__ import annotations
 import logging
 import os
 import threading
+import time
 
 import numpy as np
 
+from ..utils import faults
 from .faiss_io import load_metadata, read_index, save_metadata
 from .flat import FlatL2Index
 
@@ -26,8 +28,10 @@ log = logging.getLogger(__name__)
 
 
 class DocumentStore:
-    def __init__(self, index_path, dim, device="cpu", index_type="flat", ivf_nlist=1024, ivf_nprobe=32):
+    def __init__(self, index_path, dim, device="cpu", index_type="flat", ivf_nlist=1024, ivf_nprobe=32,
+                 recovery="rebuild"):
         self.index_path = index_path
+        self.recovery = recovery  # rebuild: quarantine an unreadable index and start empty | fail
         self.meta_path = index_path + ".metadata"
         self.dim = dim
         self.device = device
@@ -38,6 +42,7 @@ class DocumentStore:
         self._keys = set()
         self._wlock = threading.Lock()
         self._mtimes = None
+        self.recovered = None
 
     def _new_index(self):
         if self.index_type == "ivf":
@@ -54,7 +59,27 @@ class DocumentStore:
             self.persist()
         else:
             log.info("Faiss index found.")
-            self.load()
+            try:
+                self.load()
+            except Exception as e:
+                if self.recovery != "rebuild":
+                    raise
+                self._quarantine(e)
+                self.persist()
+        return self
+
+    def _quarantine(self, err):
+        """Move an unreadable index (+ metadata) aside and start empty; the startup directory
+        ingest then rebuilds it from PDF_DIR. The reference would crash-loop instead."""
+        tag = ".corrupt-%d" % int(time.time())
+        for p in (self.index_path, self.meta_path):
+            if os.path.exists(p):
+                os.replace(p, p + tag)
+        log.error("index %s unreadable (%s); moved aside as *%s, starting empty", self.index_path, err, tag)
+        self.index = self._new_index()
+        self.metadata = []
+        self._keys = set()
+        self.recovered = tag
 
     def _disk_mtimes(self):
         try:
@@ -63,10 +88,13 @@ class DocumentStore:
             return None
 
     def load(self):
+        faults.check("index_read_error", self.index_path)
         r = read_index(self.index_path)
         meta = load_metadata(self.meta_path) if os.path.exists(self.meta_path) else []
         if r["d"] != self.dim:
             raise ValueError("index dimension %d != embedder dimension %d" % (r["d"], self.dim))
+        if len(meta) != r["ntotal"]:
+            raise ValueError("index has %d vectors but metadata %d entries (torn write?)" % (r["ntotal"], len(meta)))
         idx = self._new_index()
         if r["type"] == "flat":
             if r["ntotal"]:
@@ -87,7 +115,11 @@ class DocumentStore:
         m = self._disk_mtimes()
         if m is not None and self._mtimes is not None and m != self._mtimes:
             with self._wlock:
-                self.load()
+                try:
+                    self.load()
+                except Exception as e:  # keep serving the resident snapshot; retry on the next change
+                    log.warning("index on disk changed but is unreadable (%s); keeping the resident copy", e)
+                    self._mtimes = m
 
     def persist(self):
         self.index.write(self.index_path)

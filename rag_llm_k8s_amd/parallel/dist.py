@@ -47,6 +47,8 @@ def init_distributed(tp: int = 1, backend: Optional[str] = None, timeout_s: int 
         ctx.device = "cuda:%d" % local
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # RCCL errors / timed-out collectives abort the process instead of hanging it (comm watchdog)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         be = backend or ("nccl" if use_cuda else "gloo")
         kw = dict(backend=be, timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":

@@ -17,6 +17,7 @@ import torch
 import torch.distributed as dist
 
 from ..engine.llm_engine import SamplingParams, Sequence
+from ..utils import faults
 
 log = logging.getLogger(__name__)
 
@@ -73,6 +74,9 @@ def follow(engine, cpu_group, src_rank=0):
             return
         if kind == "noop":
             continue
+        hang = faults.value("comm_hang_s")
+        if hang:  # fault injection: this rank stalls, rank 0's collectives wait (watchdog path)
+            time.sleep(float(hang))
         for prompt, params, seed in reqs:
             p = dict(params)
             p["stop_token_ids"] = tuple(p.get("stop_token_ids", ()))
@@ -87,7 +91,8 @@ def run_tp_server(cfg, rank, world):
     from .comm import TPComm
     from .dist import init_distributed
 
-    ctx = init_distributed(tp=world)
+    # a collective that outlives two watchdog periods is dead: fail it so the pod restarts
+    ctx = init_distributed(tp=world, timeout_s=int(max(600, 2 * cfg.step_timeout_s)))
     comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, ctx.device, ctx.tp_cpu_group)
     control = TPControl(ctx.tp_cpu_group) if rank == 0 else None
     svc = build_service(cfg, start_threads=(rank == 0), tp_rank=ctx.tp_rank, tp_size=ctx.tp, comm=comm,

@@ -106,6 +106,18 @@ class CheckpointReader:
                 wm = json.load(f)["weight_map"]
             for name, fn in wm.items():
                 self.where[name] = fn
+            # fail fast, naming every absent shard (the reference's downloader swallowed errors,
+            # /root/reference/llm/download_model.py:32-33, and the load failed later, opaquely)
+            shards = sorted(set(wm.values()))
+            from ..utils import faults
+
+            drop = faults.value("missing_shard")
+            missing = [fn for i, fn in enumerate(shards)
+                       if not os.path.exists(os.path.join(path, fn)) or (drop is not None and int(drop) == i + 1)]
+            if missing:
+                raise FileNotFoundError("checkpoint %s is incomplete: missing shard(s) %s of %d listed in "
+                                        "model.safetensors.index.json (re-run llm/download_model.py)"
+                                        % (path, ", ".join(missing), len(shards)))
         else:
             single = os.path.join(path, "model.safetensors")
             if not os.path.exists(single):

@@ -98,6 +98,6 @@ def build_service(cfg, start_threads=True, tp_rank=0, tp_size=1, comm=None, tp_g
     log.info("Model and tokenizer loaded successfully")
     embedder = build_embedder(cfg, device)
     store = DocumentStore(cfg.index_path, embedder.dim, device=device, index_type=cfg.index_type,
-                          ivf_nlist=cfg.ivf_nlist, ivf_nprobe=cfg.ivf_nprobe)
+                          ivf_nlist=cfg.ivf_nlist, ivf_nprobe=cfg.ivf_nprobe, recovery=cfg.index_recovery)
     svc = RagService(cfg, engine, tok, embedder, store, gen_config=gen, start_threads=start_threads, control=control)
     return svc

@@ -13,9 +13,11 @@ packed batches instead of one chunk at a time.
 """
 from __future__ import annotations
 
+import faulthandler
 import logging
 import os
 import queue
+import sys
 import threading
 import time
 
@@ -24,7 +26,7 @@ import torch
 from ..engine.llm_engine import SamplingParams
 from ..ingest import pdf as pdfmod
 from ..ingest.text import NO_RESULTS, build_context, build_prompt, chunk_metadata, postprocess, split_text
-from ..utils import metrics
+from ..utils import faults, metrics
 from ..utils.metrics import Trace
 
 log = logging.getLogger(__name__)
@@ -40,6 +42,8 @@ class EngineLoop(threading.Thread):
         self.stop_flag = False
         self.control = control  # TP control channel (rank 0 side), see parallel/tp.py
         self.error = None
+        self.step_started = None  # monotonic start of the step in flight (watchdog)
+        self.steps = 0
 
     def submit(self, prompt_ids, params, seed=None):
         if self.control is not None:  # TP: admission is broadcast to the follower ranks first
@@ -69,9 +73,12 @@ class EngineLoop(threading.Thread):
                             self.control.publish_heartbeat()
                 if self.stop_flag:
                     break
+                self.step_started = time.monotonic()
                 if self.control is not None:
                     self.control.publish_step(eng)
                 fin = eng.step()
+                self.step_started = None
+                self.steps += 1
                 metrics.set_gauge("kv_free", eng.bm.free_blocks())
                 for s in fin:
                     metrics.inc("tokens", len(s.out))
@@ -89,6 +96,35 @@ class EngineLoop(threading.Thread):
         self.stop_flag = True
         with self.cv:
             self.cv.notify_all()
+
+
+class Watchdog(threading.Thread):
+    """Declares the engine hung when one step (its kernels + RCCL collectives) exceeds
+    `step_timeout_s`: liveness turns 503 and, with `exit_on_hang`, the process dumps every
+    thread's stack and exits so k8s restarts the pod (a wedged collective never returns)."""
+
+    def __init__(self, loop, step_timeout_s, exit_on_hang, poll_s=1.0):
+        super().__init__(daemon=True, name="engine-watchdog")
+        self.loop, self.timeout, self.exit_on_hang, self.poll = loop, step_timeout_s, exit_on_hang, poll_s
+        self.hung = False
+        self.stop_flag = False
+
+    def check(self, now=None):
+        t0 = self.loop.step_started
+        now = time.monotonic() if now is None else now
+        if t0 is not None and now - t0 > self.timeout and not self.hung:
+            self.hung = True
+            log.critical("engine step running for %.1fs > step_timeout_s=%.1fs: declaring the engine hung",
+                         now - t0, self.timeout)
+            faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+            if self.exit_on_hang:
+                os._exit(70)
+        return self.hung
+
+    def run(self):
+        while not self.stop_flag:
+            time.sleep(self.poll)
+            self.check()
 
 
 class MicroBatcher(threading.Thread):
@@ -147,6 +183,7 @@ class RagService:
         self.params = SamplingParams(max_new_tokens=cfg.max_new_tokens, temperature=cfg.temperature,
                                      top_p=cfg.top_p, top_k=cfg.top_k, do_sample=do_sample, stop_token_ids=stop)
         self.loop = EngineLoop(llm_engine, control=control)
+        self.watchdog = Watchdog(self.loop, cfg.step_timeout_s, cfg.watchdog_exit)
         self.batcher = MicroBatcher(self._retrieve_batch)
         self._seed = cfg.seed
         self._seed_lock = threading.Lock()
@@ -154,11 +191,13 @@ class RagService:
         if start_threads:
             self.loop.start()
             self.batcher.start()
+            self.watchdog.start()
 
     # ------------------------------------------------------------------ retrieval
     def _retrieve_batch(self, prompts):
         tr = Trace("retrieve")
         with tr.span("embed"):
+            faults.check("embed_error")
             q = self.embedder.embed(list(prompts))
         with tr.span("search"):
             self.store.maybe_reload()
@@ -199,7 +238,11 @@ class RagService:
             ids = self._prompt_ids(build_prompt(context, user_prompt))
         metrics.inc("prompt_tokens", len(ids))
         s = self.loop.submit(ids, params or self.params, seed=self._next_seed())
-        s.done.wait()
+        if not s.done.wait(timeout=self.cfg.request_timeout_s):
+            if self.loop.control is None:  # TP: followers mirror admissions only; the sequence runs out
+                self.engine.abort(s)
+            metrics.inc("timeouts")
+            raise TimeoutError("generation timed out after %.0fs" % self.cfg.request_timeout_s)
         if s.finish_reason == "error":
             raise RuntimeError("generation engine failed: %r" % (self.loop.error,))
         tr.add("queue+prefill", (s.t_first or s.t_done) - s.t_arrive)
@@ -280,9 +323,11 @@ class RagService:
         return self.store.info()
 
     def health(self):
-        return {"engine_alive": self.loop.is_alive() and self.loop.error is None, "ready": self.ready,
+        alive = self.loop.is_alive() and self.loop.error is None and not self.watchdog.hung
+        return {"engine_alive": alive, "ready": self.ready, "engine_steps": self.loop.steps,
                 "kv_free_blocks": self.engine.bm.free_blocks(), "index_vectors": int(self.store.index.ntotal),
                 "hbm_bytes": torch.cuda.memory_allocated() if torch.cuda.is_available() else 0}
 
     def shutdown(self):
+        self.watchdog.stop_flag = True
         self.loop.stop()

@@ -31,6 +31,8 @@ def registry():
         _M["ttft"] = prom.Histogram("rag_ttft_seconds", "time to first generated token", buckets=b, registry=_REG)
         _M["tokens"] = prom.Counter("rag_generated_tokens_total", "generated tokens", registry=_REG)
         _M["prompt_tokens"] = prom.Counter("rag_prompt_tokens_total", "prompt tokens", registry=_REG)
+        _M["timeouts"] = prom.Counter("rag_request_timeouts_total", "requests aborted by request_timeout_s",
+                                      registry=_REG)
         _M["requests"] = prom.Counter("rag_requests_total", "requests", ["route", "status"], registry=_REG)
         _M["batch"] = prom.Gauge("rag_decode_batch", "sequences in the last decode step", registry=_REG)
         _M["kv_free"] = prom.Gauge("rag_kv_free_blocks", "free KV-cache blocks", registry=_REG)
