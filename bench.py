@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--max-new-tokens", type=int, default=150)
     ap.add_argument("--index", default="flat", choices=["flat", "ivf"])
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="linear-layer weights: bf16 (headline) or fp8 e4m3 (BASELINE config 5)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -78,7 +80,8 @@ def main():
     t_setup = time.time()
     wl = build_workload(model=a.model, embedder=a.embedder, n_chunks=a.chunks, retrieve_k=a.retrieve_k,
                         context_k=a.context_k, max_new_tokens=a.max_new_tokens, max_batch=a.concurrency,
-                        device=dev, ctx=ctx, tp_comm=comm, seed=0, use_graphs=not a.no_graphs, index_type=a.index)
+                        device=dev, ctx=ctx, tp_comm=comm, seed=0, use_graphs=not a.no_graphs, index_type=a.index,
+                        dtype=a.dtype)
     svc = wl.svc
     svc.engine.warmup_graphs()
     params = SamplingParams(max_new_tokens=a.max_new_tokens, temperature=0.7, top_p=0.9, top_k=50, do_sample=True,
@@ -133,7 +136,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if a.dtype == "bf16" else "fp8-weights (bf16 activations/KV)",
             "data": "synthetic (random-init weights of the named architectures; Zipfian pseudo-English corpus "
                     "of %d x 1000-word chunks; trained 128k BPE + WordPiece tokenizers)" % a.chunks,
             "config": {

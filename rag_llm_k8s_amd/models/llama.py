@@ -197,9 +197,22 @@ class LlamaWeights:
         w.vocab_valid = min(cfg.vocab_size - tp_rank * Vl, Vl)
         return w
 
+    def quantize_fp8(self, lm_head=False):
+        """BASELINE config 5: e4m3fn weights with per-row scales for every linear layer (qkv, o,
+        packed gate/up, down; optionally lm_head). Embedding and norms stay bf16."""
+        from ..ops.fp8 import quantize_weight
+
+        for L in self.layers:
+            for k in ("wqkv", "wo", "wgu", "wdown"):
+                L[k] = quantize_weight(L[k])
+        if lm_head:
+            self.lm_head = quantize_weight(self.lm_head)
+        self.dtype = "fp8"
+        return self
+
     def nbytes(self):
         t = [self.embed, self.norm, self.lm_head] + [v for l in self.layers for v in l.values()]
-        return sum(x.numel() * x.element_size() for x in t)
+        return sum(x.nbytes() if hasattr(x, "dequant") else x.numel() * x.element_size() for x in t)
 
 
 # ------------------------------------------------------------------------------------- model

@@ -43,6 +43,8 @@ _SIGS = {
     "ragk_ivf_scan": [P, I, I, P, I, P, I, I, P, P, I, P, P, S],
     "ragk_l2_append": [P, I, I, I, P, I, S],
     "ragk_l2_gather": [P, I, I, P, I, P, S],
+    "ragk_quant_fp8_rows": [P, I, P, I, P, I, I, S],
+    "ragk_gemm_fp8": [P, I, P, I, P, P, I, P, P, I, P, P, I, I, I, I, I, I, S],
     # csrc/comm/allreduce.hip (xGMI peer-mapped all-reduce)
     "ragk_ar_create": [I, I, ctypes.c_long, I],
     "ragk_ar_ipc_handle": [P, P],

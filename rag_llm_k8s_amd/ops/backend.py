@@ -18,6 +18,7 @@ from typing import List, Optional
 import torch
 
 from . import reference as R
+from .fp8 import Fp8Weight, reference_linear
 
 KV_BLOCK = 64
 
@@ -46,7 +47,10 @@ class TorchBackend:
 
     # GEMM family ---------------------------------------------------------------
     def gemm(self, x, w, bias=None, resid=None, epi="none", out=None, out_f32=False):
-        y = R.linear(x, w, bias, resid, epi=epi, out_f32=out_f32)
+        if isinstance(w, Fp8Weight):
+            y = reference_linear(x, w, bias, resid, epi=epi, out_f32=out_f32)
+        else:
+            y = R.linear(x, w, bias, resid, epi=epi, out_f32=out_f32)
         if out is not None:
             out.copy_(y)
             return out
@@ -172,6 +176,8 @@ class NativeBackend(TorchBackend):
         native._lib.lib()  # fail loudly now if the gfx950 library is missing
 
     def gemm(self, x, w, bias=None, resid=None, epi="none", out=None, out_f32=False):
+        if isinstance(w, Fp8Weight):
+            return self.n.gemm_fp8(x, w, bias=bias, resid=resid, epi=epi, out=out, out_f32=out_f32)
         return self.n.gemm(x, w, bias=bias, resid=resid, epi=epi, out=out, out_f32=out_f32)
 
     def rmsnorm(self, x, w, eps, out=None):

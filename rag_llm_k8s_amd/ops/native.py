@@ -111,6 +111,61 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
     return out
 
 
+# ----------------------------------------------------------------------------- fp8 GEMM
+def quant_fp8_rows(x, q=None, scale=None):
+    """bf16 [M,K] -> (e4m3fn [M,K], fp32 [M]) with one dynamic scale per row."""
+    _bf16_2d(x, "x")
+    M, K = x.shape
+    _req(K % 8 == 0, "K % 8")
+    q = torch.empty((M, K), dtype=torch.float8_e4m3fn, device=x.device) if q is None else q
+    scale = torch.empty(M, dtype=torch.float32, device=x.device) if scale is None else scale
+    _req(q.shape == (M, K) and q.is_contiguous() and scale.numel() == M, "quant buffers")
+    check(_lib.lib().ragk_quant_fp8_rows(x.data_ptr(), x.stride(0), q.data_ptr(), q.stride(0), scale.data_ptr(), M, K,
+                                         stream_ptr()), "ragk_quant_fp8_rows")
+    return q, scale
+
+
+def gemm_fp8(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False):
+    """out[M,N] = epi(x[M,K] @ dequant(w)^T) for an :class:`ops.fp8.Fp8Weight` w (rows = N, or 2N
+    packed gate/up for epi='silu_mul'). M <= 64: W8A16 decode kernel; else W8A8 prefill kernel."""
+    from .fp8 import DEC_MAX_M
+
+    _bf16_2d(x, "x")
+    M, K = x.shape
+    w8, sw = w.w8, w.scale
+    _req(w8.dtype == torch.float8_e4m3fn and w8.is_cuda and w8.is_contiguous() and w8.shape[1] == K, "fp8 weight")
+    _req(sw.dtype == torch.float32 and sw.numel() == w8.shape[0], "fp8 scale")
+    _req(K % 128 == 0, "K must be a multiple of 128")
+    e = EPI[epi]
+    N = w8.shape[0] // 2 if epi == "silu_mul" else w8.shape[0]
+    if epi == "silu_mul":
+        _req(N % 64 == 0 and not out_f32, "silu_mul needs N % 64 == 0, bf16 out")
+    elif M > DEC_MAX_M:
+        _req(N % 8 == 0, "N % 8")
+    if "bias" in epi:
+        _req(bias is not None and bias.dtype == torch.bfloat16 and bias.numel() == N, "bias bf16[N]")
+    if "resid" in epi:
+        _bf16_2d(resid, "resid")
+        _req(resid.shape == (M, N), "resid shape")
+    odt = torch.float32 if out_f32 else torch.bfloat16
+    out = torch.empty((M, N), dtype=odt, device=x.device) if out is None else out
+    _req(out.dtype == odt and out.shape == (M, N) and out.stride(1) == 1, "out shape/dtype")
+    if M == 0:
+        return out
+    ldr = resid.stride(0) if resid is not None else 0
+    if M <= DEC_MAX_M:
+        rc = _lib.lib().ragk_gemm_fp8(x.data_ptr(), x.stride(0), None, 0, None, w8.data_ptr(), w8.stride(0),
+                                      sw.data_ptr(), out.data_ptr(), out.stride(0), ptr(bias), ptr(resid), ldr, M, N,
+                                      K, e, int(out_f32), stream_ptr())
+    else:
+        q, sa = quant_fp8_rows(x)
+        rc = _lib.lib().ragk_gemm_fp8(None, 0, q.data_ptr(), q.stride(0), sa.data_ptr(), w8.data_ptr(), w8.stride(0),
+                                      sw.data_ptr(), out.data_ptr(), out.stride(0), ptr(bias), ptr(resid), ldr, M, N,
+                                      K, e, int(out_f32), stream_ptr())
+    check(rc, "ragk_gemm_fp8")
+    return out
+
+
 # ----------------------------------------------------------------------------- norms
 def rmsnorm(x, w, eps, out=None, resid=None):
     _bf16_2d(x, "x")

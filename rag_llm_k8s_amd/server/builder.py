@@ -59,6 +59,8 @@ def build_generator(cfg, device, tp_rank=0, tp_size=1, comm=None, tp_group=None)
 
         c = LlamaConfig.from_dict(mcfg)
         w = LlamaWeights.from_checkpoint(cfg.model_path, c, device, tp_rank, tp_size)
+        if cfg.dtype == "fp8":  # DTYPE=fp8: e4m3fn linear weights, per-row scales (BASELINE config 5)
+            w.quantize_fp8()
         max_len = min(cfg.max_model_len, c.max_position_embeddings)
         model = LlamaModel(c, w, device, comm=comm, max_positions=max_len)
         eos = c.eos_token_id

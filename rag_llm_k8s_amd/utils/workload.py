@@ -95,7 +95,7 @@ class Workload:
 def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=1000, retrieve_k=4, context_k=4,
                    max_new_tokens=150, max_batch=32, max_model_len=8192, max_prefill_tokens=32768, device="cuda",
                    ctx=None, tp_comm=None, seed=0, use_graphs=True, index_type="flat", kv_blocks=None,
-                   word_vocab=400000):
+                   word_vocab=400000, dtype="bf16"):
     from ..engine.encoder_engine import EmbeddingEngine
     from ..engine.llm_engine import LLMEngine
     from ..index.store import DocumentStore
@@ -121,6 +121,10 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     tp_rank = ctx.tp_rank if ctx is not None else 0
     tp_size = ctx.tp if ctx is not None else 1
     w = L.LlamaWeights.random(lcfg, device, tp_rank, tp_size, seed=seed)
+    if dtype == "fp8":  # BASELINE config 5: e4m3fn linear weights (bf16 embeddings / norms / lm_head)
+        w.quantize_fp8()
+        if device.startswith("cuda"):
+            torch.cuda.empty_cache()
     m = L.LlamaModel(lcfg, w, device, comm=tp_comm, max_positions=max_model_len)
     blocks = kv_blocks or (max_batch * (-(-max_model_len // 64)) + 16)
     engine = LLMEngine(m, num_blocks=blocks, max_batch=max_batch, max_prefill_tokens=max_prefill_tokens,

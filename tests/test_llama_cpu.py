@@ -98,3 +98,38 @@ def test_sampling_engine_respects_eos_and_lengths(tiny):
     seqs2 = [eng2.add_request([5, 6, 9, 10], params, seed=i) for i in range(5)]
     eng2.run_until_done()
     assert [s.out for s in seqs] == [s.out for s in seqs2]
+
+
+def test_fp8_weights_cpu_reference_close_to_bf16():
+    """BASELINE config 5 numerics on the CPU oracle: fp8 (e4m3fn, per-row scales) Llama logits stay
+    close to the bf16 model's, for both the W8A16 (M <= 64) and W8A8 (M > 64) paths."""
+    from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights, llama_tiny
+    from rag_llm_k8s_amd.ops import fp8 as F8
+    from rag_llm_k8s_amd.utils.synthetic import llama_state_dict
+
+    cfg = llama_tiny(vocab=512, layers=2, hidden=256, heads=4, kv_heads=2, inter=512)
+    sd = llama_state_dict(cfg, seed=1, std=0.05)
+    w16 = LlamaWeights.from_state_dict(cfg, sd, "cpu")
+    w8 = LlamaWeights.from_state_dict(cfg, sd, "cpu").quantize_fp8()
+    assert isinstance(w8.layers[0]["wqkv"], F8.Fp8Weight) and w8.nbytes() < w16.nbytes()
+    x = torch.randn(100, 256).bfloat16()
+    for M in (10, 100):
+        a = F8.reference_linear(x[:M], w8.layers[0]["wqkv"])
+        b = x[:M].float() @ w16.layers[0]["wqkv"].float().t()
+        assert ((a - b).norm() / b.norm()).item() < 0.08
+    l16 = _prefill_logits(LlamaModel(cfg, w16, "cpu", max_positions=512), list(range(1, 90)))
+    l8 = _prefill_logits(LlamaModel(cfg, w8, "cpu", max_positions=512), list(range(1, 90)))
+    assert ((l8 - l16).norm() / l16.norm()).item() < 0.2  # W8A8 on a random-init model: ~12 %
+
+
+def _prefill_logits(model, ids):
+    from rag_llm_k8s_amd.models.llama import StepInput
+    from rag_llm_k8s_amd.ops.backend import AttnMeta
+
+    n = len(ids)
+    model.allocate_kv_cache(4)
+    bt = torch.tensor([[1, 2, 0, 0]], dtype=torch.int32)
+    meta = AttnMeta("prefill", torch.tensor([n], dtype=torch.int32), bt, cu_q=torch.tensor([0, n], dtype=torch.int32),
+                    host_kv_lens=[n], host_q_lens=[n])
+    return model.forward(StepInput(torch.tensor(ids, dtype=torch.int32), torch.arange(n, dtype=torch.int32),
+                                   torch.arange(64, 64 + n, dtype=torch.int32), meta, None))

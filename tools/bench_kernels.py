@@ -13,6 +13,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from rag_llm_k8s_amd.ops import native as N  # noqa: E402
+from rag_llm_k8s_amd.ops import fp8 as F8  # noqa: E402
 from rag_llm_k8s_amd.ops import reference as R  # noqa: E402
 
 
@@ -49,10 +50,13 @@ def main():
             out = torch.empty(M, N_, device=dev).bfloat16()
             t = timeit(lambda: N.gemm(x, w, resid=r, epi=epi, out=out, path=2))
             t0 = timeit(lambda: N.gemm(x, w, resid=r, epi=epi, out=out, path=0))
+            w8 = F8.quantize_weight(w)
+            t8 = timeit(lambda: N.gemm_fp8(x, w8, resid=r, epi=epi, out=out))
             flops = 2 * M * wn * K
             tt = timeit(lambda: torch.matmul(x, w.t()))
             rows.append(dict(kind="gemm_prefill", name=name, M=M, N=wn, K=K, pp_us=t * 1e6, pp_tflops=flops / t / 1e12,
-                             tile128_tflops=flops / t0 / 1e12, torch_us=tt * 1e6, torch_tflops=flops / tt / 1e12))
+                             tile128_tflops=flops / t0 / 1e12, fp8_w8a8_tflops=flops / t8 / 1e12,
+                             torch_us=tt * 1e6, torch_tflops=flops / tt / 1e12))
             print(rows[-1], flush=True)
 
     # ---------------- decode GEMMs (weight streaming)
@@ -74,12 +78,22 @@ def main():
                 it[0] = (it[0] + 1) % ncopy
                 return ws_[it[0]]
 
+            w8s = [F8.quantize_weight(wc) for wc in ws_]
+            it8 = [0]
+
+            def nxt8():
+                it8[0] = (it8[0] + 1) % ncopy
+                return w8s[it8[0]]
+
+            t8 = timeit(lambda: N.gemm_fp8(x, nxt8(), resid=r, epi=epi, out=out), iters=ncopy * 4)
+            del w8s
             t3 = timeit(lambda: N.gemm(x, nxt(), resid=r, epi=epi, out=out, path=4), iters=ncopy * 4)
             t1 = timeit(lambda: N.gemm(x, nxt(), resid=r, epi=epi, out=out, path=1), iters=ncopy * 4)
             tt = timeit(lambda: torch.matmul(x, nxt().t()), iters=ncopy * 4)
             del ws_
             byts = wn * K * 2
-            rows.append(dict(kind="gemm_decode", name=name, M=M, N=wn, K=K, v3_us=t3 * 1e6, v3_TBps=byts / t3 / 1e12,
+            rows.append(dict(kind="gemm_decode", name=name, M=M, N=wn, K=K, fp8_us=t8 * 1e6,
+                             fp8_TBps=byts / 2 / t8 / 1e12, v3_us=t3 * 1e6, v3_TBps=byts / t3 / 1e12,
                              v1_TBps=byts / t1 / 1e12, torch_us=tt * 1e6, torch_TBps=byts / tt / 1e12))
             print(rows[-1], flush=True)
 
