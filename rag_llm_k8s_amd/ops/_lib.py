@@ -43,6 +43,8 @@ _SIGS = {
     "ragk_ivf_scan": [P, I, I, P, I, P, I, I, P, P, I, P, P, S],
     "ragk_l2_append": [P, I, I, I, P, I, S],
     "ragk_l2_gather": [P, I, I, P, I, P, S],
+    "ragk_gemm_stream": [P, I, P, I, P, P, I, P, P, I, I, I, I, I, I, I, P, P, S],
+    "ragk_gemm_stream_splits": [I, I, I, I],
     "ragk_quant_fp8_rows": [P, I, P, I, P, I, I, S],
     "ragk_gemm_fp8": [P, I, P, I, P, P, I, P, P, I, P, P, I, I, I, I, I, I, S],
     # csrc/comm/allreduce.hip (xGMI peer-mapped all-reduce)

@@ -50,6 +50,20 @@ def use_dec(M, N, K, epi):
     return 16 < M <= 64 and N >= 32768 and K % 256 == 0 and epi != "silu_mul"
 
 
+STREAM_DEFAULT = __import__("os").environ.get("RAGK_STREAM_GEMM", "1") == "1"
+
+
+def use_stream(M, N, K, epi, fp8=False):
+    """Decode GEMM v4 (glds ring) wins where one launch has >= ~128 n-tiles of long K-streams and
+    no split-K: the packed gate/up projection (4.5 vs 3.4 TB/s bf16 at M=32, 4.4 vs 2.2 at M=64;
+    fp8 2.6 vs 1.5 at M=32) and other 16k-32k-row weights. Below that, the fixed pipeline-fill +
+    split-K reduction latencies lose to the register-streaming kernels (profiles/tune_stream_r1.json)."""
+    rows = 2 * N if epi == "silu_mul" else N
+    if M > 64 or not (16384 <= rows < 32768) or K % 128:
+        return False
+    return M > 16 if fp8 else True
+
+
 def use_pp(M, N, K, epi):
     """Large-M GEMMs go to the 256x256 8-wave ping-pong kernel (gemm_pp.hip)."""
     if M < PP_MIN_M or K % 64:
@@ -87,9 +101,13 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
     ldr = resid.stride(0) if resid is not None else 0
     if path is None and use_pp(M, N, K, epi):
         path = 2
+    if path is None and STREAM_DEFAULT and use_stream(M, N, K, epi):
+        path = 5
     if path is None and DEC_DEFAULT and use_dec(M, N, K, epi):
         path = 4
-    if path == 4:
+    if path == 5:
+        rc = _gemm_stream(x, w, None, out, bias, resid, ldr, M, N, K, epi, e, out_f32)
+    elif path == 4:
         ws, cnt = dec_workspace(x.device)
         S = L.ragk_gemm_dec_splits(N, K, e)
         need = S * (2 if epi == "silu_mul" else 1) * M * N
@@ -111,6 +129,23 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
     return out
 
 
+STREAM_S_OVERRIDE = 0  # tuning hook (tools/tune_stream.py)
+
+
+def _gemm_stream(x, w, wscale, out, bias, resid, ldr, M, N, K, epi, e, out_f32):
+    """Decode GEMM v4 (csrc/kernels/gemm_stream.hip): glds-ring weight streaming, split-K."""
+    L = _lib.lib()
+    fp8 = wscale is not None
+    S = STREAM_S_OVERRIDE or L.ragk_gemm_stream_splits(N, K, e, int(fp8))
+    ws, cnt = dec_workspace(x.device)
+    rows = 2 * N if epi == "silu_mul" else N
+    _req(S == 1 or S * M * rows <= ws.numel(), "stream GEMM workspace too small")
+    _req(-(-rows // 128) <= cnt.numel(), "too many n-tiles for the counter buffer")
+    return L.ragk_gemm_stream(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), ptr(wscale), out.data_ptr(),
+                              out.stride(0), ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), S, ws.data_ptr(),
+                              cnt.data_ptr(), stream_ptr())
+
+
 # ----------------------------------------------------------------------------- fp8 GEMM
 def quant_fp8_rows(x, q=None, scale=None):
     """bf16 [M,K] -> (e4m3fn [M,K], fp32 [M]) with one dynamic scale per row."""
@@ -123,6 +158,9 @@ def quant_fp8_rows(x, q=None, scale=None):
     check(_lib.lib().ragk_quant_fp8_rows(x.data_ptr(), x.stride(0), q.data_ptr(), q.stride(0), scale.data_ptr(), M, K,
                                          stream_ptr()), "ragk_quant_fp8_rows")
     return q, scale
+
+
+FP8_DEC_STREAM = __import__("os").environ.get("RAGK_FP8_DEC", "auto") != "regs"
 
 
 def gemm_fp8(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False):
@@ -153,7 +191,9 @@ def gemm_fp8(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False):
     if M == 0:
         return out
     ldr = resid.stride(0) if resid is not None else 0
-    if M <= DEC_MAX_M:
+    if M <= DEC_MAX_M and FP8_DEC_STREAM and use_stream(M, N, K, epi, fp8=True):
+        rc = _gemm_stream(x, w8, sw, out, bias, resid, ldr, M, N, K, epi, e, out_f32)
+    elif M <= DEC_MAX_M:
         rc = _lib.lib().ragk_gemm_fp8(x.data_ptr(), x.stride(0), None, 0, None, w8.data_ptr(), w8.stride(0),
                                       sw.data_ptr(), out.data_ptr(), out.stride(0), ptr(bias), ptr(resid), ldr, M, N,
                                       K, e, int(out_f32), stream_ptr())

@@ -101,3 +101,23 @@ def test_fp8_engine_gpu_matches_cpu_reference(native):
     cpu = engine("cpu", False).generate(prompts, p)
     first = sum(int(g[0] == c[0]) for g, c in zip(gpu, cpu))
     assert first >= 3, (gpu, cpu)
+
+
+@pytest.mark.parametrize("M", [1, 17, 33, 64])
+@pytest.mark.parametrize("N,K", [(768, 1024), (4096, 4096), (1024, 14336)])
+def test_gemm_fp8_stream_decode(native, monkeypatch, M, N, K):
+    """The glds-ring decode kernel (gemm_stream.hip) on fp8 weights, forced for every shape."""
+    monkeypatch.setattr(native, "use_stream", lambda *a, **k: True)
+    torch.manual_seed(M + K)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    wq = F8.quantize_weight(w)
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    for epi, kw in [("none", {}), ("resid", dict(resid=r))]:
+        for _ in range(2):
+            y = native.gemm_fp8(x, wq, epi=epi, **kw)
+            assert rel_err(y, F8.reference_linear(x, wq, epi=epi, **kw)) < 1e-2
+    g = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    wgu = F8.quantize_weight(R.pack_gate_up(w[: N // 2 // 64 * 64 or 64], g[: N // 2 // 64 * 64 or 64]))
+    y = native.gemm_fp8(x, wgu, epi="silu_mul")
+    assert rel_err(y, F8.reference_linear(x, wgu, epi="silu_mul")) < 1e-2

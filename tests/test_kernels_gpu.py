@@ -377,3 +377,25 @@ def test_l2_search(native, N, d, nq, k):
     Dr, Ir = R.l2_knn(xb, q, k)
     assert torch.equal(I.cpu(), Ir)
     assert torch.allclose(D.cpu(), Dr, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
+@pytest.mark.parametrize("N,K", [(768, 1024), (4096, 4096), (6144, 4096), (1024, 14336)])
+def test_gemm_stream_bf16(native, M, N, K):
+    torch.manual_seed(M * 7 + N)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    b = torch.randn(N, device=DEV).bfloat16()
+    ref = x.float() @ w.float().t()
+    for _ in range(2):  # second call: split-K counters were reset
+        assert rel_err(native.gemm(x, w, path=5), ref) < 1e-2
+    assert rel_err(native.gemm(x, w, resid=r, epi="resid", path=5), ref + r.float()) < 1e-2
+    assert rel_err(native.gemm(x, w, bias=b, epi="bias_gelu", path=5),
+                   torch.nn.functional.gelu(ref + b.float())) < 1e-2
+    assert rel_err(native.gemm(x, w, out_f32=True, path=5), ref) < 1e-3
+    if N % 128 == 0:
+        g, u = w[: N // 2], w[N // 2:]
+        y = native.gemm(x, R.pack_gate_up(g, u), epi="silu_mul", path=5)
+        ref2 = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
+        assert rel_err(y, ref2) < 1e-2

@@ -87,13 +87,14 @@ def main():
 
             t8 = timeit(lambda: N.gemm_fp8(x, nxt8(), resid=r, epi=epi, out=out), iters=ncopy * 4)
             del w8s
+            t5 = timeit(lambda: N.gemm(x, nxt(), resid=r, epi=epi, out=out, path=5), iters=ncopy * 4)
             t3 = timeit(lambda: N.gemm(x, nxt(), resid=r, epi=epi, out=out, path=4), iters=ncopy * 4)
             t1 = timeit(lambda: N.gemm(x, nxt(), resid=r, epi=epi, out=out, path=1), iters=ncopy * 4)
             tt = timeit(lambda: torch.matmul(x, nxt().t()), iters=ncopy * 4)
             del ws_
             byts = wn * K * 2
             rows.append(dict(kind="gemm_decode", name=name, M=M, N=wn, K=K, fp8_us=t8 * 1e6,
-                             fp8_TBps=byts / 2 / t8 / 1e12, v3_us=t3 * 1e6, v3_TBps=byts / t3 / 1e12,
+                             fp8_TBps=byts / 2 / t8 / 1e12, v4_us=t5 * 1e6, v4_TBps=byts / t5 / 1e12, v3_us=t3 * 1e6, v3_TBps=byts / t3 / 1e12,
                              v1_TBps=byts / t1 / 1e12, torch_us=tt * 1e6, torch_TBps=byts / tt / 1e12))
             print(rows[-1], flush=True)
 
