@@ -2,6 +2,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstring>
 #include <fstream>
 #include <limits>
 #include <sstream>
@@ -264,21 +266,237 @@ void Tokenizer::load_model(const Json& m) {
   }
 }
 
+static std::string base64_decode(const std::string& in) {
+  static int T[256];
+  static bool init = false;
+  if (!init) {
+    for (int i = 0; i < 256; ++i) T[i] = -1;
+    const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+    for (int i = 0; i < 64; ++i) T[(unsigned char)a[i]] = i;
+    init = true;
+  }
+  std::string out;
+  uint32_t val = 0;
+  int bits = -8;
+  for (unsigned char c : in) {
+    if (T[c] < 0) continue;  // '=' padding / whitespace
+    val = ((val << 6) | (uint32_t)T[c]) & 0xFFFFFFu;  // only the last 24 bits are ever read
+    bits += 6;
+    if (bits >= 0) {
+      out.push_back((char)((val >> bits) & 0xFF));
+      bits -= 8;
+    }
+  }
+  return out;
+}
+
 void Tokenizer::load_normalizer(const Json* n) {
   if (!n || n->is_null()) return;
   const std::string t = n->at("type").str;
+  NormStep st{};
   if (t == "Sequence") {
     for (auto& x : n->at("normalizers").arr) load_normalizer(&x);
+    return;
   } else if (t == "BertNormalizer") {
-    bert_norm_ = true;
+    st.kind = NormStep::BERT;
     if (const Json* x = n->get("clean_text")) bn_clean_ = x->truthy();
     if (const Json* x = n->get("handle_chinese_chars")) bn_chinese_ = x->truthy();
     if (const Json* x = n->get("lowercase")) bn_lower_ = x->truthy();
     const Json* sa = n->get("strip_accents");
     bn_strip_ = (sa && !sa->is_null()) ? sa->truthy() : bn_lower_;
   } else if (t == "Lowercase") {
-    lowercase_ = true;
-  }  // NFC / NFKC / Precompiled / Strip / Replace: identity (documented limitation)
+    st.kind = NormStep::LOWER;
+  } else if (t == "Strip") {
+    st.kind = NormStep::STRIP;
+    if (const Json* x = n->get("strip_left")) st.left = x->truthy();
+    if (const Json* x = n->get("strip_right")) st.right = x->truthy();
+  } else if (t == "Replace") {
+    const Json& pat = n->at("pattern");
+    st.content = n->at("content").str;
+    if (const Json* lit = pat.get("String")) {
+      st.kind = NormStep::REPLACE;
+      st.pat = lit->str;
+      if (st.pat.empty()) return;
+    } else {
+      // only single-code-point runs "c{n,}" (the SentencePiece converters' " {2,}")
+      const std::string rx = pat.at("Regex").str;
+      std::vector<uint32_t> cps = utf8_decode(rx);
+      size_t brace = 0;
+      while (brace < cps.size() && cps[brace] != '{') ++brace;
+      if (brace != 1 || cps.size() < 5 || cps.back() != '}' || cps[cps.size() - 2] != ',')
+        throw std::runtime_error("unsupported Replace regex: " + rx);
+      st.kind = NormStep::REPLACE_RUN;
+      st.run_cp = cps[0];
+      st.run_min = std::stoi(utf8_encode(cps, 2, cps.size() - 2));
+    }
+  } else if (t == "Precompiled") {
+    st.kind = NormStep::PRECOMPILED;
+    const Json* pc = n->get("precompiled_charsmap");
+    const std::string blob = (pc && pc->type == Json::STR) ? base64_decode(pc->str) : std::string();
+    if (blob.size() < 4) return;  // empty charsmap = identity
+    uint32_t tsz = 0;
+    memcpy(&tsz, blob.data(), 4);
+    if (tsz % 4 || 4 + (size_t)tsz > blob.size()) throw std::runtime_error("corrupt precompiled_charsmap");
+    pc_trie_.resize(tsz / 4);
+    memcpy(pc_trie_.data(), blob.data() + 4, tsz);
+    pc_norm_ = blob.substr(4 + tsz);
+  } else {  // NFC / NFKC / NFD / NFKD / ...: identity, loudly
+    std::fprintf(stderr, "ragk tokenizer: normalizer %s not implemented (treated as identity)\n", t.c_str());
+    return;
+  }
+  norm_.push_back(st);
+}
+
+// HF spm_precompiled semantics: darts-clone common-prefix search over the chunk's bytes (stops
+// at NUL); the FIRST (shortest) hit's replacement string replaces the whole chunk.
+bool Tokenizer::pc_transform(const char* p, size_t n, std::string& out) const {
+  if (pc_trie_.empty()) return false;
+  auto offset = [](uint32_t u) { return (u >> 10) << ((u & (1u << 9)) >> 6); };
+  auto label = [](uint32_t u) { return u & ((1u << 31) | 0xFFu); };
+  auto has_leaf = [](uint32_t u) { return ((u >> 8) & 1u) == 1u; };
+  auto value = [](uint32_t u) { return u & ((1u << 31) - 1); };
+  size_t pos = 0;
+  uint32_t unit = pc_trie_[0];
+  pos ^= offset(unit);
+  for (size_t i = 0; i < n; ++i) {
+    const unsigned char c = (unsigned char)p[i];
+    if (c == 0) break;
+    pos ^= c;
+    if (pos >= pc_trie_.size()) return false;
+    unit = pc_trie_[pos];
+    if (label(unit) != c) return false;
+    pos ^= offset(unit);
+    if (pos >= pc_trie_.size()) return false;
+    if (has_leaf(unit)) {
+      const size_t v = value(pc_trie_[pos]);
+      if (v >= pc_norm_.size()) return false;
+      size_t e = v;
+      while (e < pc_norm_.size() && pc_norm_[e] != 0) ++e;
+      out.append(pc_norm_, v, e - v);
+      return true;
+    }
+  }
+  return false;
+}
+
+static bool is_gext(uint32_t c) { return in_ranges(UNI_GEXT, UNI_GEXT_N, c); }
+
+std::string Tokenizer::normalize(const std::string& in) const {
+  std::string s = in;
+  for (const NormStep& st : norm_) {
+    switch (st.kind) {
+      case NormStep::PRECOMPILED: {
+        if (pc_trie_.empty()) break;
+        // walk (approximate) extended grapheme clusters: base + extending marks / ZWJ sequences,
+        // CR LF, regional-indicator pairs
+        std::vector<uint32_t> cps = utf8_decode(s);
+        std::string out;
+        size_t i = 0;
+        while (i < cps.size()) {
+          size_t j = i + 1;
+          if (cps[i] == '\r' && j < cps.size() && cps[j] == '\n') {
+            ++j;
+          } else if (cps[i] >= 0x1F1E6 && cps[i] <= 0x1F1FF && j < cps.size() && cps[j] >= 0x1F1E6 &&
+                     cps[j] <= 0x1F1FF) {
+            ++j;
+          } else {
+            while (j < cps.size()) {
+              if (is_gext(cps[j])) {
+                ++j;
+                if (cps[j - 1] == 0x200D && j < cps.size()) ++j;  // ZWJ joins the next code point
+              } else {
+                break;
+              }
+            }
+          }
+          const std::string g = utf8_encode(cps, i, j);
+          if (!(g.size() < 6 && pc_transform(g.data(), g.size(), out))) {
+            for (size_t k = i; k < j; ++k) {
+              const std::string ch = utf8_encode(cps, k, k + 1);
+              if (!pc_transform(ch.data(), ch.size(), out)) out += ch;
+            }
+          }
+          i = j;
+        }
+        s.swap(out);
+        break;
+      }
+      case NormStep::STRIP: {
+        std::vector<uint32_t> cps = utf8_decode(s);
+        size_t b = 0, e = cps.size();
+        if (st.left) while (b < e && is_WS(cps[b])) ++b;
+        if (st.right) while (e > b && is_WS(cps[e - 1])) --e;
+        s = utf8_encode(cps, b, e);
+        break;
+      }
+      case NormStep::REPLACE: {
+        std::string out;
+        size_t pos = 0;
+        while (true) {
+          const size_t f = s.find(st.pat, pos);
+          if (f == std::string::npos) break;
+          out.append(s, pos, f - pos);
+          out += st.content;
+          pos = f + st.pat.size();
+        }
+        out.append(s, pos, std::string::npos);
+        s.swap(out);
+        break;
+      }
+      case NormStep::REPLACE_RUN: {
+        std::vector<uint32_t> cps = utf8_decode(s);
+        std::string out;
+        size_t i = 0;
+        while (i < cps.size()) {
+          size_t j = i;
+          while (j < cps.size() && cps[j] == st.run_cp) ++j;
+          if (j - i >= (size_t)st.run_min) {
+            out += st.content;
+            i = j;
+          } else if (j > i) {
+            out += utf8_encode(cps, i, j);
+            i = j;
+          } else {
+            out += utf8_encode(cps, i, i + 1);
+            ++i;
+          }
+        }
+        s.swap(out);
+        break;
+      }
+      case NormStep::LOWER: {
+        std::vector<uint32_t> cps = utf8_decode(s);
+        for (uint32_t& c : cps) c = map_lookup(UNI_LOWER, UNI_LOWER_N, c);
+        s = utf8_encode(cps, 0, cps.size());
+        break;
+      }
+      case NormStep::BERT: {
+        std::vector<uint32_t> cps = utf8_decode(s), nc;
+        nc.reserve(cps.size());
+        for (uint32_t c : cps) {
+          if (bn_clean_) {
+            if (c == 0 || c == 0xFFFD || in_ranges(UNI_CTRL, UNI_CTRL_N, c)) continue;
+            if (is_WS(c)) c = ' ';
+          }
+          if (bn_chinese_ && is_cjk(c)) {
+            nc.push_back(' ');
+            nc.push_back(c);
+            nc.push_back(' ');
+            continue;
+          }
+          if (bn_lower_) c = map_lookup(UNI_LOWER, UNI_LOWER_N, c);
+          if (bn_strip_) {
+            if (in_ranges(UNI_MN, UNI_MN_N, c)) continue;
+            c = map_lookup(UNI_STRIP, UNI_STRIP_N, c);
+          }
+          nc.push_back(c);
+        }
+        s = utf8_encode(nc, 0, nc.size());
+        break;
+      }
+    }
+  }
+  return s;
 }
 
 void Tokenizer::load_pre(const Json* p) {
@@ -475,30 +693,7 @@ void Tokenizer::unigram_word(const std::string& word, std::vector<int>& out) con
 }
 
 void Tokenizer::encode_segment(const std::string& seg, std::vector<int>& out) const {
-  std::vector<uint32_t> cps = utf8_decode(seg);
-  if (bert_norm_ || lowercase_) {
-    std::vector<uint32_t> nc;
-    nc.reserve(cps.size());
-    for (uint32_t c : cps) {
-      if (bert_norm_ && bn_clean_) {
-        if (c == 0 || c == 0xFFFD || in_ranges(UNI_CTRL, UNI_CTRL_N, c)) continue;
-        if (is_WS(c)) c = ' ';
-      }
-      if (bert_norm_ && bn_chinese_ && is_cjk(c)) {
-        nc.push_back(' ');
-        nc.push_back(c);
-        nc.push_back(' ');
-        continue;
-      }
-      if ((bert_norm_ && bn_lower_) || lowercase_) c = map_lookup(UNI_LOWER, UNI_LOWER_N, c);
-      if (bert_norm_ && bn_strip_) {
-        if (in_ranges(UNI_MN, UNI_MN_N, c)) continue;
-        c = map_lookup(UNI_STRIP, UNI_STRIP_N, c);
-      }
-      nc.push_back(c);
-    }
-    cps.swap(nc);
-  }
+  std::vector<uint32_t> cps = utf8_decode(norm_.empty() ? seg : normalize(seg));
   std::vector<std::pair<size_t, size_t>> words;
   const size_t n = cps.size();
   if (pre_ == PRE_GPT2 || pre_ == PRE_LLAMA3) {
@@ -526,7 +721,7 @@ void Tokenizer::encode_segment(const std::string& seg, std::vector<int>& out) co
   } else if (pre_ == PRE_METASPACE) {
     const uint32_t meta = utf8_decode(metaspace_)[0];
     std::vector<uint32_t> m;
-    if (meta_prepend_ && (n == 0 || cps[0] != ' ')) m.push_back(meta);
+    if (meta_prepend_ && (n == 0 || (cps[0] != ' ' && cps[0] != meta))) m.push_back(meta);
     for (uint32_t c : cps) m.push_back(c == ' ' ? meta : c);
     cps.swap(m);
     size_t i = 0;

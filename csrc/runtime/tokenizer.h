@@ -2,8 +2,10 @@
 // reference uses through AutoTokenizer / sentence-transformers).
 //   * byte-level BPE  (Llama-3 Split regex + ByteLevel, GPT-2 ByteLevel regex), ignore_merges
 //   * WordPiece       (BertNormalizer + BertPreTokenizer, greedy longest-match-first)
-//   * Unigram         (Metaspace pre-tokenizer, Viterbi; the precompiled-charsmap normalizer
-//                      is treated as identity -- exact for NFKC-clean input)
+//   * Unigram         (Metaspace pre-tokenizer, Viterbi) with the SentencePiece
+//                      Precompiled (charsmap double-array trie) normalizer of XLM-R / bge-m3
+// Normalizers run as an ordered pipeline: Precompiled, Strip, Replace (literal / "c{n,}" runs),
+// Lowercase, BertNormalizer; NFC/NFKC/NFD/NFKD are not implemented (identity + a warning).
 // Added/special tokens are split out before normalisation; TemplateProcessing / Bert /
 // Roberta post-processors; ByteLevel / WordPiece / Metaspace decoders.
 #pragma once
@@ -43,9 +45,18 @@ class Tokenizer {
   std::vector<double> scores_;
   int unk_id_ = 0;
   double min_score_ = 0.0;
-  // normalizer flags
-  bool bert_norm_ = false, bn_clean_ = true, bn_chinese_ = true, bn_lower_ = false, bn_strip_ = false;
-  bool lowercase_ = false;
+  // normalizer pipeline
+  struct NormStep {
+    enum Kind { PRECOMPILED, STRIP, REPLACE, REPLACE_RUN, LOWER, BERT } kind;
+    bool left = false, right = false;  // STRIP
+    std::string pat, content;          // REPLACE (literal); REPLACE_RUN: content
+    uint32_t run_cp = 0;               // REPLACE_RUN: runs of >= run_min run_cp
+    int run_min = 2;
+  };
+  std::vector<NormStep> norm_;
+  bool bn_clean_ = true, bn_chinese_ = true, bn_lower_ = false, bn_strip_ = false;
+  std::vector<uint32_t> pc_trie_;  // Precompiled: darts-clone double array units
+  std::string pc_norm_;            // Precompiled: NUL-separated replacement strings
   // pre-tokenizer
   enum Pre { PRE_NONE, PRE_GPT2, PRE_LLAMA3, PRE_BERT, PRE_WHITESPACE, PRE_METASPACE } pre_ = PRE_NONE;
   bool byte_level_ = false;
@@ -74,6 +85,8 @@ class Tokenizer {
   void load_post(const Json* p);
   void load_decoder(const Json* d);
   void encode_segment(const std::string& seg, std::vector<int>& out) const;
+  std::string normalize(const std::string& s) const;
+  bool pc_transform(const char* p, size_t n, std::string& out) const;
   void bpe_word(const std::string& word, std::vector<int>& out) const;
   void wordpiece_word(const std::vector<uint32_t>& cps, std::vector<int>& out) const;
   void unigram_word(const std::string& word, std::vector<int>& out) const;

@@ -198,3 +198,44 @@ def test_block_manager_native_matches_python(rt):
             assert a.table(s) == b.table(s)
     with pytest.raises(RuntimeError):
         a.ensure(99, 10 ** 6)
+
+
+PC_TEXTS = ["Hello world café naïve Übermaß", "ｆｕｌｌｗｉｄｔｈ ＡＢＣ １２３", "① ② ㈱ ﬁ ﬂ ligature ™ ½",
+            "東京 タワー ｶﾀｶﾅ ｸﾞ", "é ä ñ combining", "multiple   spaces\tand\ttabs  ",
+            "emoji 👍🏽 👨‍👩‍👧 🇯🇵 flags", " nbsp emsp　ideo", "  leading and trailing  ",
+            "Ⅻ ㎏ ㎡ ℃ № …", ""]
+
+
+def test_unigram_precompiled_charsmap_matches_hf(rt, tmp_path):
+    """XLM-R / bge-m3 style: SentencePiece nmt_nfkc charsmap (Precompiled normalizer) + Unigram;
+    oracle = HF tokenizers (Rust) on a tokenizer.json assembled like transformers' SpmConverter."""
+    spm = pytest.importorskip("sentencepiece")
+    from sentencepiece import sentencepiece_model_pb2 as pb
+    from tokenizers import Regex, Tokenizer, decoders, models, normalizers, pre_tokenizers
+
+    from rag_llm_k8s_amd.utils.synthetic import WordModel
+
+    wm = WordModel(n_words=3000, seed=9)
+    lines = wm.corpus_lines(4000) + PC_TEXTS * 30
+    corpus = tmp_path / "c.txt"
+    corpus.write_text("\n".join(lines), encoding="utf-8")
+    spm.SentencePieceTrainer.train(input=str(corpus), model_prefix=str(tmp_path / "m"), vocab_size=1200,
+                                   model_type="unigram", normalization_rule_name="nmt_nfkc",
+                                   character_coverage=1.0, minloglevel=2)
+    proto = pb.ModelProto()
+    proto.ParseFromString((tmp_path / "m.model").read_bytes())
+    charsmap = proto.normalizer_spec.precompiled_charsmap
+    assert len(charsmap) > 1000
+    vocab = [(p.piece, p.score) for p in proto.pieces]
+    for seq in ([normalizers.Precompiled(charsmap), normalizers.Replace(Regex(" {2,}"), " ")],
+                [normalizers.Precompiled(charsmap), normalizers.Strip(left=False, right=True),
+                 normalizers.Replace(Regex(" {2,}"), "▁")]):
+        tok = Tokenizer(models.Unigram(vocab, unk_id=proto.trainer_spec.unk_id))
+        tok.normalizer = normalizers.Sequence(seq)
+        tok.pre_tokenizer = pre_tokenizers.Metaspace()
+        tok.decoder = decoders.Metaspace()
+        p = str(tmp_path / "tokenizer.json")
+        tok.save(p)
+        n = rt.Tokenizer(p)
+        for t in PC_TEXTS + [wm.text(60) for _ in range(5)]:
+            assert n.encode(t, False) == tok.encode(t, add_special_tokens=False).ids, t

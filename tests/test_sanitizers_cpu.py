@@ -42,6 +42,7 @@ def run(exe, *args):
 
 
 TEXTS = ["Hello world! The quick brown fox's 42 jumps.", "  leading spaces and\ttabs", "I'M YOU'RE 1234567",
+         "ｆｕｌｌｗｉｄｔｈ ① ㈱ ﬁ ｶﾀｶﾅ 👨‍👩‍👧 🇯🇵",
          "unicode: café naïve Übermaß 東京 😀🚀", "", "a" * 300, "newline-free line with trailing space "]
 
 
@@ -71,6 +72,25 @@ def tokenizers_(tmp_path_factory):
     uni.train_from_iterator(lines, trainers.UnigramTrainer(vocab_size=1500, show_progress=False, unk_token="<unk>",
                                                            special_tokens=["<unk>"]))
     out["unigram"] = uni
+    try:  # XLM-R style Precompiled (SentencePiece nmt_nfkc charsmap) normalizer: trie walks under ASan
+        import sentencepiece as spm
+        from sentencepiece import sentencepiece_model_pb2 as pb
+        from tokenizers import normalizers
+
+        (d / "c.txt").write_text("\n".join(lines), encoding="utf-8")
+        spm.SentencePieceTrainer.train(input=str(d / "c.txt"), model_prefix=str(d / "m"), vocab_size=800,
+                                       model_type="unigram", normalization_rule_name="nmt_nfkc",
+                                       character_coverage=1.0, minloglevel=2)
+        proto = pb.ModelProto()
+        proto.ParseFromString((d / "m.model").read_bytes())
+        pc = Tokenizer(models.Unigram([(p.piece, p.score) for p in proto.pieces], unk_id=proto.trainer_spec.unk_id))
+        pc.normalizer = normalizers.Sequence([normalizers.Precompiled(proto.normalizer_spec.precompiled_charsmap),
+                                              normalizers.Replace(Regex(" {2,}"), " ")])
+        pc.pre_tokenizer = pre_tokenizers.Metaspace()
+        pc.decoder = decoders.Metaspace()
+        out["precompiled"] = pc
+    except ImportError:
+        pass
     paths = {}
     for k, t in out.items():
         p = str(d / ("%s.json" % k))
