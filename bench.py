@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--context-k", type=int, default=4)
     ap.add_argument("--max-new-tokens", type=int, default=150)
     ap.add_argument("--index", default="flat", choices=["flat", "ivf"])
+    ap.add_argument("--index-vectors", type=int, default=0,
+                    help="pad the index to this many vectors (config 4: 1000000) after the embedded corpus")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="linear-layer weights: bf16 (headline) or fp8 e4m3 (BASELINE config 5)")
@@ -81,7 +83,7 @@ def main():
     wl = build_workload(model=a.model, embedder=a.embedder, n_chunks=a.chunks, retrieve_k=a.retrieve_k,
                         context_k=a.context_k, max_new_tokens=a.max_new_tokens, max_batch=a.concurrency,
                         device=dev, ctx=ctx, tp_comm=comm, seed=0, use_graphs=not a.no_graphs, index_type=a.index,
-                        dtype=a.dtype)
+                        dtype=a.dtype, index_vectors=a.index_vectors)
     svc = wl.svc
     svc.engine.warmup_graphs()
     params = SamplingParams(max_new_tokens=a.max_new_tokens, temperature=0.7, top_p=0.9, top_k=50, do_sample=True,
@@ -143,7 +145,8 @@ def main():
                 "model": {"8b": "Llama-3.1-8B-Instruct", "70b": "Llama-3.1-70B-Instruct", "tiny": "llama-tiny"}[a.model],
                 "embedder": {"minilm": "all-MiniLM-L6-v2", "bge-large": "bge-large-en-v1.5", "bge-m3": "bge-m3",
                              "tiny": "tiny"}[a.embedder],
-                "index": "%s %d chunks (HBM-resident)" % ("FlatL2" if a.index == "flat" else "IVF-Flat", a.chunks),
+                "index": "%s %d vectors (HBM-resident; %d embedded chunks)" % (
+                    "FlatL2" if a.index == "flat" else "IVF-Flat", max(a.chunks, a.index_vectors), a.chunks),
                 "retrieve_k": a.retrieve_k, "context_k": a.context_k,
                 "global_batch": a.concurrency * ctx.dp,
                 "seq_len": int(round(sum(P) / max(1, len(P)))),

@@ -95,7 +95,7 @@ class Workload:
 def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=1000, retrieve_k=4, context_k=4,
                    max_new_tokens=150, max_batch=32, max_model_len=8192, max_prefill_tokens=32768, device="cuda",
                    ctx=None, tp_comm=None, seed=0, use_graphs=True, index_type="flat", kv_blocks=None,
-                   word_vocab=400000, dtype="bf16"):
+                   word_vocab=400000, dtype="bf16", index_vectors=0):
     from ..engine.encoder_engine import EmbeddingEngine
     from ..engine.llm_engine import LLMEngine
     from ..index.store import DocumentStore
@@ -146,6 +146,18 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     meta = [{"filename": "synthetic_%05d.pdf" % (i // 20), "chunk_id": i % 20, "text": c}
             for i, c in enumerate(chunks)]
     store.add(vecs, meta, dedupe=False, persist=False)
+    # BASELINE config 4 scale (1M-chunk index): pad the index with random unit vectors after the
+    # embedded corpus (embedding 1M x 1000-word chunks is hours of encoder time; search cost depends
+    # only on the index size). Padding rows carry empty text.
+    g = torch.Generator(device=device).manual_seed(seed + 7)
+    done = len(meta)
+    while done < index_vectors:
+        nb = min(131072, index_vectors - done)
+        pad = torch.randn(nb, emb.dim, device=device, generator=g)
+        pad = torch.nn.functional.normalize(pad, dim=1).cpu().numpy()
+        store.add(pad, [{"filename": "synthetic_pad", "chunk_id": done + i, "text": ""} for i in range(nb)],
+                  dedupe=False, persist=False)
+        done += nb
     if device.startswith("cuda"):
         torch.cuda.synchronize()
     t["ingest_s"] = time.time() - t0
