@@ -28,6 +28,19 @@ using namespace ragk;
 namespace {
 
 constexpr int KT = 64;  // keys per tile == KV-cache page size
+constexpr float RESCALE_LOG2 = 8.f;  // deferred-rescale threshold (log2 units)
+
+// max with the xor-16 / xor-32 lane partner without an LDS round trip (gfx950
+// v_permlane{16,32}_swap). With both operands = v the swap returns, per lane, {v, partner} in
+// some order, so max(r0, r1) is the pairwise max on every lane.
+__device__ __forceinline__ float max_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max_xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
 
 template <int D>
 struct Cfg {
@@ -208,7 +221,12 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
         }
       }
       // ---- online softmax (per query column, lane-local + xor 16/32) ----
+      // Max on the raw scores (scale > 0 keeps the order); the log2 scale is folded into one FMA
+      // per element. Deferred rescale: the reference max m_i only moves when the tile max exceeds
+      // it by more than RESCALE_LOG2 (p stays <= 2^RESCALE_LOG2, exact in fp32 / bf16 P), so the
+      // O *= alpha pass (DT*2*4 multiplies per lane) runs on a few early tiles instead of every tile.
       const bool need_mask = CAUSAL ? (k0 + KT - 1 > ctx0 + pbase) || (k0 + KT > kv_len) : (k0 + KT > kv_len);
+      const float c = a.scale_log2;
       float alpha[2];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
@@ -218,36 +236,41 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float x = s[t][qt][r] * a.scale_log2;
+            float x = s[t][qt][r];
             if (need_mask) {
               const int kj = k0 + 16 * t + 4 * fh + r;
               const bool ok = kj < kv_len && (!CAUSAL || kj <= qpos);
               x = ok ? x : -INFINITY;
+              s[t][qt][r] = x;
             }
-            s[t][qt][r] = x;
             mx = fmaxf(mx, x);
           }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float m_new = fmaxf(m_i[qt], mx);
-        const float m_use = m_new == -INFINITY ? 0.f : m_new;
-        alpha[qt] = exp2f(m_i[qt] - m_use);
+        mx = max_xor16(mx);
+        mx = max_xor32(mx);
+        const float mxs = mx * c;
+        alpha[qt] = 1.f;
+        if (mxs > m_i[qt] + RESCALE_LOG2) {
+          alpha[qt] = m_i[qt] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_i[qt] - mxs);
+          m_i[qt] = mxs;
+        }
+        const float mref = m_i[qt] == -INFINITY ? 0.f : m_i[qt];
         float ls = 0.f;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float p = exp2f(s[t][qt][r] - m_use);
+            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[t][qt][r], c, -mref));
             s[t][qt][r] = p;
             ls += p;
           }
         l_i[qt] = l_i[qt] * alpha[qt] + ls;
-        m_i[qt] = m_new;
       }
+      if (__builtin_amdgcn_ballot_w64(alpha[0] != 1.f || alpha[1] != 1.f)) {
 #pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt)
+        for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) o[dt][qt] *= alpha[qt];
+          for (int qt = 0; qt < 2; ++qt) o[dt][qt] *= alpha[qt];
+      }
       // ---- O^T += V^T P^T ----
       bf16x8 pb[2][2];
 #pragma unroll

@@ -328,6 +328,7 @@ def attn_prefill(q, k, v, cu_q, kv_lens, tiles, out, Hq, Hkv, D, causal=True, pa
     if paged:
         _req(k.dim() == 4 and k.shape[2] == 64 and k.shape[1] == Hkv and k.shape[3] == D, "paged cache [nb,Hkv,64,D]")
         _req(block_tables is not None and block_tables.dtype == torch.int32, "block_tables int32")
+        _req(block_tables.stride(0) <= 2048, "prefill block tables wider than 2048 blocks (128k tokens)")
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     n_tiles = tiles.shape[0]
     check(_lib.lib().ragk_attn_prefill(
