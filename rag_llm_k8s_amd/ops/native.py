@@ -27,6 +27,14 @@ def _bf16_2d(t, name):
 
 # ----------------------------------------------------------------------------- GEMM
 PP_MIN_M = int(__import__("os").environ.get("RAGK_PP_MIN_M", "1024"))
+PP_VARIANT = int(__import__("os").environ.get("RAGK_PP_VARIANT", "2"))
+_pp_variant_set = [None]
+
+
+def set_pp_variant(v):
+    """2: two 64-deep K buffers; 4: four 32-deep buffers, 3-tile-deep DMA (gemm_pp.hip)."""
+    check(_lib.lib().ragk_gemm_pp_set_variant(int(v)), "ragk_gemm_pp_set_variant")
+    _pp_variant_set[0] = int(v)
 
 
 DEC_DEFAULT = __import__("os").environ.get("RAGK_DEC_GEMM", "1") == "1"
@@ -117,6 +125,8 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
                              ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), S, ws.data_ptr(), cnt.data_ptr(),
                              stream_ptr())
     elif path == 2:
+        if _pp_variant_set[0] is None:
+            set_pp_variant(PP_VARIANT)
         rc = L.ragk_gemm_pp(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
                             ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), stream_ptr())
     elif path is None:

@@ -27,8 +27,17 @@ def test_gemm_plain(native, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 256, 128), (300, 1024, 768), (1111, 6144, 4096), (256, 256, 128),
-                                   (2049, 512, 1024), (513, 4104, 256)])
-def test_gemm_pingpong(native, M, N, K):
+                                   (2049, 512, 1024), (513, 4104, 256), (260, 768, 384)])
+@pytest.mark.parametrize("variant", [2, 4])
+def test_gemm_pingpong(native, M, N, K, variant):
+    native.set_pp_variant(variant)
+    try:
+        _check_pingpong(native, M, N, K)
+    finally:
+        native.set_pp_variant(native.PP_VARIANT)
+
+
+def _check_pingpong(native, M, N, K):
     torch.manual_seed(20)
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
