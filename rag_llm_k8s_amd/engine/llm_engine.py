@@ -20,6 +20,7 @@ Here:
 from __future__ import annotations
 
 import itertools
+import os
 import logging
 import threading
 import time
@@ -99,6 +100,8 @@ class LLMEngine:
         self.tp_group = tp_group
         self.tp_size = 1 if tp_group is None else torch.distributed.get_world_size(tp_group)
         self.K = top_k_cap
+        # TP prefill steps of at least this many tokens run as 2 micro-batches with async all-reduces
+        self.tp_overlap_min_tokens = int(os.environ.get("RAGK_TP_OVERLAP_MIN", "1024"))
         self.is_cuda = self.device.type == "cuda"
         self.use_graphs = use_graphs and self.is_cuda
         self.buckets = sorted(set(graph_buckets or [b for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
@@ -313,8 +316,8 @@ class LLMEngine:
             gi.permute(1, 0, 2).reshape(B, self.tp_size * K).contiguous()
 
     # ------------------------------------------------------------------ prefill
-    def _prefill(self, chunks):
-        t0 = time.perf_counter()
+    def _prefill_input(self, chunks):
+        """Packed StepInput for prefill chunks [(seq, start, n)] + the sequences whose prompt ends here."""
         ids, pos, slots, cu, kvl, bts, qlens, out_rows, out_seqs = [], [], [], [0], [], [], [], [], []
         for s, start, n in chunks:
             table = self.bm.table(s.id)
@@ -337,13 +340,51 @@ class LLMEngine:
         meta = AttnMeta("prefill", self._h2d_i32(kvl), self._h2d_i32(bts).reshape(len(chunks), self.max_blocks),
                         cu_q=self._h2d_i32(cu), tiles=tiles.to(self.device), host_kv_lens=kvl, host_q_lens=qlens)
         inp = StepInput(self._h2d_i32(ids), self._h2d_i32(pos), self._h2d_i32(slots), meta,
-                        self._h2d_i32(out_rows) if out_rows else None)
+                        self._h2d_i32(out_rows) if out_rows else self._h2d_i32([len(ids) - 1]))
+        return inp, out_seqs, len(ids)
+
+    @staticmethod
+    def _split_chunks(chunks, parts):
+        """Cut the packed token stream into `parts` nearly equal consecutive pieces (a chunk may be
+        cut in two: its second piece continues the same sequence at a later position)."""
+        total = sum(n for _, _, n in chunks)
+        target = -(-total // parts)
+        out, cur, room = [], [], target
+        for s, start, n in chunks:
+            while n > 0:
+                k = min(n, room)
+                cur.append((s, start, k))
+                start, n, room = start + k, n - k, room - k
+                if room == 0 and len(out) < parts - 1:
+                    out.append(cur)
+                    cur, room = [], target
+        if cur:
+            out.append(cur)
+        return out
+
+    def _prefill(self, chunks):
+        t0 = time.perf_counter()
+        m = self.model
+        ntok = sum(n for _, _, n in chunks)
+        comm = getattr(m, "comm", None)
+        overlap = (self.tp_size > 1 and comm is not None and hasattr(comm, "all_reduce_async")
+                   and ntok >= self.tp_overlap_min_tokens)
+        if overlap:
+            groups = self._split_chunks(chunks, 2)
+            built = [self._prefill_input(g) for g in groups]
+            hs = m.hidden_states_microbatched([b[0] for b in built])
+            out_seqs = [s for b in built for s in b[1]]
+            parts = [m.logits(h) for h, b in zip(hs, built) if b[1]]
+            logits = torch.cat(parts, 0) if parts else None
+        else:
+            inp, out_seqs, _ = self._prefill_input(chunks)
+            logits = m.forward(inp) if out_seqs else None
+            if logits is None:
+                m.hidden_states(inp)
         finished = []
-        if out_rows:
-            logits = m.forward(inp)
+        if out_seqs:
             tok = self._sample_rows(logits, *self._sampling_tensors(out_seqs)).cpu().tolist()
         else:
-            m.hidden_states(StepInput(inp.ids, inp.positions, inp.slots, meta, self._h2d_i32([0])))
             tok = []
             if self.is_cuda:
                 torch.cuda.current_stream(self.device).synchronize()
@@ -355,7 +396,7 @@ class LLMEngine:
                 self._finish(s, r)
                 finished.append(s)
         self.stats["prefill_steps"] += 1
-        self.stats["prefill_tokens"] += len(ids)
+        self.stats["prefill_tokens"] += ntok
         self.stats["prefill_s"] += time.perf_counter() - t0
         return finished
 

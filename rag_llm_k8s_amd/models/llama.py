@@ -251,38 +251,76 @@ class LlamaModel:
         if self.comm is not None:
             self.comm.all_reduce(x)
 
+    # one decoder layer in two halves, so tensor-parallel prefill can interleave micro-batches
+    def _attn_block(self, li, L, h, inp: StepInput, attn):
+        """h <- (rank 0: h +) o_proj(attention(rmsnorm(h))): this rank's partial sum before the all-reduce."""
+        be, c = self.be, self.cfg
+        Hq, Hkv, D = self.Hq, self.Hkv, self.D
+        kc, vc = self.kv_cache[li]
+        xn = be.rmsnorm(h, L["ln_in"], c.rms_norm_eps)
+        qkv = be.gemm(xn, L["wqkv"])
+        be.rope_kv(qkv, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
+        if inp.meta.kind == "decode":
+            be.attn_decode(qkv, kc, vc, inp.meta, attn, Hq, Hkv, D)
+        else:
+            be.attn_prefill(qkv, kc, vc, inp.meta, attn, Hq, Hkv, D)
+        if self.tp_rank == 0:
+            be.gemm(attn, L["wo"], resid=h, epi="resid", out=h)
+        else:
+            be.gemm(attn, L["wo"], out=h)
+
+    def _mlp_block(self, L, h):
+        be, c = self.be, self.cfg
+        xn = be.rmsnorm(h, L["ln_post"], c.rms_norm_eps)
+        a = be.gemm(xn, L["wgu"], epi="silu_mul")
+        if self.tp_rank == 0:
+            be.gemm(a, L["wdown"], resid=h, epi="resid", out=h)
+        else:
+            be.gemm(a, L["wdown"], out=h)
+
+    def _final(self, h, inp: StepInput):
+        if inp.logits_idx is not None:
+            h = self.be.gather_rows(h, inp.logits_idx)
+        return self.be.rmsnorm(h, self.w.norm, self.cfg.rms_norm_eps)
+
     def hidden_states(self, inp: StepInput):
         """Run the decoder stack; returns the final-norm'ed rows selected by logits_idx."""
-        be, w, c = self.be, self.w, self.cfg
-        Hq, Hkv, D = self.Hq, self.Hkv, self.D
-        first = self.tp_rank == 0
+        be, w = self.be, self.w
         h = be.embed(inp.ids, w.embed)
-        T = h.shape[0]
-        attn = torch.empty((T, Hq * D), dtype=h.dtype, device=h.device)
+        attn = torch.empty((h.shape[0], self.Hq * self.D), dtype=h.dtype, device=h.device)
         for li, L in enumerate(w.layers):
-            kc, vc = self.kv_cache[li]
-            xn = be.rmsnorm(h, L["ln_in"], c.rms_norm_eps)
-            qkv = be.gemm(xn, L["wqkv"])
-            be.rope_kv(qkv, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
-            if inp.meta.kind == "decode":
-                be.attn_decode(qkv, kc, vc, inp.meta, attn, Hq, Hkv, D)
-            else:
-                be.attn_prefill(qkv, kc, vc, inp.meta, attn, Hq, Hkv, D)
-            if first:
-                be.gemm(attn, L["wo"], resid=h, epi="resid", out=h)
-            else:
-                be.gemm(attn, L["wo"], out=h)
+            self._attn_block(li, L, h, inp, attn)
             self._allreduce(h)
-            xn = be.rmsnorm(h, L["ln_post"], c.rms_norm_eps)
-            a = be.gemm(xn, L["wgu"], epi="silu_mul")
-            if first:
-                be.gemm(a, L["wdown"], resid=h, epi="resid", out=h)
-            else:
-                be.gemm(a, L["wdown"], out=h)
+            self._mlp_block(L, h)
             self._allreduce(h)
-        if inp.logits_idx is not None:
-            h = be.gather_rows(h, inp.logits_idx)
-        return be.rmsnorm(h, w.norm, c.rms_norm_eps)
+        return self._final(h, inp)
+
+    def hidden_states_microbatched(self, inps):
+        """Tensor-parallel prefill with communication/compute overlap: the token
+        batch is split into micro-batches (consecutive pieces of the packed prompt chunks; a later
+        micro-batch's queries read the earlier one's K/V from the paged cache, which this layer has
+        already written). Every all-reduce is issued asynchronously (RCCL stream / the peer-mapped
+        kernel on a side stream) and waited on only when its micro-batch needs the result, so the
+        all-reduce of micro-batch m overlaps the GEMMs and attention of micro-batch m+1:
+            attn(A) | AR(A) ~ attn(B) | AR(B) ~ mlp(A) | AR(A) ~ mlp(B) | AR(B) ~ attn(A, next layer)
+        Returns one hidden-state tensor per micro-batch."""
+        be, w = self.be, self.w
+        hs = [be.embed(i.ids, w.embed) for i in inps]
+        attn = [torch.empty((h.shape[0], self.Hq * self.D), dtype=h.dtype, device=h.device) for h in hs]
+        pend = [None] * len(hs)
+        for li, L in enumerate(w.layers):
+            for m, inp in enumerate(inps):
+                if pend[m] is not None:
+                    pend[m].wait()
+                self._attn_block(li, L, hs[m], inp, attn[m])
+                pend[m] = self.comm.all_reduce_async(hs[m])
+            for m in range(len(inps)):
+                pend[m].wait()
+                self._mlp_block(L, hs[m])
+                pend[m] = self.comm.all_reduce_async(hs[m])
+        for p in pend:
+            p.wait()
+        return [self._final(h, inp) for h, inp in zip(hs, inps)]
 
     def logits(self, hs):
         """Rank-local vocab-shard logits (fp32)."""

@@ -24,6 +24,7 @@ class TPComm:
         self.group, self.size, self.rank, self.device = group, size, rank, device
         self.cpu_group = cpu_group
         self.ipc = None
+        self._side = None  # side stream for asynchronous peer-mapped all-reduces
         want = os.environ.get("RAGK_IPC_ALLREDUCE", "1") == "1"
         if want and size > 1 and str(device).startswith("cuda") and cpu_group is not None:
             import logging
@@ -57,6 +58,50 @@ class TPComm:
         dist.all_reduce(x, group=self.group)
         return x
 
+    def all_reduce_async(self, x: torch.Tensor):
+        """Start an in-place all-reduce of x; returns a handle whose wait() makes the CURRENT stream
+        (GPU) or the host (gloo) wait for it. x must not be touched until then."""
+        if self.size == 1:
+            return _Done()
+        if self.ipc is not None and self.ipc.fits(x):
+            cur = torch.cuda.current_stream(x.device)
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=x.device)
+            self._side.wait_stream(cur)
+            with torch.cuda.stream(self._side):
+                self.ipc.all_reduce(x)
+                ev = torch.cuda.Event()
+                ev.record(self._side)
+            x.record_stream(self._side)
+            return _StreamWait(ev, x.device)
+        if not x.is_cuda and x.dtype == torch.bfloat16:  # gloo: fp32 sum, rounded once (as all_reduce)
+            y = x.float()
+            work = dist.all_reduce(y, group=self.group, async_op=True)
+            return _CopyBack(work, y, x)
+        return dist.all_reduce(x, group=self.group, async_op=True)
+
     def all_gather_into(self, out: torch.Tensor, x: torch.Tensor):
         dist.all_gather_into_tensor(out, x, group=self.group)
         return out
+
+
+class _Done:
+    def wait(self):
+        return None
+
+
+class _StreamWait:
+    def __init__(self, ev, device):
+        self.ev, self.device = ev, device
+
+    def wait(self):
+        torch.cuda.current_stream(self.device).wait_event(self.ev)
+
+
+class _CopyBack:
+    def __init__(self, work, y, x):
+        self.work, self.y, self.x = work, y, x
+
+    def wait(self):
+        self.work.wait()
+        self.x.copy_(self.y)

@@ -126,6 +126,43 @@ def test_tp_control_broadcast_keeps_ranks_in_lockstep():
     assert [len(o) for o in out[0]] == [5, 5, 5]
 
 
+def _tp_overlap_worker(ctx, sd, prompts):
+    """TP=2 engine: prefill as 2 micro-batches with async all-reduces vs the synchronous path."""
+    from rag_llm_k8s_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights
+    from rag_llm_k8s_amd.parallel.comm import TPComm
+
+    outs = {}
+    for thr in (10 ** 9, 8):  # never / always micro-batch (8 tokens min)
+        w = LlamaWeights.from_state_dict(CFG, sd, "cpu", ctx.tp_rank, ctx.tp)
+        m = LlamaModel(CFG, w, "cpu", comm=TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, "cpu"), max_positions=512)
+        eng = LLMEngine(m, num_blocks=32, max_batch=4, max_prefill_tokens=96, max_model_len=512, use_graphs=False,
+                        tp_group=ctx.tp_group)
+        eng.tp_overlap_min_tokens = thr
+        p = SamplingParams(max_new_tokens=4, do_sample=False, ignore_eos=True)
+        outs[thr] = eng.generate(prompts, p)
+    return outs
+
+
+def test_tp_prefill_microbatch_overlap_matches_sync():
+    sd = llama_state_dict(CFG, seed=6, std=0.05)
+    # 3 prompts, 96-token prefill budget: chunks get cut across micro-batches and steps
+    prompts = [list(range(3, 73)), list(range(100, 141)), [7, 8, 9, 10, 11]]
+    out = _run(_tp_overlap_worker, 2, sd, prompts)
+    for r in range(WORLD):
+        assert out[r][8] == out[r][10 ** 9], out[r]
+    assert out[0] == out[1]
+
+
+def test_split_chunks_cuts_token_stream_evenly():
+    from rag_llm_k8s_amd.engine.llm_engine import LLMEngine
+
+    a, b, c = object(), object(), object()
+    parts = LLMEngine._split_chunks([(a, 0, 70), (b, 10, 41), (c, 0, 5)], 2)
+    assert [sum(n for _, _, n in g) for g in parts] == [58, 58]
+    assert parts[0] == [(a, 0, 58)] and parts[1] == [(a, 58, 12), (b, 10, 41), (c, 0, 5)]
+
+
 def _dp_worker(ctx, texts):
     from rag_llm_k8s_amd.engine.encoder_engine import EmbeddingEngine
     from rag_llm_k8s_amd.models import encoder as E
