@@ -319,13 +319,16 @@ def prefill_qtile(Hq, Hkv):
 
 def build_prefill_tiles(q_lens, Hq, Hkv):
     """(seq, q_start) work list, heaviest (latest query positions) first."""
+    import numpy as np
+
     qt = prefill_qtile(Hq, Hkv)
-    tiles = []
-    for s, ql in enumerate(q_lens):
-        for q0 in range(0, int(ql), qt):
-            tiles.append((s, q0))
-    tiles.sort(key=lambda t: -t[1])
-    return torch.tensor(tiles, dtype=torch.int32).reshape(-1, 2)
+    ql = np.asarray(q_lens, dtype=np.int64)
+    nt = (ql + qt - 1) // qt
+    seq = np.repeat(np.arange(len(ql)), nt)
+    first = np.repeat(np.cumsum(nt) - nt, nt)
+    q0 = (np.arange(int(nt.sum())) - first) * qt
+    order = np.argsort(-q0, kind="stable")
+    return torch.from_numpy(np.stack([seq[order], q0[order]], 1).astype(np.int32)).reshape(-1, 2)
 
 
 def attn_prefill(q, k, v, cu_q, kv_lens, tiles, out, Hq, Hkv, D, causal=True, paged=True, block_tables=None,
