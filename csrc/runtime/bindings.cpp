@@ -97,6 +97,16 @@ PYBIND11_MODULE(_ragk_rt, m) {
              return ids;
            },
            py::arg("text"), py::arg("add_special_tokens") = true)
+      .def("encode_batch",
+           [](const Tokenizer& t, const std::vector<std::string>& texts, bool add_special, int threads) {
+             std::vector<std::vector<int>> ids;
+             {
+               py::gil_scoped_release nogil;
+               ids = t.encode_batch(texts, add_special, threads);
+             }
+             return ids;
+           },
+           py::arg("texts"), py::arg("add_special_tokens") = true, py::arg("threads") = 8)
       .def("decode", &Tokenizer::decode, py::arg("ids"), py::arg("skip_special_tokens") = true)
       .def("vocab_size", &Tokenizer::vocab_size)
       .def("token_to_id",

@@ -1,6 +1,12 @@
 #include "tokenizer.h"
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <exception>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -169,7 +175,12 @@ std::string utf8_encode(const std::vector<uint32_t>& cps, size_t b, size_t e) {
   return s;
 }
 
-Tokenizer::Tokenizer(const std::string& path) {
+static unsigned long long g_tok_uid_next() {
+  static std::atomic<unsigned long long> c{1};
+  return c++;
+}
+
+Tokenizer::Tokenizer(const std::string& path) : uid_(g_tok_uid_next()) {
   std::ifstream f(path, std::ios::binary);
   if (!f) throw std::runtime_error("cannot open " + path);
   std::stringstream ss;
@@ -573,11 +584,20 @@ int Tokenizer::token_to_id(const std::string& t) const {
   return it == vocab_.end() ? -1 : it->second;
 }
 
-void Tokenizer::bpe_word(const std::string& word, std::vector<int>& out) const {
-  auto c = cache_.find(word);
-  if (c != cache_.end()) {
-    out.insert(out.end(), c->second.begin(), c->second.end());
-    return;
+void Tokenizer::bpe_word(const std::string& word, std::vector<int>& out, WordCache* local) const {
+  if (local) {  // encode_batch worker: private cache, no locking
+    auto c = local->find(word);
+    if (c != local->end()) {
+      out.insert(out.end(), c->second.begin(), c->second.end());
+      return;
+    }
+  } else {  // shared word cache: encode() runs without the GIL from several server threads
+    std::shared_lock<std::shared_mutex> rd(cache_mu_);
+    auto c = cache_.find(word);
+    if (c != cache_.end()) {
+      out.insert(out.end(), c->second.begin(), c->second.end());
+      return;
+    }
   }
   std::vector<int> ids;
   auto whole = vocab_.find(word);
@@ -615,8 +635,108 @@ void Tokenizer::bpe_word(const std::string& word, std::vector<int>& out) const {
       ids.erase(ids.begin() + bi + 1);
     }
   }
-  if (cache_.size() < 200000) cache_.emplace(word, ids);
+  if (local) {
+    if (local->size() < 200000) local->emplace(word, ids);
+  } else {
+    std::unique_lock<std::shared_mutex> wr(cache_mu_);
+    if (cache_.size() < 200000) cache_.emplace(word, ids);
+  }
   out.insert(out.end(), ids.begin(), ids.end());
+}
+
+namespace {
+
+// Process-wide worker pool for encode_batch. Workers live for the process, so their per-thread
+// BPE word caches (keyed by tokenizer uid) stay warm across calls.
+class EncodePool {
+ public:
+  static EncodePool& get() {
+    static EncodePool p;
+    return p;
+  }
+  int size() const { return (int)threads_.size(); }
+  // run fn(worker_index) on `n` workers and wait
+  void run(int n, const std::function<void(int)>& fn) {
+    std::unique_lock<std::mutex> lk(mu_);
+    job_ = &fn;
+    want_ = std::min(n, size());
+    started_ = 0;
+    done_ = 0;
+    ++gen_;
+    cv_.notify_all();
+    done_cv_.wait(lk, [&] { return done_ == want_; });
+    job_ = nullptr;
+  }
+
+ private:
+  EncodePool() {
+    const int n = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+    for (int i = 0; i < n; ++i) threads_.emplace_back([this] { loop(); });
+  }
+  ~EncodePool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      cv_.notify_all();
+    }
+    for (auto& t : threads_) t.join();
+  }
+  void loop() {
+    unsigned long long seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    while (true) {
+      cv_.wait(lk, [&] { return stop_ || (gen_ != seen && started_ < want_); });
+      if (stop_) return;
+      if (started_ >= want_) {
+        seen = gen_;
+        continue;
+      }
+      const int idx = started_++;
+      seen = gen_;
+      const std::function<void(int)>* fn = job_;
+      lk.unlock();
+      (*fn)(idx);
+      lk.lock();
+      if (++done_ == want_) done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* job_ = nullptr;
+  int want_ = 0, started_ = 0, done_ = 0;
+  unsigned long long gen_ = 0;
+  bool stop_ = false;
+};
+
+}  // namespace
+
+std::vector<std::vector<int>> Tokenizer::encode_batch(const std::vector<std::string>& texts, bool add_special,
+                                                      int threads) const {
+  std::vector<std::vector<int>> out(texts.size());
+  const int n = (int)texts.size();
+  EncodePool& pool = EncodePool::get();
+  const int nt = std::max(1, std::min({threads, n, pool.size()}));
+  if (nt == 1) {
+    for (int i = 0; i < n; ++i) out[i] = encode(texts[i], add_special);
+    return out;
+  }
+  std::atomic<int> next{0};
+  std::exception_ptr err = nullptr;
+  std::mutex err_mu;
+  const unsigned long long uid = uid_;
+  pool.run(nt, [&](int) {
+    thread_local std::unordered_map<unsigned long long, WordCache> caches;
+    WordCache& local = caches[uid];
+    try {
+      for (int i = next++; i < n; i = next++) out[i] = encode_impl(texts[i], add_special, &local);
+    } catch (...) {
+      std::lock_guard<std::mutex> g(err_mu);
+      if (!err) err = std::current_exception();
+    }
+  });
+  if (err) std::rethrow_exception(err);
+  return out;
 }
 
 void Tokenizer::wordpiece_word(const std::vector<uint32_t>& cps, std::vector<int>& out) const {
@@ -692,7 +812,7 @@ void Tokenizer::unigram_word(const std::string& word, std::vector<int>& out) con
   }
 }
 
-void Tokenizer::encode_segment(const std::string& seg, std::vector<int>& out) const {
+void Tokenizer::encode_segment(const std::string& seg, std::vector<int>& out, WordCache* local) const {
   std::vector<uint32_t> cps = utf8_decode(norm_.empty() ? seg : normalize(seg));
   std::vector<std::pair<size_t, size_t>> words;
   const size_t n = cps.size();
@@ -743,7 +863,7 @@ void Tokenizer::encode_segment(const std::string& seg, std::vector<int>& out) co
         for (unsigned char b : piece) mapped += byte_to_uni_[b];
         piece.swap(mapped);
       }
-      bpe_word(piece, out);
+      bpe_word(piece, out, local);
     } else if (model_ == WORDPIECE) {
       wordpiece_word(std::vector<uint32_t>(cps.begin() + w.first, cps.begin() + w.second), out);
     } else {
@@ -753,6 +873,10 @@ void Tokenizer::encode_segment(const std::string& seg, std::vector<int>& out) co
 }
 
 std::vector<int> Tokenizer::encode(const std::string& text, bool add_special_tokens) const {
+  return encode_impl(text, add_special_tokens, nullptr);
+}
+
+std::vector<int> Tokenizer::encode_impl(const std::string& text, bool add_special_tokens, WordCache* local) const {
   std::vector<int> body;
   size_t seg_start = 0, i = 0;
   const size_t n = text.size();
@@ -761,7 +885,7 @@ std::vector<int> Tokenizer::encode(const std::string& text, bool add_special_tok
       bool hit = false;
       for (auto& a : added_) {
         if (!a.content.empty() && text.compare(i, a.content.size(), a.content) == 0) {
-          if (i > seg_start) encode_segment(text.substr(seg_start, i - seg_start), body);
+          if (i > seg_start) encode_segment(text.substr(seg_start, i - seg_start), body, local);
           body.push_back(a.id);
           i += a.content.size();
           seg_start = i;
@@ -773,7 +897,7 @@ std::vector<int> Tokenizer::encode(const std::string& text, bool add_special_tok
     }
     ++i;
   }
-  if (seg_start < n) encode_segment(text.substr(seg_start), body);
+  if (seg_start < n) encode_segment(text.substr(seg_start), body, local);
   if (!add_special_tokens || !has_template_) return body;
   std::vector<int> out;
   for (int t : template_single_) {

@@ -10,6 +10,7 @@
 // Roberta post-processors; ByteLevel / WordPiece / Metaspace decoders.
 #pragma once
 #include <cstdint>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -22,7 +23,10 @@ namespace ragk_rt {
 class Tokenizer {
  public:
   explicit Tokenizer(const std::string& path);
-  std::vector<int> encode(const std::string& text, bool add_special_tokens) const;
+  std::vector<int> encode(const std::string& text, bool add_special_tokens) const;  // thread-safe
+  // many texts on `threads` worker threads (the per-word BPE cache is shared under a shared_mutex)
+  std::vector<std::vector<int>> encode_batch(const std::vector<std::string>& texts, bool add_special_tokens,
+                                             int threads) const;
   std::string decode(const std::vector<int>& ids, bool skip_special_tokens) const;
   int vocab_size() const { return (int)id_to_tok_.size(); }
   int token_to_id(const std::string& t) const;
@@ -78,16 +82,21 @@ class Tokenizer {
   std::string byte_to_uni_[256];
   std::unordered_map<uint32_t, unsigned char> uni_to_byte_;
   mutable std::unordered_map<std::string, std::vector<int>> cache_;
+  mutable std::shared_mutex cache_mu_;
+  unsigned long long uid_ = 0;  // keys the encode_batch workers' thread-local word caches
 
   void load_model(const Json& m);
   void load_normalizer(const Json* n);
   void load_pre(const Json* p);
   void load_post(const Json* p);
   void load_decoder(const Json* d);
-  void encode_segment(const std::string& seg, std::vector<int>& out) const;
+  using WordCache = std::unordered_map<std::string, std::vector<int>>;
+  // local != null: a caller-owned (per-thread) word cache, used without locking
+  std::vector<int> encode_impl(const std::string& text, bool add_special_tokens, WordCache* local) const;
+  void encode_segment(const std::string& seg, std::vector<int>& out, WordCache* local) const;
   std::string normalize(const std::string& s) const;
   bool pc_transform(const char* p, size_t n, std::string& out) const;
-  void bpe_word(const std::string& word, std::vector<int>& out) const;
+  void bpe_word(const std::string& word, std::vector<int>& out, WordCache* local) const;
   void wordpiece_word(const std::vector<uint32_t>& cps, std::vector<int>& out) const;
   void unigram_word(const std::string& word, std::vector<int>& out) const;
 };

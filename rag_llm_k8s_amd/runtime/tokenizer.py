@@ -15,6 +15,8 @@ from __future__ import annotations
 import json
 import os
 
+ENCODE_THREADS = int(os.environ.get("RAGK_TOKENIZER_THREADS", "8"))
+
 
 class Tokenizer:
     def __init__(self, path_or_dir, backend=None):
@@ -93,6 +95,8 @@ class Tokenizer:
         if self.backend == "hf":
             encs = self.impl.encode_batch(list(texts), add_special_tokens=add_special_tokens)
             out = [e.ids for e in encs]
+        elif hasattr(self.impl, "encode_batch"):  # C++ worker threads, GIL released
+            out = self.impl.encode_batch(list(texts), add_special_tokens, ENCODE_THREADS)
         else:
             out = [self.impl.encode(t, add_special_tokens) for t in texts]
         if max_length is not None:

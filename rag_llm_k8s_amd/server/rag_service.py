@@ -213,8 +213,8 @@ class RagService:
             self._seed += 1
             return self._seed
 
-    def _prompt_ids(self, full_prompt):
-        ids = self.tok.encode(full_prompt, add_special_tokens=True)
+    def _prompt_ids(self, full_prompt, ids=None):
+        ids = self.tok.encode(full_prompt, add_special_tokens=True) if ids is None else list(ids)
         limit = self.engine.max_model_len - self.params.max_new_tokens
         if len(ids) > limit:
             if self.cfg.truncate_prompt != "left":
@@ -265,18 +265,27 @@ class RagService:
         t0 = time.perf_counter()
         q = self.embedder.embed(list(prompts))
         res = self.store.search(q, self.cfg.retrieve_k)
-        seqs, ctxs = [], []
-        for i, (p, r) in enumerate(zip(prompts, res)):
-            if not r:
+        t_ret = time.perf_counter()
+        seqs, ctxs, fulls = [], [], []
+        for p, r in zip(prompts, res):
+            ctx = build_context(r, self.cfg.context_k) if r else None
+            ctxs.append(ctx)
+            if ctx is not None:
+                fulls.append(build_prompt(ctx, p))
+        # one multi-threaded tokenizer call for the whole batch (C++ workers, GIL released)
+        all_ids = iter(self.tok.encode_batch(fulls, add_special_tokens=True)) if fulls else iter(())
+        for i, ctx in enumerate(ctxs):
+            if ctx is None:
                 seqs.append(None)
-                ctxs.append(None)
                 continue
-            ctx = build_context(r, self.cfg.context_k)
-            ids = self._prompt_ids(build_prompt(ctx, p))
+            ids = self._prompt_ids(None, ids=next(all_ids))
             seqs.append(self.engine.add_request(ids, params or self.params,
                                                 seed=(seeds[i] if seeds is not None else self._next_seed())))
-            ctxs.append(ctx)
+        t_prep = time.perf_counter()
         self.engine.run_until_done()
+        st = self.engine.stats
+        st["retrieve_s"] = st.get("retrieve_s", 0.0) + (t_ret - t0)
+        st["prompt_build_s"] = st.get("prompt_build_s", 0.0) + (t_prep - t_ret)
         outs = []
         for s, ctx in zip(seqs, ctxs):
             if s is None:

@@ -7,6 +7,7 @@
 //   faiss <index> <out>                 read an IxF2 file and write it back
 //   bm   <seed>                         randomized BlockManager ops with invariant checks
 //   json                                malformed JSON must throw, never crash
+//   tokmt <tokenizer.json> <texts.txt>  encode_batch on 8 threads == sequential encode (TSan build: races)
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -39,6 +40,24 @@ static int cmd_tok(const char* tj, const char* texts) {
     std::vector<int> again = t.encode(back, false);  // exercise decode output through encode again
     (void)again;
   }
+  return 0;
+}
+
+static int cmd_tokmt(const char* tj, const char* texts) {
+  Tokenizer t(tj);
+  std::ifstream f(texts);
+  std::vector<std::string> lines;
+  std::string line;
+  while (std::getline(f, line)) lines.push_back(line);
+  std::vector<std::string> many;
+  for (int r = 0; r < 20; ++r)
+    for (auto& l : lines) many.push_back(l + " " + std::to_string(r));
+  for (int rep = 0; rep < 3; ++rep) {  // cold and warm shared word cache
+    std::vector<std::vector<int>> par = t.encode_batch(many, true, 8);
+    for (size_t i = 0; i < many.size(); ++i)
+      if (par[i] != t.encode(many[i], true)) return fail("encode_batch differs from encode");
+  }
+  std::printf("tokmt ok %zu\n", many.size());
   return 0;
 }
 
@@ -163,6 +182,7 @@ int main(int argc, char** argv) {
   const std::string c = argv[1];
   try {
     if (c == "tok" && argc == 4) return cmd_tok(argv[2], argv[3]);
+    if (c == "tokmt" && argc == 4) return cmd_tokmt(argv[2], argv[3]);
     if (c == "fuzz" && argc == 5) return cmd_fuzz(argv[2], (unsigned)std::stoul(argv[3]), std::stoi(argv[4]));
     if (c == "st" && argc == 3) return cmd_st(argv[2]);
     if (c == "faiss" && argc == 4) return cmd_faiss(argv[2], argv[3]);

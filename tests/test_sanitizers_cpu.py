@@ -18,20 +18,30 @@ RT = os.path.join(ROOT, "csrc", "runtime")
 SRC = [os.path.join(ROOT, "tests", "cpp", "runtime_selftest.cpp"), os.path.join(RT, "tokenizer.cpp"),
        os.path.join(RT, "runtime.cpp")]
 EXE = os.path.join(ROOT, "build", "asan", "runtime_selftest")
+TSAN_EXE = os.path.join(ROOT, "build", "tsan", "runtime_selftest")
 ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
            UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
 
 
-@pytest.fixture(scope="module")
-def exe():
+def _build(path, san_flags):
     deps = SRC + [os.path.join(RT, h) for h in os.listdir(RT) if h.endswith(".h")]
-    if not os.path.exists(EXE) or any(os.path.getmtime(s) > os.path.getmtime(EXE) for s in deps):
-        os.makedirs(os.path.dirname(EXE), exist_ok=True)
-        cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
-               "-fno-sanitize-recover=undefined", "-I" + RT] + SRC + ["-o", EXE]
+    if not os.path.exists(path) or any(os.path.getmtime(s) > os.path.getmtime(path) for s in deps):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        cmd = ["g++", "-std=c++17", "-O1", "-g", "-pthread", "-fno-omit-frame-pointer"] + san_flags + \
+            ["-I" + RT] + SRC + ["-o", path]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, r.stderr[-4000:]
-    return EXE
+    return path
+
+
+@pytest.fixture(scope="module")
+def exe():
+    return _build(EXE, ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"])
+
+
+@pytest.fixture(scope="module")
+def tsan_exe():
+    return _build(TSAN_EXE, ["-fsanitize=thread"])
 
 
 def run(exe, *args):
@@ -109,6 +119,20 @@ def test_tokenizers_under_asan_match_hf(exe, tokenizers_):
         for t, line in zip(TEXTS, got):
             ids = [int(x) for x in line.split()] if line.strip() else []
             assert ids == tok.encode(t, add_special_tokens=True).ids, (k, t)
+
+
+def test_tokenizer_threads_under_asan_and_tsan(exe, tsan_exe, tokenizers_):
+    """encode_batch (8 worker threads sharing the BPE word cache) == sequential encode; ThreadSanitizer
+    build must report no data race (the race detection tier of SURVEY §5)."""
+    _, paths, d = tokenizers_
+    texts = os.path.join(d, "texts.txt")
+    with open(texts, "w", encoding="utf-8") as f:
+        f.write("\n".join(TEXTS) + "\n")
+    for k, p in paths.items():
+        assert "tokmt ok" in run(exe, "tokmt", p, texts)
+        r = subprocess.run([tsan_exe, "tokmt", p, texts], capture_output=True, text=True, timeout=600,
+                           env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+        assert "ThreadSanitizer" not in r.stderr and r.returncode == 0, r.stderr[-3000:]
 
 
 def test_tokenizer_fuzz_under_asan(exe, tokenizers_):
