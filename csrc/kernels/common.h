@@ -99,6 +99,29 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
 }
 __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// ---- buffer-resource LDS-DMA (buffer_load_dwordx4 ... lds): the per-lane source is a 32-bit byte
+// offset (one VGPR, reusable across K-steps) + a wave-uniform SGPR offset, no 64-bit VALU address
+// math per load. The LDS destination is M0 (wave-uniform base) + lane*16, as for glds16.
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+__device__ void ragk_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) unsigned* lds, int size,
+                                         int voffset, int soffset, int offset,
+                                         int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+
+// Raw buffer descriptor (stride 0, bounds = `bytes`); dword3 = gfx9 data-format bits.
+__device__ __forceinline__ i32x4 make_srd(const void* base, unsigned bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(base);
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(a & 0xffffffffu));
+  r[1] = __builtin_amdgcn_readfirstlane((int)(a >> 32));
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+
+__device__ __forceinline__ void blds16(i32x4 srd, int voff, int soff, void* lds_wave_base) {
+  ragk_raw_buffer_load_lds(srd, (__attribute__((address_space(3))) unsigned*)lds_wave_base, 16, voff, soff, 0, 0);
+}
+
 }  // namespace ragk
 
 // Epilogue selector shared by the GEMM family.

@@ -1,0 +1,379 @@
+// 256x256x64 bf16 GEMM, 4 waves x (128x128) per workgroup, one wave per SIMD (large-M prefill GEMMs).
+//
+// C[M,N] = A[M,K] . B[N,K]^T (+ fused epilogue); same operands / epilogues as gemm.hip / gemm_pp.hip.
+//
+// Why a second 256x256 design next to the 8-wave ping-pong (gemm_pp.hip): rocprofv3 PMC on the
+// Llama-8B prefill shapes (profiles/pmc_gemm_r1.txt) put the ping-pong at 64 % MFMA-pipe utilisation
+// vs 75 % for hipBLASLt's 256x256x64 4-wave kernel at the same clock. The ping-pong pays one
+// workgroup barrier per 64 MFMAs per SIMD, gives its K-tile DMA only ~1 interval (~1k cycles) to land
+// before a vmcnt(0), and re-reads every A fragment from LDS for each of 4 column waves (192 KiB of
+// ds_read per K-tile). Here each wave owns a 128x128 output tile (8 x 8 mfma_f32_16x16x32_bf16
+// accumulators = 256 AGPRs), so per K-tile (64-deep) and SIMD: 128 MFMAs, one barrier, 128 KiB of
+// LDS reads per CU, and each DMA is issued 128 MFMAs (~2k cycles) before its wait.
+//
+// Per-wave software pipeline, one K-tile per iteration (fragment sets F0 = k 0..31, F1 = k 32..63;
+// tile t lives in LDS buffer t&1, lane-linear image, source-swizzled as gemm_pp):
+//   seg 1: ds_read F1(t), one per MFMA | MFMA F0 #0..23           -> lgkmcnt(0); barrier 1
+//   seg 2: 16 buffer-DMAs of tile t+2 -> buffer t&1 (every wave finished reading tile t before
+//          barrier 1), one per 5 MFMAs | MFMA F0 #24..63, F1 #0..47 -> vmcnt(16) [tile t+1 landed,
+//          t+2 in flight]; barrier 2
+//   seg 3: ds_read F0(t+1) from buffer (t+1)&1, one per MFMA | MFMA F1 #48..63
+// A DMA is issued 1-1.7 K-tiles (2-3.5k cycles) before the wait that retires it, and DMA issue is
+// spread over the MFMA stream: with one wave per SIMD nothing else hides its issue cost (a first
+// version that issued all 16 back to back ran at 49-61 % MFMA utilisation). The DMA is
+// buffer_load ... lds with per-lane byte offsets precomputed once (16 VGPRs) and the K position in
+// an SGPR (as hipBLASLt's gfx950 256x256 kernels do), so no address VALU in the loop.
+//
+// Build note: the loop is written in its final instruction order and this file is compiled with
+// `-mllvm -enable-misched=0 -mllvm -disable-post-ra` (_build.py EXTRA_FLAGS), so neither machine
+// scheduler reorders it (the post-RA one bunched the DMAs at the end of segment 2).
+#include "common.h"
+using namespace ragk;
+
+namespace {
+
+constexpr int WBM = 256, WBN = 256, WBK = 64;
+constexpr int W4_THREADS = 256;
+constexpr int W_TILE_A = WBM * WBK * 2;  // 32 KiB
+constexpr int W_TILE_B = WBN * WBK * 2;  // 32 KiB
+constexpr int W_BUF = W_TILE_A + W_TILE_B;
+constexpr int WEPI_LD = WBN + 4;                 // padded fp32 row
+constexpr int WEPI_BYTES = 128 * WEPI_LD * 4;    // one 128-row half of the output tile
+constexpr int W4_LDS = (2 * W_BUF > WEPI_BYTES) ? 2 * W_BUF : WEPI_BYTES;
+constexpr int WGROUP_M = 8;
+
+__device__ __forceinline__ int wswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// 256 rows x 128 B = 32 pieces of 8 rows; wave w stages pieces 8w..8w+7 of each operand. Per-lane
+// byte offsets of those 8 pieces (row clamped to the last valid row, chunk source-swizzled).
+__device__ __forceinline__ void w4_offsets(int ld, int row0, int rows_valid, int wid, int lane, int (&off)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = (wid * 8 + i) * 8 + (lane >> 3);
+    const int c = wswz(r, lane & 7);
+    int gr = row0 + r;
+    gr = gr < rows_valid ? gr : rows_valid - 1;
+    off[i] = gr * ld * 2 + c * 16;
+  }
+}
+
+__device__ __forceinline__ void w4_stage(i32x4 srd, const int (&off)[8], int k0, char* lds, int wid) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) blds16(srd, off[i], k0 * 2, lds + (wid * 8 + i) * 1024);
+}
+
+__device__ __forceinline__ void w4_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// fragments of one 32-deep sub-step: A rows wr*128 + 16i + fr, B rows wc*128 + 16j + fr, chunk 4s + fh
+__device__ __forceinline__ void w4_read(const char* buf, int s, int wr, int wc, int fr, int fh, bf16x8 (&a)[8],
+                                        bf16x8 (&b)[8]) {
+  const char* sa = buf;
+  const char* sb = buf + W_TILE_A;
+  const int c = 4 * s + fh;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int R = wr * 128 + 16 * i + fr;
+    a[i] = *reinterpret_cast<const bf16x8*>(sa + R * 128 + 16 * wswz(R, c));
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int R = wc * 128 + 16 * j + fr;
+    b[j] = *reinterpret_cast<const bf16x8*>(sb + R * 128 + 16 * wswz(R, c));
+  }
+}
+
+// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0]+[15:14], expcnt [6:4], lgkmcnt [11:8])
+constexpr int W_LGKM0 = 0xC07F;  // lgkmcnt(0), others don't-care
+constexpr int W_VM0 = 0x0F70;    // vmcnt(0), others don't-care
+constexpr int W_VM16 = 0x4F70;   // vmcnt(16)
+
+template <int EPI, bool OUT_F32>
+__device__ __forceinline__ void w4_epilogue(const f32x4 (&acc)[8][8], char* smem, int tid, int wr, int wc, int fr,
+                                            int fh, int m0, int n0, void* C, int ldc, const bf16_t* __restrict__ bias,
+                                            const bf16_t* resid, int ldr, int M, int N) {
+  float* sC = reinterpret_cast<float*>(smem);
+  constexpr bool RES = (EPI == EPI_RESID || EPI == EPI_BIAS_RESID);
+  // the half's residual tile is loaded into registers before its LDS staging (one memory latency,
+  // overlapped with the staging, instead of a dependent load per output vector)
+  u32x4 rpre[RES ? 16 : 1];
+#pragma unroll 1
+  for (int h = 0; h < 2; ++h) {
+    if constexpr (RES) {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int v = tid + it * W4_THREADS;
+        const int gr = m0 + h * 128 + (v >> 5), gc = n0 + (v & 31) * 8;
+        rpre[it] = (gr < M && gc < N) ? *reinterpret_cast<const u32x4*>(resid + (size_t)gr * ldr + gc)
+                                      : (u32x4){0u, 0u, 0u, 0u};
+      }
+    }
+    __syncthreads();
+    if (wr == h) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            sC[(16 * i + 4 * fh + r) * WEPI_LD + wc * 128 + 16 * j + fr] = acc[i][j][r];
+    }
+    __syncthreads();
+    const int mrow0 = m0 + h * 128;
+    if constexpr (EPI == EPI_SILU_MUL) {
+      // 256 packed cols = two [64 gate | 64 up] tiles -> 128 output cols
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int v = tid + it * W4_THREADS;  // 128 rows x 16 vec (2 halves x 8)
+        const int row = v >> 4, hv = (v >> 3) & 1, c8 = (v & 7) * 8;
+        const int gr = mrow0 + row;
+        if (gr < M) {
+          float o[8];
+          const float* g = sC + row * WEPI_LD + hv * 128 + c8;
+          const float* u = g + 64;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = silu(g[e]) * u[e];
+          bf16_t* dst = reinterpret_cast<bf16_t*>(C) + (size_t)gr * ldc + (n0 >> 1) + hv * 64 + c8;
+          *reinterpret_cast<u32x4*>(dst) = pack8(o);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int v = tid + it * W4_THREADS;  // 128 rows x 32 vec
+        const int row = v >> 5, c8 = (v & 31) * 8;
+        const int gr = mrow0 + row, gc = n0 + c8;
+        if (gr < M && gc < N) {
+          float o[8];
+          const float* s = sC + row * WEPI_LD + c8;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = s[e];
+          if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU ||
+                        EPI == EPI_BIAS_GELU_TANH) {
+            float b[8];
+            unpack8(*reinterpret_cast<const u32x4*>(bias + gc), b);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] += b[e];
+          }
+          if constexpr (RES) {
+            float rr[8];
+            unpack8(rpre[it], rr);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] += rr[e];
+          }
+          if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_GELU) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = gelu_erf(o[e]);
+          }
+          if constexpr (EPI == EPI_BIAS_GELU_TANH) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = gelu_tanh(o[e]);
+          }
+          if constexpr (OUT_F32) {
+            float* dst = reinterpret_cast<float*>(C) + (size_t)gr * ldc + gc;
+            *reinterpret_cast<f32x4*>(dst) = (f32x4){o[0], o[1], o[2], o[3]};
+            *reinterpret_cast<f32x4*>(dst + 4) = (f32x4){o[4], o[5], o[6], o[7]};
+          } else {
+            bf16_t* dst = reinterpret_cast<bf16_t*>(C) + (size_t)gr * ldc + gc;
+            *reinterpret_cast<u32x4*>(dst) = pack8(o);
+          }
+        }
+      }
+    }
+  }
+}
+
+// MFMA #m (= 8i + j) of a sub-step. Inline asm with the accumulator tied in an AGPR ("+a"): with the
+// builtin, hipcc picks dst != srcC for the loop-carried accumulators and adds 84-500 v_accvgpr copies
+// per K-tile. volatile + "memory" keep the statement in source order relative to the LDS reads and
+// DMAs around it (the loop is written in its final order). Hazards the compiler no longer pads:
+// acc init -> first MFMA and last MFMA -> epilogue reads (w4_pin_acc below); the accumulate chain
+// itself (same acc every 64 MFMAs) and ds_read -> srcA/B (s_waitcnt, inserted by hipcc) need none.
+__device__ __forceinline__ void w4_mfma(f32x4 (&acc)[8][8], const bf16x8 (&a)[8], const bf16x8 (&b)[8], int m) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+               : "+a"(acc[m >> 3][m & 7])
+               : "v"(a[m >> 3]), "v"(b[m & 7])
+               : "memory");
+}
+
+// Orders every accumulator access after an s_nop pad (>= 16 wait states covers MFMA D -> VALU/DS read
+// and v_accvgpr_write -> MFMA srcC).
+__device__ __forceinline__ void w4_pin_acc(f32x4 (&acc)[8][8]) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 1" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j])::"memory");
+}
+
+// Fragment q (0..15) of a sub-step in the order the next MFMAs consume them: a[0], b[0..7], a[1..7].
+__device__ __forceinline__ void w4_read_frag(const char* buf, int s, int q, int wr, int wc, int fr, int fh,
+                                             bf16x8 (&a)[8], bf16x8 (&b)[8]) {
+  const int c = 4 * s + fh;
+  if (q == 0 || q > 8) {
+    const int i = q == 0 ? 0 : q - 8;
+    const int R = wr * 128 + 16 * i + fr;
+    a[i] = *reinterpret_cast<const bf16x8*>(buf + R * 128 + 16 * wswz(R, c));
+  } else {
+    const int j = q - 1;
+    const int R = wc * 128 + 16 * j + fr;
+    b[j] = *reinterpret_cast<const bf16x8*>(buf + W_TILE_A + R * 128 + 16 * wswz(R, c));
+  }
+}
+
+// One K-tile, written in final instruction order (file built with -enable-misched=0).
+// STAGE: issue tile t+2's DMA; READ: read F0(t+1).
+template <bool STAGE, bool READ>
+__device__ __forceinline__ void w4_iter(char* smem, int t, i32x4 srd_a, i32x4 srd_b, const int (&off_a)[8],
+                                        const int (&off_b)[8], int wid, int wr, int wc, int fr, int fh,
+                                        f32x4 (&acc)[8][8], bf16x8 (&a0)[8], bf16x8 (&b0)[8], bf16x8 (&a1)[8],
+                                        bf16x8 (&b1)[8]) {
+  char* buf = smem + (t & 1) * W_BUF;
+  // ---------------- seg 1: read F1(t), one per MFMA | MFMA F0 #0..23 ----------------------
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    w4_read_frag(buf, 1, q, wr, wc, fr, fh, a1, b1);
+    w4_mfma(acc, a0, b0, q);
+  }
+#pragma unroll
+  for (int m = 16; m < 24; ++m) w4_mfma(acc, a0, b0, m);
+  __builtin_amdgcn_s_waitcnt(W_LGKM0);  // every read of buffer t&1 retired
+  w4_barrier();
+  // ---------------- seg 2: 16 DMAs of tile t+2 -> buffer t&1, one per 5 MFMAs | F0 #24..63, F1 #0..47
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    if constexpr (STAGE) {
+      if (q < 8) blds16(srd_a, off_a[q], (t + 2) * WBK * 2, buf + (wid * 8 + q) * 1024);
+      else blds16(srd_b, off_b[q - 8], (t + 2) * WBK * 2, buf + W_TILE_A + (wid * 8 + q - 8) * 1024);
+    }
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      const int m = 24 + 5 * q + u;  // 24..103 over F0 (24..63) then F1 (64..103 -> 0..39)
+      if (m < 64) w4_mfma(acc, a0, b0, m);
+      else w4_mfma(acc, a1, b1, m - 64);
+    }
+  }
+#pragma unroll
+  for (int m = 40; m < 48; ++m) w4_mfma(acc, a1, b1, m);
+  if constexpr (STAGE) __builtin_amdgcn_s_waitcnt(W_VM16);  // tile t+1 landed (t+2's 16 in flight)
+  else __builtin_amdgcn_s_waitcnt(W_VM0);
+  w4_barrier();
+  // ---------------- seg 3: read F0(t+1) from buffer (t+1)&1, one per MFMA | F1 #48..63 ------
+  const char* nbuf = smem + ((t + 1) & 1) * W_BUF;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    if constexpr (READ) w4_read_frag(nbuf, 0, q, wr, wc, fr, fh, a0, b0);
+    w4_mfma(acc, a1, b1, 48 + q);
+  }
+}
+
+template <int EPI, bool OUT_F32>
+__global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __restrict__ A, int lda,
+                                                                const bf16_t* __restrict__ B, int ldb, void* C,
+                                                                int ldc, const bf16_t* __restrict__ bias,
+                                                                const bf16_t* resid, int ldr, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char smem[W4_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int fr = lane & 15, fh = lane >> 4;
+
+  const int tiles_m = (M + WBM - 1) / WBM, tiles_n = (N + WBN - 1) / WBN;
+  const int nwg = tiles_m * tiles_n;
+  const int logical = xcd_remap(blockIdx.x, nwg);
+  const int group = logical / (WGROUP_M * tiles_n);
+  const int first_m = group * WGROUP_M;
+  const int gm = min(tiles_m - first_m, WGROUP_M);
+  const int in_group = logical % (WGROUP_M * tiles_n);
+  const int m0 = (first_m + in_group % gm) * WBM;
+  const int n0 = (in_group / gm) * WBN;
+  const int nk = K / WBK;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  w4_pin_acc(acc);
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+
+  // byte offsets are 32-bit: the launcher guarantees rows * ld * 2 < 2^31 for both operands
+  const i32x4 srd_a = make_srd(A, (unsigned)M * (unsigned)lda * 2u);
+  const i32x4 srd_b = make_srd(B, (unsigned)N * (unsigned)ldb * 2u);
+  int off_a[8], off_b[8];
+  w4_offsets(lda, m0, M, wid, lane, off_a);
+  w4_offsets(ldb, n0, N, wid, lane, off_b);
+
+  // prologue: tiles 0 and 1 in flight, wait for tile 0 (tile 1's 16 DMAs are younger)
+  w4_stage(srd_a, off_a, 0, smem, wid);
+  w4_stage(srd_b, off_b, 0, smem + W_TILE_A, wid);
+  if (nk > 1) {
+    w4_stage(srd_a, off_a, WBK, smem + W_BUF, wid);
+    w4_stage(srd_b, off_b, WBK, smem + W_BUF + W_TILE_A, wid);
+    __builtin_amdgcn_s_waitcnt(W_VM16);
+  } else {
+    __builtin_amdgcn_s_waitcnt(W_VM0);
+  }
+  w4_barrier();
+  w4_read(smem, 0, wr, wc, fr, fh, a0, b0);
+  __builtin_amdgcn_s_waitcnt(W_LGKM0);
+  __builtin_amdgcn_sched_barrier(0);
+
+  int t = 0;
+  for (; t + 2 < nk; ++t)
+    w4_iter<true, true>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1, b1);
+  if (t + 1 < nk) {
+    w4_iter<false, true>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1, b1);
+    ++t;
+  }
+  w4_iter<false, false>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1, b1);
+  __builtin_amdgcn_s_waitcnt(W_VM0);
+  w4_pin_acc(acc);
+
+  w4_epilogue<EPI, OUT_F32>(acc, smem, tid, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr, M, N);
+}
+
+template <int EPI, bool F32>
+int launch_w4(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias, const void* resid,
+              int ldr, int M, int N, int K, hipStream_t st) {
+  const int nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI, F32>), dim3(nwg), dim3(W4_THREADS), 0, st, (const bf16_t*)A, lda,
+                     (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// N = output columns (for EPI_SILU_MUL the weight has 2N rows, N % 128 == 0). Requires K % 64 == 0.
+RAGK_API int ragk_gemm_w4(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
+                          const void* resid, int ldr, int M, int N, int K, int epi, int out_f32, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (K % WBK != 0) return (int)hipErrorInvalidValue;
+  const long long rows_b = (epi == EPI_SILU_MUL) ? 2LL * N : (long long)N;
+  if ((long long)M * lda * 2 >= (1LL << 31) || rows_b * ldb * 2 >= (1LL << 31))
+    return (int)hipErrorInvalidValue;  // 32-bit buffer offsets
+  if (epi == EPI_SILU_MUL) {
+    if (N % 128 != 0 || out_f32) return (int)hipErrorInvalidValue;
+    return launch_w4<EPI_SILU_MUL, false>(A, lda, B, ldb, C, ldc, bias, resid, ldr, M, 2 * N, K, st);
+  }
+  if (N % 8 != 0) return (int)hipErrorInvalidValue;
+#define RAGK_W4_CASE(E) \
+  case E:               \
+    return out_f32 ? launch_w4<E, true>(A, lda, B, ldb, C, ldc, bias, resid, ldr, M, N, K, st) \
+                   : launch_w4<E, false>(A, lda, B, ldb, C, ldc, bias, resid, ldr, M, N, K, st);
+  switch (epi) {
+    RAGK_W4_CASE(EPI_NONE)
+    RAGK_W4_CASE(EPI_BIAS)
+    RAGK_W4_CASE(EPI_RESID)
+    RAGK_W4_CASE(EPI_BIAS_RESID)
+    RAGK_W4_CASE(EPI_BIAS_GELU)
+    RAGK_W4_CASE(EPI_GELU)
+    RAGK_W4_CASE(EPI_BIAS_GELU_TANH)
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+#undef RAGK_W4_CASE
+}

@@ -28,6 +28,10 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIP_LIB = os.path.join(LIB_DIR, "libragk_hip.so")
 
 
+# per-file flags: gemm_w4.hip is written in its final instruction order (see its header)
+EXTRA_FLAGS = {"gemm_w4.hip": ["-mllvm", "-enable-misched=0", "-mllvm", "-disable-post-ra"]}
+
+
 def _newer(src_files, target):
     if not os.path.exists(target):
         return True
@@ -55,11 +59,12 @@ def build_hip(verbose=False, jobs=None):
     for s in srcs:
         o = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
         objs.append(o)
-        if _newer([s] + headers, o):
+        if _newer([s] + headers + [os.path.abspath(__file__)], o):
             todo.append((s, o))
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        futs = [ex.submit(_run, [HIPCC] + flags + ["-c", s, "-o", o]) for s, o in todo]
+        futs = [ex.submit(_run, [HIPCC] + flags + EXTRA_FLAGS.get(os.path.basename(s), []) + ["-c", s, "-o", o])
+                for s, o in todo]
         for f in futs:
             out = f.result()
             if verbose and out.strip():

@@ -24,6 +24,7 @@ _SIGS = {
     "ragk_gemm_path": [I, P, I, P, I, P, I, P, P, I, I, I, I, I, S],
     "ragk_gemm_pp": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_pp_set_variant": [I],
+    "ragk_gemm_w4": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_dec": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, I, P, P, S],
     "ragk_gemm_dec_splits": [I, I, I],
     "ragk_rmsnorm": [P, I, P, I, P, P, I, I, I, F, S],

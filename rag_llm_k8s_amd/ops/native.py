@@ -28,6 +28,8 @@ def _bf16_2d(t, name):
 # ----------------------------------------------------------------------------- GEMM
 PP_MIN_M = int(__import__("os").environ.get("RAGK_PP_MIN_M", "1024"))
 PP_VARIANT = int(__import__("os").environ.get("RAGK_PP_VARIANT", "2"))
+# large-M kernel: "w4" = 4-wave 128x128-per-wave (gemm_w4.hip, path 6), "pp" = 8-wave ping-pong (path 2)
+PREFILL_GEMM = __import__("os").environ.get("RAGK_PREFILL_GEMM", "w4")
 _pp_variant_set = [None]
 
 
@@ -73,7 +75,8 @@ def use_stream(M, N, K, epi, fp8=False):
 
 
 def use_pp(M, N, K, epi):
-    """Large-M GEMMs go to the 256x256 8-wave ping-pong kernel (gemm_pp.hip)."""
+    """Large-M GEMMs go to a 256x256 MFMA kernel: gemm_w4.hip (default, 4 waves x 128x128, 9-16 %
+    faster on the Llama-8B prefill shapes, profiles/gemm_w4_r1.txt) or the 8-wave ping-pong gemm_pp.hip."""
     if M < PP_MIN_M or K % 64:
         return False
     return N % 128 == 0 if epi == "silu_mul" else N % 8 == 0
@@ -108,7 +111,10 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
     L = _lib.lib()
     ldr = resid.stride(0) if resid is not None else 0
     if path is None and use_pp(M, N, K, epi):
-        path = 2
+        rows = w.shape[0]
+        # gemm_w4 addresses operands with 32-bit buffer offsets
+        fits = x.stride(0) * M * 2 < 2 ** 31 and w.stride(0) * rows * 2 < 2 ** 31
+        path = 6 if (PREFILL_GEMM == "w4" and fits) else 2
     if path is None and STREAM_DEFAULT and use_stream(M, N, K, epi):
         path = 5
     if path is None and DEC_DEFAULT and use_dec(M, N, K, epi):
@@ -128,6 +134,9 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
         if _pp_variant_set[0] is None:
             set_pp_variant(PP_VARIANT)
         rc = L.ragk_gemm_pp(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
+                            ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), stream_ptr())
+    elif path == 6:
+        rc = L.ragk_gemm_w4(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
                             ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), stream_ptr())
     elif path is None:
         rc = L.ragk_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),

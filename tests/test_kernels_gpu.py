@@ -28,8 +28,11 @@ def test_gemm_plain(native, M, N, K):
 
 @pytest.mark.parametrize("M,N,K", [(1, 256, 128), (300, 1024, 768), (1111, 6144, 4096), (256, 256, 128),
                                    (2049, 512, 1024), (513, 4104, 256), (260, 768, 384)])
-@pytest.mark.parametrize("variant", [2, 4])
+@pytest.mark.parametrize("variant", [2, 4, "w4"])
 def test_gemm_pingpong(native, M, N, K, variant):
+    if variant == "w4":  # 4-wave 128x128-per-wave kernel (gemm_w4.hip)
+        _check_pingpong(native, M, N, K, path=6)
+        return
     native.set_pp_variant(variant)
     try:
         _check_pingpong(native, M, N, K)
@@ -37,22 +40,22 @@ def test_gemm_pingpong(native, M, N, K, variant):
         native.set_pp_variant(native.PP_VARIANT)
 
 
-def _check_pingpong(native, M, N, K):
+def _check_pingpong(native, M, N, K, path=2):
     torch.manual_seed(20)
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
     b = torch.randn(N, device=DEV).bfloat16()
     r = torch.randn(M, N, device=DEV).bfloat16()
-    y = native.gemm(x, w, path=2)
+    y = native.gemm(x, w, path=path)
     assert rel_err(y, x.float() @ w.float().t()) < 1e-2
     for epi in ["bias", "resid", "bias_resid", "bias_gelu"]:
-        y = native.gemm(x, w, bias=b, resid=r, epi=epi, path=2)
+        y = native.gemm(x, w, bias=b, resid=r, epi=epi, path=path)
         assert rel_err(y.cpu(), R.linear(x.cpu(), w.cpu(), b.cpu(), r.cpu(), epi=epi)) < 1e-2, epi
-    yf = native.gemm(x, w, out_f32=True, path=2)
+    yf = native.gemm(x, w, out_f32=True, path=path)
     assert rel_err(yf, x.float() @ w.float().t()) < 1e-3
     if N % 256 == 0:
         g, u = w[: N // 2], w[N // 2:]
-        y = native.gemm(x, R.pack_gate_up(g, u), epi="silu_mul", path=2)
+        y = native.gemm(x, R.pack_gate_up(g, u), epi="silu_mul", path=path)
         ref = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
         assert rel_err(y, ref) < 1e-2
 
