@@ -1,0 +1,172 @@
+// Decode GEMM v5 for gfx950: split-K partial products, reduction left to the consumer kernel.
+//
+// P[s][M][N] (fp32) = X[M, s*KS:(s+1)*KS] . W[N, s*KS:(s+1)*KS]^T,  M <= 16*MT <= 64, s < S = K/KS.
+//
+// Why: at decode batch sizes the small-N projections (qkv, o_proj, down: 33-117 MB of weights)
+// are latency-bound, not bandwidth-bound: the skinny / split-K kernels ran them at 2.0-2.8 TB/s
+// (profiles/rocprof_bench_r1_kernels_v2.txt) because a block issues its weight loads one chunk at a
+// time and split-K blocks then serialise on a last-arriver reduction. Here
+//   * a block = 8 waves = 64 output columns x one K-slice; wave w owns n-tile (w & 3) and half
+//     (w >> 2) of the slice, and issues ALL of its weight loads (NKS x 16 B per lane, straight to
+//     VGPRs, non-temporal) before touching anything else -> the whole matrix is in flight within
+//     the first microsecond;
+//   * the activation slice (16*MT rows x KS) is DMA'd once per block into LDS (XOR-swizzled rows,
+//     conflict-free ds_read_b128) and shared by the 4 n-tile waves;
+//   * the two K-halves meet in LDS, and the block writes its fp32 partial tile to slab s. There is
+//     no inter-block synchronisation: the consumer (ragk_add_partials_rmsnorm / rope_kv_partials in
+//     norm.hip) sums the S slabs while doing its own row work, so the reduction costs no extra
+//     launch and no atomics (deterministic).
+#include "common.h"
+using namespace ragk;
+
+namespace {
+
+constexpr int PT_THREADS = 512;
+constexpr int PT_NB = 64;  // output columns per block
+
+__device__ __forceinline__ int pswz16(int row, int chunk) { return chunk ^ (row & 15); }
+
+template <int MT, int NKS>
+__global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* __restrict__ X, int ldx,
+                                                                  const bf16_t* __restrict__ W, int ldw,
+                                                                  float* __restrict__ P, int M, int N, int K) {
+  constexpr int KS = NKS * 64;          // K-slice of the block (two halves of NKS k-steps of 32)
+  constexpr int XROWS = 16 * MT;
+  constexpr int ROWB = KS * 2;          // bytes per LDS row
+  constexpr int XBYTES = XROWS * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[XBYTES > 16384 ? XBYTES : 16384];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nt = wid & 3, kh = wid >> 2;
+  const int fr = lane & 15, fh = lane >> 4;
+  const int n0 = blockIdx.x * PT_NB, s = blockIdx.y;
+  const int kbase = s * KS;
+
+  // 1) activation slice -> LDS first (so a counted vmcnt can retire it before the weights): 16-B
+  //    chunk c of row r lives at chunk slot c ^ (r & 15) (source-swizzled LDS-DMA: the LDS image is
+  //    lane-linear, the global address carries the XOR)
+  constexpr int CPR = ROWB / 16;                 // chunks per row
+  constexpr int PIECES = XBYTES / 1024;          // 1-KiB pieces (64 lanes x 16 B)
+  constexpr int PPW = PIECES / (PT_THREADS / 64);
+  static_assert(PIECES % (PT_THREADS / 64) == 0 && CPR >= 64, "activation slice shape");
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int p = wid * PPW + i;
+    const int e = p * 64 + lane;                 // destination chunk index (lane-linear)
+    const int r = e / CPR, slot = e % CPR;
+    const int c = (slot & ~15) | ((slot & 15) ^ (r & 15));
+    const int gr = min(r, M - 1);
+    glds16(X + (size_t)gr * ldx + kbase + c * 8, smem + p * 1024);
+  }
+
+  __builtin_amdgcn_sched_barrier(0);
+  // 2) this wave's whole weight stream, all loads in flight: row n0 + 16nt + fr,
+  //    k = kbase + kh*KS/2 + 32ks + 8fh
+  const int wrow = min(n0 + 16 * nt + fr, N - 1);
+  const bf16_t* wp = W + (size_t)wrow * ldw + kbase + kh * (KS / 2) + fh * 8;
+  bf16x8 wf[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
+  // vmcnt(NKS): the DMA (older than the NKS weight loads) has landed
+  __builtin_amdgcn_s_waitcnt((NKS & 15) | (((NKS >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();  // raw: __syncthreads() would drain the weight loads too (vmcnt(0))
+  __builtin_amdgcn_sched_barrier(0);
+
+  // 3) MFMA: A = activation fragment (rows 16t + fr), B = weight fragment (cols 16nt + fr)
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int chunk = (kh * (KS / 2) + 32 * ks) / 8 + fh;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int r = 16 * t + fr;
+      const bf16x8 xf = *reinterpret_cast<const bf16x8*>(smem + r * ROWB + 16 * ((chunk & ~15) | ((chunk & 15) ^ (r & 15))));
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[ks], acc[t], 0, 0, 0);
+    }
+  }
+
+  // 4) K-halves meet in LDS (the activation slice is dead), half 0 writes the partial slab
+  __syncthreads();
+  f32x4* red = reinterpret_cast<f32x4*>(smem);
+  if (kh == 1) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t) red[(nt * MT + t) * 64 + lane] = acc[t];
+  }
+  __syncthreads();
+  if (kh == 0) {
+    const int col = n0 + 16 * nt + fr;
+    float* ps = P + (size_t)s * M * N;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const f32x4 o = red[(nt * MT + t) * 64 + lane];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * t + 4 * fh + r;
+        if (row < M && col < N) ps[(size_t)row * N + col] = acc[t][r] + o[r];
+      }
+    }
+  }
+}
+
+template <int MT>
+int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K, int ks_steps,
+                   hipStream_t st) {
+  const int KS = ks_steps * 64;
+  const dim3 grid((N + PT_NB - 1) / PT_NB, K / KS);
+#define RAGK_PART(NK)                                                                                       \
+  case NK:                                                                                                  \
+    if constexpr (16 * MT * NK * 64 * 2 <= 128 * 1024) {                                                    \
+      hipLaunchKernelGGL((gemm_part_kernel<MT, NK>), grid, dim3(PT_THREADS), 0, st, (const bf16_t*)X, ldx, \
+                         (const bf16_t*)W, ldw, P, M, N, K);                                                \
+      break;                                                                                                \
+    } else {                                                                                                \
+      return (int)hipErrorInvalidValue;                                                                     \
+    }
+  switch (ks_steps) {
+    RAGK_PART(8)
+    RAGK_PART(16)
+    RAGK_PART(32)
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+#undef RAGK_PART
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// Slice choice: K-slice KS = 64 * ks_steps (ks_steps in {8, 16, 32}); S = K / KS slabs.
+// Picks the largest slice that still gives >= 256 blocks and fits the activation slice in LDS.
+RAGK_API int ragk_gemm_part_ksteps(int M, int N, int K) {
+  const int mt = (M + 15) / 16;
+  const int nb = (N + PT_NB - 1) / PT_NB;
+  int best = 0;
+  for (int ks : {32, 16, 8}) {
+    const int KS = ks * 64;
+    if (K % KS) continue;
+    if (16 * mt * KS * 2 > 128 * 1024) continue;
+    if (best == 0) best = ks;  // largest legal slice
+    if (nb * (K / KS) >= 256) return ks;
+  }
+  return best;
+}
+
+// P must hold (K / (64*ks_steps)) * M * N floats. M <= 64, K % (64*ks_steps) == 0.
+RAGK_API int ragk_gemm_part(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K,
+                            int ks_steps, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (M > 64 || ks_steps <= 0 || K % (64 * ks_steps) != 0) return (int)hipErrorInvalidValue;
+  const int mt = (M + 15) / 16;
+  if (16 * mt * ks_steps * 64 * 2 > 128 * 1024) return (int)hipErrorInvalidValue;
+  switch (mt) {
+    case 1: return launch_part_mt<1>(X, ldx, W, ldw, P, M, N, K, ks_steps, st);
+    case 2: return launch_part_mt<2>(X, ldx, W, ldw, P, M, N, K, ks_steps, st);
+    case 3: return launch_part_mt<3>(X, ldx, W, ldw, P, M, N, K, ks_steps, st);
+    case 4: return launch_part_mt<4>(X, ldx, W, ldw, P, M, N, K, ks_steps, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}

@@ -330,6 +330,129 @@ __global__ __launch_bounds__(NT) void gather_rows_kernel(const bf16_t* x, int ld
     *reinterpret_cast<u32x4*>(out + (size_t)i * ldo + v * 8) = *reinterpret_cast<const u32x4*>(src + v * 8);
 }
 
+
+// ---- consumers of the split-K decode GEMM (gemm_part.hip): they sum the S fp32 partial slabs
+// P[S][M][ldp] while doing their own row work, so the reduction needs no extra launch.
+
+// h = bf16(h + bf16(sum_s P[s][row]))  (HF: bf16 linear output, then the bf16 residual add), written
+// back to h; out = rmsnorm(h) * w exactly as rmsnorm_kernel. One block of 512 threads per row.
+constexpr int PNT = 512;
+__global__ __launch_bounds__(PNT) void add_partials_rmsnorm_kernel(const float* __restrict__ P, int S, int M,
+                                                                   bf16_t* h, int ldh,
+                                                                   const bf16_t* __restrict__ w, bf16_t* out,
+                                                                   int ldo, int H, float eps) {
+  __shared__ float red[PNT / 64];
+  const int row = blockIdx.x;
+  bf16_t* hr = h + (size_t)row * ldh;
+  constexpr int MAXV = 2;  // up to 2 x 8 x 512 = 8192 columns in registers
+  float v[MAXV][8];
+  const int nvec = H >> 3;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int vi = threadIdx.x + i * PNT;
+    if (vi < nvec) {
+      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < S; ++s) {
+        const f32x4* ps = reinterpret_cast<const f32x4*>(P + ((size_t)s * M + row) * H + vi * 8);
+        const f32x4 p0 = ps[0], p1 = ps[1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] += p0[e];
+          a[4 + e] += p1[e];
+        }
+      }
+      unpack8(*reinterpret_cast<const u32x4*>(hr + vi * 8), v[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = bf2f(f2bf(v[i][e] + bf2f(f2bf(a[e]))));
+      *reinterpret_cast<u32x4*>(hr + vi * 8) = pack8(v[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += v[i][e] * v[i][e];
+    }
+  }
+  ss = block_sum(ss, red);
+  const float inv = rsqrtf(ss / (float)H + eps);
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int vi = threadIdx.x + i * PNT;
+    if (vi < nvec) {
+      float wv[8], o[8];
+      unpack8(*reinterpret_cast<const u32x4*>(w + vi * 8), wv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = wv[e] * bf2f(f2bf(v[i][e] * inv));
+      *reinterpret_cast<u32x4*>(out + (size_t)row * ldo + vi * 8) = pack8(o);
+    }
+  }
+}
+
+// rope_kv_kernel fed by qkv partial slabs: qkv = bf16(sum_s P[s][t]) (the bf16 linear output), then
+// the same rotate_half RoPE (HF bf16 op rounding) and paged-KV write. Rotated q goes to q_out
+// (row stride ldq); k / v go to the cache only. grid = (T, HG): head groups split over blocks.
+__device__ __forceinline__ void sum_partials8(const float* P, int S, size_t slab, float* a) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = 0.f;
+  for (int s = 0; s < S; ++s) {
+    const f32x4* ps = reinterpret_cast<const f32x4*>(P + (size_t)s * slab);
+    const f32x4 p0 = ps[0], p1 = ps[1];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      a[e] += p0[e];
+      a[4 + e] += p1[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = bf2f(f2bf(a[e]));
+}
+
+__global__ __launch_bounds__(NT) void rope_kv_partials_kernel(const float* __restrict__ P, int S, int T, int ldp,
+                                                              bf16_t* q_out, int ldq,
+                                                              const int* __restrict__ positions,
+                                                              const float* __restrict__ cos_t,
+                                                              const float* __restrict__ sin_t,
+                                                              const int* __restrict__ slots, bf16_t* kc, bf16_t* vc,
+                                                              int Hq, int Hkv, int D, int BS) {
+  const int t = blockIdx.x, hg = blockIdx.y, ngroups = gridDim.y;
+  const int pos = positions[t];
+  const int slot = slots ? slots[t] : -1;
+  const size_t slab = (size_t)T * ldp;
+  const float* prow = P + (size_t)t * ldp;
+  const int half = D >> 1;
+  const int vpr = half >> 3;
+  const float* ct = cos_t + (size_t)pos * half;
+  const float* st = sin_t + (size_t)pos * half;
+  const int nh = Hq + 2 * Hkv;
+  for (int i = threadIdx.x + hg * NT; i < nh * vpr; i += NT * ngroups) {
+    const int hd = i / vpr, v = i % vpr;
+    float x1[8], x2[8];
+    sum_partials8(prow + hd * D + v * 8, S, slab, x1);
+    sum_partials8(prow + hd * D + half + v * 8, S, slab, x2);
+    if (hd >= Hq + Hkv) {  // v head: straight to the cache
+      if (slot >= 0) {
+        bf16_t* dst = vc + (((size_t)(slot / BS) * Hkv + (hd - Hq - Hkv)) * BS + (slot % BS)) * D;
+        *reinterpret_cast<u32x4*>(dst + v * 8) = pack8(x1);
+        *reinterpret_cast<u32x4*>(dst + half + v * 8) = pack8(x2);
+      }
+      continue;
+    }
+    float o1[8], o2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float c = ct[v * 8 + e], sn = st[v * 8 + e];
+      o1[e] = bf2f(f2bf(bf2f(f2bf(x1[e] * c)) + bf2f(f2bf(-x2[e] * sn))));
+      o2[e] = bf2f(f2bf(bf2f(f2bf(x2[e] * c)) + bf2f(f2bf(x1[e] * sn))));
+    }
+    if (hd < Hq) {
+      bf16_t* qp = q_out + (size_t)t * ldq + hd * D;
+      *reinterpret_cast<u32x4*>(qp + v * 8) = pack8(o1);
+      *reinterpret_cast<u32x4*>(qp + half + v * 8) = pack8(o2);
+    } else if (slot >= 0) {
+      bf16_t* dst = kc + (((size_t)(slot / BS) * Hkv + (hd - Hq)) * BS + (slot % BS)) * D;
+      *reinterpret_cast<u32x4*>(dst + v * 8) = pack8(o1);
+      *reinterpret_cast<u32x4*>(dst + half + v * 8) = pack8(o2);
+    }
+  }
+}
+
 }  // namespace
 
 RAGK_API int ragk_rmsnorm(const void* x, int ldx, void* resid, int ldr, const void* w, void* out, int ldo, int rows,
@@ -399,5 +522,26 @@ RAGK_API int ragk_gather_rows(const void* x, int ldx, const int* idx, void* out,
   if (n <= 0) return 0;
   if (H % 8) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(gather_rows_kernel, dim3(n), dim3(NT), 0, st, (const bf16_t*)x, ldx, idx, (bf16_t*)out, ldo, H);
+  return (int)hipGetLastError();
+}
+
+RAGK_API int ragk_add_partials_rmsnorm(const float* P, int S, int M, void* h, int ldh, const void* w, void* out,
+                                       int ldo, int H, float eps, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (H % 8 || H > 8 * PNT * 2 || S < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(add_partials_rmsnorm_kernel, dim3(M), dim3(PNT), 0, st, P, S, M, (bf16_t*)h, ldh,
+                     (const bf16_t*)w, (bf16_t*)out, ldo, H, eps);
+  return (int)hipGetLastError();
+}
+
+// P: [S][T][ldp] fp32 qkv partials (ldp >= (Hq + 2 Hkv) * D); q_out: rotated q [T][ldq] bf16.
+RAGK_API int ragk_rope_kv_partials(const float* P, int S, int T, int ldp, void* q_out, int ldq,
+                                   const int* positions, const float* cos_t, const float* sin_t, const int* slots,
+                                   void* kc, void* vc, int Hq, int Hkv, int D, int BS, hipStream_t st) {
+  if (T <= 0) return 0;
+  if (D % 16 || S < 1) return (int)hipErrorInvalidValue;
+  const int groups = 4;
+  hipLaunchKernelGGL(rope_kv_partials_kernel, dim3(T, groups), dim3(NT), 0, st, P, S, T, ldp, (bf16_t*)q_out, ldq,
+                     positions, cos_t, sin_t, slots, (bf16_t*)kc, (bf16_t*)vc, Hq, Hkv, D, BS);
   return (int)hipGetLastError();
 }

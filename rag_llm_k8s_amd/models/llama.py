@@ -283,10 +283,48 @@ class LlamaModel:
             h = self.be.gather_rows(h, inp.logits_idx)
         return self.be.rmsnorm(h, self.w.norm, self.cfg.rms_norm_eps)
 
+    def _decode_part_ok(self, inp: StepInput, h):
+        if self.comm is not None or inp.meta is None or inp.meta.kind != "decode" or inp.slots is None:
+            return False
+        L, M = self.w.layers[0], h.shape[0]
+        return self.be.part_ok(M, L["wqkv"]) and self.be.part_ok(M, L["wo"]) and self.be.part_ok(M, L["wdown"])
+
+    def hidden_states_decode_part(self, inp: StepInput, h):
+        """Decode step with the split-K partial GEMM (csrc/kernels/gemm_part.hip) for the three
+        small-N projections: qkv / o_proj / down write fp32 partial slabs and the following row
+        kernel reduces them -- rope_kv_partials (qkv) and add_partials_rmsnorm (o_proj -> post-attention
+        norm, down -> next layer's input norm / the final norm), so the reduction adds no launch and
+        the GEMMs stream their weights with every load in flight (qkv 26.7 -> 15 us, o_proj 15 -> 11.6,
+        down 43 -> 30 at batch 32; tools/bench_decode_gemm.py). Same math and bf16 rounding points as
+        hidden_states (bf16 linear outputs, bf16 residual adds)."""
+        be, w, c = self.be, self.w, self.cfg
+        Hq, Hkv, D = self.Hq, self.Hkv, self.D
+        M = h.shape[0]
+        attn = torch.empty((M, Hq * D), dtype=h.dtype, device=h.device)
+        q = torch.empty((M, Hq * D), dtype=h.dtype, device=h.device)
+        layers = w.layers
+        xn = be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
+        for li, L in enumerate(layers):
+            kc, vc = self.kv_cache[li]
+            P = be.gemm_part(xn, L["wqkv"])
+            be.rope_kv_partials(P, q, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
+            be.attn_decode(q, kc, vc, inp.meta, attn, Hq, Hkv, D)
+            P = be.gemm_part(attn, L["wo"])
+            xn = be.add_partials_rmsnorm(P, h, L["ln_post"], c.rms_norm_eps)
+            a = be.gemm(xn, L["wgu"], epi="silu_mul")
+            P = be.gemm_part(a, L["wdown"])
+            nxt = layers[li + 1]["ln_in"] if li + 1 < len(layers) else w.norm
+            xn = be.add_partials_rmsnorm(P, h, nxt, c.rms_norm_eps)
+        if inp.logits_idx is not None:
+            xn = be.gather_rows(xn, inp.logits_idx)
+        return xn
+
     def hidden_states(self, inp: StepInput):
         """Run the decoder stack; returns the final-norm'ed rows selected by logits_idx."""
         be, w = self.be, self.w
         h = be.embed(inp.ids, w.embed)
+        if self._decode_part_ok(inp, h):
+            return self.hidden_states_decode_part(inp, h)
         attn = torch.empty((h.shape[0], self.Hq * self.D), dtype=h.dtype, device=h.device)
         for li, L in enumerate(w.layers):
             self._attn_block(li, L, h, inp, attn)

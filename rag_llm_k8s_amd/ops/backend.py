@@ -108,6 +108,24 @@ class TorchBackend:
             kc[s // KV_BLOCK, :, s % KV_BLOCK] = k[ok]
             vc[s // KV_BLOCK, :, s % KV_BLOCK] = v[ok]
 
+    # split-K decode path (GPU: gemm_part.hip + the consumers in norm.hip) ----------------
+    enable_part = False  # the torch oracle runs the same dataflow when a test switches it on
+
+    def part_ok(self, M, w):
+        return self.enable_part and not isinstance(w, Fp8Weight) and M <= 64
+
+    def gemm_part(self, x, w):
+        return (x.float() @ w.float().t()).unsqueeze(0)
+
+    def add_partials_rmsnorm(self, P, h, w, eps):
+        h.copy_((h.float() + P.sum(0).to(h.dtype).float()).to(h.dtype))
+        return R.rmsnorm(h, w, eps)
+
+    def rope_kv_partials(self, P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D):
+        qkv = P.sum(0).to(q_out.dtype)
+        self.rope_kv(qkv, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)
+        q_out[:, :Hq * D].copy_(qkv[:, :Hq * D])
+
     def attn_prefill(self, q, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
         T = q.shape[0]
         qq = q[:, :Hq * D].reshape(T, Hq, D)
@@ -200,6 +218,22 @@ class NativeBackend(TorchBackend):
 
     def rope_kv(self, qkv, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D, apply_rope=True):
         self.n.rope_kv(qkv, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D, apply_rope=apply_rope)
+
+    enable_part = __import__("os").environ.get("RAGK_DECODE_PART", "1") == "1"
+
+    def part_ok(self, M, w):
+        if not self.enable_part or isinstance(w, Fp8Weight) or M > 64:
+            return False
+        return self.n.gemm_part_slabs(M, w.shape[0], w.shape[1])[1] > 0
+
+    def gemm_part(self, x, w):
+        return self.n.gemm_part(x, w)
+
+    def add_partials_rmsnorm(self, P, h, w, eps):
+        return self.n.add_partials_rmsnorm(P, h, w, eps)
+
+    def rope_kv_partials(self, P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D):
+        self.n.rope_kv_partials(P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)
 
     def attn_prefill(self, q, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
         return self.n.attn_prefill(q, kc, vc, meta.cu_q, meta.kv_lens, meta.tiles, out, Hq, Hkv, D, causal=True,

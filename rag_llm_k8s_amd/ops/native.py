@@ -148,6 +148,32 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
     return out
 
 
+def gemm_part_slabs(M, N, K, ks=None):
+    """(ks_steps, S) of the split-K partial GEMM for this shape (0, 0 if unsupported)."""
+    ks = ks or _lib.lib().ragk_gemm_part_ksteps(M, N, K)
+    if ks <= 0 or K % (64 * ks):
+        return 0, 0
+    return ks, K // (64 * ks)
+
+
+def gemm_part(x, w, out=None, ks=None):
+    """Decode GEMM v5 (csrc/kernels/gemm_part.hip): fp32 split-K partials P[S, M, N] with
+    P.sum(0) = x @ w^T. The consumer (add_partials_rmsnorm / rope_kv_partials) does the reduction."""
+    _bf16_2d(x, "x")
+    _bf16_2d(w, "w")
+    M, K = x.shape
+    N = w.shape[0]
+    _req(w.shape[1] == K and M <= 64, "gemm_part shape %s x %s" % (tuple(x.shape), tuple(w.shape)))
+    ks, S = gemm_part_slabs(M, N, K, ks)
+    _req(S > 0, "gemm_part: unsupported K=%d" % K)
+    if out is None:
+        out = torch.empty((S, M, N), dtype=torch.float32, device=x.device)
+    _req(out.dtype == torch.float32 and out.is_contiguous() and out.numel() >= S * M * N, "gemm_part out")
+    check(_lib.lib().ragk_gemm_part(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), M, N, K,
+                                    ks, stream_ptr()), "ragk_gemm_part")
+    return out[:S] if out.dim() == 3 else out
+
+
 STREAM_S_OVERRIDE = 0  # tuning hook (tools/tune_stream.py)
 
 
@@ -285,6 +311,36 @@ def rope_kv(qkv, positions, cos_t, sin_t, slots, k_cache, v_cache, Hq, Hkv, D, a
     check(_lib.lib().ragk_rope_kv(qkv.data_ptr(), qkv.stride(0), positions.data_ptr(), ptr(cos_t), ptr(sin_t),
                                   ptr(slots), ptr(k_cache), ptr(v_cache), T, Hq, Hkv, D, BS, int(apply_rope),
                                   stream_ptr()), "ragk_rope_kv")
+
+
+def add_partials_rmsnorm(P, h, w, eps, out=None):
+    """h <- bf16(h + bf16(P.sum(0))) in place; returns rmsnorm(h) * w (split-K decode consumer)."""
+    _bf16_2d(h, "h")
+    M, H = h.shape
+    _req(P.dtype == torch.float32 and P.is_contiguous() and P.dim() == 3 and P.shape[1:] == (M, H), "partials shape")
+    _req(w.is_cuda and w.dtype == torch.bfloat16 and w.numel() == H, "norm weight")
+    out = torch.empty_like(h) if out is None else out
+    _req(out.shape == (M, H) and out.stride(1) == 1, "out")
+    check(_lib.lib().ragk_add_partials_rmsnorm(P.data_ptr(), P.shape[0], M, h.data_ptr(), h.stride(0), w.data_ptr(),
+                                               out.data_ptr(), out.stride(0), H, float(eps), stream_ptr()),
+          "ragk_add_partials_rmsnorm")
+    return out
+
+
+def rope_kv_partials(P, q_out, positions, cos_t, sin_t, slots, k_cache, v_cache, Hq, Hkv, D):
+    """qkv = bf16(P.sum(0)); RoPE'd q -> q_out[:, :Hq*D]; RoPE'd k and v -> paged cache."""
+    _req(P.dtype == torch.float32 and P.is_contiguous() and P.dim() == 3, "partials")
+    S, T, ldp = P.shape
+    _req(ldp >= (Hq + 2 * Hkv) * D, "qkv width")
+    _bf16_2d(q_out, "q_out")
+    _req(q_out.shape[0] == T and q_out.shape[1] >= Hq * D, "q_out shape")
+    _req(positions.dtype == torch.int32 and positions.numel() == T, "positions")
+    _req(slots is not None and slots.dtype == torch.int32 and slots.numel() == T, "slots")
+    _req(k_cache.dim() == 4 and k_cache.shape[1] == Hkv and k_cache.shape[3] == D, "cache layout")
+    check(_lib.lib().ragk_rope_kv_partials(P.data_ptr(), S, T, ldp, q_out.data_ptr(), q_out.stride(0),
+                                           positions.data_ptr(), ptr(cos_t), ptr(sin_t), slots.data_ptr(),
+                                           k_cache.data_ptr(), v_cache.data_ptr(), Hq, Hkv, D, k_cache.shape[2],
+                                           stream_ptr()), "ragk_rope_kv_partials")
 
 
 def pool_l2norm(hidden, cu, mode="cls", normalize=True, out=None):

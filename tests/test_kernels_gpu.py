@@ -411,3 +411,58 @@ def test_gemm_stream_bf16(native, M, N, K):
         y = native.gemm(x, R.pack_gate_up(g, u), epi="silu_mul", path=5)
         ref2 = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
         assert rel_err(y, ref2) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 32, 33, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (384, 512), (1000, 1024)])
+def test_gemm_part(native, M, N, K):
+    """Decode GEMM v5: fp32 split-K partial slabs sum to x @ w^T."""
+    torch.manual_seed(3)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    ks, S = native.gemm_part_slabs(M, N, K)
+    if S == 0:
+        pytest.skip("shape not supported by gemm_part")
+    P = native.gemm_part(x, w)
+    assert P.shape == (S, M, N)
+    assert rel_err(P.sum(0), x.float() @ w.float().t()) < 2e-3
+
+
+@pytest.mark.parametrize("S,M,H", [(1, 3, 384), (4, 32, 4096), (7, 17, 4096)])
+def test_add_partials_rmsnorm(native, S, M, H):
+    """Split-K consumer: h <- bf16(h + bf16(sum P)), out = rmsnorm(h) (bit-exact with the torch oracle
+    for h; the norm within bf16 rounding)."""
+    torch.manual_seed(11)
+    P = torch.randn(S, M, H, device=DEV)
+    h = torch.randn(M, H, device=DEV).bfloat16()
+    w = torch.randn(H, device=DEV).bfloat16()
+    h_ref = (h.cpu().float() + P.cpu().sum(0).bfloat16().float()).bfloat16()
+    ref = R.rmsnorm(h_ref, w.cpu(), 1e-5)
+    y = native.add_partials_rmsnorm(P, h, w, 1e-5)
+    # fp32 slab sums may differ in the last ulp from torch's order -> rare 1-ulp bf16 flips
+    assert (h.cpu().float() - h_ref.float()).abs().max().item() <= 0.0625
+    assert rel_err(h.cpu(), h_ref) < 1e-3
+    assert rel_err(y.cpu(), ref) < 4e-3
+
+
+def test_rope_kv_partials(native):
+    torch.manual_seed(12)
+    S, T, Hq, Hkv, D, BS = 4, 33, 8, 2, 128, 64
+    W = (Hq + 2 * Hkv) * D
+    P = torch.randn(S, T, W, device=DEV)
+    pos = torch.arange(T, dtype=torch.int32, device=DEV) + 7
+    cos, sin = R.rope_tables(D, 1024, theta=500000.0,
+                             scaling={"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                      "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    slots = torch.arange(T, dtype=torch.int32, device=DEV) + 64
+    kc = torch.zeros(4, Hkv, BS, D, device=DEV).bfloat16()
+    vc = torch.zeros_like(kc)
+    q = torch.zeros(T, Hq * D, device=DEV).bfloat16()
+    native.rope_kv_partials(P, q, pos, cos, sin, slots, kc, vc, Hq, Hkv, D)
+    # oracle: plain rope_kv on the bf16-rounded sum
+    qkv = P.sum(0).bfloat16()
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    native.rope_kv(qkv, pos, cos, sin, slots, kc2, vc2, Hq, Hkv, D)
+    assert rel_err(q, qkv[:, :Hq * D]) < 1e-3
+    assert rel_err(kc, kc2) < 1e-3 and rel_err(vc, vc2) < 1e-3

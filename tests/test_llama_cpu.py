@@ -133,3 +133,24 @@ def _prefill_logits(model, ids):
                     host_kv_lens=[n], host_q_lens=[n])
     return model.forward(StepInput(torch.tensor(ids, dtype=torch.int32), torch.arange(n, dtype=torch.int32),
                                    torch.arange(64, 64 + n, dtype=torch.int32), meta, None))
+
+
+def test_split_k_decode_path_matches_plain_decode(tiny):
+    """The split-K decode dataflow (partial slabs reduced by rope_kv_partials / add_partials_rmsnorm,
+    the GPU decode path) generates the same greedy tokens as the plain decode path."""
+    cfg, hf, sd = tiny
+    w = LlamaWeights.from_state_dict(cfg, sd, "cpu")
+    torch.manual_seed(5)
+    prompts = [torch.randint(3, cfg.vocab_size, (n,)).tolist() for n in (23, 40, 9)]
+    params = SamplingParams(max_new_tokens=10, do_sample=False, ignore_eos=True)
+    outs = []
+    for part in (False, True):
+        model = LlamaModel(cfg, w, "cpu", max_positions=512)
+        model.be.enable_part = part
+        calls = []
+        orig = model.hidden_states_decode_part
+        model.hidden_states_decode_part = lambda inp, h: (calls.append(1), orig(inp, h))[1]
+        eng = LLMEngine(model, num_blocks=32, max_batch=4, max_model_len=512, use_graphs=False)
+        outs.append(eng.generate(prompts, params))
+        assert bool(calls) == part
+    assert outs[0] == outs[1]
