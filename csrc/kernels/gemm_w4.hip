@@ -225,56 +225,142 @@ __device__ __forceinline__ void w4_read_frag(const char* buf, int s, int q, int 
 }
 
 // One K-tile, written in final instruction order (file built with -enable-misched=0).
-// STAGE: issue tile t+2's DMA; READ: read F0(t+1).
-template <bool STAGE, bool READ>
+// STAGE: issue tile t+2's DMA; READ: read F0(t+1). The 128 MFMAs (m < 64: F0, m >= 64: F1) are split
+// S1 | 128-S1-S3 | S3 by the two barriers; the 16 F1 reads go 1:1 into the first MFMAs of segment 1,
+// the 16 DMAs evenly through segment 2, the 16 F0(t+1) reads evenly through segment 3. The split
+// was set from the stamp build's cycle anatomy (tools/gemm_stamps.py).
+constexpr int W4_S1 = 32, W4_S3 = 16;
+
+__device__ __forceinline__ void w4_mfma_m(f32x4 (&acc)[8][8], const bf16x8 (&a0)[8], const bf16x8 (&b0)[8],
+                                          const bf16x8 (&a1)[8], const bf16x8 (&b1)[8], int m) {
+  if (m < 64) w4_mfma(acc, a0, b0, m);
+  else w4_mfma(acc, a1, b1, m - 64);
+}
+
+template <bool STAGE, bool READ, bool STAMP = false, int S1 = W4_S1, int S3 = W4_S3>
 __device__ __forceinline__ void w4_iter(char* smem, int t, i32x4 srd_a, i32x4 srd_b, const int (&off_a)[8],
                                         const int (&off_b)[8], int wid, int wr, int wc, int fr, int fh,
                                         f32x4 (&acc)[8][8], bf16x8 (&a0)[8], bf16x8 (&b0)[8], bf16x8 (&a1)[8],
-                                        bf16x8 (&b1)[8]) {
+                                        bf16x8 (&b1)[8], unsigned long long (&stp)[5]) {
+  static_assert(S1 >= 16 && S1 <= 64 && S3 >= 16 && S3 <= 64, "segment split");
+  constexpr int N2 = 128 - S1 - S3;
   char* buf = smem + (t & 1) * W_BUF;
-  // ---------------- seg 1: read F1(t), one per MFMA | MFMA F0 #0..23 ----------------------
+  unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+  if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
+  // ---------------- seg 1: read F1(t), one per MFMA | MFMA #0..S1-1 ------------------------
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    w4_read_frag(buf, 1, q, wr, wc, fr, fh, a1, b1);
-    w4_mfma(acc, a0, b0, q);
+  for (int m = 0; m < S1; ++m) {
+    if (m < 16) w4_read_frag(buf, 1, m, wr, wc, fr, fh, a1, b1);
+    w4_mfma_m(acc, a0, b0, a1, b1, m);
   }
-#pragma unroll
-  for (int m = 16; m < 24; ++m) w4_mfma(acc, a0, b0, m);
+  if constexpr (STAMP) t1 = __builtin_amdgcn_s_memtime();
+  // builtin (not inline-asm) waits: hipcc's waitcnt pass sees them and adds no redundant waits
   __builtin_amdgcn_s_waitcnt(W_LGKM0);  // every read of buffer t&1 retired
   w4_barrier();
-  // ---------------- seg 2: 16 DMAs of tile t+2 -> buffer t&1, one per 5 MFMAs | F0 #24..63, F1 #0..47
+  if constexpr (STAMP) t2 = __builtin_amdgcn_s_memtime();
+  // ---------------- seg 2: 16 DMAs of tile t+2 -> buffer t&1 (spread) | MFMA #S1..127-S3 -----
+  static_assert(N2 % 16 == 0 && (S3 == 16 || S3 == 24 || S3 == 32), "segment split");
+  constexpr int DSTEP = N2 / 16;  // MFMAs per DMA
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
+  for (int i = 0; i < N2; ++i) {
     if constexpr (STAGE) {
-      if (q < 8) blds16(srd_a, off_a[q], (t + 2) * WBK * 2, buf + (wid * 8 + q) * 1024);
-      else blds16(srd_b, off_b[q - 8], (t + 2) * WBK * 2, buf + W_TILE_A + (wid * 8 + q - 8) * 1024);
+      if (i % DSTEP == 0) {
+        const int q = i / DSTEP;
+        if (q < 8) blds16(srd_a, off_a[q], (t + 2) * WBK * 2, buf + (wid * 8 + q) * 1024);
+        else blds16(srd_b, off_b[q - 8], (t + 2) * WBK * 2, buf + W_TILE_A + (wid * 8 + q - 8) * 1024);
+      }
     }
-#pragma unroll
-    for (int u = 0; u < 5; ++u) {
-      const int m = 24 + 5 * q + u;  // 24..103 over F0 (24..63) then F1 (64..103 -> 0..39)
-      if (m < 64) w4_mfma(acc, a0, b0, m);
-      else w4_mfma(acc, a1, b1, m - 64);
-    }
+    w4_mfma_m(acc, a0, b0, a1, b1, S1 + i);
   }
-#pragma unroll
-  for (int m = 40; m < 48; ++m) w4_mfma(acc, a1, b1, m);
+  if constexpr (STAMP) t3 = __builtin_amdgcn_s_memtime();
   if constexpr (STAGE) __builtin_amdgcn_s_waitcnt(W_VM16);  // tile t+1 landed (t+2's 16 in flight)
   else __builtin_amdgcn_s_waitcnt(W_VM0);
   w4_barrier();
-  // ---------------- seg 3: read F0(t+1) from buffer (t+1)&1, one per MFMA | F1 #48..63 ------
+  if constexpr (STAMP) {
+    const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+    stp[0] += t1 - t0;  // seg 1 issue
+    stp[1] += t2 - t1;  // lgkmcnt(0) + barrier 1
+    stp[2] += t3 - t2;  // seg 2 issue
+    stp[3] += t4 - t3;  // vmcnt(16) + barrier 2
+  }
+  // ---------------- seg 3: read F0(t+1) from buffer (t+1)&1 (spread) | MFMA #128-S3..127 ----
   const char* nbuf = smem + ((t + 1) & 1) * W_BUF;
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    if constexpr (READ) w4_read_frag(nbuf, 0, q, wr, wc, fr, fh, a0, b0);
-    w4_mfma(acc, a1, b1, 48 + q);
+  for (int i = 0; i < S3; ++i) {
+    if constexpr (READ) {
+      if constexpr (S3 == 16) {
+        w4_read_frag(nbuf, 0, i, wr, wc, fr, fh, a0, b0);
+      } else if constexpr (S3 == 32) {
+        if (i % 2 == 0) w4_read_frag(nbuf, 0, i / 2, wr, wc, fr, fh, a0, b0);
+      } else {  // 24: two reads per three MFMAs
+        if (i % 3 < 2) w4_read_frag(nbuf, 0, 2 * (i / 3) + i % 3, wr, wc, fr, fh, a0, b0);
+      }
+    }
+    w4_mfma_m(acc, a0, b0, a1, b1, 128 - S3 + i);
+  }
+  if constexpr (STAMP) stp[4] += __builtin_amdgcn_s_memtime() - t0;  // whole iteration
+}
+
+// Single-barrier iteration (S3 == 0 selects it): one barrier per K-tile retires both the F1(t) reads
+// (lgkmcnt(0)) and this wave's DMA of tile t+1 (vmcnt(0)); after it the 16 DMAs of tile t+2 go
+// through the first 32 MFMAs of segment 2 (F0 #S1..63) and the 16 F0(t+1) reads through the 64 F1
+// MFMAs (a0/b0 are dead once F0 #63 has issued). No third segment, no second barrier.
+template <bool STAGE, bool READ, bool STAMP, int S1>
+__device__ __forceinline__ void w4_iter1(char* smem, int t, i32x4 srd_a, i32x4 srd_b, const int (&off_a)[8],
+                                         const int (&off_b)[8], int wid, int wr, int wc, int fr, int fh,
+                                         f32x4 (&acc)[8][8], bf16x8 (&a0)[8], bf16x8 (&b0)[8], bf16x8 (&a1)[8],
+                                         bf16x8 (&b1)[8], unsigned long long (&stp)[5]) {
+  static_assert(S1 >= 16 && S1 <= 48, "segment split");
+  constexpr int NF0 = 64 - S1;  // F0 MFMAs after the barrier
+  char* buf = smem + (t & 1) * W_BUF;
+  const char* nbuf = smem + ((t + 1) & 1) * W_BUF;
+  unsigned long long t0 = 0, t1 = 0, t2 = 0;
+  if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+  for (int m = 0; m < S1; ++m) {
+    if (m < 16) w4_read_frag(buf, 1, m, wr, wc, fr, fh, a1, b1);
+    w4_mfma(acc, a0, b0, m);
+  }
+  if constexpr (STAMP) t1 = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_s_waitcnt(W_LGKM0);  // F1(t) in registers: buffer t&1 free
+  __builtin_amdgcn_s_waitcnt(W_VM0);    // this wave's part of tile t+1 landed
+  w4_barrier();
+  if constexpr (STAMP) t2 = __builtin_amdgcn_s_memtime();
+  // F0 #S1..63 with the 16 DMAs spread over them
+#pragma unroll
+  for (int i = 0; i < NF0; ++i) {
+    if constexpr (STAGE) {
+      if ((i * 16) % NF0 < 16) {
+        const int q = (i * 16) / NF0;
+        if (q < 8) blds16(srd_a, off_a[q], (t + 2) * WBK * 2, buf + (wid * 8 + q) * 1024);
+        else blds16(srd_b, off_b[q - 8], (t + 2) * WBK * 2, buf + W_TILE_A + (wid * 8 + q - 8) * 1024);
+      }
+    }
+    w4_mfma(acc, a0, b0, S1 + i);
+  }
+  // F1 #0..63 with the 16 F0(t+1) reads, one per 4 MFMAs
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    if constexpr (READ) {
+      if (i % 4 == 0) w4_read_frag(nbuf, 0, i / 4, wr, wc, fr, fh, a0, b0);
+    }
+    w4_mfma(acc, a1, b1, i);
+  }
+  if constexpr (STAMP) {
+    const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+    stp[0] += t1 - t0;
+    stp[1] += t2 - t1;
+    stp[2] += t3 - t2;
+    stp[4] += t3 - t0;
   }
 }
 
-template <int EPI, bool OUT_F32>
+template <int EPI, bool OUT_F32, bool STAMP = false, int S1 = W4_S1, int S3 = W4_S3>
 __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __restrict__ A, int lda,
                                                                 const bf16_t* __restrict__ B, int ldb, void* C,
                                                                 int ldc, const bf16_t* __restrict__ bias,
-                                                                const bf16_t* resid, int ldr, int M, int N, int K) {
+                                                                const bf16_t* resid, int ldr, int M, int N, int K,
+                                                                unsigned long long* dbg) {
   __shared__ __attribute__((aligned(16))) char smem[W4_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -322,14 +408,39 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
   __builtin_amdgcn_s_waitcnt(W_LGKM0);
   __builtin_amdgcn_sched_barrier(0);
 
+  unsigned long long stp[5] = {0, 0, 0, 0, 0};
   int t = 0;
+  if constexpr (S3 == 0) {
+    for (; t + 2 < nk; ++t)
+      w4_iter1<true, true, STAMP, S1>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1, b1,
+                                      stp);
+    if (t + 1 < nk) {
+      w4_iter1<false, true, false, S1>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1,
+                                       b1, stp);
+      ++t;
+    }
+    w4_iter1<false, false, false, S1>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1, b1,
+                                      stp);
+  } else {
   for (; t + 2 < nk; ++t)
-    w4_iter<true, true>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1, b1);
+    w4_iter<true, true, STAMP, S1, S3>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1,
+                                       b1, stp);
   if (t + 1 < nk) {
-    w4_iter<false, true>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1, b1);
+    w4_iter<false, true, false, S1, S3>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1,
+                                        b1, stp);
     ++t;
   }
-  w4_iter<false, false>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1, b1);
+  w4_iter<false, false, false, S1, S3>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1, b1,
+                                       stp);
+  }
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      unsigned long long* d = dbg + ((size_t)blockIdx.x * 4 + wid) * 6;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) d[i] = stp[i];
+      d[5] = (unsigned long long)(nk - 2);
+    }
+  }
   __builtin_amdgcn_s_waitcnt(W_VM0);
   w4_pin_acc(acc);
 
@@ -341,7 +452,8 @@ int launch_w4(const void* A, int lda, const void* B, int ldb, void* C, int ldc, 
               int ldr, int M, int N, int K, hipStream_t st) {
   const int nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
   hipLaunchKernelGGL((gemm_w4_kernel<EPI, F32>), dim3(nwg), dim3(W4_THREADS), 0, st, (const bf16_t*)A, lda,
-                     (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K);
+                     (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K,
+                     nullptr);
   return (int)hipGetLastError();
 }
 
@@ -376,4 +488,42 @@ RAGK_API int ragk_gemm_w4(const void* A, int lda, const void* B, int ldb, void* 
       return (int)hipErrorInvalidValue;
   }
 #undef RAGK_W4_CASE
+}
+
+// Diagnostic / tuning builds of the EPI_NONE kernel (tools/gemm_stamps.py). variant selects the
+// segment split (S1, S3); stamp != 0 adds s_memtime stamps around the K-loop segments, dbg:
+// [nwg][4 waves][6] u64 = seg1, barrier1, seg2, barrier2, whole iteration (sums over the
+// steady-state iterations), iteration count.
+template <bool STAMP, int S1, int S3>
+int launch_w4_diag(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
+                   unsigned long long* dbg, hipStream_t st) {
+  const int nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI_NONE, false, STAMP, S1, S3>), dim3(nwg), dim3(W4_THREADS), 0, st,
+                     (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, nullptr, nullptr, 0, M, N, K, dbg);
+  return (int)hipGetLastError();
+}
+
+RAGK_API int ragk_gemm_w4_diag(int variant, int stamp, const void* A, int lda, const void* B, int ldb, void* C,
+                               int ldc, int M, int N, int K, unsigned long long* dbg, hipStream_t st) {
+  if (K % WBK != 0 || N % 8 != 0 || (long long)M * lda * 2 >= (1LL << 31) || (long long)N * ldb * 2 >= (1LL << 31))
+    return (int)hipErrorInvalidValue;
+  if (stamp && dbg == nullptr) return (int)hipErrorInvalidValue;
+#define RAGK_W4D(V, S1, S3)                                                                                  \
+  case V:                                                                                                    \
+    return stamp ? launch_w4_diag<true, S1, S3>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)                    \
+                 : launch_w4_diag<false, S1, S3>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);
+  switch (variant) {
+    RAGK_W4D(0, 32, 16)
+    RAGK_W4D(1, 24, 24)
+    RAGK_W4D(2, 40, 24)
+    RAGK_W4D(3, 32, 32)
+    RAGK_W4D(4, 48, 16)
+    RAGK_W4D(5, 56, 24)
+    RAGK_W4D(6, 32, 0)
+    RAGK_W4D(7, 24, 0)
+    RAGK_W4D(8, 40, 0)
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+#undef RAGK_W4D
 }

@@ -26,6 +26,7 @@ _SIGS = {
     "ragk_gemm_pp_set_variant": [I],
     "ragk_gemm_w4": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_part": [P, I, P, I, P, I, I, I, I, S],
+    "ragk_gemm_w4_diag": [I, I, P, I, P, I, P, I, I, I, I, P, S],
     "ragk_gemm_part_ksteps": [I, I, I],
     "ragk_add_partials_rmsnorm": [P, I, I, P, I, P, P, I, I, F, S],
     "ragk_rope_kv_partials": [P, I, I, I, P, I, P, P, P, P, P, P, I, I, I, I, S],
