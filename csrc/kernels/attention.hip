@@ -23,11 +23,13 @@
 // Replaces reference ops K5/K6 (causal GQA attention in transformers' Llama SDPA path,
 // [dep] modeling_llama.py:191-215) and E3 (XLM-R/BERT bidirectional attention).
 #include "common.h"
+#include <type_traits>
 using namespace ragk;
 
 namespace {
 
 constexpr int KT = 64;  // keys per tile == KV-cache page size
+constexpr int MAX_BT = 2048;  // prefill block-table row cached in LDS (128k tokens)
 constexpr float RESCALE_LOG2 = 8.f;  // deferred-rescale threshold (log2 units)
 
 // max with the xor-16 / xor-32 lane partner without an LDS round trip (gfx950
@@ -73,14 +75,22 @@ __device__ __forceinline__ bf16x4 tr_read(const char* p) {
 
 // Stage one 64-row tile (K or V) into LDS with glds; `pieces_per_wave` pieces per wave.
 // row_src(row) returns the global row pointer for tile row `row`.
-template <int D, bool IS_V, typename RowSrc>
+template <int D, bool IS_V, bool NT = false, int NW = 0, typename RowSrc>
 __device__ __forceinline__ void stage_kv(char* lds_tile, int wid, int nwaves, int lane, RowSrc row_src) {
   constexpr int NC = Cfg<D>::NC, PIECES = Cfg<D>::PIECES, RPP = Cfg<D>::RPP;
-  for (int p = wid; p < PIECES; p += nwaves) {
+  constexpr int PPW = NW > 0 ? PIECES / NW : PIECES;  // NW > 0: compile-time wave count, unrolled
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int p = NW > 0 ? wid + NW * i : wid + nwaves * i;
+    if (NW == 0 && p >= PIECES) break;
     const int row = p * RPP + lane / NC;
     const int ph = lane % NC;
     const int c = ph ^ (IS_V ? vswz<D>(row) : kswz<D>(row));
-    glds16(row_src(row) + c * 8, lds_tile + p * 1024);
+    if constexpr (NT)  // once-read K/V stream (decode): non-temporal LDS-DMA
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(row_src(row) + c * 8),
+                                       (__attribute__((address_space(3))) void*)(lds_tile + p * 1024), 16, 0, 2);
+    else
+      glds16(row_src(row) + c * 8, lds_tile + p * 1024);
   }
 }
 
@@ -125,8 +135,11 @@ struct PrefillArgs {
   float scale_log2;
 };
 
-template <int D, int GB, bool CAUSAL, bool PAGED>
+__device__ unsigned long long* g_attn_dbg = nullptr;  // stamp build only
+
+template <int D, int GB, bool CAUSAL, bool PAGED, bool STAMP = false>
 __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
+  unsigned long long stp[6] = {0, 0, 0, 0, 0, 0};
   using C = Cfg<D>;
   constexpr int QT = 32 * (4 / GB);  // query positions per block
   __shared__ __attribute__((aligned(16))) char smem[4 * C::TILEB];  // [buf][K|V]
@@ -175,15 +188,24 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
   const int kv_off = PAGED ? 0 : a.cu_kv[seq];
   const int* bt = PAGED ? a.block_tables + (size_t)seq * a.bt_stride : nullptr;
 
+  // the sequence's block-table row, cached in LDS once (a global load per tile sat on the DMA
+  // issue path: ~1.2k of ~5.7k wave cycles per tile in the stamp build, tools/attn_stamps.py)
+  __shared__ int s_bt[PAGED ? MAX_BT : 1];
+  if constexpr (PAGED) {
+    for (int i = threadIdx.x; i < n_kt; i += 256) s_bt[i] = bt[i];
+    __syncthreads();
+  }
+  int bt_next = PAGED && n_kt > 0 ? s_bt[0] : 0;  // block of the tile staged next
+
   auto stage = [&](int kt, int buf) {
     char* sK = smem + buf * 2 * C::TILEB;
     char* sV = sK + C::TILEB;
     if constexpr (PAGED) {
-      const size_t base = ((size_t)bt[kt] * a.Hkv + kvh) * KT * D;
+      const size_t base = ((size_t)bt_next * a.Hkv + kvh) * KT * D;
       const bf16_t* kb = a.k + base;
       const bf16_t* vb = a.v + base;
-      stage_kv<D, false>(sK, wid_u, 4, lane, [&](int r) { return kb + (size_t)r * D; });
-      stage_kv<D, true>(sV, wid_u, 4, lane, [&](int r) { return vb + (size_t)r * D; });
+      stage_kv<D, false, false, 4>(sK, wid_u, 4, lane, [&](int r) { return kb + (size_t)r * D; });
+      stage_kv<D, true, false, 4>(sV, wid_u, 4, lane, [&](int r) { return vb + (size_t)r * D; });
     } else {
       const int k0 = kt * KT;
       auto rowp = [&](const bf16_t* base, int r) {
@@ -191,24 +213,27 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
         tok = tok < kv_len ? tok : kv_len - 1;
         return base + (size_t)(kv_off + tok) * a.kv_stride + kvh * D;
       };
-      stage_kv<D, false>(sK, wid_u, 4, lane, [&](int r) { return rowp(a.k, r); });
-      stage_kv<D, true>(sV, wid_u, 4, lane, [&](int r) { return rowp(a.v, r); });
+      stage_kv<D, false, false, 4>(sK, wid_u, 4, lane, [&](int r) { return rowp(a.k, r); });
+      stage_kv<D, true, false, 4>(sV, wid_u, 4, lane, [&](int r) { return rowp(a.v, r); });
     }
   };
 
   if (n_kt > 0) stage(0, 0);
+  if constexpr (PAGED) bt_next = n_kt > 1 ? s_bt[1] : 0;
   wait_vmcnt0();
   __syncthreads();
 
   for (int kt = 0; kt < n_kt; ++kt) {
+    unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+    if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
     const int cur = kt & 1;
-    if (kt + 1 < n_kt) stage(kt + 1, cur ^ 1);
     const char* sK = smem + cur * 2 * C::TILEB;
     const char* sV = sK + C::TILEB;
     const int k0 = kt * KT;
-    if (!CAUSAL || k0 <= wave_pmax) {
-      // ---- S^T = K Q^T ----
-      f32x4 s[4][2];
+    const bool active = !CAUSAL || k0 <= wave_pmax;
+    // ---- S^T = K Q^T ----
+    f32x4 s[4][2];
+    if (active) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         s[t][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -220,6 +245,14 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
           s[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][ks], s[t][1], 0, 0, 0);
         }
       }
+    }
+    if constexpr (STAMP) t1 = __builtin_amdgcn_s_memtime();
+    // next tile's DMA issued behind the QK^T MFMAs (async-STAGE split: the issue overlaps the MFMA
+    // pipe instead of delaying it); every wave stages its pieces, active or not
+    if (kt + 1 < n_kt) stage(kt + 1, cur ^ 1);
+    if constexpr (PAGED) bt_next = kt + 2 < n_kt ? s_bt[kt + 2] : 0;  // consumed next iteration
+    if constexpr (STAMP) t2 = t3 = t4 = __builtin_amdgcn_s_memtime();
+    if (active) {
       // ---- online softmax (per query column, lane-local + xor 16/32) ----
       // Max on the raw scores (scale > 0 keeps the order); the log2 scale is folded into one FMA
       // per element. Deferred rescale: the reference max m_i only moves when the tile max exceeds
@@ -228,8 +261,9 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
       const bool need_mask = CAUSAL ? (k0 + KT - 1 > ctx0 + pbase) || (k0 + KT > kv_len) : (k0 + KT > kv_len);
       const float c = a.scale_log2;
       float alpha[2];
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
+      // one wave-uniform branch per tile (the masked body only runs on diagonal / ragged tiles)
+      auto softmax = [&](auto mask_tag, const int qt) {
+        constexpr bool MASK = decltype(mask_tag)::value;
         const int qpos = ctx0 + pbase + 16 * qt + fr;
         float mx = -INFINITY;
 #pragma unroll
@@ -237,7 +271,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float x = s[t][qt][r];
-            if (need_mask) {
+            if constexpr (MASK) {
               const int kj = k0 + 16 * t + 4 * fh + r;
               const bool ok = kj < kv_len && (!CAUSAL || kj <= qpos);
               x = ok ? x : -INFINITY;
@@ -264,6 +298,13 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
             ls += p;
           }
         l_i[qt] = l_i[qt] * alpha[qt] + ls;
+      };
+      if (need_mask) {
+        softmax(std::true_type{}, 0);
+        softmax(std::true_type{}, 1);
+      } else {
+        softmax(std::false_type{}, 0);
+        softmax(std::false_type{}, 1);
       }
       if (__builtin_amdgcn_ballot_w64(alpha[0] != 1.f || alpha[1] != 1.f)) {
 #pragma unroll
@@ -277,6 +318,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) pb[ks][qt] = pack_p(s[2 * ks][qt], s[2 * ks + 1][qt]);
+      if constexpr (STAMP) t3 = __builtin_amdgcn_s_memtime();
 #pragma unroll
       for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
@@ -285,9 +327,26 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
           o[dt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[ks][0], o[dt][0], 0, 0, 0);
           o[dt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[ks][1], o[dt][1], 0, 0, 0);
         }
+      if constexpr (STAMP) t4 = __builtin_amdgcn_s_memtime();
     }
     wait_vmcnt0();
     __syncthreads();
+    if constexpr (STAMP) {
+      const unsigned long long t5 = __builtin_amdgcn_s_memtime();
+      stp[0] += t2 - t1;  // DMA issue of the next tile
+      stp[1] += t1 - t0;  // QK^T (K reads + 32 MFMA issue)
+      stp[2] += t3 - t2;  // softmax (+ waiting for the QK^T results)
+      stp[3] += t4 - t3;  // PV (V tr-reads + 32 MFMA issue)
+      stp[4] += t5 - t4;  // vmcnt(0) + barrier
+      stp[5] += 1;
+    }
+  }
+  if constexpr (STAMP) {
+    if (lane == 0 && g_attn_dbg) {
+      unsigned long long* d = g_attn_dbg + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wid) * 6;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) d[i] = stp[i];
+    }
   }
 
   // ---- finalize: O = O^T / l, store 4 consecutive d (8 B) per (dt, qt) ----
@@ -326,7 +385,7 @@ struct DecodeArgs {
   float scale_log2;
 };
 
-template <int D, int G>
+template <int D, int G, bool NT = false>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a) {
   using C = Cfg<D>;
   static_assert(G <= 16, "at most 16 query heads per KV head");
@@ -365,14 +424,16 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a) {
     const bf16_t* vb = a.vc + base;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous tile's V reads retired
     // V tile -> wave-private LDS (transposed reads later)
-    stage_kv<D, true>(sV, 0, 1, lane, [&](int r) { return vb + (size_t)r * D; });
+    stage_kv<D, true, NT, 1>(sV, 0, 1, lane, [&](int r) { return vb + (size_t)r * D; });
     // K fragments straight to VGPRs
     bf16x8 kf[4][C::KS];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int s = 0; s < C::KS; ++s)
-        kf[t][s] = *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
+        kf[t][s] = NT ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D +
+                                                                                  32 * s + 8 * fh))
+                      : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
     f32x4 s4[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -488,6 +549,22 @@ hipError_t launch_prefill(const PrefillArgs& a, int n_tiles, hipStream_t st) {
 
 }  // namespace
 
+// Stamp build of the Llama prefill config (D 128, 4 heads per block, causal, paged): per wave
+// [DMA issue, QK^T, softmax, PV, wait+barrier, tiles] s_memtime sums into dbg[grid][4 waves][6].
+RAGK_API int ragk_attn_prefill_stamp(const void* q, int q_stride, const void* k, const void* v,
+                                     const int* block_tables, int bt_stride, const int* cu_q, const int* kv_lens,
+                                     const int* tiles, int n_tiles, void* out, int out_stride, int Hq, int Hkv,
+                                     float scale, unsigned long long* dbg, hipStream_t st) {
+  if (n_tiles <= 0 || Hq % Hkv || (Hq / Hkv) % 4) return (int)hipErrorInvalidValue;
+  hipMemcpyToSymbolAsync(HIP_SYMBOL(g_attn_dbg), &dbg, sizeof(dbg), 0, hipMemcpyHostToDevice, st);
+  PrefillArgs a{(const bf16_t*)q, q_stride, (const bf16_t*)k, (const bf16_t*)v, 0, block_tables, bt_stride,
+                cu_q, nullptr, kv_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, scale * 1.4426950408889634f};
+  const int G = Hq / Hkv;
+  dim3 grid(n_tiles, Hkv * (G / 4));
+  hipLaunchKernelGGL((attn_prefill_kernel<128, 4, true, true, true>), grid, dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
 // Returns the query positions per block (the host builds `tiles` with this step).
 RAGK_API int ragk_attn_prefill_qtile(int Hq, int Hkv) {
   const int G = Hq / Hkv;
@@ -522,6 +599,14 @@ RAGK_API int ragk_attn_prefill(const void* q, int q_stride, const void* k, const
   return (int)hipErrorInvalidValue;
 }
 
+// K/V cache-policy switch for decode (0 = default, 1 = non-temporal loads; the KV stream is read
+// once per step). A/B in tools/bench_kernels.py --quick.
+static int g_decode_nt = 0;
+RAGK_API int ragk_attn_decode_set_nt(int nt) {
+  g_decode_nt = nt ? 1 : 0;
+  return 0;
+}
+
 RAGK_API int ragk_attn_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                               int bt_stride, const int* kv_lens, float* part_o, float* part_ml, void* out,
                               int out_stride, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
@@ -535,7 +620,10 @@ RAGK_API int ragk_attn_decode(const void* q, int q_stride, const void* kc, const
   dim3 grid(max_parts, Hkv, B);
 #define RAGK_DC(DD, GG)                                                            \
   if (D == DD && G == GG) {                                                          \
-    hipLaunchKernelGGL((attn_decode_kernel<DD, GG>), grid, dim3(256), 0, st, a);     \
+    if (g_decode_nt)                                                                 \
+      hipLaunchKernelGGL((attn_decode_kernel<DD, GG, true>), grid, dim3(256), 0, st, a); \
+    else                                                                             \
+      hipLaunchKernelGGL((attn_decode_kernel<DD, GG, false>), grid, dim3(256), 0, st, a); \
     if (max_parts > 1)                                                               \
       hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(Hq, B), dim3(DD), 0, st, a, DD); \
     return (int)hipGetLastError();                                                   \

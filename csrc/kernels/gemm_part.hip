@@ -141,6 +141,12 @@ int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int
 
 // Slice choice: K-slice KS = 64 * ks_steps (ks_steps in {8, 16, 32}); S = K / KS slabs.
 // Picks the largest slice that still gives >= 256 blocks and fits the activation slice in LDS.
+static int g_part_min_blocks = 256;
+RAGK_API int ragk_gemm_part_set_min_blocks(int n) {
+  g_part_min_blocks = n > 0 ? n : 256;
+  return 0;
+}
+
 RAGK_API int ragk_gemm_part_ksteps(int M, int N, int K) {
   const int mt = (M + 15) / 16;
   const int nb = (N + PT_NB - 1) / PT_NB;
@@ -150,7 +156,8 @@ RAGK_API int ragk_gemm_part_ksteps(int M, int N, int K) {
     if (K % KS) continue;
     if (16 * mt * KS * 2 > 128 * 1024) continue;
     if (best == 0) best = ks;  // largest legal slice
-    if (nb * (K / KS) >= 256) return ks;
+    if (nb * (K / KS) >= g_part_min_blocks) return ks;
+    best = ks;
   }
   return best;
 }

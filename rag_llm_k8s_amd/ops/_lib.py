@@ -26,8 +26,11 @@ _SIGS = {
     "ragk_gemm_pp_set_variant": [I],
     "ragk_gemm_w4": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_part": [P, I, P, I, P, I, I, I, I, S],
+    "ragk_attn_decode_set_nt": [I],
+    "ragk_attn_prefill_stamp": [P, I, P, P, P, I, P, P, P, I, P, I, I, I, F, P, S],
     "ragk_gemm_w4_diag": [I, I, P, I, P, I, P, I, I, I, I, P, S],
     "ragk_gemm_part_ksteps": [I, I, I],
+    "ragk_gemm_part_set_min_blocks": [I],
     "ragk_add_partials_rmsnorm": [P, I, I, P, I, P, P, I, I, F, S],
     "ragk_rope_kv_partials": [P, I, I, I, P, I, P, P, P, P, P, P, I, I, I, I, S],
     "ragk_gemm_dec": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, I, P, P, S],

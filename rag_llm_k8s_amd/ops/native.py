@@ -148,8 +148,15 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
     return out
 
 
+PART_MIN_BLOCKS = int(__import__("os").environ.get("RAGK_PART_MIN_BLOCKS", "256"))
+_part_cfg = [False]
+
+
 def gemm_part_slabs(M, N, K, ks=None):
     """(ks_steps, S) of the split-K partial GEMM for this shape (0, 0 if unsupported)."""
+    if not _part_cfg[0]:
+        check(_lib.lib().ragk_gemm_part_set_min_blocks(PART_MIN_BLOCKS), "ragk_gemm_part_set_min_blocks")
+        _part_cfg[0] = True
     ks = ks or _lib.lib().ragk_gemm_part_ksteps(M, N, K)
     if ks <= 0 or K % (64 * ks):
         return 0, 0
