@@ -137,11 +137,12 @@ struct PrefillArgs {
 
 __device__ unsigned long long* g_attn_dbg = nullptr;  // stamp build only
 
-template <int D, int GB, bool CAUSAL, bool PAGED, bool STAMP = false>
-__global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
+template <int D, int GB, bool CAUSAL, bool PAGED, bool STAMP = false, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_prefill_kernel(PrefillArgs a) {
   unsigned long long stp[6] = {0, 0, 0, 0, 0, 0};
   using C = Cfg<D>;
-  constexpr int QT = 32 * (4 / GB);  // query positions per block
+  constexpr int NTH = NWV * 64;
+  constexpr int QT = 32 * (NWV / GB);  // query positions per block
   __shared__ __attribute__((aligned(16))) char smem[4 * C::TILEB];  // [buf][K|V]
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
   // issue path: ~1.2k of ~5.7k wave cycles per tile in the stamp build, tools/attn_stamps.py)
   __shared__ int s_bt[PAGED ? MAX_BT : 1];
   if constexpr (PAGED) {
-    for (int i = threadIdx.x; i < n_kt; i += 256) s_bt[i] = bt[i];
+    for (int i = threadIdx.x; i < n_kt; i += NTH) s_bt[i] = bt[i];
     __syncthreads();
   }
   int bt_next = PAGED && n_kt > 0 ? s_bt[0] : 0;  // block of the tile staged next
@@ -204,8 +205,8 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
       const size_t base = ((size_t)bt_next * a.Hkv + kvh) * KT * D;
       const bf16_t* kb = a.k + base;
       const bf16_t* vb = a.v + base;
-      stage_kv<D, false, false, 4>(sK, wid_u, 4, lane, [&](int r) { return kb + (size_t)r * D; });
-      stage_kv<D, true, false, 4>(sV, wid_u, 4, lane, [&](int r) { return vb + (size_t)r * D; });
+      stage_kv<D, false, false, NWV>(sK, wid_u, NWV, lane, [&](int r) { return kb + (size_t)r * D; });
+      stage_kv<D, true, false, NWV>(sV, wid_u, NWV, lane, [&](int r) { return vb + (size_t)r * D; });
     } else {
       const int k0 = kt * KT;
       auto rowp = [&](const bf16_t* base, int r) {
@@ -213,8 +214,8 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(PrefillArgs a) {
         tok = tok < kv_len ? tok : kv_len - 1;
         return base + (size_t)(kv_off + tok) * a.kv_stride + kvh * D;
       };
-      stage_kv<D, false, false, 4>(sK, wid_u, 4, lane, [&](int r) { return rowp(a.k, r); });
-      stage_kv<D, true, false, 4>(sV, wid_u, 4, lane, [&](int r) { return rowp(a.v, r); });
+      stage_kv<D, false, false, NWV>(sK, wid_u, NWV, lane, [&](int r) { return rowp(a.k, r); });
+      stage_kv<D, true, false, NWV>(sV, wid_u, NWV, lane, [&](int r) { return rowp(a.v, r); });
     }
   };
 
@@ -539,11 +540,18 @@ __global__ void attn_decode_reduce_kernel(DecodeArgs a, int D) {
   a.out[(size_t)b * a.out_stride + hq * D + d] = f2bf(L > 0.f ? O / L : 0.f);
 }
 
+// Waves per block when 4 query heads share a KV head (Llama GQA): 8 = two 32-row groups share each
+// K/V tile (half the DMA issue and K/V traffic per wave).
+int g_prefill_waves = 4;
+
 template <int D, int GB, bool CAUSAL, bool PAGED>
 hipError_t launch_prefill(const PrefillArgs& a, int n_tiles, hipStream_t st) {
   const int G = a.Hq / a.Hkv;
   dim3 grid(n_tiles, a.Hkv * (G / GB));
-  hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED>), grid, dim3(256), 0, st, a);
+  if (GB == 4 && g_prefill_waves == 8)
+    hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 8>), grid, dim3(512), 0, st, a);
+  else
+    hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -566,10 +574,17 @@ RAGK_API int ragk_attn_prefill_stamp(const void* q, int q_stride, const void* k,
 }
 
 // Returns the query positions per block (the host builds `tiles` with this step).
+RAGK_API int ragk_attn_prefill_set_waves(int w) {
+  if (w != 4 && w != 8) return (int)hipErrorInvalidValue;
+  g_prefill_waves = w;
+  return 0;
+}
+
+// (every GB == 4 config follows g_prefill_waves; the host builds tiles with this value)
 RAGK_API int ragk_attn_prefill_qtile(int Hq, int Hkv) {
   const int G = Hq / Hkv;
   const int GB = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
-  return 32 * (4 / GB);
+  return 32 * ((GB == 4 ? g_prefill_waves : 4) / GB);
 }
 
 RAGK_API int ragk_attn_prefill(const void* q, int q_stride, const void* k, const void* v, int kv_stride,

@@ -383,10 +383,25 @@ def gather_rows(x, idx, out=None):
 
 
 # ----------------------------------------------------------------------------- attention
+PREFILL_WAVES = int(__import__("os").environ.get("RAGK_PREFILL_WAVES", "4"))
+_prefill_waves_set = [None]
+
+
+def set_prefill_waves(w):
+    """Waves per prefill-attention block when 4 query heads share a KV head (4 or 8)."""
+    check(_lib.lib().ragk_attn_prefill_set_waves(int(w)), "ragk_attn_prefill_set_waves")
+    _prefill_waves_set[0] = int(w)
+
+
 def prefill_qtile(Hq, Hkv):
-    G = Hq // Hkv
-    GB = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
-    return 32 * (4 // GB)
+    """Query rows per prefill-attention block (the tile list must be built with the kernel's value)."""
+    if not torch.cuda.is_available():  # CPU engine: tiles are unused by the torch backend
+        G = Hq // Hkv
+        GB = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
+        return 32 * (4 // GB)
+    if _prefill_waves_set[0] is None:
+        set_prefill_waves(PREFILL_WAVES)
+    return _lib.lib().ragk_attn_prefill_qtile(Hq, Hkv)
 
 
 def build_prefill_tiles(q_lens, Hq, Hkv):
