@@ -386,6 +386,15 @@ struct DecodeArgs {
   float scale_log2;
 };
 
+// Tiles per partition of one sequence: its KV tiles spread evenly over all max_parts partitions
+// (never fewer than part_tiles per partition). The grid is sized once for max_parts (hipGraph
+// capture), so sizing the split from the actual length keeps every launched block busy with the
+// same amount of KV: splitting a 5.3k-token context by a fixed 32-tile partition left 1 of 4
+// partitions idle and 8 vs 5 tiles per wave on the others.
+__device__ __forceinline__ int decode_part_tiles(int n_kt, const DecodeArgs& a) {
+  return max(a.part_tiles, (n_kt + a.max_parts - 1) / a.max_parts);
+}
+
 template <int D, int G, bool NT = false>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a) {
   using C = Cfg<D>;
@@ -396,10 +405,11 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a) {
   const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int kv_len = a.kv_lens[b];
   const int n_kt = (kv_len + KT - 1) / KT;
-  const int kt0 = part * a.part_tiles;
+  const int pt = decode_part_tiles(n_kt, a);
+  const int kt0 = part * pt;
   if (kt0 >= n_kt) return;  // block-uniform early exit (before any barrier)
-  const int kt1 = min(kt0 + a.part_tiles, n_kt);
-  const int nparts = (n_kt + a.part_tiles - 1) / a.part_tiles;
+  const int kt1 = min(kt0 + pt, n_kt);
+  const int nparts = (n_kt + pt - 1) / pt;
   const int fr = lane & 15, fh = lane >> 4;
   const int* bt = a.block_tables + (size_t)b * a.bt_stride;
 
@@ -525,7 +535,8 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a) {
 __global__ void attn_decode_reduce_kernel(DecodeArgs a, int D) {
   const int hq = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const int n_kt = (a.kv_lens[b] + KT - 1) / KT;
-  const int nparts = (n_kt + a.part_tiles - 1) / a.part_tiles;
+  const int pt = decode_part_tiles(n_kt, a);
+  const int nparts = (n_kt + pt - 1) / pt;
   if (nparts <= 1 || d >= D) return;
   const size_t p0 = ((size_t)b * a.Hq + hq) * a.max_parts;
   float M = -INFINITY;

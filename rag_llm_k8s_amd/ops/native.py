@@ -7,6 +7,7 @@ HIP stream, so everything here is capturable in a hipGraph (torch.cuda.CUDAGraph
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -26,10 +27,10 @@ def _bf16_2d(t, name):
 
 
 # ----------------------------------------------------------------------------- GEMM
-PP_MIN_M = int(__import__("os").environ.get("RAGK_PP_MIN_M", "1024"))
-PP_VARIANT = int(__import__("os").environ.get("RAGK_PP_VARIANT", "2"))
+PP_MIN_M = int(os.environ.get("RAGK_PP_MIN_M", "1024"))
+PP_VARIANT = int(os.environ.get("RAGK_PP_VARIANT", "2"))
 # large-M kernel: "w4" = 4-wave 128x128-per-wave (gemm_w4.hip, path 6), "pp" = 8-wave ping-pong (path 2)
-PREFILL_GEMM = __import__("os").environ.get("RAGK_PREFILL_GEMM", "w4")
+PREFILL_GEMM = os.environ.get("RAGK_PREFILL_GEMM", "w4")
 _pp_variant_set = [None]
 
 
@@ -39,8 +40,8 @@ def set_pp_variant(v):
     _pp_variant_set[0] = int(v)
 
 
-DEC_DEFAULT = __import__("os").environ.get("RAGK_DEC_GEMM", "1") == "1"
-DEC_WS_BYTES = int(__import__("os").environ.get("RAGK_DEC_WS_MB", "96")) << 20
+DEC_DEFAULT = os.environ.get("RAGK_DEC_GEMM", "1") == "1"
+DEC_WS_BYTES = int(os.environ.get("RAGK_DEC_WS_MB", "96")) << 20
 _dec_ws = {}
 
 
@@ -60,7 +61,7 @@ def use_dec(M, N, K, epi):
     return 16 < M <= 64 and N >= 32768 and K % 256 == 0 and epi != "silu_mul"
 
 
-STREAM_DEFAULT = __import__("os").environ.get("RAGK_STREAM_GEMM", "1") == "1"
+STREAM_DEFAULT = os.environ.get("RAGK_STREAM_GEMM", "1") == "1"
 
 
 def use_stream(M, N, K, epi, fp8=False):
@@ -148,7 +149,7 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
     return out
 
 
-PART_MIN_BLOCKS = int(__import__("os").environ.get("RAGK_PART_MIN_BLOCKS", "256"))
+PART_MIN_BLOCKS = int(os.environ.get("RAGK_PART_MIN_BLOCKS", "256"))
 _part_cfg = [False]
 
 
@@ -212,7 +213,7 @@ def quant_fp8_rows(x, q=None, scale=None):
     return q, scale
 
 
-FP8_DEC_STREAM = __import__("os").environ.get("RAGK_FP8_DEC", "auto") != "regs"
+FP8_DEC_STREAM = os.environ.get("RAGK_FP8_DEC", "auto") != "regs"
 
 
 def gemm_fp8(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False):
@@ -383,7 +384,7 @@ def gather_rows(x, idx, out=None):
 
 
 # ----------------------------------------------------------------------------- attention
-PREFILL_WAVES = int(__import__("os").environ.get("RAGK_PREFILL_WAVES", "4"))
+PREFILL_WAVES = int(os.environ.get("RAGK_PREFILL_WAVES", "4"))
 _prefill_waves_set = [None]
 
 
@@ -439,12 +440,19 @@ def attn_prefill(q, k, v, cu_q, kv_lens, tiles, out, Hq, Hkv, D, causal=True, pa
     return out
 
 
-def decode_partitions(max_kv_len, batch, Hkv, target_blocks=1024):
-    """(part_tiles, max_parts) for split-K decode sized for >= target_blocks blocks."""
+DECODE_TARGET_BLOCKS = int(os.environ.get("RAGK_DECODE_BLOCKS", "512"))
+
+
+def decode_partitions(max_kv_len, batch, Hkv, target_blocks=None, min_tiles=4):
+    """(part_tiles, max_parts) for split-K decode: grid = max_parts x Hkv x batch >= target_blocks.
+
+    The kernel spreads each sequence's actual KV tiles evenly over the max_parts partitions
+    (at least ``part_tiles`` = min_tiles tiles each, attention.hip:decode_part_tiles), so the grid can
+    be sized once for the longest allowed context (hipGraph capture) without idle partitions."""
+    target_blocks = DECODE_TARGET_BLOCKS if target_blocks is None else target_blocks
     max_kt = max(1, (max_kv_len + 63) // 64)
-    pt = max(4, -(-max_kt * batch * Hkv // target_blocks))
-    pt = -(-pt // 4) * 4
-    return pt, -(-max_kt // pt)
+    mp = max(1, min(-(-target_blocks // (batch * Hkv)), -(-max_kt // min_tiles)))
+    return min_tiles, mp
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, part_tiles, max_parts, ws_o=None,
