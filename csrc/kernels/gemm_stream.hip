@@ -67,7 +67,14 @@ struct StreamGeom {
   static constexpr int EPI_LD = WROWS + 4;
 };
 
-template <int MT, bool FP8>
+// Weight-stream LDS-DMA with the non-temporal policy (aux = 2): each weight row is read by exactly
+// one block once per decode step, from a stream far larger than the Infinity Cache.
+__device__ __forceinline__ void glds16_nt(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 2);
+}
+
+template <int MT, bool FP8, bool NT = false>
 __device__ __forceinline__ void stage_load(const bf16_t* __restrict__ X, int ldx, int M,
                                            const unsigned char* __restrict__ Wb, int ldw_bytes, int Nrows, int n0,
                                            int kel, char* st, int wid, int lane) {
@@ -80,7 +87,8 @@ __device__ __forceinline__ void stage_load(const bf16_t* __restrict__ X, int ldx
     const int r = q * 8 + (lane >> 3);
     const int c = swz(r, lane & 7);
     const int gr = min(n0 + r, Nrows - 1);
-    glds16(Wb + (size_t)gr * ldw_bytes + kbyte + c * 16, st + q * 1024);
+    if constexpr (NT) glds16_nt(Wb + (size_t)gr * ldw_bytes + kbyte + c * 16, st + q * 1024);
+    else glds16(Wb + (size_t)gr * ldw_bytes + kbyte + c * 16, st + q * 1024);
   }
   // activations: XROWS rows x XROW bytes, as 128-B half-rows for the fp8 (256-B) case
   char* xs = st + G::WBYTES;
@@ -104,7 +112,7 @@ __device__ __forceinline__ void stage_load(const bf16_t* __restrict__ X, int ldx
   }
 }
 
-template <int MT, int EPI, bool OUT_F32, bool FP8>
+template <int MT, int EPI, bool OUT_F32, bool FP8, bool NT = false>
 __global__ __launch_bounds__(ST_THREADS, 1) void gemm_stream_kernel(
     const bf16_t* __restrict__ X, int ldx, const void* __restrict__ Wv, int ldw, const float* __restrict__ wscale,
     void* C, int ldc, const bf16_t* __restrict__ bias, const bf16_t* resid, int ldr, int M, int N, int K, int S,
@@ -134,7 +142,7 @@ __global__ __launch_bounds__(ST_THREADS, 1) void gemm_stream_kernel(
   // prologue: NS-1 stages in flight
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
-    if (p < nst) stage_load<MT, FP8>(X, ldx, M, Wb, ldw_bytes, Nrows, n0, k0 + p * G::KSTEP, smem + p * G::STAGE,
+    if (p < nst) stage_load<MT, FP8, NT>(X, ldx, M, Wb, ldw_bytes, Nrows, n0, k0 + p * G::KSTEP, smem + p * G::STAGE,
                                      wid_u, lane);
 
   for (int t = 0; t < nst; ++t) {
@@ -145,7 +153,7 @@ __global__ __launch_bounds__(ST_THREADS, 1) void gemm_stream_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier_raw();  // every wave's part of stage t landed; every wave finished reading stage t-1
     if (t + NS - 1 < nst)
-      stage_load<MT, FP8>(X, ldx, M, Wb, ldw_bytes, Nrows, n0, k0 + (t + NS - 1) * G::KSTEP,
+      stage_load<MT, FP8, NT>(X, ldx, M, Wb, ldw_bytes, Nrows, n0, k0 + (t + NS - 1) * G::KSTEP,
                           smem + ((t + NS - 1) % NS) * G::STAGE, wid_u, lane);
     const char* wt = smem + (t % NS) * G::STAGE;
     const char* xt = wt + G::WBYTES;
@@ -303,12 +311,23 @@ __global__ __launch_bounds__(ST_THREADS, 1) void gemm_stream_kernel(
   if (tid == 0) __hip_atomic_store(counters + ntile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Weight-stream cache policy for the SiLU*up (gate/up) instantiations: 1 = non-temporal.
+int g_stream_nt = 1;
+
 template <int MT, int EPI, bool F32, bool FP8>
 int launch_stream(const void* X, int ldx, const void* W, int ldw, const float* wscale, void* C, int ldc,
                   const void* bias, const void* resid, int ldr, int M, int N, int K, int S, float* ws, int* cnt,
                   hipStream_t st) {
   const int Nrows = EPI == EPI_SILU_MUL ? 2 * N : N;
   const dim3 grid((Nrows + WROWS - 1) / WROWS, S);
+  if constexpr (EPI == EPI_SILU_MUL) {
+    if (g_stream_nt) {
+      hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI, F32, FP8, true>), grid, dim3(ST_THREADS), 0, st,
+                         (const bf16_t*)X, ldx, W, ldw, wscale, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid,
+                         ldr, M, N, K, S, ws, cnt);
+      return (int)hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI, F32, FP8>), grid, dim3(ST_THREADS), 0, st, (const bf16_t*)X, ldx,
                      W, ldw, wscale, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K, S, ws, cnt);
   return (int)hipGetLastError();
@@ -331,6 +350,11 @@ int dispatch_stream(const void* X, int ldx, const void* W, int ldw, const float*
 
 // Split count for the stream decode GEMM: enough blocks for 256 CUs (one block per CU), at least
 // 8 K-steps per block, S | K-steps.
+RAGK_API int ragk_gemm_stream_set_nt(int nt) {
+  g_stream_nt = nt ? 1 : 0;
+  return 0;
+}
+
 RAGK_API int ragk_gemm_stream_splits(int N, int K, int epi, int fp8) {
   static const int s_env = [] {
     const char* v = getenv("RAGK_STREAM_S");

@@ -27,6 +27,8 @@
 // Build note: the loop is written in its final instruction order and this file is compiled with
 // `-mllvm -enable-misched=0 -mllvm -disable-post-ra` (_build.py EXTRA_FLAGS), so neither machine
 // scheduler reorders it (the post-RA one bunched the DMAs at the end of segment 2).
+#include <stdlib.h>
+
 #include "common.h"
 using namespace ragk;
 
@@ -37,9 +39,7 @@ constexpr int W4_THREADS = 256;
 constexpr int W_TILE_A = WBM * WBK * 2;  // 32 KiB
 constexpr int W_TILE_B = WBN * WBK * 2;  // 32 KiB
 constexpr int W_BUF = W_TILE_A + W_TILE_B;
-constexpr int WEPI_LD = WBN + 4;                 // padded fp32 row
-constexpr int WEPI_BYTES = 128 * WEPI_LD * 4;    // one 128-row half of the output tile
-constexpr int W4_LDS = (2 * W_BUF > WEPI_BYTES) ? 2 * W_BUF : WEPI_BYTES;
+constexpr int W4_LDS = 2 * W_BUF;  // two K-tile buffers; the epilogue needs no LDS
 constexpr int WGROUP_M = 8;
 
 __device__ __forceinline__ int wswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -91,95 +91,117 @@ constexpr int W_LGKM0 = 0xC07F;  // lgkmcnt(0), others don't-care
 constexpr int W_VM0 = 0x0F70;    // vmcnt(0), others don't-care
 constexpr int W_VM16 = 0x4F70;   // vmcnt(16)
 
+// Vector-memory ops one wave issues in w4_epilogue_reg on a full tile (no row/column guard): the
+// persistent loop's wait for the next tile's first K-tile counts them as younger than its DMA.
 template <int EPI, bool OUT_F32>
-__device__ __forceinline__ void w4_epilogue(const f32x4 (&acc)[8][8], char* smem, int tid, int wr, int wc, int fr,
-                                            int fh, int m0, int n0, void* C, int ldc, const bf16_t* __restrict__ bias,
-                                            const bf16_t* resid, int ldr, int M, int N) {
-  float* sC = reinterpret_cast<float*>(smem);
+constexpr int w4_epi_vmem() {
+  if constexpr (EPI == EPI_SILU_MUL) return 32;
   constexpr bool RES = (EPI == EPI_RESID || EPI == EPI_BIAS_RESID);
-  // the half's residual tile is loaded into registers before its LDS staging (one memory latency,
-  // overlapped with the staging, instead of a dependent load per output vector)
-  u32x4 rpre[RES ? 16 : 1];
-#pragma unroll 1
-  for (int h = 0; h < 2; ++h) {
-    if constexpr (RES) {
+  constexpr bool BIAS = (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU ||
+                         EPI == EPI_BIAS_GELU_TANH);
+  return 64 + (RES ? 64 : 0) + (BIAS ? 8 : 0);
+}
+
+__device__ __forceinline__ void w4_store4(void* C, size_t idx, const float (&o)[4], bool f32) {
+  if (f32) {
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + idx) = (f32x4){o[0], o[1], o[2], o[3]};
+  } else {
+    const unsigned lo = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
+    const unsigned hi = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(C) + idx) = make_uint2(lo, hi);
+  }
+}
+
+__device__ __forceinline__ void unpack4(uint2 v, float (&f)[4]) {
+  f[0] = __uint_as_float(v.x << 16);
+  f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16);
+  f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+
+// Epilogue straight from the (transposed) accumulators, no LDS and no barrier: lane (fr, fh) writes
+// 4 consecutive columns (8 B bf16 / 16 B fp32) of row 16i + fr for each of its 64 fragments. LDS is
+// left to the next tile's K-tile DMAs, which the persistent loop issues before this runs. FULL: the
+// tile lies inside [M, N], every lane stores unguarded (exactly w4_epi_vmem ops per wave).
+// resid may alias C: every element is read and written by the same lane.
+template <int EPI, bool OUT_F32, bool FULL>
+__device__ __forceinline__ void w4_epilogue_reg(const f32x4 (&acc)[8][8], int wr, int wc, int fr, int fh, int m0,
+                                                int n0, void* C, int ldc, const bf16_t* __restrict__ bias,
+                                                const bf16_t* resid, int ldr, int M, int N) {
+  const int row0 = m0 + wr * 128 + fr;
+  if constexpr (EPI == EPI_SILU_MUL) {
+    // packed columns: this wave's 128 = [64 gate | 64 up] -> 64 output columns; gate fragment j
+    // and up fragment j + 4 hold the same output columns in the same lane
+    const int col0 = (n0 >> 1) + wc * 64 + 4 * fh;
 #pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        const int v = tid + it * W4_THREADS;
-        const int gr = m0 + h * 128 + (v >> 5), gc = n0 + (v & 31) * 8;
-        rpre[it] = (gr < M && gc < N) ? *reinterpret_cast<const u32x4*>(resid + (size_t)gr * ldr + gc)
-                                      : (u32x4){0u, 0u, 0u, 0u};
+    for (int i = 0; i < 8; ++i) {
+      const int gr = row0 + 16 * i;
+      if (FULL || gr < M) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = silu(acc[i][j][r]) * acc[i][j + 4][r];
+          w4_store4(C, (size_t)gr * ldc + col0 + 16 * j, o, false);
+        }
       }
     }
-    __syncthreads();
-    if (wr == h) {
+  } else {
+    constexpr bool RES = (EPI == EPI_RESID || EPI == EPI_BIAS_RESID);
+    constexpr bool BIAS = (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU ||
+                           EPI == EPI_BIAS_GELU_TANH);
+    const int col0 = n0 + wc * 128 + 4 * fh;
+    uint2 bv[BIAS ? 8 : 1];
+    if constexpr (BIAS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        bv[j] = *reinterpret_cast<const uint2*>(bias + (FULL ? col0 + 16 * j : min(col0 + 16 * j, N - 4)));
+    }
+    // the whole residual tile of this lane is requested before the first use (one memory latency).
+    // Loads are never predicated (edge tiles clamp the address instead): a load under a branch
+    // makes hipcc's waitcnt pass drain vmcnt(0) at every join.
+    uint2 rv[RES ? 64 : 1];
+    if constexpr (RES) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            sC[(16 * i + 4 * fh + r) * WEPI_LD + wc * 128 + 16 * j + fr] = acc[i][j][r];
-    }
-    __syncthreads();
-    const int mrow0 = m0 + h * 128;
-    if constexpr (EPI == EPI_SILU_MUL) {
-      // 256 packed cols = two [64 gate | 64 up] tiles -> 128 output cols
-#pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const int v = tid + it * W4_THREADS;  // 128 rows x 16 vec (2 halves x 8)
-        const int row = v >> 4, hv = (v >> 3) & 1, c8 = (v & 7) * 8;
-        const int gr = mrow0 + row;
-        if (gr < M) {
-          float o[8];
-          const float* g = sC + row * WEPI_LD + hv * 128 + c8;
-          const float* u = g + 64;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = silu(g[e]) * u[e];
-          bf16_t* dst = reinterpret_cast<bf16_t*>(C) + (size_t)gr * ldc + (n0 >> 1) + hv * 64 + c8;
-          *reinterpret_cast<u32x4*>(dst) = pack8(o);
+        for (int j = 0; j < 8; ++j) {
+          const int gr = FULL ? row0 + 16 * i : min(row0 + 16 * i, M - 1);
+          const int gc = FULL ? col0 + 16 * j : min(col0 + 16 * j, N - 4);
+          rv[8 * i + j] = *reinterpret_cast<const uint2*>(resid + (size_t)gr * ldr + gc);
         }
-      }
-    } else {
+    }
 #pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        const int v = tid + it * W4_THREADS;  // 128 rows x 32 vec
-        const int row = v >> 5, c8 = (v & 31) * 8;
-        const int gr = mrow0 + row, gc = n0 + c8;
-        if (gr < M && gc < N) {
-          float o[8];
-          const float* s = sC + row * WEPI_LD + c8;
+    for (int i = 0; i < 8; ++i) {
+      const int gr = row0 + 16 * i;
 #pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = s[e];
-          if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU ||
-                        EPI == EPI_BIAS_GELU_TANH) {
-            float b[8];
-            unpack8(*reinterpret_cast<const u32x4*>(bias + gc), b);
+      for (int j = 0; j < 8; ++j) {
+        const int gc = col0 + 16 * j;
+        if (FULL || (gr < M && gc < N)) {
+          float o[4];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] += b[e];
+          for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r];
+          if constexpr (BIAS) {
+            float b[4];
+            unpack4(bv[j], b);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] += b[r];
           }
           if constexpr (RES) {
-            float rr[8];
-            unpack8(rpre[it], rr);
+            float rr[4];
+            unpack4(rv[8 * i + j], rr);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] += rr[e];
+            for (int r = 0; r < 4; ++r) o[r] += rr[r];
           }
           if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_GELU) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = gelu_erf(o[e]);
+            for (int r = 0; r < 4; ++r) o[r] = gelu_erf(o[r]);
           }
           if constexpr (EPI == EPI_BIAS_GELU_TANH) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = gelu_tanh(o[e]);
+            for (int r = 0; r < 4; ++r) o[r] = gelu_tanh(o[r]);
           }
-          if constexpr (OUT_F32) {
-            float* dst = reinterpret_cast<float*>(C) + (size_t)gr * ldc + gc;
-            *reinterpret_cast<f32x4*>(dst) = (f32x4){o[0], o[1], o[2], o[3]};
-            *reinterpret_cast<f32x4*>(dst + 4) = (f32x4){o[4], o[5], o[6], o[7]};
-          } else {
-            bf16_t* dst = reinterpret_cast<bf16_t*>(C) + (size_t)gr * ldc + gc;
-            *reinterpret_cast<u32x4*>(dst) = pack8(o);
-          }
+          w4_store4(C, (size_t)gr * ldc + gc, o, OUT_F32);
         }
       }
     }
@@ -192,8 +214,11 @@ __device__ __forceinline__ void w4_epilogue(const f32x4 (&acc)[8][8], char* smem
 // DMAs around it (the loop is written in its final order). Hazards the compiler no longer pads:
 // acc init -> first MFMA and last MFMA -> epilogue reads (w4_pin_acc below); the accumulate chain
 // itself (same acc every 64 MFMAs) and ds_read -> srcA/B (s_waitcnt, inserted by hipcc) need none.
+// The weight fragment is srcA and the activation fragment srcB, so the accumulator comes out
+// transposed: lane (fr, fh) of acc[i][j] holds C[16i + fr][16j + 4fh .. 16j + 4fh + 3] -- four
+// consecutive output columns of one row, stored straight from registers by w4_epilogue_reg.
 __device__ __forceinline__ void w4_mfma(f32x4 (&acc)[8][8], const bf16x8 (&a)[8], const bf16x8 (&b)[8], int m) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %2, %1, %0"
                : "+a"(acc[m >> 3][m & 7])
                : "v"(a[m >> 3]), "v"(b[m & 7])
                : "memory");
@@ -355,6 +380,30 @@ __device__ __forceinline__ void w4_iter1(char* smem, int t, i32x4 srd_a, i32x4 s
   }
 }
 
+// Output tile `tile` (of nwg) -> origin. Tiles are numbered so that the 8 XCDs each own a contiguous
+// range (xcd_remap; a persistent block keeps its XCD since the grid is a multiple of 8), grouped
+// WGROUP_M M-tiles deep for L2 reuse of the weight tiles.
+__device__ __forceinline__ void w4_origin(int tile, int nwg, int tiles_m, int tiles_n, int& m0, int& n0) {
+  const int logical = xcd_remap(tile, nwg);
+  const int group = logical / (WGROUP_M * tiles_n);
+  const int first_m = group * WGROUP_M;
+  const int gm = min(tiles_m - first_m, WGROUP_M);
+  const int in_group = logical % (WGROUP_M * tiles_n);
+  m0 = (first_m + in_group % gm) * WBM;
+  n0 = (in_group / gm) * WBN;
+}
+
+__device__ __forceinline__ void w4_zero(f32x4 (&acc)[8][8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+}
+
+// Persistent: block b computes tiles b, b + G, b + 2G, ... (G = gridDim.x; G = nwg gives the plain
+// one-tile-per-block launch). Between two tiles, LDS is free as soon as the K-loop's last barrier has
+// passed, so the next tile's first two K-tiles are DMA'd BEFORE this tile's epilogue runs: the DMA
+// latency that a fresh block pays in its prologue hides behind the epilogue's stores.
 template <int EPI, bool OUT_F32, bool STAMP = false, int S1 = W4_S1, int S3 = W4_S3>
 __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __restrict__ A, int lda,
                                                                 const bf16_t* __restrict__ B, int ldb, void* C,
@@ -369,95 +418,156 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
 
   const int tiles_m = (M + WBM - 1) / WBM, tiles_n = (N + WBN - 1) / WBN;
   const int nwg = tiles_m * tiles_n;
-  const int logical = xcd_remap(blockIdx.x, nwg);
-  const int group = logical / (WGROUP_M * tiles_n);
-  const int first_m = group * WGROUP_M;
-  const int gm = min(tiles_m - first_m, WGROUP_M);
-  const int in_group = logical % (WGROUP_M * tiles_n);
-  const int m0 = (first_m + in_group % gm) * WBM;
-  const int n0 = (in_group / gm) * WBN;
   const int nk = K / WBK;
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  w4_pin_acc(acc);
-  bf16x8 a0[8], b0[8], a1[8], b1[8];
 
   // byte offsets are 32-bit: the launcher guarantees rows * ld * 2 < 2^31 for both operands
   const i32x4 srd_a = make_srd(A, (unsigned)M * (unsigned)lda * 2u);
   const i32x4 srd_b = make_srd(B, (unsigned)N * (unsigned)ldb * 2u);
+
+  int tile = blockIdx.x;
+  int m0, n0;
+  w4_origin(tile, nwg, tiles_m, tiles_n, m0, n0);
   int off_a[8], off_b[8];
   w4_offsets(lda, m0, M, wid, lane, off_a);
   w4_offsets(ldb, n0, N, wid, lane, off_b);
-
-  // prologue: tiles 0 and 1 in flight, wait for tile 0 (tile 1's 16 DMAs are younger)
+  // prologue: K-tiles 0 and 1 in flight
   w4_stage(srd_a, off_a, 0, smem, wid);
   w4_stage(srd_b, off_b, 0, smem + W_TILE_A, wid);
   if (nk > 1) {
     w4_stage(srd_a, off_a, WBK, smem + W_BUF, wid);
     w4_stage(srd_b, off_b, WBK, smem + W_BUF + W_TILE_A, wid);
-    __builtin_amdgcn_s_waitcnt(W_VM16);
-  } else {
-    __builtin_amdgcn_s_waitcnt(W_VM0);
   }
-  w4_barrier();
-  w4_read(smem, 0, wr, wc, fr, fh, a0, b0);
-  __builtin_amdgcn_s_waitcnt(W_LGKM0);
-  __builtin_amdgcn_sched_barrier(0);
 
+  f32x4 acc[8][8];
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
   unsigned long long stp[5] = {0, 0, 0, 0, 0};
-  int t = 0;
-  if constexpr (S3 == 0) {
-    for (; t + 2 < nk; ++t)
-      w4_iter1<true, true, STAMP, S1>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1, b1,
-                                      stp);
-    if (t + 1 < nk) {
-      w4_iter1<false, true, false, S1>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1,
-                                       b1, stp);
-      ++t;
+  // vector-memory ops issued after the current tile's K-tile-0 DMA: its 16 K-tile-1 DMAs, plus the
+  // previous tile's full-tile epilogue (0 = none, or a guarded epilogue that drained itself)
+  int younger_epi = 0, done = 0;
+  for (;;) {
+    w4_zero(acc);
+    w4_pin_acc(acc);
+    if (nk == 1) {
+      __builtin_amdgcn_s_waitcnt(W_VM0);
+    } else if (younger_epi == 0) {
+      __builtin_amdgcn_s_waitcnt(W_VM16);
+    } else {
+      constexpr int E = 16 + w4_epi_vmem<EPI, OUT_F32>();
+      constexpr int V = E > 63 ? 63 : E;
+      __builtin_amdgcn_s_waitcnt((V & 15) | (((V >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
     }
-    w4_iter1<false, false, false, S1>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1, b1,
-                                      stp);
-  } else {
-  for (; t + 2 < nk; ++t)
-    w4_iter<true, true, STAMP, S1, S3>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1,
-                                       b1, stp);
-  if (t + 1 < nk) {
-    w4_iter<false, true, false, S1, S3>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1,
+    w4_barrier();
+    w4_read(smem, 0, wr, wc, fr, fh, a0, b0);
+    __builtin_amdgcn_s_waitcnt(W_LGKM0);
+    __builtin_amdgcn_sched_barrier(0);
+
+    int t = 0;
+    if constexpr (S3 == 0) {
+      for (; t + 2 < nk; ++t)
+        w4_iter1<true, true, STAMP, S1>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1,
                                         b1, stp);
-    ++t;
-  }
-  w4_iter<false, false, false, S1, S3>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1, b1,
-                                       stp);
+      if (t + 1 < nk) {
+        w4_iter1<false, true, false, S1>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1,
+                                         b1, stp);
+        ++t;
+      }
+      w4_iter1<false, false, false, S1>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1,
+                                        b1, stp);
+      // w4_iter1 has no barrier after its last LDS reads: every wave must be done with them before
+      // the next tile's DMAs overwrite the buffers
+      w4_barrier();
+    } else {
+      for (; t + 2 < nk; ++t)
+        w4_iter<true, true, STAMP, S1, S3>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0,
+                                           a1, b1, stp);
+      if (t + 1 < nk) {
+        w4_iter<false, true, false, S1, S3>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0,
+                                            a1, b1, stp);
+        ++t;
+      }
+      // last K-tile: its F1 reads retire before its barrier 1, its segment 3 reads nothing, so
+      // after its barrier 2 no wave touches LDS again for this tile
+      w4_iter<false, false, false, S1, S3>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0,
+                                           a1, b1, stp);
+    }
+
+    const int next = tile + (int)gridDim.x;
+    if (next < nwg) {
+      int nm0, nn0;
+      w4_origin(next, nwg, tiles_m, tiles_n, nm0, nn0);
+      // opaque copy of the lane id: keeps hipcc from hoisting the lane-only half of the offset math
+      // out of the tile loop (it did, and spilled those 16 values to scratch at 256 VGPRs)
+      int ln;  // == lane, recomputed here (volatile: not hoisted)
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      w4_offsets(lda, nm0, M, wid, ln, off_a);
+      w4_offsets(ldb, nn0, N, wid, ln, off_b);
+      w4_stage(srd_a, off_a, 0, smem, wid);
+      w4_stage(srd_b, off_b, 0, smem + W_TILE_A, wid);
+      if (nk > 1) {
+        w4_stage(srd_a, off_a, WBK, smem + W_BUF, wid);
+        w4_stage(srd_b, off_b, WBK, smem + W_BUF + W_TILE_A, wid);
+      }
+    }
+    w4_pin_acc(acc);
+    if (m0 + WBM <= M && n0 + WBN <= N) {
+      w4_epilogue_reg<EPI, OUT_F32, true>(acc, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr, M, N);
+      younger_epi = 1;
+    } else {
+      w4_epilogue_reg<EPI, OUT_F32, false>(acc, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr, M, N);
+      __builtin_amdgcn_s_waitcnt(W_VM0);  // guarded stores: count unknown, drain them here
+      younger_epi = 0;
+    }
+    ++done;
+    if (next >= nwg) break;
+    tile = next;
+    w4_origin(tile, nwg, tiles_m, tiles_n, m0, n0);
   }
   if constexpr (STAMP) {
     if (lane == 0) {
       unsigned long long* d = dbg + ((size_t)blockIdx.x * 4 + wid) * 6;
 #pragma unroll
       for (int i = 0; i < 5; ++i) d[i] = stp[i];
-      d[5] = (unsigned long long)(nk - 2);
+      d[5] = (unsigned long long)done * (unsigned long long)(nk - 2);  // steady-state iterations
     }
   }
-  __builtin_amdgcn_s_waitcnt(W_VM0);
-  w4_pin_acc(acc);
+}
 
-  w4_epilogue<EPI, OUT_F32>(acc, smem, tid, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr, M, N);
+// Persistent grid: one block per CU (the kernel holds 128 KiB of LDS and 4 waves x 512 registers,
+// so a CU never runs two), rounded down to a multiple of 8 so a block keeps its XCD across tiles.
+// RAGK_W4_GRID=0 launches one block per tile instead (A/B), N > 0 caps the grid at N.
+static int g_w4_grid = -1;
+static int w4_grid(int nwg) {
+  if (g_w4_grid < 0) {
+    const char* e = getenv("RAGK_W4_GRID");
+    int cus = 0, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    g_w4_grid = e ? atoi(e) : (cus / 8) * 8;
+    if (g_w4_grid < 0) g_w4_grid = 0;
+  }
+  return (g_w4_grid == 0 || g_w4_grid >= nwg) ? nwg : g_w4_grid;
 }
 
 template <int EPI, bool F32>
 int launch_w4(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias, const void* resid,
               int ldr, int M, int N, int K, hipStream_t st) {
   const int nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
-  hipLaunchKernelGGL((gemm_w4_kernel<EPI, F32>), dim3(nwg), dim3(W4_THREADS), 0, st, (const bf16_t*)A, lda,
+  const int grid = w4_grid(nwg);
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI, F32>), dim3(grid), dim3(W4_THREADS), 0, st, (const bf16_t*)A, lda,
                      (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K,
                      nullptr);
   return (int)hipGetLastError();
 }
 
 }  // namespace
+
+// Persistent-grid override (tests / A/B): 0 = one block per tile, g > 0 = at most g blocks (a
+// multiple of 8 keeps each block on one XCD), < 0 = back to the CU count.
+RAGK_API int ragk_gemm_w4_set_grid(int g) {
+  g_w4_grid = g < 0 ? -1 : g;
+  return 0;
+}
 
 // N = output columns (for EPI_SILU_MUL the weight has 2N rows, N % 128 == 0). Requires K % 64 == 0.
 RAGK_API int ragk_gemm_w4(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,
@@ -498,7 +608,7 @@ template <bool STAMP, int S1, int S3>
 int launch_w4_diag(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
                    unsigned long long* dbg, hipStream_t st) {
   const int nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
-  hipLaunchKernelGGL((gemm_w4_kernel<EPI_NONE, false, STAMP, S1, S3>), dim3(nwg), dim3(W4_THREADS), 0, st,
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI_NONE, false, STAMP, S1, S3>), dim3(w4_grid(nwg)), dim3(W4_THREADS), 0, st,
                      (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, nullptr, nullptr, 0, M, N, K, dbg);
   return (int)hipGetLastError();
 }

@@ -40,6 +40,12 @@ def set_pp_variant(v):
     _pp_variant_set[0] = int(v)
 
 
+def set_w4_grid(g):
+    """gemm_w4 persistent grid: -1 = one block per CU (default), 0 = one block per output tile,
+    g > 0 = at most g blocks (each block loops over tiles g apart)."""
+    check(_lib.lib().ragk_gemm_w4_set_grid(int(g)), "ragk_gemm_w4_set_grid")
+
+
 DEC_DEFAULT = os.environ.get("RAGK_DEC_GEMM", "1") == "1"
 DEC_WS_BYTES = int(os.environ.get("RAGK_DEC_WS_MB", "96")) << 20
 _dec_ws = {}

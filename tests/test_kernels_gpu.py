@@ -40,6 +40,18 @@ def test_gemm_pingpong(native, M, N, K, variant):
         native.set_pp_variant(native.PP_VARIANT)
 
 
+@pytest.mark.parametrize("grid", [8, 16])
+@pytest.mark.parametrize("M,N,K", [(1111, 1024, 256), (513, 4104, 128), (2048, 512, 128)])
+def test_gemm_w4_persistent(native, M, N, K, grid):
+    """Persistent gemm_w4: a few blocks loop over every tile (full and edge tiles, one-K-tile K),
+    so the next-tile DMA / register-epilogue overlap and its counted waits run many times per block."""
+    native.set_w4_grid(grid)
+    try:
+        _check_pingpong(native, M, N, K, path=6)
+    finally:
+        native.set_w4_grid(-1)
+
+
 def _check_pingpong(native, M, N, K, path=2):
     torch.manual_seed(20)
     x = torch.randn(M, K, device=DEV).bfloat16()

@@ -32,6 +32,14 @@ def main():
         for p in paths:
             if p == "torch":
                 fns[p] = lambda: torch.matmul(x, w.t())  # noqa: E731
+            elif "@" in p:  # "6@0": gemm_w4 with the persistent grid set to 0 (one block per tile)
+                path, grid = (int(v) for v in p.split("@"))
+
+                def fn(path=path, grid=grid):
+                    N.set_w4_grid(grid)
+                    N.gemm(x, w, resid=r, epi=epi, out=out, path=path)
+                    N.set_w4_grid(-1)
+                fns[p] = fn
             else:
                 fns[p] = lambda p=p: N.gemm(x, w, resid=r, epi=epi, out=out, path=int(p))  # noqa: E731
             fns[p]()

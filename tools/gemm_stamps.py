@@ -52,7 +52,8 @@ for (M, N, K) in [(16384, 4096, 4096), (16384, 6144, 4096), (16384, 4096, 14336)
         run(v, 1, x, w, out, M, N, K, dbg)
         torch.cuda.synchronize()
         d = dbg.view(nwg, 4, 6).double().cpu()
-        it = d[:, :, 5].clamp(min=1)
+        d = d[d[:, 0, 5] > 0]  # persistent grid: only blocks that ran
+        it = d[:, :, 5]
         per = (d[:, :, :5] / it.unsqueeze(-1)).reshape(-1, 5).median(0).values.tolist()
         print("  v%d S1=%d S3=%d  %.1f us %.0f TF | stamped cycles/K-tile: seg1 %.0f b1 %.0f seg2 %.0f b2 %.0f "
               "seg3 %.0f = %.0f" % (v, s1, s3, t * 1e6, 2 * M * N * K / t / 1e12, per[0], per[1], per[2], per[3],
