@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
                     help="linear-layer weights: bf16 (headline) or fp8 e4m3 (BASELINE config 5)")
+    ap.add_argument("--seq-parallel", action="store_true",
+                    help="TP prefill with Megatron sequence parallelism (reduce-scatter/all-gather)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -70,6 +72,8 @@ def main():
     from rag_llm_k8s_amd.parallel.comm import TPComm
     from rag_llm_k8s_amd.utils.workload import build_workload, make_queries
 
+    if a.seq_parallel:
+        os.environ["RAGK_SEQ_PARALLEL"] = "1"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
@@ -126,6 +130,8 @@ def main():
         P = [x for s in allstats for x in s["ptoks"]]
         value = total_tokens / elapsed_max
         par = "dp%d" % ctx.dp if ctx.tp == 1 else ("tp%d" % ctx.tp if ctx.dp == 1 else "tp%d_dp%d" % (ctx.tp, ctx.dp))
+        if ctx.tp > 1 and a.seq_parallel:
+            par += "_sp"
         eng = allstats[0]["eng"]
         res = {
             "metric": METRIC,

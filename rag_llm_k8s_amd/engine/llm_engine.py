@@ -387,7 +387,7 @@ class LLMEngine:
         ntok = sum(n for _, _, n in chunks)
         comm = getattr(m, "comm", None)
         overlap = (self.tp_size > 1 and comm is not None and hasattr(comm, "all_reduce_async")
-                   and ntok >= self.tp_overlap_min_tokens)
+                   and ntok >= self.tp_overlap_min_tokens and not getattr(m, "seq_parallel", False))
         if overlap:
             groups = self._split_chunks(chunks, 2)
             built = [self._prefill_input(g) for g in groups]

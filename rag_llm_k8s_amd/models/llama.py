@@ -237,6 +237,8 @@ class LlamaModel:
         cos, sin = rope_tables(self.D, mp, cfg.rope_theta, cfg.rope_scaling)
         self.cos, self.sin = cos.to(self.device), sin.to(self.device)
         self.kv_cache = None  # list of (k, v) per layer: [nblocks, Hkv, 64, D]
+        self.seq_parallel = os.environ.get("RAGK_SEQ_PARALLEL", "0") == "1"
+        self.sp_min_tokens = int(os.environ.get("RAGK_SP_MIN_TOKENS", "256"))
 
     def allocate_kv_cache(self, num_blocks, dtype=torch.bfloat16):
         self.kv_cache = [(torch.zeros(num_blocks, self.Hkv, 64, self.D, dtype=dtype, device=self.device),
@@ -333,6 +335,48 @@ class LlamaModel:
             self._allreduce(h)
         return self._final(h, inp)
 
+    def hidden_states_sp(self, inp: StepInput):
+        """Tensor-parallel prefill with Megatron sequence parallelism: the residual
+        stream stays sharded over tokens -- rank r owns rows [r*S, (r+1)*S) of the (padded) batch --
+        so embedding, both RMSNorms and both residual adds run on T/tp rows per rank, and each
+        row-parallel projection's all-reduce becomes a reduce-scatter into the owner's rows, paired
+        with an all-gather of the normed rows in front of the next column-parallel GEMM:
+            h_r -> rmsnorm -> AG -> qkv/rope/attention -> o_proj (partial) -> RS -> h_r +=
+                -> rmsnorm -> AG -> gate/up/SiLU -> down (partial) -> RS -> h_r +=
+        Same bytes on xGMI as the two all-reduces (RS + AG), a tp-th of the norm/residual traffic, and
+        a [T/tp, H] residual per rank. Attention, the paged KV cache and the GEMMs see all T tokens of
+        this rank's heads, exactly as in hidden_states. Returns the final-norm'ed logits rows."""
+        be, w, c, comm = self.be, self.w, self.cfg, self.comm
+        tp, r = comm.size, comm.rank
+        Hq, Hkv, D, H = self.Hq, self.Hkv, self.D, c.hidden_size
+        T = inp.ids.shape[0]
+        S = -(-T // tp)
+        Tp = S * tp
+        ids = inp.ids
+        if Tp != T:
+            ids = torch.cat([ids, ids.new_zeros(Tp - T)])
+        h = be.embed(ids[r * S:(r + 1) * S].contiguous(), w.embed)  # [S, H] this rank's rows
+        dev, dt = h.device, h.dtype
+        xg = torch.empty((Tp, H), dtype=dt, device=dev)  # gathered normed rows
+        part = torch.zeros((Tp, H), dtype=dt, device=dev)  # row-parallel partial sums (pad rows stay 0)
+        attn = torch.empty((T, Hq * D), dtype=dt, device=dev)
+        rs = torch.empty((S, H), dtype=dt, device=dev)
+        for li, L in enumerate(w.layers):
+            kc, vc = self.kv_cache[li]
+            comm.all_gather_into(xg, be.rmsnorm(h, L["ln_in"], c.rms_norm_eps))
+            qkv = be.gemm(xg[:T], L["wqkv"])
+            be.rope_kv(qkv, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
+            be.attn_prefill(qkv, kc, vc, inp.meta, attn, Hq, Hkv, D)
+            be.gemm(attn, L["wo"], out=part[:T])
+            h += comm.reduce_scatter(part, rs)
+            comm.all_gather_into(xg, be.rmsnorm(h, L["ln_post"], c.rms_norm_eps))
+            a = be.gemm(xg[:T], L["wgu"], epi="silu_mul")
+            be.gemm(a, L["wdown"], out=part[:T])
+            h += comm.reduce_scatter(part, rs)
+        comm.all_gather_into(xg, be.rmsnorm(h, w.norm, c.rms_norm_eps))
+        x = xg[:T]
+        return be.gather_rows(x, inp.logits_idx) if inp.logits_idx is not None else x
+
     def hidden_states_microbatched(self, inps):
         """Tensor-parallel prefill with communication/compute overlap: the token
         batch is split into micro-batches (consecutive pieces of the packed prompt chunks; a later
@@ -365,4 +409,12 @@ class LlamaModel:
         return self.be.gemm(hs, self.w.lm_head, out_f32=True)
 
     def forward(self, inp: StepInput):
+        if self.use_sp(inp):
+            return self.logits(self.hidden_states_sp(inp))
         return self.logits(self.hidden_states(inp))
+
+    def use_sp(self, inp: StepInput):
+        """Sequence-parallel prefill: TP > 1, RAGK_SEQ_PARALLEL=1 (default off: same xGMI bytes as the
+        all-reduce path, which overlaps micro-batches), at least sp_min_tokens tokens."""
+        return (self.seq_parallel and self.comm is not None and self.comm.size > 1 and inp.meta is not None
+                and inp.meta.kind == "prefill" and inp.ids.shape[0] >= self.sp_min_tokens)

@@ -81,7 +81,31 @@ class TPComm:
         return dist.all_reduce(x, group=self.group, async_op=True)
 
     def all_gather_into(self, out: torch.Tensor, x: torch.Tensor):
-        dist.all_gather_into_tensor(out, x, group=self.group)
+        """out[r*S:(r+1)*S] = rank r's x (S = x.shape[0]): RCCL all-gather; gloo via a list gather."""
+        if self.size == 1:
+            out.copy_(x)
+            return out
+        if x.is_cuda:
+            dist.all_gather_into_tensor(out, x, group=self.group)
+        else:
+            dist.all_gather(list(out.chunk(self.size)), x.contiguous(), group=self.group)
+        return out
+
+    def reduce_scatter(self, x: torch.Tensor, out: torch.Tensor = None):
+        """Sum of every rank's x [size*S, ...], this rank's S-row slice: RCCL reduce-scatter (each
+        byte crosses xGMI once, half an all-reduce); gloo has none -- fp32 all-reduce + slice."""
+        S = x.shape[0] // self.size
+        if out is None:
+            out = torch.empty((S,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        if self.size == 1:
+            out.copy_(x)
+            return out
+        if x.is_cuda:
+            dist.reduce_scatter_tensor(out, x, group=self.group)
+        else:
+            y = x.float()
+            dist.all_reduce(y, group=self.group)
+            out.copy_(y[self.rank * S:(self.rank + 1) * S])
         return out
 
 

@@ -92,6 +92,40 @@ def test_tp2_logits_match_tp1():
     assert torch.equal(out[0], out[1])
 
 
+def _tp_sp_worker(ctx, sd, ids):
+    """TP=2 prefill logits with Megatron sequence parallelism vs the all-reduce path."""
+    from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights
+    from rag_llm_k8s_amd.parallel.comm import TPComm
+
+    w = LlamaWeights.from_state_dict(CFG, sd, "cpu", ctx.tp_rank, ctx.tp)
+    m = LlamaModel(CFG, w, "cpu", comm=TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, "cpu"), max_positions=512)
+    out = {}
+    for sp in (False, True):
+        m.seq_parallel, m.sp_min_tokens = sp, 1
+        local = _prefill_logits(m, ids)
+        parts = [torch.empty_like(local) for _ in range(ctx.tp)]
+        dist.all_gather(parts, local, group=ctx.tp_group)
+        out[sp] = torch.cat(parts, 1)[:, :CFG.vocab_size]
+    return out
+
+
+@pytest.mark.parametrize("n", [40, 41])  # 41: token count not divisible by TP (padded rows)
+def test_tp2_sequence_parallel_matches_allreduce_path(n):
+    from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights
+
+    sd = llama_state_dict(CFG, seed=8, std=0.05)
+    ids = torch.randint(3, CFG.vocab_size, (n,)).tolist()
+    ref = _prefill_logits(LlamaModel(CFG, LlamaWeights.from_state_dict(CFG, sd, "cpu"), "cpu", max_positions=512), ids)
+    out = _run(_tp_sp_worker, 2, sd, ids)
+    for r in range(WORLD):
+        for sp in (False, True):
+            rel = ((out[r][sp] - ref).norm() / ref.norm()).item()
+            assert rel < 2e-2, (sp, rel)
+        rel = ((out[r][True] - out[r][False]).norm() / out[r][False].norm()).item()
+        assert rel < 1e-2, rel
+    assert torch.equal(out[0][True], out[1][True])
+
+
 def _tp_control_worker(ctx, sd, prompts):
     import threading
 
@@ -133,12 +167,13 @@ def _tp_overlap_worker(ctx, sd, prompts):
     from rag_llm_k8s_amd.parallel.comm import TPComm
 
     outs = {}
-    for thr in (10 ** 9, 8):  # never / always micro-batch (8 tokens min)
+    for thr in (10 ** 9, 8, "sp"):  # never / always micro-batch (8 tokens min) / sequence parallel
         w = LlamaWeights.from_state_dict(CFG, sd, "cpu", ctx.tp_rank, ctx.tp)
         m = LlamaModel(CFG, w, "cpu", comm=TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, "cpu"), max_positions=512)
+        m.seq_parallel, m.sp_min_tokens = thr == "sp", 8
         eng = LLMEngine(m, num_blocks=32, max_batch=4, max_prefill_tokens=96, max_model_len=512, use_graphs=False,
                         tp_group=ctx.tp_group)
-        eng.tp_overlap_min_tokens = thr
+        eng.tp_overlap_min_tokens = 8 if thr == "sp" else thr
         p = SamplingParams(max_new_tokens=4, do_sample=False, ignore_eos=True)
         outs[thr] = eng.generate(prompts, p)
     return outs
@@ -151,6 +186,7 @@ def test_tp_prefill_microbatch_overlap_matches_sync():
     out = _run(_tp_overlap_worker, 2, sd, prompts)
     for r in range(WORLD):
         assert out[r][8] == out[r][10 ** 9], out[r]
+        assert out[r]["sp"] == out[r][10 ** 9], out[r]
     assert out[0] == out[1]
 
 
