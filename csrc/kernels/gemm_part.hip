@@ -119,7 +119,7 @@ int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int
   const dim3 grid((N + PT_NB - 1) / PT_NB, K / KS);
 #define RAGK_PART(NK)                                                                                       \
   case NK:                                                                                                  \
-    if constexpr (16 * MT * NK * 64 * 2 <= 128 * 1024) {                                                    \
+    if constexpr (16 * MT * NK * 64 * 2 <= 128 * 1024 && (16 * MT * NK * 64 * 2) % 8192 == 0) {           \
       hipLaunchKernelGGL((gemm_part_kernel<MT, NK>), grid, dim3(PT_THREADS), 0, st, (const bf16_t*)X, ldx, \
                          (const bf16_t*)W, ldw, P, M, N, K);                                                \
       break;                                                                                                \
@@ -128,7 +128,9 @@ int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int
     }
   switch (ks_steps) {
     RAGK_PART(8)
+    RAGK_PART(14)
     RAGK_PART(16)
+    RAGK_PART(28)
     RAGK_PART(32)
     default:
       return (int)hipErrorInvalidValue;
@@ -139,7 +141,8 @@ int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int
 
 }  // namespace
 
-// Slice choice: K-slice KS = 64 * ks_steps (ks_steps in {8, 16, 32}); S = K / KS slabs.
+// Slice choice: K-slice KS = 64 * ks_steps (ks_steps in {8, 14, 16, 28, 32}; 14 / 28 divide the
+// K = 14336 of Llama's down projection into 16 / 8 slabs); S = K / KS slabs.
 // Picks the largest slice that still gives >= 256 blocks and fits the activation slice in LDS.
 static int g_part_min_blocks = 256;
 RAGK_API int ragk_gemm_part_set_min_blocks(int n) {
@@ -151,10 +154,10 @@ RAGK_API int ragk_gemm_part_ksteps(int M, int N, int K) {
   const int mt = (M + 15) / 16;
   const int nb = (N + PT_NB - 1) / PT_NB;
   int best = 0;
-  for (int ks : {32, 16, 8}) {
+  for (int ks : {32, 28, 16, 14, 8}) {
     const int KS = ks * 64;
     if (K % KS) continue;
-    if (16 * mt * KS * 2 > 128 * 1024) continue;
+    if (16 * mt * KS * 2 > 128 * 1024 || (16 * mt * KS * 2) % 8192) continue;  // LDS; 8 waves x 1-KiB DMA pieces
     if (best == 0) best = ks;  // largest legal slice
     if (nb * (K / KS) >= g_part_min_blocks) return ks;
     best = ks;

@@ -155,7 +155,7 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
     return out
 
 
-PART_MIN_BLOCKS = int(os.environ.get("RAGK_PART_MIN_BLOCKS", "256"))
+PART_MIN_BLOCKS = int(os.environ.get("RAGK_PART_MIN_BLOCKS", "512"))
 _part_cfg = [False]
 
 
