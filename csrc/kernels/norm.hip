@@ -11,6 +11,8 @@
 //   E1 BERT/XLM-R embeddings (+LayerNorm), E4/E6 post-LN LayerNorm,
 //   E7 CLS / masked-mean pooling + L2 normalise (sentence-transformers
 //   Normalize(), /root/reference/llm/rag.py:55 normalize_embeddings=True).
+#include <algorithm>
+
 #include "common.h"
 using namespace ragk;
 
@@ -334,6 +336,35 @@ __global__ __launch_bounds__(NT) void gather_rows_kernel(const bf16_t* x, int ld
 // ---- consumers of the split-K decode GEMM (gemm_part.hip): they sum the S fp32 partial slabs
 // P[S][M][ldp] while doing their own row work, so the reduction needs no extra launch.
 
+// Sum of S fp32 slabs of 8 consecutive floats (slab stride in floats), added in slab order 0..S-1.
+// Loads go out in unrolled groups of PSU slabs (index clamped, the excess not added), so a thread
+// has 2 x PSU loads in flight instead of one slab's pair per memory latency (a runtime-S loop made
+// hipcc wait on every slab: 7.7 us for the qkv slabs at S = 8).
+constexpr int PSU = 8;
+__device__ __forceinline__ void sum_slabs8(const float* P, int S, size_t slab, float* a) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = 0.f;
+  for (int s0 = 0; s0 < S; s0 += PSU) {
+    f32x4 p[PSU][2];
+#pragma unroll
+    for (int u = 0; u < PSU; ++u) {
+      const f32x4* ps = reinterpret_cast<const f32x4*>(P + (size_t)min(s0 + u, S - 1) * slab);
+      p[u][0] = ps[0];
+      p[u][1] = ps[1];
+    }
+#pragma unroll
+    for (int u = 0; u < PSU; ++u) {
+      if (s0 + u < S) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] += p[u][0][e];
+          a[4 + e] += p[u][1][e];
+        }
+      }
+    }
+  }
+}
+
 // h = bf16(h + bf16(sum_s P[s][row]))  (HF: bf16 linear output, then the bf16 residual add), written
 // back to h; out = rmsnorm(h) * w exactly as rmsnorm_kernel. One block of 512 threads per row.
 constexpr int PNT = 512;
@@ -352,16 +383,8 @@ __global__ __launch_bounds__(PNT) void add_partials_rmsnorm_kernel(const float* 
   for (int i = 0; i < MAXV; ++i) {
     const int vi = threadIdx.x + i * PNT;
     if (vi < nvec) {
-      float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int s = 0; s < S; ++s) {
-        const f32x4* ps = reinterpret_cast<const f32x4*>(P + ((size_t)s * M + row) * H + vi * 8);
-        const f32x4 p0 = ps[0], p1 = ps[1];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          a[e] += p0[e];
-          a[4 + e] += p1[e];
-        }
-      }
+      float a[8];
+      sum_slabs8(P + (size_t)row * H + vi * 8, S, (size_t)M * H, a);
       unpack8(*reinterpret_cast<const u32x4*>(hr + vi * 8), v[i]);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[i][e] = bf2f(f2bf(v[i][e] + bf2f(f2bf(a[e]))));
@@ -389,17 +412,7 @@ __global__ __launch_bounds__(PNT) void add_partials_rmsnorm_kernel(const float* 
 // the same rotate_half RoPE (HF bf16 op rounding) and paged-KV write. Rotated q goes to q_out
 // (row stride ldq); k / v go to the cache only. grid = (T, HG): head groups split over blocks.
 __device__ __forceinline__ void sum_partials8(const float* P, int S, size_t slab, float* a) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) a[e] = 0.f;
-  for (int s = 0; s < S; ++s) {
-    const f32x4* ps = reinterpret_cast<const f32x4*>(P + (size_t)s * slab);
-    const f32x4 p0 = ps[0], p1 = ps[1];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      a[e] += p0[e];
-      a[4 + e] += p1[e];
-    }
-  }
+  sum_slabs8(P, S, slab, a);
 #pragma unroll
   for (int e = 0; e < 8; ++e) a[e] = bf2f(f2bf(a[e]));
 }
@@ -540,7 +553,10 @@ RAGK_API int ragk_rope_kv_partials(const float* P, int S, int T, int ldp, void* 
                                    void* kc, void* vc, int Hq, int Hkv, int D, int BS, hipStream_t st) {
   if (T <= 0) return 0;
   if (D % 16 || S < 1) return (int)hipErrorInvalidValue;
-  const int groups = 4;
+  // head groups per row: enough blocks to spread the slab reads over the CUs at decode batch sizes,
+  // at least one wave of (head, 8-column) items per block
+  const int items = (Hq + 2 * Hkv) * (D / 16);
+  const int groups = std::max(1, std::min((items + 63) / 64, std::max(4, (512 + T - 1) / T)));
   hipLaunchKernelGGL(rope_kv_partials_kernel, dim3(T, groups), dim3(NT), 0, st, P, S, T, ldp, (bf16_t*)q_out, ldq,
                      positions, cos_t, sin_t, slots, (bf16_t*)kc, (bf16_t*)vc, Hq, Hkv, D, BS);
   return (int)hipGetLastError();

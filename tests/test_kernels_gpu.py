@@ -440,7 +440,7 @@ def test_gemm_part(native, M, N, K):
     assert rel_err(P.sum(0), x.float() @ w.float().t()) < 2e-3
 
 
-@pytest.mark.parametrize("S,M,H", [(1, 3, 384), (4, 32, 4096), (7, 17, 4096)])
+@pytest.mark.parametrize("S,M,H", [(1, 3, 384), (4, 32, 4096), (7, 17, 4096), (9, 32, 4096), (16, 5, 4096)])
 def test_add_partials_rmsnorm(native, S, M, H):
     """Split-K consumer: h <- bf16(h + bf16(sum P)), out = rmsnorm(h) (bit-exact with the torch oracle
     for h; the norm within bf16 rounding)."""
@@ -457,9 +457,10 @@ def test_add_partials_rmsnorm(native, S, M, H):
     assert rel_err(y.cpu(), ref) < 4e-3
 
 
-def test_rope_kv_partials(native):
+@pytest.mark.parametrize("S,T", [(4, 33), (9, 32), (16, 1)])  # S > 8: more than one unrolled slab group
+def test_rope_kv_partials(native, S, T):
     torch.manual_seed(12)
-    S, T, Hq, Hkv, D, BS = 4, 33, 8, 2, 128, 64
+    Hq, Hkv, D, BS = 8, 2, 128, 64
     W = (Hq + 2 * Hkv) * D
     P = torch.randn(S, T, W, device=DEV)
     pos = torch.arange(T, dtype=torch.int32, device=DEV) + 7
