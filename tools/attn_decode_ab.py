@@ -14,7 +14,7 @@ from rag_llm_k8s_amd.ops import native as N  # noqa: E402
 
 Hq, Hkv, D = 32, 8, 128
 MAX_LEN = 8192
-for B, Lk in [(32, 5300), (32, 2000), (1, 5300), (64, 2048)]:
+for B, Lk in [(32, 5300), (32, 2000), (16, 5300), (64, 2048)]:
     nbs = (Lk + 63) // 64
     kc = torch.randn(B * nbs + 4, Hkv, 64, D, device="cuda").bfloat16()
     vc = torch.randn_like(kc)
@@ -22,7 +22,7 @@ for B, Lk in [(32, 5300), (32, 2000), (1, 5300), (64, 2048)]:
     q = torch.randn(B, Hq * D, device="cuda").bfloat16()
     kvl = torch.full((B,), Lk, dtype=torch.int32, device="cuda")
     arms = {"fixed32": (32, -(-((MAX_LEN + 63) // 64) // 32))}
-    for tb in (512, 1024, 2048):
+    for tb in (256, 512, 1024):
         arms["bal%d" % tb] = N.decode_partitions(MAX_LEN, B, Hkv, target_blocks=tb)
     ts = {k: [] for k in arms}
     ref = None
