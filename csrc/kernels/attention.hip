@@ -137,7 +137,10 @@ struct PrefillArgs {
 
 __device__ unsigned long long* g_attn_dbg = nullptr;  // stamp build only
 
-template <int D, int GB, bool CAUSAL, bool PAGED, bool STAMP = false, int NWV = 4>
+// PRIO: wave priority around the MFMA clusters (0 none, 1 QK^T and PV, 2 PV only). Two waves share
+// each SIMD (2 blocks per CU); raising the priority of the wave that is issuing MFMAs lets the
+// other wave's softmax VALU fill around them instead of delaying them.
+template <int D, int GB, bool CAUSAL, bool PAGED, bool STAMP = false, int NWV = 4, int PRIO = 0>
 __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_prefill_kernel(PrefillArgs a) {
   unsigned long long stp[6] = {0, 0, 0, 0, 0, 0};
   using C = Cfg<D>;
@@ -235,6 +238,7 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_prefill_kernel(Prefill
     // ---- S^T = K Q^T ----
     f32x4 s[4][2];
     if (active) {
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         s[t][0] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -246,6 +250,7 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_prefill_kernel(Prefill
           s[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][ks], s[t][1], 0, 0, 0);
         }
       }
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
     }
     if constexpr (STAMP) t1 = __builtin_amdgcn_s_memtime();
     // next tile's DMA issued behind the QK^T MFMAs (async-STAGE split: the issue overlaps the MFMA
@@ -320,6 +325,7 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_prefill_kernel(Prefill
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) pb[ks][qt] = pack_p(s[2 * ks][qt], s[2 * ks + 1][qt]);
       if constexpr (STAMP) t3 = __builtin_amdgcn_s_memtime();
+      if constexpr (PRIO != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int dt = 0; dt < C::DT; ++dt)
 #pragma unroll
@@ -328,6 +334,7 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_prefill_kernel(Prefill
           o[dt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[ks][0], o[dt][0], 0, 0, 0);
           o[dt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[ks][1], o[dt][1], 0, 0, 0);
         }
+      if constexpr (PRIO != 0) __builtin_amdgcn_s_setprio(0);
       if constexpr (STAMP) t4 = __builtin_amdgcn_s_memtime();
     }
     wait_vmcnt0();
@@ -554,6 +561,7 @@ __global__ void attn_decode_reduce_kernel(DecodeArgs a, int D) {
 // Waves per block when 4 query heads share a KV head (Llama GQA): 8 = two 32-row groups share each
 // K/V tile (half the DMA issue and K/V traffic per wave).
 int g_prefill_waves = 4;
+int g_prefill_prio = 1;  // PRIO variant of the Llama config (D 128, 4 heads per block, causal, paged)
 
 template <int D, int GB, bool CAUSAL, bool PAGED>
 hipError_t launch_prefill(const PrefillArgs& a, int n_tiles, hipStream_t st) {
@@ -561,6 +569,10 @@ hipError_t launch_prefill(const PrefillArgs& a, int n_tiles, hipStream_t st) {
   dim3 grid(n_tiles, a.Hkv * (G / GB));
   if (GB == 4 && g_prefill_waves == 8)
     hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 8>), grid, dim3(512), 0, st, a);
+  else if (D == 128 && GB == 4 && CAUSAL && PAGED && g_prefill_prio == 1)
+    hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 4, 1>), grid, dim3(256), 0, st, a);
+  else if (D == 128 && GB == 4 && CAUSAL && PAGED && g_prefill_prio == 2)
+    hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 4, 2>), grid, dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
@@ -582,6 +594,12 @@ RAGK_API int ragk_attn_prefill_stamp(const void* q, int q_stride, const void* k,
   dim3 grid(n_tiles, Hkv * (G / 4));
   hipLaunchKernelGGL((attn_prefill_kernel<128, 4, true, true, true>), grid, dim3(256), 0, st, a);
   return (int)hipGetLastError();
+}
+
+RAGK_API int ragk_attn_prefill_set_prio(int v) {
+  if (v < 0 || v > 2) return (int)hipErrorInvalidValue;
+  g_prefill_prio = v;
+  return 0;
 }
 
 // Returns the query positions per block (the host builds `tiles` with this step).
