@@ -133,6 +133,7 @@ struct PrefillArgs {
   bf16_t* out; int out_stride;
   int Hq, Hkv;
   float scale_log2;
+  unsigned kv_bytes;                       // PAGED: bytes of one cache (K or V) if < 4 GiB, else 0
 };
 
 __device__ unsigned long long* g_attn_dbg = nullptr;  // stamp build only
@@ -140,7 +141,12 @@ __device__ unsigned long long* g_attn_dbg = nullptr;  // stamp build only
 // PRIO: wave priority around the MFMA clusters (0 none, 1 QK^T and PV, 2 PV only). Two waves share
 // each SIMD (2 blocks per CU); raising the priority of the wave that is issuing MFMAs lets the
 // other wave's softmax VALU fill around them instead of delaying them.
-template <int D, int GB, bool CAUSAL, bool PAGED, bool STAMP = false, int NWV = 4, int PRIO = 0>
+// BUF (PAGED only, cache < 4 GiB): K/V tiles staged by buffer_load ... lds with the per-lane byte
+// offsets (row, swizzled chunk) computed once and the tile's cache offset in an SGPR, instead of
+// 64-bit address math per piece per tile (the stamp build put the DMA issue at ~490 of ~4300 wave
+// cycles per tile).
+template <int D, int GB, bool CAUSAL, bool PAGED, bool STAMP = false, int NWV = 4, int PRIO = 0,
+          bool BUF = false>
 __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_prefill_kernel(PrefillArgs a) {
   unsigned long long stp[6] = {0, 0, 0, 0, 0, 0};
   using C = Cfg<D>;
@@ -201,10 +207,34 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_prefill_kernel(Prefill
   }
   int bt_next = PAGED && n_kt > 0 ? s_bt[0] : 0;  // block of the tile staged next
 
+  static_assert(!BUF || (PAGED && C::PIECES % NWV == 0), "buffer staging: paged caches, whole pieces per wave");
+  constexpr int BPW = BUF ? C::PIECES / NWV : 1;
+  int koff[BPW], voff[BPW];
+  i32x4 srd_k, srd_v;
+  if constexpr (BUF) {
+#pragma unroll
+    for (int i = 0; i < BPW; ++i) {
+      const int p = wid_u + NWV * i;
+      const int row = p * C::RPP + lane / C::NC, ph = lane % C::NC;
+      koff[i] = row * C::ROWB + 16 * (ph ^ kswz<D>(row));
+      voff[i] = row * C::ROWB + 16 * (ph ^ vswz<D>(row));
+    }
+    srd_k = make_srd(a.k, a.kv_bytes);
+    srd_v = make_srd(a.v, a.kv_bytes);
+  }
   auto stage = [&](int kt, int buf) {
     char* sK = smem + buf * 2 * C::TILEB;
     char* sV = sK + C::TILEB;
-    if constexpr (PAGED) {
+    if constexpr (BUF) {
+      // unsigned: a cache of 2-4 GiB has tile offsets past INT_MAX (soffset is an unsigned 32-bit add)
+      const int soff = __builtin_amdgcn_readfirstlane((int)((unsigned)(bt_next * a.Hkv + kvh) * (unsigned)(KT * D * 2)));
+#pragma unroll
+      for (int i = 0; i < BPW; ++i) {
+        const int p = wid_u + NWV * i;
+        blds16(srd_k, koff[i], soff, sK + p * 1024);
+        blds16(srd_v, voff[i], soff, sV + p * 1024);
+      }
+    } else if constexpr (PAGED) {
       const size_t base = ((size_t)bt_next * a.Hkv + kvh) * KT * D;
       const bf16_t* kb = a.k + base;
       const bf16_t* vb = a.v + base;
@@ -562,11 +592,18 @@ __global__ void attn_decode_reduce_kernel(DecodeArgs a, int D) {
 // K/V tile (half the DMA issue and K/V traffic per wave).
 int g_prefill_waves = 4;
 int g_prefill_prio = 1;  // PRIO variant of the Llama config (D 128, 4 heads per block, causal, paged)
+int g_prefill_buf = 1;   // BUF staging for that config when the cache is < 4 GiB
 
 template <int D, int GB, bool CAUSAL, bool PAGED>
 hipError_t launch_prefill(const PrefillArgs& a, int n_tiles, hipStream_t st) {
   const int G = a.Hq / a.Hkv;
   dim3 grid(n_tiles, a.Hkv * (G / GB));
+  if constexpr (D == 128 && GB == 4 && CAUSAL && PAGED) {
+    if (g_prefill_waves == 4 && g_prefill_prio == 1 && g_prefill_buf && a.kv_bytes) {
+      hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 4, 1, true>), grid, dim3(256), 0, st, a);
+      return hipGetLastError();
+    }
+  }
   if (GB == 4 && g_prefill_waves == 8)
     hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 8>), grid, dim3(512), 0, st, a);
   else if (D == 128 && GB == 4 && CAUSAL && PAGED && g_prefill_prio == 1)
@@ -602,6 +639,11 @@ RAGK_API int ragk_attn_prefill_set_prio(int v) {
   return 0;
 }
 
+RAGK_API int ragk_attn_prefill_set_buf(int v) {
+  g_prefill_buf = v ? 1 : 0;
+  return 0;
+}
+
 // Returns the query positions per block (the host builds `tiles` with this step).
 RAGK_API int ragk_attn_prefill_set_waves(int w) {
   if (w != 4 && w != 8) return (int)hipErrorInvalidValue;
@@ -622,8 +664,11 @@ RAGK_API int ragk_attn_prefill(const void* q, int q_stride, const void* k, const
                                int Hq, int Hkv, int D, int causal, int paged, float scale, hipStream_t st) {
   if (n_tiles <= 0) return 0;
   if (Hq % Hkv) return (int)hipErrorInvalidValue;
+  // paged: kv_stride = number of cache blocks (sizes the buffer descriptors of the BUF staging)
+  const unsigned long long cache_bytes = paged ? (unsigned long long)kv_stride * Hkv * KT * D * 2 : 0ull;
   PrefillArgs a{(const bf16_t*)q, q_stride, (const bf16_t*)k, (const bf16_t*)v, kv_stride, block_tables, bt_stride,
-                cu_q, cu_kv, kv_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, scale * 1.4426950408889634f};
+                cu_q, cu_kv, kv_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, scale * 1.4426950408889634f,
+                cache_bytes < (1ull << 32) ? (unsigned)cache_bytes : 0u};
   const int G = Hq / Hkv;
   const int GB = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
 #define RAGK_PF(DD, GG, CC, PP)                                                          \

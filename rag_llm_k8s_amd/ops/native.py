@@ -438,6 +438,9 @@ def attn_prefill(q, k, v, cu_q, kv_lens, tiles, out, Hq, Hkv, D, causal=True, pa
         _req(block_tables.stride(0) <= 2048, "prefill block tables wider than 2048 blocks (128k tokens)")
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     n_tiles = tiles.shape[0]
+    if paged:
+        _req(v.shape == k.shape, "paged k/v caches differ in shape")
+        kv_stride = k.shape[0]  # paged: the cache block count (sizes the kernel's buffer descriptors)
     check(_lib.lib().ragk_attn_prefill(
         q.data_ptr(), q.stride(0), k.data_ptr(), v.data_ptr(), kv_stride, ptr(block_tables),
         block_tables.stride(0) if block_tables is not None else 0, cu_q.data_ptr(), ptr(cu_kv), kv_lens.data_ptr(),

@@ -12,7 +12,7 @@ from rag_llm_k8s_amd.ops import native as N  # noqa: E402
 L = _lib.lib()
 Hq, Hkv, D = 32, 8, 128
 dev = "cuda"
-VARIANTS = (0, 1, 2)
+VARIANTS = (0, 1, 3)  # 3 = prio 1 + buffer-descriptor K/V staging
 for B, S in [(6, 5184), (2, 2048)]:
     nb = B * S // 64 + 8
     kc = torch.randn(nb, Hkv, 64, D, device=dev).bfloat16()
@@ -30,7 +30,8 @@ for B, S in [(6, 5184), (2, 2048)]:
 
     for r in range(5):
         for v in VARIANTS:
-            L.ragk_attn_prefill_set_prio(v)
+            L.ragk_attn_prefill_set_prio(min(v, 1) if v != 2 else 2)
+            L.ragk_attn_prefill_set_buf(1 if v == 3 else 0)
             fn()
             torch.cuda.synchronize()
             res[v] = out.clone()
@@ -41,7 +42,8 @@ for B, S in [(6, 5184), (2, 2048)]:
             e.record()
             torch.cuda.synchronize()
             ts[v].append(s.elapsed_time(e) / 5 * 1e-3)
-    L.ragk_attn_prefill_set_prio(0)
+    L.ragk_attn_prefill_set_prio(1)
+    L.ragk_attn_prefill_set_buf(1)
     for v in VARIANTS:
         assert torch.equal(res[v], res[0]), v
     flops = 4 * B * S * S * Hq * D / 2
