@@ -26,10 +26,31 @@ constexpr int PT_NB = 64;  // output columns per block
 
 __device__ __forceinline__ int pswz16(int row, int chunk) { return chunk ^ (row & 15); }
 
-template <int MT, int NKS>
+// e4m3fn x 8 -> bf16 x 8, exact (3 mantissa bits fit bf16's 7; the f32 -> bf16 step truncates bits
+// that are zero)
+__device__ __forceinline__ unsigned pf32x2_bf16(f32x2 f) {
+  return __builtin_amdgcn_perm(__float_as_uint(f[1]), __float_as_uint(f[0]), 0x07060302u);
+}
+__device__ __forceinline__ bf16x8 p_fp8x8_bf16(unsigned lo, unsigned hi) {
+  u32x4 r;
+  r[0] = pf32x2_bf16(__builtin_amdgcn_cvt_pk_f32_fp8((int)lo, false));
+  r[1] = pf32x2_bf16(__builtin_amdgcn_cvt_pk_f32_fp8((int)lo, true));
+  r[2] = pf32x2_bf16(__builtin_amdgcn_cvt_pk_f32_fp8((int)hi, false));
+  r[3] = pf32x2_bf16(__builtin_amdgcn_cvt_pk_f32_fp8((int)hi, true));
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// FP8 (W8A16, BASELINE config 5): W is e4m3fn [N][K] bytes with one fp32 scale per row. A lane's
+// 16-B load is 16 consecutive k of one row, i.e. two MFMA k-steps: lane (fr, fh) of 64-k block j
+// holds k = 64j + 16fh + [0, 8) for the first MFMA and + [8, 16) for the second; the activation
+// fragments are read from LDS at the same k (chunks 8j + 2fh and 8j + 2fh + 1), so both operands
+// see the same permutation of K and the dot product is unchanged. Half the weight bytes of bf16 per
+// K-slice; the row scale is applied to the partial before it is written.
+template <int MT, int NKS, bool FP8 = false>
 __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* __restrict__ X, int ldx,
                                                                   const bf16_t* __restrict__ W, int ldw,
-                                                                  float* __restrict__ P, int M, int N, int K) {
+                                                                  float* __restrict__ P, int M, int N, int K,
+                                                                  const float* __restrict__ wscale = nullptr) {
   constexpr int KS = NKS * 64;          // K-slice of the block (two halves of NKS k-steps of 32)
   constexpr int XROWS = 16 * MT;
   constexpr int ROWB = KS * 2;          // bytes per LDS row
@@ -62,14 +83,23 @@ __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* 
 
   __builtin_amdgcn_sched_barrier(0);
   // 2) this wave's whole weight stream, all loads in flight: row n0 + 16nt + fr,
-  //    k = kbase + kh*KS/2 + 32ks + 8fh
+  //    bf16: k = kbase + kh*KS/2 + 32ks + 8fh;  fp8: k = kbase + kh*KS/2 + 64j + 16fh (16 k per load)
+  constexpr int NLD = FP8 ? NKS / 2 : NKS;  // 16-B loads per lane
+  static_assert(!FP8 || NKS % 2 == 0, "fp8 slices cover whole 64-k blocks");
   const int wrow = min(n0 + 16 * nt + fr, N - 1);
-  const bf16_t* wp = W + (size_t)wrow * ldw + kbase + kh * (KS / 2) + fh * 8;
-  bf16x8 wf[NKS];
+  bf16x8 wf[NLD];
+  if constexpr (FP8) {
+    const unsigned char* wp = reinterpret_cast<const unsigned char*>(W) + (size_t)wrow * ldw + kbase + kh * (KS / 2) +
+                              fh * 16;
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
-  // vmcnt(NKS): the DMA (older than the NKS weight loads) has landed
-  __builtin_amdgcn_s_waitcnt((NKS & 15) | (((NKS >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
+    for (int j = 0; j < NLD; ++j) wf[j] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 64 * j));
+  } else {
+    const bf16_t* wp = W + (size_t)wrow * ldw + kbase + kh * (KS / 2) + fh * 8;
+#pragma unroll
+    for (int ks = 0; ks < NLD; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
+  }
+  // vmcnt(NLD): the DMA (older than the NLD weight loads) has landed
+  __builtin_amdgcn_s_waitcnt((NLD & 15) | (((NLD >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();  // raw: __syncthreads() would drain the weight loads too (vmcnt(0))
   __builtin_amdgcn_sched_barrier(0);
@@ -78,14 +108,28 @@ __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* 
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto xfrag = [&](int chunk, int t) {
+    const int r = 16 * t + fr;
+    return *reinterpret_cast<const bf16x8*>(smem + r * ROWB + 16 * ((chunk & ~15) | ((chunk & 15) ^ (r & 15))));
+  };
+  if constexpr (FP8) {
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    const int chunk = (kh * (KS / 2) + 32 * ks) / 8 + fh;
+    for (int j = 0; j < NLD; ++j) {
+      const u32x4 raw = __builtin_bit_cast(u32x4, wf[j]);
+      const bf16x8 w0 = p_fp8x8_bf16(raw[0], raw[1]), w1 = p_fp8x8_bf16(raw[2], raw[3]);
+      const int chunk = (kh * (KS / 2) + 64 * j) / 8 + 2 * fh;
 #pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      const int r = 16 * t + fr;
-      const bf16x8 xf = *reinterpret_cast<const bf16x8*>(smem + r * ROWB + 16 * ((chunk & ~15) | ((chunk & 15) ^ (r & 15))));
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[ks], acc[t], 0, 0, 0);
+      for (int t = 0; t < MT; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xfrag(chunk, t), w0, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xfrag(chunk + 1, t), w1, acc[t], 0, 0, 0);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < NLD; ++ks) {
+      const int chunk = (kh * (KS / 2) + 32 * ks) / 8 + fh;
+#pragma unroll
+      for (int t = 0; t < MT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xfrag(chunk, t), wf[ks], acc[t], 0, 0, 0);
     }
   }
 
@@ -100,28 +144,29 @@ __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* 
   if (kh == 0) {
     const int col = n0 + 16 * nt + fr;
     float* ps = P + (size_t)s * M * N;
+    const float sc = FP8 ? wscale[min(col, N - 1)] : 1.f;
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const f32x4 o = red[(nt * MT + t) * 64 + lane];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * t + 4 * fh + r;
-        if (row < M && col < N) ps[(size_t)row * N + col] = acc[t][r] + o[r];
+        if (row < M && col < N) ps[(size_t)row * N + col] = FP8 ? (acc[t][r] + o[r]) * sc : acc[t][r] + o[r];
       }
     }
   }
 }
 
-template <int MT>
+template <int MT, bool FP8 = false>
 int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K, int ks_steps,
-                   hipStream_t st) {
+                   hipStream_t st, const float* wscale = nullptr) {
   const int KS = ks_steps * 64;
   const dim3 grid((N + PT_NB - 1) / PT_NB, K / KS);
 #define RAGK_PART(NK)                                                                                       \
   case NK:                                                                                                  \
     if constexpr (16 * MT * NK * 64 * 2 <= 128 * 1024 && (16 * MT * NK * 64 * 2) % 8192 == 0) {           \
-      hipLaunchKernelGGL((gemm_part_kernel<MT, NK>), grid, dim3(PT_THREADS), 0, st, (const bf16_t*)X, ldx, \
-                         (const bf16_t*)W, ldw, P, M, N, K);                                                \
+      hipLaunchKernelGGL((gemm_part_kernel<MT, NK, FP8>), grid, dim3(PT_THREADS), 0, st, (const bf16_t*)X, ldx, \
+                         (const bf16_t*)W, ldw, P, M, N, K, wscale);                                        \
       break;                                                                                                \
     } else {                                                                                                \
       return (int)hipErrorInvalidValue;                                                                     \
@@ -177,6 +222,23 @@ RAGK_API int ragk_gemm_part(const void* X, int ldx, const void* W, int ldw, floa
     case 2: return launch_part_mt<2>(X, ldx, W, ldw, P, M, N, K, ks_steps, st);
     case 3: return launch_part_mt<3>(X, ldx, W, ldw, P, M, N, K, ks_steps, st);
     case 4: return launch_part_mt<4>(X, ldx, W, ldw, P, M, N, K, ks_steps, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// W8A16 variant: W = e4m3fn [N][K] bytes (ldw in bytes), wscale = fp32 [N]; same slabs / slices.
+RAGK_API int ragk_gemm_part_fp8(const void* X, int ldx, const void* W8, int ldw, const float* wscale, float* P, int M,
+                                int N, int K, int ks_steps, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (M > 64 || ks_steps <= 0 || ks_steps % 2 || K % (64 * ks_steps) != 0 || !wscale || ldw % 16)
+    return (int)hipErrorInvalidValue;
+  const int mt = (M + 15) / 16;
+  if (16 * mt * ks_steps * 64 * 2 > 128 * 1024) return (int)hipErrorInvalidValue;
+  switch (mt) {
+    case 1: return launch_part_mt<1, true>(X, ldx, W8, ldw, P, M, N, K, ks_steps, st, wscale);
+    case 2: return launch_part_mt<2, true>(X, ldx, W8, ldw, P, M, N, K, ks_steps, st, wscale);
+    case 3: return launch_part_mt<3, true>(X, ldx, W8, ldw, P, M, N, K, ks_steps, st, wscale);
+    case 4: return launch_part_mt<4, true>(X, ldx, W8, ldw, P, M, N, K, ks_steps, st, wscale);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -30,6 +30,7 @@ _SIGS = {
     "ragk_gemm_stream_set_nt": [I],
     "ragk_gemm_w4": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_part": [P, I, P, I, P, I, I, I, I, S],
+    "ragk_gemm_part_fp8": [P, I, P, I, P, P, I, I, I, I, S],
     "ragk_attn_decode_set_nt": [I],
     "ragk_attn_prefill_set_waves": [I],
     "ragk_attn_prefill_stamp": [P, I, P, P, P, I, P, P, P, I, P, I, I, I, F, P, S],

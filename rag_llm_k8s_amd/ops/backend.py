@@ -112,10 +112,11 @@ class TorchBackend:
     enable_part = False  # the torch oracle runs the same dataflow when a test switches it on
 
     def part_ok(self, M, w):
-        return self.enable_part and not isinstance(w, Fp8Weight) and M <= 64
+        return self.enable_part and M <= 64
 
     def gemm_part(self, x, w):
-        return (x.float() @ w.float().t()).unsqueeze(0)
+        wf = w.dequant() if isinstance(w, Fp8Weight) else w.float()
+        return (x.float() @ wf.t()).unsqueeze(0)
 
     def add_partials_rmsnorm(self, P, h, w, eps):
         h.copy_((h.float() + P.sum(0).to(h.dtype).float()).to(h.dtype))
@@ -222,7 +223,7 @@ class NativeBackend(TorchBackend):
     enable_part = __import__("os").environ.get("RAGK_DECODE_PART", "1") == "1"
 
     def part_ok(self, M, w):
-        if not self.enable_part or isinstance(w, Fp8Weight) or M > 64:
+        if not self.enable_part or M > 64:
             return False
         return self.n.gemm_part_slabs(M, w.shape[0], w.shape[1])[1] > 0
 

@@ -172,19 +172,34 @@ def gemm_part_slabs(M, N, K, ks=None):
 
 def gemm_part(x, w, out=None, ks=None):
     """Decode GEMM v5 (csrc/kernels/gemm_part.hip): fp32 split-K partials P[S, M, N] with
-    P.sum(0) = x @ w^T. The consumer (add_partials_rmsnorm / rope_kv_partials) does the reduction."""
+    P.sum(0) = x @ w^T. The consumer (add_partials_rmsnorm / rope_kv_partials) does the reduction.
+    w: bf16 [N, K], or an :class:`ops.fp8.Fp8Weight` (W8A16: e4m3fn rows, per-row scale applied to
+    the partials)."""
+    from .fp8 import Fp8Weight
+
     _bf16_2d(x, "x")
-    _bf16_2d(w, "w")
+    fp8 = isinstance(w, Fp8Weight)
+    wt = w.w8 if fp8 else w
+    if fp8:
+        _req(wt.is_cuda and wt.dim() == 2 and wt.stride(1) == 1 and wt.element_size() == 1, "fp8 weight rows")
+        _req(w.scale.dtype == torch.float32 and w.scale.is_contiguous(), "fp8 weight scales fp32")
+    else:
+        _bf16_2d(wt, "w")
     M, K = x.shape
-    N = w.shape[0]
-    _req(w.shape[1] == K and M <= 64, "gemm_part shape %s x %s" % (tuple(x.shape), tuple(w.shape)))
+    N = wt.shape[0]
+    _req(wt.shape[1] == K and M <= 64, "gemm_part shape %s x %s" % (tuple(x.shape), tuple(wt.shape)))
     ks, S = gemm_part_slabs(M, N, K, ks)
     _req(S > 0, "gemm_part: unsupported K=%d" % K)
     if out is None:
         out = torch.empty((S, M, N), dtype=torch.float32, device=x.device)
     _req(out.dtype == torch.float32 and out.is_contiguous() and out.numel() >= S * M * N, "gemm_part out")
-    check(_lib.lib().ragk_gemm_part(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), M, N, K,
-                                    ks, stream_ptr()), "ragk_gemm_part")
+    if fp8:
+        check(_lib.lib().ragk_gemm_part_fp8(x.data_ptr(), x.stride(0), wt.data_ptr(), wt.stride(0),
+                                            w.scale.data_ptr(), out.data_ptr(), M, N, K, ks, stream_ptr()),
+              "ragk_gemm_part_fp8")
+    else:
+        check(_lib.lib().ragk_gemm_part(x.data_ptr(), x.stride(0), wt.data_ptr(), wt.stride(0), out.data_ptr(), M, N,
+                                        K, ks, stream_ptr()), "ragk_gemm_part")
     return out[:S] if out.dim() == 3 else out
 
 

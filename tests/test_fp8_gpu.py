@@ -121,3 +121,22 @@ def test_gemm_fp8_stream_decode(native, monkeypatch, M, N, K):
     wgu = F8.quantize_weight(R.pack_gate_up(w[: N // 2 // 64 * 64 or 64], g[: N // 2 // 64 * 64 or 64]))
     y = native.gemm_fp8(x, wgu, epi="silu_mul")
     assert rel_err(y, F8.reference_linear(x, wgu, epi="silu_mul")) < 1e-2
+
+
+@pytest.mark.parametrize("M", [1, 32, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (1000, 1024)])
+def test_gemm_part_fp8(native, M, N, K):
+    """W8A16 split-K partial GEMM (gemm_part.hip FP8): the slabs (row scale applied) sum to
+    x @ dequant(w)^T, for every slice size the planner can pick."""
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    wq = F8.quantize_weight((torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16())
+    ref = x.float() @ wq.dequant().t()
+    ks0, S0 = native.gemm_part_slabs(M, N, K)
+    assert S0 > 0
+    for ks in sorted({ks0, 8, 16}):
+        if K % (64 * ks):
+            continue
+        P = native.gemm_part(x, wq, ks=ks)
+        assert P.shape == (K // (64 * ks), M, N)
+        assert rel_err(P.sum(0), ref) < 2e-3, ks
