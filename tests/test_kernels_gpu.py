@@ -52,6 +52,27 @@ def test_gemm_w4_persistent(native, M, N, K, grid):
         native.set_w4_grid(-1)
 
 
+def test_gemm_blaslt_path_and_auto_choice(native):
+    """Path 7 (hipBLASLt for plain / residual prefill GEMMs), in place on the residual as the model
+    calls it, and the measured w4-vs-hipBLASLt choice: correct whichever kernel wins."""
+    torch.manual_seed(21)
+    M, N, K = 8192 + 17, 1024, 512
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    ref = x.float() @ w.float().t()
+    assert rel_err(native.gemm(x, w, path=7), ref) < 1e-2
+    h = r.clone()
+    native.gemm(x, w, resid=h, epi="resid", out=h, path=7)
+    assert rel_err(h, ref + r.float()) < 1e-2
+    native._blaslt_choice.clear()
+    h = r.clone()
+    native.gemm(x, w, resid=h, epi="resid", out=h)  # times both on scratch, then runs the winner once
+    assert (N, K, "resid") in native._blaslt_choice
+    assert rel_err(h, ref + r.float()) < 1e-2
+    assert rel_err(native.gemm(x, w), ref) < 1e-2
+
+
 def _check_pingpong(native, M, N, K, path=2):
     torch.manual_seed(20)
     x = torch.randn(M, K, device=DEV).bfloat16()
