@@ -111,8 +111,24 @@ class LLMEngine:
         self.graphs = {}
         self.stats = dict(prefill_steps=0, decode_steps=0, prefill_tokens=0, decode_tokens=0, prefill_s=0.0,
                           decode_s=0.0)
-        self._pin = torch.empty(1 << 20 if self.is_cuda else 0, dtype=torch.int32, pin_memory=self.is_cuda)
+        # two pinned staging buffers, alternated per step: with the asynchronous decode pipeline a
+        # step's H2D copy may still be pending while the host stages the next one
+        self._pins = [torch.empty(1 << 20 if self.is_cuda else 0, dtype=torch.int32, pin_memory=self.is_cuda)
+                      for _ in range(2)]
+        self._pin_idx = 0
+        self._pin = self._pins[0]
         self._pin_off = 0
+        # Asynchronous decode (hipGraph path, TP=1): step t+1 is enqueued before step t's tokens are
+        # read back; its input ids come from step t's sampled tokens on the device (D2D), so the GPU
+        # never waits for the host round trip between decode steps. Tokens are accepted one step late;
+        # a sequence that stops on EOS has computed one extra (discarded) row, and its KV blocks are
+        # freed only after that step has completed.
+        self.async_decode = self.use_graphs and self.tp_size == 1 and os.environ.get("RAGK_ASYNC_DECODE", "1") == "1"
+        self._inflight = None  # dict(seqs, rows, entry, event, host_out, n)
+        self._free_after = []  # seq ids whose blocks are freed once the in-flight step has completed
+        self._out_pins = [torch.empty(max(1, max_batch), dtype=torch.int32, pin_memory=self.is_cuda)
+                          for _ in range(2)]
+        self._out_idx = 0
 
     # ------------------------------------------------------------------ requests
     def add_request(self, prompt_ids, params: SamplingParams, seed: Optional[int] = None) -> Sequence:
@@ -141,7 +157,7 @@ class LLMEngine:
         return s
 
     def has_work(self):
-        return bool(self.waiting) or bool(self.running)
+        return bool(self.waiting) or bool(self.running) or self._inflight is not None
 
     # ------------------------------------------------------------------ scheduling
     def _admit(self):
@@ -196,18 +212,28 @@ class LLMEngine:
             time.sleep(float(f["step_delay_ms"]) / 1000.0)
 
     def step(self):
-        """One engine step. Returns the sequences that finished in it."""
+        """One engine step. Returns the sequences that finished in it (with asynchronous decode:
+        whose last token was read back in it)."""
+        self._pin_idx ^= 1
+        self._pin = self._pins[self._pin_idx]
         self._pin_off = 0
+        fin = []
         if self._aborts:
+            fin += self._drain()
             self._apply_aborts()
         self._fault_hooks()
         chunks = self._admit()
         if chunks:
-            return self._prefill(chunks)
+            fin += self._drain()
+            return fin + self._prefill(chunks)
+        ready = [s for s in self.running if s.computed >= len(s.prompt)]
+        if ready and self.async_decode:
+            return fin + self._decode_async(ready)
+        fin += self._drain()
         ready = [s for s in self.running if s.computed >= len(s.prompt)]
         if ready:
-            return self._decode(ready)
-        return []
+            return fin + self._decode(ready)
+        return fin
 
     def run_until_done(self, callback=None):
         finished = []
@@ -239,17 +265,21 @@ class LLMEngine:
             cap = max(1 << 20, 2 * (self._pin_off + n))
             torch.cuda.current_stream(self.device).synchronize()
             self._pin = torch.empty(cap, dtype=torch.int32, pin_memory=True)
+            self._pins[self._pin_idx] = self._pin
             self._pin_off = 0
         buf = self._pin[self._pin_off:self._pin_off + n]
         self._pin_off += n
         buf.copy_(t.reshape(-1))
         return buf.to(self.device, non_blocking=True).reshape(t.shape)
 
-    def _finish(self, s, reason):
+    def _finish(self, s, reason, defer_free=False):
         s.status = FINISHED
         s.finish_reason = reason
         s.t_done = time.perf_counter()
-        self.bm.free(s.id)
+        if defer_free:  # a step still in flight writes this sequence's KV row
+            self._free_after.append(s.id)
+        else:
+            self.bm.free(s.id)
         self.running.remove(s)
         s.done.set()
 
@@ -501,6 +531,107 @@ class LLMEngine:
     def warmup_graphs(self, sizes=None):
         for b in sizes or self.buckets:
             self._decode_graph(b)
+
+    # ------------------------------------------------------------------ asynchronous decode
+    def _decode_inputs_async(self, seqs, B, carried):
+        """As _decode_inputs_host, for a step whose rows with carried[i] feed the previous step's
+        in-flight token (position = committed length; id patched on the device)."""
+        mb = self.max_blocks
+        n = len(seqs)
+        out = np.zeros(4 * B + B * mb + (4 * B + B * mb) % 2, dtype=np.int32)
+        ids, pos, slots, kvl = (out[i * B:(i + 1) * B] for i in range(4))
+        bt = out[4 * B:4 * B + B * mb].reshape(B, mb)
+        kvl[:] = 1
+        if n:
+            c = np.asarray(carried, dtype=np.int32)
+            p = np.fromiter((s.length - 1 for s in seqs), dtype=np.int32, count=n) + c
+            ids[:n] = np.fromiter((0 if ci else s.token_at(int(q)) for s, q, ci in zip(seqs, p, carried)),
+                                  dtype=np.int32, count=n)
+            bt[:n] = np.stack([self._bt_row(s, int(q) // BLOCK + 1) for s, q in zip(seqs, p)])
+            pos[:n] = p
+            slots[:n] = bt[np.arange(n), p // BLOCK] * BLOCK + p % BLOCK
+            kvl[:n] = p + 1
+        return out
+
+    def _decode_async(self, ready):
+        t0 = time.perf_counter()
+        prev = self._inflight
+        prev_row = {} if prev is None else {id(s): i for i, s in enumerate(prev["seqs"])}
+        seqs = []
+        for s in ready:
+            if id(s) in prev_row:  # its in-flight token will be accepted: does it get another step?
+                L = len(s.out) + 1
+                if L >= s.params.max_new_tokens or s.length + 1 >= self.max_model_len:
+                    continue
+            seqs.append(s)
+        if not seqs:
+            return self._drain()
+        n = len(seqs)
+        carried = [id(s) in prev_row for s in seqs]
+        B = self._bucket(n)
+        e = self._decode_graph(B)
+        samp = self._sampling_host(seqs, pad_to=B)
+        steps = samp[5 * B:5 * B + n]
+        steps += np.asarray(carried, dtype=np.int32)  # sampling step index of the token being produced
+        host = np.concatenate([self._decode_inputs_async(seqs, B, carried), samp])
+        e["packed"].copy_(self._h2d_i32(host), non_blocking=True)
+        if any(carried):
+            ids = e["packed"][:B]
+            src = [prev_row[id(s)] for s, c in zip(seqs, carried) if c]
+            if all(carried) and src == list(range(n)):
+                ids[:n].copy_(prev["out"][:n])
+            else:
+                dst = [i for i, c in enumerate(carried) if c]
+                idx = self._h2d_i32(np.asarray(src + dst, dtype=np.int32)).long()
+                k = len(src)
+                ids.index_copy_(0, idx[k:], prev["out"].index_select(0, idx[:k]))
+        e["graph"].replay()
+        self._out_idx ^= 1
+        host_out = self._out_pins[self._out_idx]
+        host_out[:n].copy_(e["out"][:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        for s in seqs:
+            s.computed = s.length + (1 if id(s) in prev_row else 0)
+        cur = dict(seqs=seqs, out=e["out"], event=ev, host_out=host_out, n=n)
+        fin = self._collect(prev, in_flight=set(id(s) for s in seqs))
+        self._inflight = cur
+        self.stats["decode_steps"] += 1
+        self.stats["decode_s"] += time.perf_counter() - t0
+        return fin
+
+    def _collect(self, step, in_flight=frozenset()):
+        """Wait for an in-flight decode step, accept its tokens, free what it no longer touches."""
+        if step is None:
+            return []
+        step["event"].synchronize()
+        for sid in self._free_after:  # rows of the step before `step`: done with those blocks now
+            self.bm.free(sid)
+        self._free_after = []
+        tok = step["host_out"][:step["n"]].tolist()
+        finished = []
+        for s, t in zip(step["seqs"], tok):
+            if s.status == FINISHED:  # stopped (or aborted) before this step's token was read
+                continue
+            r = self._accept(s, t)
+            self.stats["decode_tokens"] += 1
+            if r:
+                self._finish(s, r, defer_free=id(s) in in_flight)
+                finished.append(s)
+        return finished
+
+    def _drain(self):
+        """Complete the in-flight decode step (before a prefill, an abort, or when nothing is left)."""
+        if self._inflight is None:
+            return []
+        t0 = time.perf_counter()
+        step, self._inflight = self._inflight, None
+        fin = self._collect(step)
+        for sid in self._free_after:
+            self.bm.free(sid)
+        self._free_after = []
+        self.stats["decode_s"] += time.perf_counter() - t0
+        return fin
 
     def _decode(self, seqs):
         t0 = time.perf_counter()

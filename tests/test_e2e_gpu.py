@@ -45,6 +45,30 @@ def test_graph_decode_equals_eager(native, tiny_llama):
     assert a == b
 
 
+def test_async_decode_equals_sync(native, tiny_llama):
+    """Asynchronous decode pipeline (ids fed on the device, tokens accepted one step late, deferred
+    KV frees) vs the synchronous graph path: identical tokens with early stops (stop tokens), per-request
+    lengths (batch composition changes -> the gather path) and more requests than batch slots
+    (prefills drain the pipeline mid-run); sampled, so the per-step seeds must line up too."""
+    cfg, sd = tiny_llama
+    torch.manual_seed(4)
+    prompts = [torch.randint(3, 1000, (n,)).tolist() for n in (9, 40, 200, 5, 77, 130, 31)]
+    stop = list(range(3, 1000, 9))  # ~1/9 of the vocabulary ends a sequence
+    params = [SamplingParams(max_new_tokens=m, temperature=0.9, top_p=0.95, top_k=50, stop_token_ids=stop)
+              for m in (12, 3, 20, 7, 16, 1, 9)]
+    outs = {}
+    for mode in (True, False):
+        eng = _engine(cfg, sd, "cuda", graphs=True, mb=4)
+        eng.async_decode = mode
+        seqs = [eng.add_request(pr, pa, seed=10 + i) for i, (pr, pa) in enumerate(zip(prompts, params))]
+        eng.run_until_done()
+        assert eng._inflight is None and not eng.running
+        assert eng.bm.free_blocks() == 64 - 1  # every block back (block 0 is the scratch block)
+        outs[mode] = [(s.out, s.finish_reason) for s in seqs]
+    assert outs[True] == outs[False]
+    assert any(r == "stop" for _, r in outs[True]) and any(r == "length" for _, r in outs[True])
+
+
 def test_gpu_prefill_logits_vs_cpu(native, tiny_llama):
     cfg, sd = tiny_llama
     from rag_llm_k8s_amd.models.llama import StepInput
