@@ -213,6 +213,16 @@ class RagService:
             self._seed += 1
             return self._seed
 
+    def _decode_answer(self, prompt_ids, out_ids):
+        """decode(prompt + out) as the reference does before its split on "Chatbot:", without
+        re-decoding the ~5k prompt tokens: when the prompt's bytes end with "Chatbot:" (an ASCII
+        boundary, so byte-level decoding of the concatenation is the concatenation of the decodes),
+        the text after the last "Chatbot:" only depends on the generated part."""
+        tail = self.tok.decode(prompt_ids[-8:], skip_special_tokens=True)
+        if tail.endswith("Chatbot:"):
+            return "Chatbot:" + self.tok.decode(out_ids, skip_special_tokens=True)
+        return self.tok.decode(list(prompt_ids) + list(out_ids), skip_special_tokens=True)
+
     def _prompt_ids(self, full_prompt, ids=None):
         ids = self.tok.encode(full_prompt, add_special_tokens=True) if ids is None else list(ids)
         limit = self.engine.max_model_len - self.params.max_new_tokens
@@ -249,7 +259,7 @@ class RagService:
         tr.add("decode", s.t_done - (s.t_first or s.t_done))
         metrics.observe("ttft", (s.t_first or s.t_done) - s.t_arrive)
         with tr.span("detokenize"):
-            text = postprocess(self.tok.decode(s.prompt + s.out, skip_special_tokens=True))
+            text = postprocess(self._decode_answer(s.prompt, s.out))
         metrics.observe("request", tr.total())
         log.debug("Generated response: %s...", text[:200])
         out = {"generated_text": text, "context": context}
@@ -272,17 +282,42 @@ class RagService:
             ctxs.append(ctx)
             if ctx is not None:
                 fulls.append(build_prompt(ctx, p))
-        # one multi-threaded tokenizer call for the whole batch (C++ workers, GIL released)
-        all_ids = iter(self.tok.encode_batch(fulls, add_special_tokens=True)) if fulls else iter(())
-        for i, ctx in enumerate(ctxs):
-            if ctx is None:
-                seqs.append(None)
-                continue
-            ids = self._prompt_ids(None, ids=next(all_ids))
-            seqs.append(self.engine.add_request(ids, params or self.params,
-                                                seed=(seeds[i] if seeds is not None else self._next_seed())))
+        # Multi-threaded tokenizer calls (C++ workers, GIL released). The first few prompts -- about
+        # one prefill step's worth -- are tokenized and submitted right away; the rest are tokenized
+        # on a helper thread while the GPU runs that first prefill step, and join the queue in order.
+        rows = [i for i, c in enumerate(ctxs) if c is not None]
+        seqs = [None] * len(ctxs)
+        seed_of = {i: (seeds[i] if seeds is not None else self._next_seed()) for i in rows}
+
+        def submit(idx, texts):
+            for i, ids in zip(idx, self.tok.encode_batch(texts, add_special_tokens=True)):
+                seqs[i] = self.engine.add_request(self._prompt_ids(None, ids=ids), params or self.params,
+                                                  seed=seed_of[i])
+
+        head = max(1, self.engine.max_prefill_tokens // max(1, 4 * self.cfg.chunk_words))  # ~1 step of prompts
+        submit(rows[:head], fulls[:head])
+        err = []
+        rest = None
+        if len(rows) > head:
+            def _rest():
+                try:
+                    submit(rows[head:], fulls[head:])
+                except Exception as e:  # surfaced below, after the engine drains
+                    err.append(e)
+            rest = threading.Thread(target=_rest, daemon=True)
+            rest.start()
         t_prep = time.perf_counter()
-        self.engine.run_until_done()
+        while True:
+            if self.engine.has_work():
+                self.engine.step()
+            elif rest is not None and rest.is_alive():
+                rest.join(0.001)
+            elif not self.engine.has_work():  # re-check: the helper may have queued its last rows and exited
+                break
+        if rest is not None:
+            rest.join()
+        if err:
+            raise err[0]
         st = self.engine.stats
         st["retrieve_s"] = st.get("retrieve_s", 0.0) + (t_ret - t0)
         st["prompt_build_s"] = st.get("prompt_build_s", 0.0) + (t_prep - t_ret)
@@ -291,7 +326,7 @@ class RagService:
             if s is None:
                 outs.append({"generated_text": NO_RESULTS})
                 continue
-            text = postprocess(self.tok.decode(s.prompt + s.out, skip_special_tokens=True))
+            text = postprocess(self._decode_answer(s.prompt, s.out))
             outs.append({"generated_text": text, "context": ctx, "_latency_s": s.t_done - t0,
                          "_ttft_s": (s.t_first or s.t_done) - t0, "_prompt_tokens": len(s.prompt),
                          "_gen_tokens": len(s.out)})

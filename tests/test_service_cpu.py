@@ -139,3 +139,30 @@ def test_empty_index_reply(assets, tmp_path):
         assert svc.generate("anything") == {"generated_text": NO_RESULTS}
     finally:
         svc.shutdown()
+
+
+def test_generate_batch_matches_per_query_generation(assets, tmp_path):
+    """generate_batch (helper-thread tokenization overlapped with the first prefill, answers decoded
+    from the generated ids only) == the same queries run one at a time with the same seeds."""
+    from rag_llm_k8s_amd.engine.llm_engine import SamplingParams
+
+    root, pdfs = assets
+    svc = make_service(make_cfg(root, pdfs, tmp_path))
+    try:
+        assert svc.ingest_directory() == 3
+        svc.engine.max_prefill_tokens = 4000  # head = 1 prompt: the other 6 come from the helper thread
+        qs = ["what does document %d say about topic %d" % (i, i * 7) for i in range(7)]
+        p = SamplingParams(max_new_tokens=5, temperature=0.8, top_p=0.9, top_k=20, ignore_eos=True)
+        batch = svc.generate_batch(qs, params=p, seeds=list(range(100, 107)))
+        single = [svc.generate_batch([q], params=p, seeds=[100 + i])[0] for i, q in enumerate(qs)]
+        assert [b["generated_text"] for b in batch] == [s["generated_text"] for s in single]
+        assert all(b["_gen_tokens"] == 5 for b in batch)
+        # the short-cut answer decode equals decoding prompt + output and splitting as the reference
+        from rag_llm_k8s_amd.ingest.text import postprocess
+
+        s = svc.engine.add_request(svc._prompt_ids(None, ids=svc.tok.encode("Context: x\\n\\nChatbot:")), p, seed=3)
+        svc.engine.run_until_done()
+        full = postprocess(svc.tok.decode(s.prompt + s.out, skip_special_tokens=True))
+        assert postprocess(svc._decode_answer(s.prompt, s.out)) == full
+    finally:
+        svc.shutdown()
