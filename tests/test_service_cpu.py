@@ -30,10 +30,10 @@ def make_cfg(root, pdfs, index_dir):
                      max_batch=4, use_cuda_graphs=False, kv_cache_blocks=64, seed=1)
 
 
-def make_service(cfg):
+def make_service(cfg, start_threads=True):
     from rag_llm_k8s_amd.server.builder import build_service
 
-    svc = build_service(cfg)
+    svc = build_service(cfg, start_threads=start_threads)
     svc.store.ensure_exists()
     return svc
 
@@ -147,7 +147,7 @@ def test_generate_batch_matches_per_query_generation(assets, tmp_path):
     from rag_llm_k8s_amd.engine.llm_engine import SamplingParams
 
     root, pdfs = assets
-    svc = make_service(make_cfg(root, pdfs, tmp_path))
+    svc = make_service(make_cfg(root, pdfs, tmp_path), start_threads=False)  # generate_batch owns the engine
     try:
         assert svc.ingest_directory() == 3
         svc.engine.max_prefill_tokens = 4000  # head = 1 prompt: the other 6 come from the helper thread
