@@ -9,9 +9,12 @@ tokenize -> continuous-batching prefill + hipGraph decode (temperature 0.7, top-
 150 tokens, EOS ignored so every request produces exactly 150 tokens) -> detokenize ->
 "Chatbot:" post-processing.
 
-Multi-GPU: one process per GPU (torchrun). Default parallelism is data-parallel replicas
-(weak scaling: per-GPU work fixed, like k8s replicas behind the Service); --tp T groups T GPUs
-into one tensor-parallel engine over RCCL/xGMI.
+Multi-GPU: one process per GPU (torchrun). With N > 1 GPUs the default layout is BASELINE config 3:
+ONE tensor-parallel engine over all N GPUs (Megatron TP over xGMI: peer-mapped all-reduce /
+all-gather kernels for decode-sized messages, RCCL for bulk prefill all-reduces, overlapped with
+the next micro-batch's GEMMs), with the concurrency scaled to 32 x N queries per step (weak
+scaling: per-GPU work fixed). `--dp` runs N independent data-parallel replicas instead (k8s
+replicas behind the Service); `--tp T` picks any TP degree dividing N (tp x dp layouts).
 
 value = total generated tokens of all ranks / max-over-ranks wall time of the K timed steps.
 """
@@ -32,8 +35,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--concurrency", type=int, default=32, help="concurrent queries per replica per step")
-    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--concurrency", type=int, default=None,
+                    help="concurrent queries per engine (TP group) per step; default 32 x TP degree")
+    ap.add_argument("--tp", type=int, default=None, help="TP degree (default: all N GPUs, or 1 with --dp)")
+    ap.add_argument("--dp", action="store_true", help="N data-parallel replicas (TP=1) instead of one TP=N engine")
     ap.add_argument("--model", default="8b", choices=["8b", "70b", "tiny"])
     ap.add_argument("--embedder", default="minilm", choices=["minilm", "bge-large", "bge-m3", "tiny"])
     ap.add_argument("--chunks", type=int, default=10000)
@@ -77,6 +82,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
+    if a.tp is None:
+        a.tp = 1 if a.dp else world
+    if a.concurrency is None:
+        a.concurrency = 32 * a.tp
     if int(os.environ.get("LOCAL_RANK", "0")) == 0:
         _build.build_all()
     ctx = D.init_distributed(tp=a.tp)

@@ -25,8 +25,9 @@
 //
 // The whole region is allocated uncached (hipDeviceMallocUncached): payload stores and
 // peer loads bypass the per-XCD L2s; flag stores/polls are system-scope atomics and the
-// reader issues a system-scope acquire after its poll. Every spin is bounded: a peer
-// that never arrives sets an error word (ragk_ar_error) instead of hanging the GPU.
+// reader issues a system-scope acquire after its poll. Every spin is bounded (wall-clock, via
+// s_memrealtime): a peer that never arrives sets an error word -- on the device (ragk_ar_error) and
+// in pinned host memory (polled by the engine after each step) -- and the block reads no peer data.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -39,7 +40,10 @@ namespace {
 constexpr int AR_MAX_RANKS = 8;
 constexpr int AR_MAX_BLOCKS = 80;
 constexpr int AR_THREADS = 512;
-constexpr unsigned AR_SPIN_LIMIT = 1u << 24;  // x ~100 ns sleep ≈ 2 s, then give up
+// Default bound of one peer wait: 5 s of s_memrealtime (constant 100 MHz clock), then give up.
+// Ranks step in lockstep, so a healthy wait is microseconds; the bound only has to cover host-side
+// skew between ranks (a Python pause) and must stay far below the engine watchdog.
+constexpr unsigned AR_TIMEOUT_TICKS = 500000000u;
 
 struct ArFlags {
   unsigned start[AR_MAX_BLOCKS][AR_MAX_RANKS];  // written by peers: "rank p reached epoch e (phase 1)"
@@ -52,6 +56,8 @@ constexpr size_t FLAG_BYTES = (sizeof(ArFlags) + 4095) & ~size_t(4095);
 
 struct ArPeers {
   char* base[AR_MAX_RANKS];  // every rank's region (own one included), mapped in this process
+  unsigned* host_err;        // host-mapped pinned word: the engine polls it after every step, no sync
+  unsigned spin_limit;       // bound of one peer wait, in s_memrealtime ticks (100 MHz)
 };
 
 __device__ __forceinline__ unsigned ld_sys(const unsigned* p) {
@@ -63,7 +69,11 @@ __device__ __forceinline__ void st_sys(unsigned* p, unsigned v) {
 
 // Block-level barrier with the same block of every peer: release my writes, publish `ep` into
 // slot [b][rank] of every peer's `which` array, wait until all peers published `ep` into mine.
-__device__ void peer_barrier(const ArPeers& P, int rank, int world, int which, unsigned ep) {
+// Returns false (block-uniform) if a peer did not arrive within the bounded spin: the caller then
+// reads no peer data (the result is garbage either way and the host raises CommError).
+__device__ bool peer_barrier(const ArPeers& P, int rank, int world, int which, unsigned ep) {
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) s_ok = 1;
   __syncthreads();
   const int b = blockIdx.x;
   if (threadIdx.x < world) {
@@ -72,17 +82,20 @@ __device__ void peer_barrier(const ArPeers& P, int rank, int world, int which, u
     st_sys(which ? &pf->mid[b][rank] : &pf->start[b][rank], ep);
     ArFlags* mf = reinterpret_cast<ArFlags*>(P.base[rank]);
     const unsigned* slot = which ? &mf->mid[b][threadIdx.x] : &mf->start[b][threadIdx.x];
-    unsigned n = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (ld_sys(slot) < ep) {
       __builtin_amdgcn_s_sleep(2);
-      if (++n > AR_SPIN_LIMIT) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > P.spin_limit) {  // a peer never arrived: report, never hang
         st_sys(&mf->error, 1u);
+        if (P.host_err) st_sys(P.host_err, 1u);
+        s_ok = 0;
         break;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
+  return s_ok != 0;
 }
 
 __device__ __forceinline__ u32x4 ld16(const void* p) {
@@ -109,10 +122,12 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPeers P, int ra
   u32x4* my_stage = reinterpret_cast<u32x4*>(P.base[rank] + stage_off);
   const u32x4* in4 = reinterpret_cast<const u32x4*>(in);
   for (long v = v0 + threadIdx.x; v < v1; v += AR_THREADS) my_stage[v] = in4[v];
-  peer_barrier(P, rank, world, 0, ep);
+  const bool ok = peer_barrier(P, rank, world, 0, ep);
 
   u32x4* out4 = reinterpret_cast<u32x4*>(out);
-  if (!TWO_SHOT) {
+  if (!ok) {
+    // no peer reads after a failed wait
+  } else if (!TWO_SHOT) {
     for (long v = v0 + threadIdx.x; v < v1; v += AR_THREADS) {
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int p = 0; p < world; ++p) {
@@ -138,7 +153,7 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPeers P, int ra
       }
       my_res[v] = pack8(acc);
     }
-    peer_barrier(P, rank, world, 1, ep);
+    if (peer_barrier(P, rank, world, 1, ep))
     for (int p = 0; p < world; ++p) {
       const long t0 = min(v0 + p * sub, v1), t1 = min(t0 + sub, v1);
       for (long v = t0 + threadIdx.x; v < t1; v += AR_THREADS) out4[v] = ld16(P.base[p] + result_off + v * 16);
@@ -148,10 +163,34 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPeers P, int ra
   if (threadIdx.x == 0) mine->epoch[b] = ep;
 }
 
+// All-gather: out[p * n16 + v] = rank p's in[v] (16-byte vectors). Used for the vocab-parallel
+// sampler's candidate exchange (a few KB per decode step), so tensor-parallel decode runs with no
+// RCCL call at all and stays inside the captured hipGraph. Same epochs / halves as the all-reduce.
+__global__ __launch_bounds__(AR_THREADS) void allgather_kernel(ArPeers P, int rank, int world, const u32x4* in,
+                                                               u32x4* out, long n16, size_t data_bytes) {
+  const int b = blockIdx.x;
+  ArFlags* mine = reinterpret_cast<ArFlags*>(P.base[rank]);
+  __shared__ unsigned s_ep;
+  if (threadIdx.x == 0) s_ep = mine->epoch[b] + 1;
+  __syncthreads();
+  const unsigned ep = s_ep;
+  const size_t stage_off = FLAG_BYTES + (size_t)(ep & 1) * data_bytes;
+  const long per = (n16 + gridDim.x - 1) / gridDim.x;
+  const long v0 = min((long)b * per, n16), v1 = min(v0 + per, n16);
+  u32x4* my_stage = reinterpret_cast<u32x4*>(P.base[rank] + stage_off);
+  for (long v = v0 + threadIdx.x; v < v1; v += AR_THREADS) my_stage[v] = in[v];
+  if (peer_barrier(P, rank, world, 0, ep))
+  for (int p = 0; p < world; ++p)
+    for (long v = v0 + threadIdx.x; v < v1; v += AR_THREADS) out[(long)p * n16 + v] = ld16(P.base[p] + stage_off + v * 16);
+  __syncthreads();
+  if (threadIdx.x == 0) mine->epoch[b] = ep;
+}
+
 struct ArHandle {
   int rank, world, blocks;
   size_t data_bytes;  // capacity of one staging half (= max message bytes)
   char* local;
+  unsigned* host_err;  // pinned, mapped: host view
   ArPeers peers;
   bool opened[AR_MAX_RANKS];
 };
@@ -182,6 +221,14 @@ RAGK_API void* ragk_ar_create(int rank, int world, long max_bytes, int blocks) {
   }
   h->local = (char*)p;
   h->peers.base[rank] = h->local;
+  h->peers.spin_limit = AR_TIMEOUT_TICKS;
+  void* he = nullptr;
+  if (hipHostMalloc(&he, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+    h->host_err = (unsigned*)he;
+    *h->host_err = 0;
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, he, 0) == hipSuccess) h->peers.host_err = (unsigned*)dp;
+  }
   return h;
 }
 
@@ -214,6 +261,32 @@ RAGK_API int ragk_ar_open_peers(void* hp, const void* handles) {
 }
 
 RAGK_API long ragk_ar_max_bytes(void* hp) { return (long)((ArHandle*)hp)->data_bytes; }
+
+// Bound of each peer wait in microseconds (default 5 s); tests shorten it.
+RAGK_API int ragk_ar_set_spin_limit(void* hp, unsigned limit_us) {
+  const unsigned long long ticks = (unsigned long long)limit_us * 100ull;  // 100 MHz
+  const unsigned limit = ticks > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (unsigned)ticks;
+  ArHandle* h = (ArHandle*)hp;
+  if (!h || limit_us == 0) return (int)hipErrorInvalidValue;
+  h->peers.spin_limit = limit;
+  return 0;
+}
+
+// Host address of the pinned error word (0 = healthy): readable at any time without a device sync.
+RAGK_API void* ragk_ar_error_host_ptr(void* hp) { return ((ArHandle*)hp)->host_err; }
+
+// in: nbytes per rank (multiple of 16, 16-byte aligned); out: world * nbytes, rank order.
+RAGK_API int ragk_ar_allgather(void* hp, const void* in, void* out, long nbytes, hipStream_t st) {
+  ArHandle* h = (ArHandle*)hp;
+  if (!h || nbytes <= 0) return nbytes == 0 ? 0 : (int)hipErrorInvalidValue;
+  if (nbytes % 16 || (size_t)nbytes > h->data_bytes || ((uintptr_t)in & 15) || ((uintptr_t)out & 15))
+    return (int)hipErrorInvalidValue;
+  for (int p = 0; p < h->world; ++p)
+    if (!h->peers.base[p]) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(allgather_kernel, dim3(h->blocks), dim3(AR_THREADS), 0, st, h->peers, h->rank, h->world,
+                     (const u32x4*)in, (u32x4*)out, nbytes / 16, h->data_bytes);
+  return (int)hipGetLastError();
+}
 
 // in/out: bf16[n] (n % 8 == 0, 16-byte aligned; in == out allowed). mode 0 = one-shot, 1 = two-shot.
 RAGK_API int ragk_ar_allreduce(void* hp, const void* in, void* out, long n, int mode, hipStream_t st) {
@@ -248,5 +321,6 @@ RAGK_API void ragk_ar_destroy(void* hp) {
   for (int p = 0; p < h->world; ++p)
     if (h->opened[p]) (void)hipIpcCloseMemHandle(h->peers.base[p]);
   (void)hipFree(h->local);
+  if (h->host_err) (void)hipHostFree(h->host_err);
   delete h;
 }

@@ -100,8 +100,15 @@ class LLMEngine:
         self.lock = threading.Lock()
         self._aborts = []
         self.tp_group = tp_group
-        self.tp_size = 1 if tp_group is None else torch.distributed.get_world_size(tp_group)
+        self.comm = getattr(model, "comm", None)
+        if self.comm is not None and self.comm.size > 1:
+            self.tp_size = self.comm.size
+        else:
+            self.tp_size = 1 if tp_group is None else torch.distributed.get_world_size(tp_group)
+        # candidate-list width of the native sampler (top-k <= K served inside the decode graph);
+        # requests with a larger top_k, or top_k = 0 (HF: disabled), take the exact full-vocabulary path
         self.K = top_k_cap
+        self._warned_topk = False
         # TP prefill steps of at least this many tokens run as 2 micro-batches with async all-reduces
         self.tp_overlap_min_tokens = int(os.environ.get("RAGK_TP_OVERLAP_MIN", "1024"))
         self.is_cuda = self.device.type == "cuda"
@@ -118,12 +125,13 @@ class LLMEngine:
         self._pin_idx = 0
         self._pin = self._pins[0]
         self._pin_off = 0
-        # Asynchronous decode (hipGraph path, TP=1): step t+1 is enqueued before step t's tokens are
-        # read back; its input ids come from step t's sampled tokens on the device (D2D), so the GPU
-        # never waits for the host round trip between decode steps. Tokens are accepted one step late;
-        # a sequence that stops on EOS has computed one extra (discarded) row, and its KV blocks are
-        # freed only after that step has completed.
-        self.async_decode = self.use_graphs and self.tp_size == 1 and os.environ.get("RAGK_ASYNC_DECODE", "1") == "1"
+        # Asynchronous decode (hipGraph path): step t+1 is enqueued before step t's tokens are read
+        # back; its input ids come from step t's sampled tokens on the device (D2D), so the GPU never
+        # waits for the host round trip between decode steps. Tokens are accepted one step late; a
+        # sequence that stops on EOS has computed one extra (discarded) row, and its KV blocks are
+        # freed only after that step has completed. Under TP every rank samples the same token from
+        # the same gathered candidates, so all ranks take the same decisions one step late.
+        self.async_decode = self.use_graphs and os.environ.get("RAGK_ASYNC_DECODE", "1") == "1"
         self._inflight = None  # dict(seqs, rows, entry, event, host_out, n)
         self._free_after = []  # seq ids whose blocks are freed once the in-flight step has completed
         self._out_pins = [torch.empty(max(1, max_batch), dtype=torch.int32, pin_memory=self.is_cuda)
@@ -213,7 +221,13 @@ class LLMEngine:
 
     def step(self):
         """One engine step. Returns the sequences that finished in it (with asynchronous decode:
-        whose last token was read back in it)."""
+        whose last token was read back in it). Under TP a failed collective raises CommError."""
+        fin = self._step()
+        if self.comm is not None and self.tp_size > 1:
+            self.comm.check()
+        return fin
+
+    def _step(self):
         self._pin_idx ^= 1
         self._pin = self._pins[self._pin_idx]
         self._pin_off = 0
@@ -227,6 +241,10 @@ class LLMEngine:
             fin += self._drain()
             return fin + self._prefill(chunks)
         ready = [s for s in self.running if s.computed >= len(s.prompt)]
+        if ready and self._needs_full_vocab(ready):
+            fin += self._drain()
+            ready = [s for s in self.running if s.computed >= len(s.prompt)]
+            return fin + self._decode(ready, full_vocab=True)
         if ready and self.async_decode:
             return fin + self._decode_async(ready)
         fin += self._drain()
@@ -252,8 +270,12 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ helpers
     def _h2d_i32(self, host_list):
-        """Stage a host int list / int32 array through a reusable pinned buffer (reset every step;
-        every step ends with a device->host sync, so the buffer is free again by then)."""
+        """Stage a host int list / int32 array through a pinned buffer. Two buffers alternate per step
+        (step() flips _pin_idx and resets the offset). Invariant: pin[i] is reused by step t+2 only;
+        every path that enqueues step t+1 first synchronises step t-1 (a synchronous step ends with a
+        device->host sync; the asynchronous decode pipeline _collect()s step t-1 before returning from
+        step t+1, and _drain()s before any prefill), so step t-1's H2D copies out of pin[i] have
+        completed before step t+1 overwrites it. A third in-flight step would break this."""
         if isinstance(host_list, np.ndarray):
             t = torch.from_numpy(np.ascontiguousarray(host_list, dtype=np.int32))
         else:
@@ -307,7 +329,7 @@ class LLMEngine:
         for i, s in enumerate(seqs):
             p = s.params
             temps[i] = p.temperature if p.do_sample else 0.0
-            ks[i] = min(p.top_k, self.K) if p.top_k > 0 else self.K
+            ks[i] = p.top_k if 0 < p.top_k <= self.K else self.K  # wider top_k: see _needs_full_vocab
             ps[i] = p.top_p
             seeds[i] = int(s.seed) & 0x7FFFFFFFFFFFFFFF
             steps[i] = len(s.out)
@@ -323,6 +345,62 @@ class LLMEngine:
         n = pad_to or len(seqs)
         buf = self._h2d_i32(self._sampling_host(seqs, pad_to))
         return self._sampling_views(buf, n)
+
+    def _needs_full_vocab(self, seqs):
+        """True if a sampled request's top_k does not fit the K-wide candidate lists (top_k = 0 means
+        "disabled" as in transformers' TopKLogitsWarper, top_k > K): such a step samples from the full
+        vocabulary (exact, slower, outside the decode graph) instead of silently clamping top_k."""
+        bad = any(s.params.do_sample and s.params.temperature > 0 and not (0 < s.params.top_k <= self.K)
+                  for s in seqs)
+        if bad and not self._warned_topk:
+            log.warning("top_k outside 1..%d requested: sampling those steps from the full vocabulary", self.K)
+            self._warned_topk = True
+        return bad
+
+    def _sample_full_vocab(self, logits, seqs):
+        """Exact temperature -> top-k (if 0 < top_k) -> top-p -> multinomial over the whole vocabulary
+        (transformers' LogitsProcessor order, [dep] generation/utils.py:1311-1322). Under TP the vocab
+        shards are all-gathered first. Uniforms come from torch.Generator(seed * 1000003 + step), as in
+        the torch backend's sampler."""
+        w = self.model.w
+        lg = logits[:, :w.vocab_valid].float().contiguous()
+        if self.tp_size > 1:
+            parts = [torch.empty_like(lg) for _ in range(self.tp_size)]
+            if lg.is_cuda and self.comm is not None and self.comm.ipc is None:
+                import torch.distributed as dist
+                dist.all_gather(parts, lg, group=self.tp_group)
+            else:  # pad shards to equal width host-side (gloo / peer-mapped ranks)
+                import torch.distributed as dist
+                grp = getattr(self.comm, "cpu_group", None) or self.tp_group
+                full_w = logits.shape[1]
+                lp = torch.full((lg.shape[0], full_w), float("-inf"))
+                lp[:, :lg.shape[1]] = lg.cpu()
+                parts = [torch.empty_like(lp) for _ in range(self.tp_size)]
+                dist.all_gather(parts, lp, group=grp)
+            lg = torch.cat([p.cpu() for p in parts], 1)[:, :self.model.cfg.vocab_size]
+        lg = lg.cpu()
+        toks = []
+        for b, s in enumerate(seqs):
+            p = s.params
+            x = lg[b]
+            if not p.do_sample or p.temperature <= 0:
+                toks.append(int(torch.argmax(x)))
+                continue
+            x = x / p.temperature
+            if p.top_k > 0:
+                kth = torch.topk(x, min(p.top_k, x.numel())).values[-1]
+                x = torch.where(x < kth, torch.full_like(x, float("-inf")), x)
+            sv, order = torch.sort(x, descending=True)
+            probs = torch.softmax(sv, 0)
+            keep = (torch.cumsum(probs, 0) - probs) < p.top_p
+            keep[0] = True
+            q = torch.where(keep, probs, torch.zeros_like(probs))
+            c = torch.cumsum(q, 0)
+            g = torch.Generator().manual_seed((int(s.seed) * 1000003 + len(s.out)) & 0x7FFFFFFFFFFFFFFF)
+            u = float(torch.rand(1, generator=g)) * float(c[-1])
+            j = min(int(torch.searchsorted(c, torch.tensor([u]), right=True)[0]), int(keep.sum()) - 1)
+            toks.append(int(order[j]))
+        return toks
 
     def _sample_rows(self, logits, temps, ks, ps, seeds, steps, out=None):
         be = self.model.be
@@ -343,6 +421,8 @@ class LLMEngine:
         return tok
 
     def _gather_candidates(self, cv, ci):
+        if self.comm is not None:
+            return self.comm.gather_candidates(cv, ci)
         import torch.distributed as dist
 
         B, K = cv.shape
@@ -431,7 +511,9 @@ class LLMEngine:
             if logits is None:
                 m.hidden_states(inp)
         finished = []
-        if out_seqs:
+        if out_seqs and self._needs_full_vocab(out_seqs):
+            tok = self._sample_full_vocab(logits, out_seqs)
+        elif out_seqs:
             tok = self._sample_rows(logits, *self._sampling_tensors(out_seqs)).cpu().tolist()
         else:
             tok = []
@@ -512,7 +594,7 @@ class LLMEngine:
             self._sample_rows(logits, samp["temps"], samp["ks"], samp["ps"], samp["seeds"], samp["steps"],
                               out=out_tok)
 
-        entry = dict(packed=packed, samp=samp, out=out_tok, run=run, graph=None, meta=meta)
+        entry = dict(packed=packed, samp=samp, out=out_tok, run=run, graph=None, meta=meta, inp=inp)
         if self.use_graphs:
             kvl.fill_(1)  # scratch-only rows while capturing
             s = torch.cuda.Stream(device=dev)
@@ -633,20 +715,25 @@ class LLMEngine:
         self.stats["decode_s"] += time.perf_counter() - t0
         return fin
 
-    def _decode(self, seqs):
+    def _decode(self, seqs, full_vocab=False):
         t0 = time.perf_counter()
         n = len(seqs)
         finished = []
+        if not seqs:
+            return finished
         if self.is_cuda:
             B = self._bucket(n)
             e = self._decode_graph(B)
             host = np.concatenate([self._decode_inputs_host(seqs, B), self._sampling_host(seqs, pad_to=B)])
             e["packed"].copy_(self._h2d_i32(host), non_blocking=True)
-            if e["graph"] is not None:
+            if full_vocab:  # eager forward, exact sampler over the whole vocabulary
+                tok = self._sample_full_vocab(self.model.forward(e["inp"])[:n], seqs)
+            elif e["graph"] is not None:
                 e["graph"].replay()
+                tok = e["out"][:n].cpu().tolist()
             else:
                 e["run"]()
-            tok = e["out"][:n].cpu().tolist()
+                tok = e["out"][:n].cpu().tolist()
         else:
             host = self._decode_inputs_host(seqs, n)
             mb = self.max_blocks
@@ -655,7 +742,10 @@ class LLMEngine:
             meta = AttnMeta("decode", kvl, t[4 * n:4 * n + n * mb].view(n, mb), host_kv_lens=kvl.tolist())
             inp = StepInput(t[:n], t[n:2 * n], t[2 * n:3 * n], meta, None)
             logits = self.model.forward(inp)
-            tok = self._sample_rows(logits, *self._sampling_tensors(seqs)).tolist()
+            if full_vocab:
+                tok = self._sample_full_vocab(logits, seqs)
+            else:
+                tok = self._sample_rows(logits, *self._sampling_tensors(seqs)).tolist()
         for s in seqs:
             s.computed = s.length
         for s, t in zip(seqs, tok):

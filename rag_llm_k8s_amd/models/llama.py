@@ -143,7 +143,7 @@ class LlamaWeights:
         name = "model.embed_tokens.weight" if cfg.tie_word_embeddings else "lm_head.weight"
         lm = get(name, rows=(lo, hi))
         if lm.shape[0] < Vl:  # pad the last vocab shard
-            lm = torch.cat([lm, torch.zeros(Vl - lm.shape[0], lm.shape[1], dtype=lm.dtype)], 0)
+            lm = torch.cat([lm, torch.zeros(Vl - lm.shape[0], lm.shape[1], dtype=lm.dtype, device=lm.device)], 0)
         w.lm_head = dev(lm)
         w.vocab_offset = lo
         w.vocab_valid = hi - lo

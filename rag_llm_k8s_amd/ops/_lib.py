@@ -71,9 +71,12 @@ _SIGS = {
     "ragk_ar_max_bytes": [P],
     "ragk_ar_allreduce": [P, P, P, ctypes.c_long, I, S],
     "ragk_ar_error": [P],
+    "ragk_ar_set_spin_limit": [P, ctypes.c_uint],
+    "ragk_ar_error_host_ptr": [P],
+    "ragk_ar_allgather": [P, P, P, ctypes.c_long, S],
     "ragk_ar_destroy": [P],
 }
-_RESTYPES = {"ragk_ar_create": ctypes.c_void_p, "ragk_ar_max_bytes": ctypes.c_long, "ragk_ar_destroy": None}
+_RESTYPES = {"ragk_ar_create": ctypes.c_void_p, "ragk_ar_error_host_ptr": ctypes.c_void_p, "ragk_ar_max_bytes": ctypes.c_long, "ragk_ar_destroy": None}
 
 _lib = None
 _lock = threading.Lock()

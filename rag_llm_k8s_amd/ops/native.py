@@ -29,10 +29,11 @@ def _bf16_2d(t, name):
 # ----------------------------------------------------------------------------- GEMM
 PP_MIN_M = int(os.environ.get("RAGK_PP_MIN_M", "1024"))
 PP_VARIANT = int(os.environ.get("RAGK_PP_VARIANT", "2"))
-# large-M kernel: "w4" = 4-wave 128x128-per-wave (gemm_w4.hip, path 6), "pp" = 8-wave ping-pong (path 2),
-# "auto" = w4, except that a plain (epi none) or residual-add GEMM whose shape hipBLASLt runs faster,
-# timed once per (N, K, epi) at the first call with M >= BLASLT_MIN_M, goes to hipBLASLt (path 7)
-PREFILL_GEMM = os.environ.get("RAGK_PREFILL_GEMM", "auto")
+# large-M kernel: "w4" (default) = 4-wave 128x128-per-wave (gemm_w4.hip, path 6), "pp" = 8-wave
+# ping-pong (path 2). hipBLASLt is a yardstick only, never on the default path: "auto" (A/B tooling)
+# sends a plain (epi none) or residual-add GEMM to hipBLASLt (path 7) when it measured faster, timed
+# once per (N, K, epi, M bucket) at the first call with M >= BLASLT_MIN_M; "blaslt" always does.
+PREFILL_GEMM = os.environ.get("RAGK_PREFILL_GEMM", "w4")
 BLASLT_MIN_M = int(os.environ.get("RAGK_BLASLT_MIN_M", "8192"))
 BLASLT_MARGIN = float(os.environ.get("RAGK_BLASLT_MARGIN", "0.03"))  # required relative win
 _blaslt_choice = {}  # (N, K, epi) -> bool (hipBLASLt measured faster)
@@ -184,7 +185,7 @@ def _prefer_blaslt(x, w, resid, epi, out, w4_ok):
         return True
     if not w4_ok:
         return True
-    key = (w.shape[0], w.shape[1], epi)
+    key = (w.shape[0], w.shape[1], epi, max(0, int(x.shape[0]).bit_length() - 1))  # M bucket: power of 2
     hit = _blaslt_choice.get(key)
     if hit is not None:
         return hit

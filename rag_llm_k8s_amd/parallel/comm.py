@@ -1,53 +1,85 @@
 """Tensor-parallel communicator.
 
-Llama TP (Megatron layout) needs two all-reduces of the [T, hidden] residual per layer.
-* Default: RCCL all_reduce through torch.distributed on the TP group (ring/tree over xGMI;
-  capturable in the decode hipGraph).
+Llama TP (Megatron layout) needs two all-reduces of the [T, hidden] residual per layer and one
+all-gather of the sampler's per-rank top-k candidates per step.
+* Default: RCCL all_reduce / all_gather through torch.distributed on the TP group (ring/tree over
+  xGMI; capturable in the decode hipGraph).
 * Small / medium messages (decode: 8 KB x batch) are latency-bound on a ring over 7
-  point-to-point xGMI links; the peer-mapped path (parallel/ipc_allreduce.py, kernel in
+  point-to-point xGMI links; the peer-mapped path (parallel/ipc_allreduce.py, kernels in
   csrc/comm/allreduce.hip) maps every peer's staging buffer into each rank (hipIpc handles
   exchanged over the gloo group) and does the collective in one kernel with direct xGMI
-  loads: one-shot <= 512 KB, two-shot <= 8 MB, RCCL above. On by default on GPUs
-  (RAGK_IPC_ALLREDUCE=0 disables); it is cross-checked against RCCL at start-up and
-  disabled, loudly, if the check fails.
+  loads: one-shot <= 512 KB, two-shot <= 8 MB, RCCL above; the candidate all-gather goes the
+  same way, so a TP decode step issues no RCCL call. On by default on GPUs
+  (RAGK_IPC_ALLREDUCE=0 disables); it is cross-checked against a host sum at start-up and
+  disabled, loudly, if the check fails on any rank.
+
+Comm watchdog: every peer wait in those kernels is bounded; a peer that never arrives sets a pinned
+host word. :meth:`TPComm.check` (called by the engine after every step) turns it into
+:class:`CommError`, after which the communicator refuses every further call -- the epochs of the
+ranks are out of step, so continuing would all-reduce stale data (reference error path: the 500
+of /root/reference/llm/rag.py:179-181; here the engine loop fails and /healthz reports 503).
 """
 from __future__ import annotations
 
+import logging
 import os
 
 import torch
 import torch.distributed as dist
 
+log = logging.getLogger(__name__)
+
+
+class CommError(RuntimeError):
+    """A tensor-parallel collective failed (a peer did not arrive within the bounded wait)."""
+
 
 class TPComm:
-    def __init__(self, group, size, rank, device, cpu_group=None):
+    def __init__(self, group, size, rank, device, cpu_group=None, ipc_max_bytes=None, ipc_spin_limit=None):
         self.group, self.size, self.rank, self.device = group, size, rank, device
         self.cpu_group = cpu_group
         self.ipc = None
+        self.broken = None  # error message once a collective failed
         self._side = None  # side stream for asynchronous peer-mapped all-reduces
         want = os.environ.get("RAGK_IPC_ALLREDUCE", "1") == "1"
         if want and size > 1 and str(device).startswith("cuda") and cpu_group is not None:
-            import logging
-
-            log = logging.getLogger(__name__)
+            ok, ipc = 0, None
             try:
-                from .ipc_allreduce import IPCAllReduce
+                from .ipc_allreduce import MAX_BYTES, IPCAllReduce
 
-                ipc = IPCAllReduce(group, cpu_group, size, rank, device)
-                ok = torch.tensor([1 if ipc.self_test(group) else 0], device=device)
-                dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)  # all ranks agree
-                if int(ok.item()) == 1:
-                    self.ipc = ipc
-                else:
+                ipc = IPCAllReduce(group, cpu_group, size, rank, device,
+                                   max_bytes=ipc_max_bytes or MAX_BYTES, spin_limit=ipc_spin_limit)
+                ok = 1 if ipc.self_test(cpu_group) else 0
+            except Exception as e:  # fall back to RCCL, loudly
+                log.warning("IPC all-reduce unavailable on rank %d (%s); using RCCL", rank, e)
+            flag = torch.tensor([ok], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=cpu_group)  # all ranks agree
+            if int(flag.item()) == 1:
+                self.ipc = ipc
+            else:
+                if ipc is not None:
                     log.warning("IPC all-reduce self-test failed; using RCCL")
                     ipc.close()
-            except Exception as e:  # fall back to RCCL, loudly
-                log.warning("IPC all-reduce unavailable (%s); using RCCL", e)
-                self.ipc = None
 
+    # ------------------------------------------------------------------ watchdog
+    def check(self):
+        """Raise CommError if a peer-mapped collective gave up waiting for a peer (cheap: reads a
+        pinned host word). Once raised, every later call raises too."""
+        if self.broken is None and self.ipc is not None and self.ipc.error():
+            self.broken = "peer-mapped collective timed out waiting for a peer (rank %d)" % self.rank
+            log.critical(self.broken)
+        if self.broken is not None:
+            raise CommError(self.broken)
+
+    def _guard(self):
+        if self.broken is not None:
+            raise CommError(self.broken)
+
+    # ------------------------------------------------------------------ collectives
     def all_reduce(self, x: torch.Tensor):
         if self.size == 1:
             return x
+        self._guard()
         if self.ipc is not None and self.ipc.fits(x):
             return self.ipc.all_reduce(x)
         if not x.is_cuda and x.dtype == torch.bfloat16:  # gloo: reduce in fp32, round once
@@ -63,6 +95,7 @@ class TPComm:
         (GPU) or the host (gloo) wait for it. x must not be touched until then."""
         if self.size == 1:
             return _Done()
+        self._guard()
         if self.ipc is not None and self.ipc.fits(x):
             cur = torch.cuda.current_stream(x.device)
             if self._side is None:
@@ -81,15 +114,48 @@ class TPComm:
         return dist.all_reduce(x, group=self.group, async_op=True)
 
     def all_gather_into(self, out: torch.Tensor, x: torch.Tensor):
-        """out[r*S:(r+1)*S] = rank r's x (S = x.shape[0]): RCCL all-gather; gloo via a list gather."""
+        """out[r*S:(r+1)*S] = rank r's x (S = x.shape[0]): peer-mapped kernel when it fits, else RCCL
+        all-gather; gloo via a list gather."""
         if self.size == 1:
             out.copy_(x)
             return out
-        if x.is_cuda:
+        self._guard()
+        if self.ipc is not None and out.is_contiguous() and self.ipc.gather_fits(x):
+            self.ipc.all_gather(x.contiguous(), out=out.view(-1))
+        elif x.is_cuda:
             dist.all_gather_into_tensor(out, x, group=self.group)
         else:
             dist.all_gather(list(out.chunk(self.size)), x.contiguous(), group=self.group)
         return out
+
+    def gather_candidates(self, cv: torch.Tensor, ci: torch.Tensor):
+        """Vocab-parallel sampler exchange: per-rank top-k candidates [B, K] (fp32 values, int32 ids)
+        -> [B, size*K] each, rank-major within a row (identical on every rank)."""
+        B, K = cv.shape
+        if self.size == 1:
+            return cv, ci
+        self._guard()
+        if self.ipc is not None and cv.is_cuda:
+            packed = torch.cat([cv.contiguous().view(torch.int32).reshape(-1), ci.contiguous().reshape(-1)])
+            if self.ipc.gather_fits(packed):
+                g = self.ipc.all_gather(packed).view(self.size, 2, B, K)
+                gv = g[:, 0].view(torch.float32)
+                gi = g[:, 1]
+                return (gv.permute(1, 0, 2).reshape(B, self.size * K).contiguous(),
+                        gi.permute(1, 0, 2).reshape(B, self.size * K).contiguous())
+        if cv.is_cuda:
+            gv = torch.empty((self.size, B, K), dtype=cv.dtype, device=cv.device)
+            gi = torch.empty((self.size, B, K), dtype=ci.dtype, device=ci.device)
+            dist.all_gather_into_tensor(gv, cv.contiguous(), group=self.group)
+            dist.all_gather_into_tensor(gi, ci.contiguous(), group=self.group)
+        else:  # gloo (CPU plumbing / tests)
+            lv = [torch.empty_like(cv) for _ in range(self.size)]
+            li = [torch.empty_like(ci) for _ in range(self.size)]
+            dist.all_gather(lv, cv.contiguous(), group=self.group)
+            dist.all_gather(li, ci.contiguous(), group=self.group)
+            gv, gi = torch.stack(lv), torch.stack(li)
+        return gv.permute(1, 0, 2).reshape(B, self.size * K).contiguous(), \
+            gi.permute(1, 0, 2).reshape(B, self.size * K).contiguous()
 
     def reduce_scatter(self, x: torch.Tensor, out: torch.Tensor = None):
         """Sum of every rank's x [size*S, ...], this rank's S-row slice: RCCL reduce-scatter (each
@@ -100,7 +166,11 @@ class TPComm:
         if self.size == 1:
             out.copy_(x)
             return out
-        if x.is_cuda:
+        self._guard()
+        if x.is_cuda and self.ipc is not None and self.ipc.fits(x):
+            self.ipc.all_reduce(x)  # peer-mapped two-shot: the slice of the full sum
+            out.copy_(x[self.rank * S:(self.rank + 1) * S])
+        elif x.is_cuda:
             dist.reduce_scatter_tensor(out, x, group=self.group)
         else:
             y = x.float()

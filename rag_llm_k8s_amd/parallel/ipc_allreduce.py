@@ -23,12 +23,14 @@ from ..ops import _lib
 from ..ops._lib import check, stream_ptr
 
 ONE_SHOT_MAX = int(os.environ.get("RAGK_AR_ONESHOT_MAX", str(512 << 10)))
+SPIN_LIMIT = int(os.environ.get("RAGK_AR_TIMEOUT_US", "0"))  # 0 = kernel default (5 s per peer wait)
 MAX_BYTES = int(os.environ.get("RAGK_AR_MAX_BYTES", str(8 << 20)))
 BLOCKS = int(os.environ.get("RAGK_AR_BLOCKS", "64"))
 
 
 class IPCAllReduce:
-    def __init__(self, group, cpu_group, size, rank, device, max_bytes=MAX_BYTES, blocks=BLOCKS):
+    def __init__(self, group, cpu_group, size, rank, device, max_bytes=MAX_BYTES, blocks=BLOCKS, spin_limit=None):
+        """spin_limit: bound of one peer wait inside the kernels, in microseconds (None: env / 5 s)."""
         if size > 8:
             raise ValueError("peer-mapped all-reduce supports <= 8 ranks (one xGMI node)")
         self.size, self.rank, self.device = size, rank, torch.device(device)
@@ -40,6 +42,12 @@ class IPCAllReduce:
             raise _lib.NativeLibraryError("ragk_ar_create failed (uncached HBM allocation)")
         self.h = ctypes.c_void_p(h)
         self.max_bytes = int(L.ragk_ar_max_bytes(self.h))
+        spin = SPIN_LIMIT if spin_limit is None else int(spin_limit)
+        if spin > 0:
+            check(L.ragk_ar_set_spin_limit(self.h, spin), "ragk_ar_set_spin_limit")
+        ep = L.ragk_ar_error_host_ptr(self.h)
+        # pinned host word the kernel sets when a peer wait gives up: polled after every engine step
+        self._err_word = ctypes.c_uint.from_address(ep) if ep else None
         hs = L.ragk_ar_handle_size()
         buf = ctypes.create_string_buffer(hs)
         check(L.ragk_ar_ipc_handle(self.h, buf), "hipIpcGetMemHandle")
@@ -52,15 +60,19 @@ class IPCAllReduce:
         dist.barrier(group=cpu_group)
 
     def self_test(self, group=None) -> bool:
-        """Cross-check one call of each mode against RCCL/gloo; False disables the path."""
+        """Cross-check one call of each mode against a host (gloo) sum; False disables the path."""
         ok = True
         for n, mode in ((8 * 4096, 0), (min(self.max_bytes // 2, 1 << 20) // 8 * 8, 1)):
             g = torch.Generator(device="cpu").manual_seed(1234 + self.rank)
-            x = torch.randn(n, generator=g).bfloat16().to(self.device)
-            ref = x.float()
+            xh = torch.randn(n, generator=g).bfloat16()
+            ref = xh.float()
             dist.all_reduce(ref, group=group)
-            y = self.all_reduce(x.clone(), mode=mode)
-            ok &= bool(torch.allclose(y.float(), ref, rtol=1e-2, atol=1e-2)) and not self.error()
+            y = self.all_reduce(xh.to(self.device), mode=mode)
+            ok &= bool(torch.allclose(y.float().cpu(), ref, rtol=1e-2, atol=1e-2)) and not self.error()
+        mine = torch.arange(64, dtype=torch.int32) + 1000 * self.rank
+        got = self.all_gather(mine.to(self.device)).cpu()
+        ok &= bool(torch.equal(got, torch.cat([torch.arange(64, dtype=torch.int32) + 1000 * r
+                                               for r in range(self.size)])))
         return ok
 
     def fits(self, x: torch.Tensor) -> bool:
@@ -77,8 +89,29 @@ class IPCAllReduce:
               "ragk_ar_allreduce")
         return out
 
+    def all_gather(self, x: torch.Tensor, out: torch.Tensor | None = None):
+        """out = cat over ranks of x (any dtype; x.nbytes % 16 == 0, <= max_bytes): one kernel,
+        peer loads over xGMI, graph-capturable."""
+        nb = x.numel() * x.element_size()
+        _ok = x.is_cuda and x.is_contiguous() and nb % 16 == 0 and nb <= self.max_bytes and x.data_ptr() % 16 == 0
+        if not _ok:
+            raise ValueError("IPC all-gather: contiguous, nbytes % 16 == 0, <= %d bytes" % self.max_bytes)
+        if out is None:
+            out = torch.empty((self.size * x.numel(),), dtype=x.dtype, device=x.device)
+        if not (out.is_contiguous() and out.numel() == self.size * x.numel() and out.dtype == x.dtype):
+            raise ValueError("IPC all-gather: out must hold world * x")
+        check(self.L.ragk_ar_allgather(self.h, x.data_ptr(), out.data_ptr(), nb, stream_ptr()), "ragk_ar_allgather")
+        return out
+
+    def gather_fits(self, x: torch.Tensor) -> bool:
+        nb = x.numel() * x.element_size()
+        return x.is_cuda and x.is_contiguous() and nb % 16 == 0 and nb <= self.max_bytes and x.data_ptr() % 16 == 0
+
     def error(self) -> bool:
-        """True if a peer failed to arrive within the kernel's bounded spin (comm watchdog)."""
+        """True if a peer failed to arrive within the kernel's bounded spin (comm watchdog). Reads the
+        pinned host word (no device sync); falls back to a device read."""
+        if self._err_word is not None:
+            return self._err_word.value != 0
         return self.L.ragk_ar_error(self.h) != 0
 
     def close(self):

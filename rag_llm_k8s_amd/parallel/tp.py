@@ -1,18 +1,34 @@
 """Tensor-parallel serving: one process per GPU, rank 0 serves HTTP.
 
 The engine is deterministic given its inputs, so TP ranks only need to agree on WHICH requests
-enter WHEN. Rank 0's engine loop drains newly submitted requests once per step and broadcasts
-them (token ids, sampling params, seed) over a gloo control group before stepping; followers
-receive the same list, add the same sequences in the same order and step. All GPU-side
-exchange (2 all-reduces per layer, top-k candidate all-gather) runs over RCCL inside the step.
+enter WHEN. Rank 0's engine loop drains newly submitted requests once per step and publishes one
+control record per step on a channel to the follower ranks before stepping; followers receive
+the same record, add the same sequences in the same order and step. All GPU-side exchange (2
+all-reduces per layer, top-k candidate all-gather) runs over xGMI inside the step.
+
+Control record = fixed 16-byte header (kind, payload bytes) + a payload only when there is
+something to admit (the pickled request list). Two transports:
+* ``ShmChannel`` (default when every TP rank is on this host, i.e. one xGMI node): a POSIX
+  shared-memory mailbox; rank 0 writes payload then header then bumps a sequence word, followers
+  poll it (spin briefly, then back off) and acknowledge. A step with nothing to admit costs a few
+  microseconds, not a gloo round trip.
+* ``GlooChannel``: a fixed-size int64 header broadcast over the TP gloo group every step, plus a
+  uint8 payload broadcast only when there is something to admit.
+The reference has no distribution; this is the "step metadata broadcast" row of the
+collective table in SURVEY §2.6.
 """
 from __future__ import annotations
 
 import dataclasses
 import logging
+import os
+import pickle
+import socket
 import threading
 import time
+import uuid
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -22,14 +38,149 @@ from ..utils import faults
 log = logging.getLogger(__name__)
 
 HEARTBEAT_S = 30.0
+K_STEP, K_NOOP, K_SHUTDOWN = 1, 2, 3
+
+
+class GlooChannel:
+    """Header [kind, nbytes] (int64) broadcast per record; payload bytes only when nbytes > 0."""
+
+    def __init__(self, cpu_group, src=0):
+        self.group, self.src = cpu_group, src
+
+    def send(self, kind, payload=b""):
+        hdr = torch.tensor([kind, len(payload)], dtype=torch.int64)
+        dist.broadcast(hdr, src=self.src, group=self.group)
+        if payload:
+            dist.broadcast(torch.frombuffer(bytearray(payload), dtype=torch.uint8), src=self.src, group=self.group)
+
+    def recv(self):
+        hdr = torch.zeros(2, dtype=torch.int64)
+        dist.broadcast(hdr, src=self.src, group=self.group)
+        kind, n = int(hdr[0]), int(hdr[1])
+        payload = b""
+        if n:
+            buf = torch.empty(n, dtype=torch.uint8)
+            dist.broadcast(buf, src=self.src, group=self.group)
+            payload = buf.numpy().tobytes()
+        return kind, payload
+
+    def close(self):
+        pass
+
+
+class ShmChannel:
+    """Single-producer mailbox in POSIX shared memory (every TP rank on one host).
+
+    Layout (int64 words): [0] seq, [1] kind, [2] nbytes, [8 + r] ack of rank r, then the payload
+    area. Rank 0 waits until every follower acknowledged record seq-1, writes payload, kind,
+    nbytes, then seq (x86 stores are not reordered with other stores, and numpy writes them in
+    program order), so a follower that sees the new seq reads a complete record."""
+
+    HDR_WORDS = 64
+    POLL_SPIN_S = 0.002
+
+    def __init__(self, cpu_group, rank, world, capacity=1 << 20, src=0, timeout_s=600.0):
+        from multiprocessing import shared_memory
+
+        self.rank, self.world, self.src, self.timeout_s = rank, world, src, timeout_s
+        name = [None]
+        if rank == src:
+            name[0] = "ragk_tp_%s" % uuid.uuid4().hex[:16]
+            self.shm = shared_memory.SharedMemory(name=name[0], create=True,
+                                                  size=self.HDR_WORDS * 8 + capacity)
+            self.shm.buf[:self.HDR_WORDS * 8] = bytes(self.HDR_WORDS * 8)
+        dist.broadcast_object_list(name, src=src, group=cpu_group)
+        if rank != src:
+            self.shm = shared_memory.SharedMemory(name=name[0], create=False)
+            try:  # the producer owns the segment; followers must not unlink it at exit
+                from multiprocessing import resource_tracker
+                resource_tracker.unregister(self.shm._name, "shared_memory")
+            except Exception:
+                pass
+        dist.barrier(group=cpu_group)
+        if rank == src:  # every rank has mapped it: the name can go (the mapping stays)
+            self.shm.unlink()
+        self.words = np.ndarray((self.HDR_WORDS,), dtype=np.int64, buffer=self.shm.buf)
+        self.cap = len(self.shm.buf) - self.HDR_WORDS * 8
+        self.seq = 0
+        self.group = cpu_group  # big payloads (> capacity) go over gloo
+
+    def _wait(self, cond, what):
+        t0 = time.monotonic()
+        while not cond():
+            dt = time.monotonic() - t0
+            if dt > self.POLL_SPIN_S:
+                time.sleep(min(0.001, dt * 0.1))
+            if dt > self.timeout_s:
+                raise TimeoutError("TP control channel: %s timed out after %.0fs" % (what, dt))
+
+    def send(self, kind, payload=b""):
+        w = self.words
+        if self.seq > 0:  # previous record consumed by every follower
+            self._wait(lambda: all(int(w[8 + r]) >= self.seq for r in range(self.world) if r != self.src),
+                       "follower acknowledgement")
+        big = len(payload) > self.cap
+        if not big and payload:
+            self.shm.buf[self.HDR_WORDS * 8:self.HDR_WORDS * 8 + len(payload)] = payload
+        w[1] = kind
+        w[2] = -len(payload) if big else len(payload)
+        self.seq += 1
+        w[0] = self.seq
+        if big:
+            dist.broadcast(torch.frombuffer(bytearray(payload), dtype=torch.uint8), src=self.src, group=self.group)
+
+    def recv(self):
+        w = self.words
+        nxt = self.seq + 1
+        self._wait(lambda: int(w[0]) >= nxt, "waiting for rank 0")
+        kind, n = int(w[1]), int(w[2])
+        if n >= 0:
+            payload = bytes(self.shm.buf[self.HDR_WORDS * 8:self.HDR_WORDS * 8 + n]) if n else b""
+        else:
+            buf = torch.empty(-n, dtype=torch.uint8)
+            dist.broadcast(buf, src=self.src, group=self.group)
+            payload = buf.numpy().tobytes()
+        self.seq = nxt
+        w[8 + self.rank] = nxt
+        return kind, payload
+
+    def close(self):
+        try:
+            self.words = None
+            self.shm.close()
+        except Exception:
+            pass
+
+
+def make_channel(cpu_group, rank, world, src=0):
+    """Shared memory when every TP rank runs on this host (RAGK_TP_CONTROL=gloo forces gloo)."""
+    mode = os.environ.get("RAGK_TP_CONTROL", "auto")
+    if mode != "gloo":
+        hosts = [None] * world
+        dist.all_gather_object(hosts, socket.gethostname(), group=cpu_group)
+        if len(set(hosts)) == 1:
+            try:
+                return ShmChannel(cpu_group, rank, world, src=src)
+            except Exception as e:  # e.g. /dev/shm not writable: fall back, loudly
+                log.warning("shared-memory TP control channel unavailable (%s); using gloo", e)
+    return GlooChannel(cpu_group, src)
+
+
+def _encode(seqs):
+    return pickle.dumps([(s.prompt, dataclasses.asdict(s.params), s.seed) for s in seqs],
+                        protocol=pickle.HIGHEST_PROTOCOL)
 
 
 class TPControl:
     """Rank-0 side: queue of submitted sequences, published in order once per engine step."""
 
-    def __init__(self, cpu_group, src_rank=0):
+    def __init__(self, cpu_group, src_rank=0, channel=None):
         self.group = cpu_group
         self.src = src_rank
+        if channel is None:
+            world = dist.get_world_size(cpu_group)
+            channel = make_channel(cpu_group, dist.get_rank(cpu_group), world, src_rank)
+        self.chan = channel
         self.pending = []
         self.lock = threading.Lock()
         self.last_publish = time.time()
@@ -42,46 +193,46 @@ class TPControl:
         with self.lock:
             return bool(self.pending)
 
-    def _bcast(self, msg):
-        obj = [msg]
-        dist.broadcast_object_list(obj, src=self.src, group=self.group)
-        self.last_publish = time.time()
-
     def publish_step(self, engine):
         with self.lock:
             new, self.pending = self.pending, []
-        self._bcast(("step", [(s.prompt, dataclasses.asdict(s.params), s.seed) for s in new]))
+        self.chan.send(K_STEP, _encode(new) if new else b"")
+        self.last_publish = time.time()
         for s in new:
             engine.add_sequence(s)
 
     def publish_heartbeat(self):
-        self._bcast(("noop", []))
+        self.chan.send(K_NOOP)
+        self.last_publish = time.time()
 
     def publish_shutdown(self):
         try:
-            self._bcast(("shutdown", []))
+            self.chan.send(K_SHUTDOWN)
         except Exception:
             pass
 
 
-def follow(engine, cpu_group, src_rank=0):
+def follow(engine, cpu_group, src_rank=0, channel=None):
     """Follower loop (ranks != 0): mirror rank 0's admissions and steps until shutdown."""
-    while True:
-        obj = [None]
-        dist.broadcast_object_list(obj, src=src_rank, group=cpu_group)
-        kind, reqs = obj[0]
-        if kind == "shutdown":
-            return
-        if kind == "noop":
-            continue
-        hang = faults.value("comm_hang_s")
-        if hang:  # fault injection: this rank stalls, rank 0's collectives wait (watchdog path)
-            time.sleep(float(hang))
-        for prompt, params, seed in reqs:
-            p = dict(params)
-            p["stop_token_ids"] = tuple(p.get("stop_token_ids", ()))
-            engine.add_request(prompt, SamplingParams(**p), seed=seed)
-        engine.step()
+    if channel is None:
+        channel = make_channel(cpu_group, dist.get_rank(cpu_group), dist.get_world_size(cpu_group), src_rank)
+    try:
+        while True:
+            kind, payload = channel.recv()
+            if kind == K_SHUTDOWN:
+                return
+            if kind == K_NOOP:
+                continue
+            hang = faults.value("comm_hang_s")
+            if hang:  # fault injection: this rank stalls, rank 0's collectives wait (watchdog path)
+                time.sleep(float(hang))
+            for prompt, params, seed in (pickle.loads(payload) if payload else []):
+                p = dict(params)
+                p["stop_token_ids"] = tuple(p.get("stop_token_ids", ()))
+                engine.add_request(prompt, SamplingParams(**p), seed=seed)
+            engine.step()
+    finally:
+        channel.close()
 
 
 def run_tp_server(cfg, rank, world):
@@ -94,11 +245,12 @@ def run_tp_server(cfg, rank, world):
     # a collective that outlives two watchdog periods is dead: fail it so the pod restarts
     ctx = init_distributed(tp=world, timeout_s=int(max(600, 2 * cfg.step_timeout_s)))
     comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, ctx.device, ctx.tp_cpu_group)
-    control = TPControl(ctx.tp_cpu_group) if rank == 0 else None
+    chan = make_channel(ctx.tp_cpu_group, ctx.tp_rank, ctx.tp)
+    control = TPControl(ctx.tp_cpu_group, channel=chan) if rank == 0 else None
     svc = build_service(cfg, start_threads=(rank == 0), tp_rank=ctx.tp_rank, tp_size=ctx.tp, comm=comm,
                         tp_group=ctx.tp_group, control=control)
     if rank != 0:
-        follow(svc.engine, ctx.tp_cpu_group)
+        follow(svc.engine, ctx.tp_cpu_group, channel=chan)
         return
     svc.store.ensure_exists()
     svc.ingest_directory()

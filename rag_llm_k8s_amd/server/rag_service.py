@@ -32,6 +32,38 @@ from ..utils.metrics import Trace
 log = logging.getLogger(__name__)
 
 
+def _tp_bcast_prompts(comm, rows, id_lists, seeds):
+    """TP leader -> every TP rank: row indices, token ids and seeds of the prompts to queue
+    (int tensors over the TP gloo group; no pickling)."""
+    import torch.distributed as dist
+
+    grp = comm.cpu_group if comm.cpu_group is not None else comm.group
+    src = dist.get_global_rank(grp, 0) if grp is not None else 0
+    if comm.rank == 0:
+        lens = [len(x) for x in id_lists]
+        hdr = torch.tensor([len(rows), sum(lens)], dtype=torch.int64)
+    else:
+        hdr = torch.zeros(2, dtype=torch.int64)
+    dist.broadcast(hdr, src=src, group=grp)
+    nr, nt = int(hdr[0]), int(hdr[1])
+    if comm.rank == 0:
+        meta = torch.tensor([rows, lens, seeds], dtype=torch.int64).reshape(3, nr)
+        flat = torch.tensor([t for x in id_lists for t in x], dtype=torch.int32)
+    else:
+        meta = torch.zeros((3, nr), dtype=torch.int64)
+        flat = torch.zeros(nt, dtype=torch.int32)
+    dist.broadcast(meta, src=src, group=grp)
+    if nt:
+        dist.broadcast(flat, src=src, group=grp)
+    rows, lens, seeds = (meta[i].tolist() for i in range(3))
+    out, off = [], 0
+    fl = flat.tolist()
+    for n_ in lens:
+        out.append(fl[off:off + n_])
+        off += n_
+    return rows, out, seeds
+
+
 class EngineLoop(threading.Thread):
     """Drives LLMEngine.step() on one thread; wakes when requests arrive."""
 
@@ -271,57 +303,87 @@ class RagService:
 
     def generate_batch(self, prompts, params=None, seeds=None):
         """Many queries at once (benchmark / offline): one embed + one search + one engine run.
-        Must not be mixed with the background loop (call with start_threads=False)."""
+        Must not be mixed with the background loop (call with start_threads=False).
+
+        Tensor parallel (every TP rank calls this with the same arguments): the TP leader embeds,
+        searches, builds and tokenizes every prompt, broadcasts the token ids and seeds over the TP
+        gloo group, and every rank queues ALL of them before its first step -- each rank's engine must
+        see the same admissions at the same steps (TP has no per-step metadata exchange here)."""
         if self.loop.is_alive():  # two threads stepping one engine corrupt its running set
             raise RuntimeError("generate_batch needs exclusive use of the engine: build the service "
                                "with start_threads=False")
         t0 = time.perf_counter()
-        q = self.embedder.embed(list(prompts))
-        res = self.store.search(q, self.cfg.retrieve_k)
+        eng = self.engine
+        comm = getattr(eng, "comm", None)
+        tp = eng.tp_size > 1 and comm is not None
+        lead = (not tp) or comm.rank == 0
+        n = len(prompts)
+        ctxs, fulls = [None] * n, [None] * n
+        if lead:
+            q = self.embedder.embed(list(prompts))
+            res = self.store.search(q, self.cfg.retrieve_k)
+            for i, (p, r) in enumerate(zip(prompts, res)):
+                if r:
+                    ctxs[i] = build_context(r, self.cfg.context_k)
+                    fulls[i] = build_prompt(ctxs[i], p)
         t_ret = time.perf_counter()
-        seqs, ctxs, fulls = [], [], []
-        for p, r in zip(prompts, res):
-            ctx = build_context(r, self.cfg.context_k) if r else None
-            ctxs.append(ctx)
-            if ctx is not None:
-                fulls.append(build_prompt(ctx, p))
-        # Multi-threaded tokenizer calls (C++ workers, GIL released). The first few prompts -- about
-        # one prefill step's worth -- are tokenized and submitted right away; the rest are tokenized
-        # on a helper thread while the GPU runs that first prefill step, and join the queue in order.
-        rows = [i for i, c in enumerate(ctxs) if c is not None]
-        seqs = [None] * len(ctxs)
+        rows = [i for i in range(n) if fulls[i] is not None]
+        seqs = [None] * n
         seed_of = {i: (seeds[i] if seeds is not None else self._next_seed()) for i in rows}
+        p_use = params or self.params
+        queued = []
 
-        def submit(idx, texts):
-            for i, ids in zip(idx, self.tok.encode_batch(texts, add_special_tokens=True)):
-                seqs[i] = self.engine.add_request(self._prompt_ids(None, ids=ids), params or self.params,
-                                                  seed=seed_of[i])
+        def submit(idx, id_lists):
+            for i, ids in zip(idx, id_lists):
+                seqs[i] = eng.add_request(self._prompt_ids(None, ids=ids), p_use, seed=seed_of[i])
+                queued.append(seqs[i])
 
-        head = max(1, self.engine.max_prefill_tokens // max(1, 4 * self.cfg.chunk_words))  # ~1 step of prompts
-        submit(rows[:head], fulls[:head])
-        err = []
-        rest = None
-        if len(rows) > head:
-            def _rest():
-                try:
-                    submit(rows[head:], fulls[head:])
-                except Exception as e:  # surfaced below, after the engine drains
-                    err.append(e)
-            rest = threading.Thread(target=_rest, daemon=True)
-            rest.start()
+        rest, err = None, []
+        if tp:
+            id_lists = self.tok.encode_batch([fulls[i] for i in rows], add_special_tokens=True) if lead else None
+            rows, id_lists, sd = _tp_bcast_prompts(comm, rows, id_lists, [seed_of[i] for i in rows] if lead else None)
+            seed_of = dict(zip(rows, sd))
+            submit(rows, id_lists)
+        else:
+            # Multi-threaded tokenizer calls (C++ workers, GIL released). The first few prompts -- about
+            # one prefill step's worth -- are tokenized and submitted right away; the rest are tokenized
+            # on a helper thread while the GPU runs that first prefill step, and join the queue in order.
+            head = max(1, eng.max_prefill_tokens // max(1, 4 * self.cfg.chunk_words))  # ~1 step of prompts
+            submit(rows[:head], self.tok.encode_batch([fulls[i] for i in rows[:head]], add_special_tokens=True))
+            if len(rows) > head:
+                def _rest():
+                    try:
+                        tail = rows[head:]
+                        submit(tail, self.tok.encode_batch([fulls[i] for i in tail], add_special_tokens=True))
+                    except Exception as e:  # surfaced below, after the engine drains
+                        err.append(e)
+                rest = threading.Thread(target=_rest, daemon=True)
+                rest.start()
         t_prep = time.perf_counter()
-        while True:
-            if self.engine.has_work():
-                self.engine.step()
-            elif rest is not None and rest.is_alive():
-                rest.join(0.001)
-            elif not self.engine.has_work():  # re-check: the helper may have queued its last rows and exited
-                break
-        if rest is not None:
-            rest.join()
+        ok = False
+        try:
+            while True:
+                if eng.has_work():
+                    eng.step()
+                elif rest is not None and rest.is_alive():
+                    rest.join(0.001)
+                elif not eng.has_work():  # re-check: the helper may have queued its last rows and exited
+                    break
+            ok = True
+        finally:
+            if rest is not None:
+                rest.join()
+            if not ok:  # a failed step: nothing this call queued may run in a later call
+                for s in queued:
+                    if s.status != 2:
+                        eng.abort(s)
+                try:
+                    eng._apply_aborts()
+                except Exception:
+                    pass
         if err:
             raise err[0]
-        st = self.engine.stats
+        st = eng.stats
         st["retrieve_s"] = st.get("retrieve_s", 0.0) + (t_ret - t0)
         st["prompt_build_s"] = st.get("prompt_build_s", 0.0) + (t_prep - t_ret)
         outs = []
@@ -370,8 +432,11 @@ class RagService:
         return self.store.info()
 
     def health(self):
-        alive = self.loop.is_alive() and self.loop.error is None and not self.watchdog.hung
-        return {"engine_alive": alive, "ready": self.ready, "engine_steps": self.loop.steps,
+        comm = getattr(self.engine, "comm", None)
+        comm_ok = comm is None or getattr(comm, "broken", None) is None
+        alive = self.loop.is_alive() and self.loop.error is None and not self.watchdog.hung and comm_ok
+        return {"engine_alive": alive, "ready": self.ready, "engine_steps": self.loop.steps, "comm_ok": comm_ok,
+                "engine_error": None if self.loop.error is None else repr(self.loop.error),
                 "kv_free_blocks": self.engine.bm.free_blocks(), "index_vectors": int(self.store.index.ntotal),
                 "hbm_bytes": torch.cuda.memory_allocated() if torch.cuda.is_available() else 0}
 

@@ -234,3 +234,58 @@ def test_dp_embedding_and_sharded_search():
         D, I = ref.search(out[r]["q"], 4)
         assert torch.equal(out[r]["I"], I)
         assert torch.allclose(out[r]["D"], D, atol=1e-5)
+
+
+def _tp_batch_worker(ctx, n_queries):
+    """TP=2 generate_batch with more prompts than one prefill step holds: both ranks must queue the
+    same prompts at the same steps (the leader broadcasts the token ids) and sample the same tokens."""
+    from rag_llm_k8s_amd.engine.llm_engine import SamplingParams
+    from rag_llm_k8s_amd.parallel.comm import TPComm
+    from rag_llm_k8s_amd.utils.workload import build_workload, make_queries
+
+    comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, "cpu")
+    wl = build_workload(model="tiny", embedder="tiny", n_chunks=48, chunk_words=60, retrieve_k=2, context_k=2,
+                        max_new_tokens=4, max_batch=8, max_model_len=1024, max_prefill_tokens=256, device="cpu",
+                        ctx=ctx, tp_comm=comm, use_graphs=False, word_vocab=5000)
+    qs = make_queries(wl.wm, n_queries, seed=3)
+    p = SamplingParams(max_new_tokens=4, temperature=0.8, top_p=0.9, top_k=20, ignore_eos=True)
+    outs = wl.svc.generate_batch(qs, params=p, seeds=list(range(100, 100 + n_queries)))
+    return [(o.get("_gen_tokens"), o.get("_prompt_tokens"), o["generated_text"]) for o in outs]
+
+
+def test_tp_generate_batch_same_schedule_on_every_rank():
+    out = _run(_tp_batch_worker, 2, 10)
+    assert len(out[0]) == 10
+    assert all(o[0] == 4 for o in out[0])
+    assert out[0] == out[1]
+
+
+def _tp_channel_worker(ctx, mode):
+    import os as _os
+
+    _os.environ["RAGK_TP_CONTROL"] = mode
+    from rag_llm_k8s_amd.parallel.tp import K_SHUTDOWN, K_STEP, GlooChannel, ShmChannel, make_channel
+
+    ch = make_channel(ctx.tp_cpu_group, ctx.rank, ctx.world)
+    kind = type(ch).__name__
+    msgs = [b"", b"abc", bytes(range(256)) * 50, b"", bytes(3 << 20)]  # last one exceeds the shm mailbox
+    got = []
+    if ctx.rank == 0:
+        for m in msgs:
+            ch.send(K_STEP, m)
+        ch.send(K_SHUTDOWN)
+    else:
+        while True:
+            k, p = ch.recv()
+            if k == K_SHUTDOWN:
+                break
+            got.append(p)
+    ch.close()
+    return dict(kind=kind, got=got, ok=(got == msgs) if ctx.rank else True)
+
+
+@pytest.mark.parametrize("mode", ["auto", "gloo"])
+def test_tp_control_channel_transports(mode):
+    out = _run(_tp_channel_worker, 2, mode)
+    assert out[1]["ok"]
+    assert out[0]["kind"] == ("ShmChannel" if mode == "auto" else "GlooChannel")

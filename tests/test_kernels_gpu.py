@@ -65,12 +65,20 @@ def test_gemm_blaslt_path_and_auto_choice(native):
     h = r.clone()
     native.gemm(x, w, resid=h, epi="resid", out=h, path=7)
     assert rel_err(h, ref + r.float()) < 1e-2
+    assert native.PREFILL_GEMM == "w4"  # default route: hand-written kernel only, never hipBLASLt
     native._blaslt_choice.clear()
-    h = r.clone()
-    native.gemm(x, w, resid=h, epi="resid", out=h)  # times both on scratch, then runs the winner once
-    assert (N, K, "resid") in native._blaslt_choice
-    assert rel_err(h, ref + r.float()) < 1e-2
-    assert rel_err(native.gemm(x, w), ref) < 1e-2
+    native.gemm(x, w, resid=r.clone(), epi="resid", out=torch.empty_like(r))
+    assert not native._blaslt_choice
+    old = native.PREFILL_GEMM
+    native.PREFILL_GEMM = "auto"  # A/B tooling: measured choice
+    try:
+        h = r.clone()
+        native.gemm(x, w, resid=h, epi="resid", out=h)  # times both on scratch, then runs the winner once
+        assert (N, K, "resid", 13) in native._blaslt_choice
+        assert rel_err(h, ref + r.float()) < 1e-2
+        assert rel_err(native.gemm(x, w), ref) < 1e-2
+    finally:
+        native.PREFILL_GEMM = old
 
 
 def _check_pingpong(native, M, N, K, path=2):

@@ -1,0 +1,241 @@
+"""Tensor parallelism on the GPU, as far as one MI355X allows: two ranks on cuda:0.
+
+Both ranks run the real TP code path -- Megatron-sharded Llama weights at Llama-3.1-8B widths
+(hidden 4096, 32/8 heads, FFN 14336, 128,256-token vocabulary; 2 layers), the peer-mapped
+all-reduce / all-gather kernels (csrc/comm/allreduce.hip, hipIpc handles exchanged over gloo),
+the vocab-parallel sampler with its candidate all-gather, graph-captured and asynchronous decode --
+only the xGMI hop is replaced by local HBM. RCCL itself cannot run two ranks on one device, so
+bulk messages are kept under the peer-mapped size limit here.
+
+Oracles: the TP=1 model on the same weights (prefill logits), the eager synchronous engine (graph
++ async decode must produce the same tokens), and the other rank (identical samples).
+"""
+import os
+import socket
+import tempfile
+import time
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg(layers=2):
+    from rag_llm_k8s_amd.models.llama import llama31_8b
+
+    c = llama31_8b()
+    c.num_hidden_layers = layers
+    return c
+
+
+def _state_dict(cfg, seed=1234):
+    """HF-named full weights generated on the GPU (same values in every process)."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    H, D, I, V = cfg.hidden_size, cfg.head_dim, cfg.intermediate_size, cfg.vocab_size
+    Hq, Hkv = cfg.num_attention_heads, cfg.num_key_value_heads
+
+    def rnd(*shape, std=0.02):
+        return (torch.randn(*shape, generator=g, device="cuda") * std).bfloat16()
+
+    def ones(n):
+        return (1.0 + 0.1 * torch.randn(n, generator=g, device="cuda")).bfloat16()
+
+    sd = {"model.embed_tokens.weight": rnd(V, H, std=0.5)}
+    for i in range(cfg.num_hidden_layers):
+        p = "model.layers.%d." % i
+        sd[p + "input_layernorm.weight"] = ones(H)
+        sd[p + "post_attention_layernorm.weight"] = ones(H)
+        sd[p + "self_attn.q_proj.weight"] = rnd(Hq * D, H)
+        sd[p + "self_attn.k_proj.weight"] = rnd(Hkv * D, H)
+        sd[p + "self_attn.v_proj.weight"] = rnd(Hkv * D, H)
+        sd[p + "self_attn.o_proj.weight"] = rnd(H, Hq * D)
+        sd[p + "mlp.gate_proj.weight"] = rnd(I, H)
+        sd[p + "mlp.up_proj.weight"] = rnd(I, H)
+        sd[p + "mlp.down_proj.weight"] = rnd(H, I)
+    sd["model.norm.weight"] = ones(H)
+    sd["lm_head.weight"] = rnd(V, H)
+    return sd
+
+
+def _prefill_logits(model, ids):
+    """Full-prompt prefill through the native kernels; logits of the last position (vocab shard)."""
+    from rag_llm_k8s_amd.models.llama import StepInput
+    from rag_llm_k8s_amd.ops.backend import AttnMeta
+    from rag_llm_k8s_amd.ops.native import build_prefill_tiles
+
+    n = len(ids)
+    nb = -(-n // 64)
+    model.allocate_kv_cache(nb + 1)
+    dev = model.device
+    i32 = dict(dtype=torch.int32, device=dev)
+    bt = torch.zeros((1, nb + 1), **i32)
+    bt[0, :nb] = torch.arange(1, nb + 1, **i32)
+    meta = AttnMeta("prefill", torch.tensor([n], **i32), bt, cu_q=torch.tensor([0, n], **i32),
+                    tiles=build_prefill_tiles([n], model.Hq, model.Hkv).to(dev), host_kv_lens=[n], host_q_lens=[n])
+    inp = StepInput(torch.tensor(ids, **i32), torch.arange(n, **i32), torch.arange(64, 64 + n, **i32), meta,
+                    torch.tensor([n - 1], **i32))
+    return model.forward(inp)
+
+
+def _init(rank, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK="0", RAGK_TP_CONTROL="gloo")
+    from rag_llm_k8s_amd.parallel.dist import init_distributed
+
+    return init_distributed(tp=WORLD, backend="gloo")
+
+
+def _tp_worker(rank, port, d):
+    ctx = _init(rank, port)
+    from rag_llm_k8s_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights
+    from rag_llm_k8s_amd.parallel.comm import TPComm
+
+    res = {}
+    comm = None
+    try:
+        cfg = _cfg()
+        sd = _state_dict(cfg)
+        comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, ctx.device, ctx.tp_cpu_group, ipc_max_bytes=16 << 20)
+        res["ipc"] = comm.ipc is not None
+        w = LlamaWeights.from_state_dict(cfg, sd, ctx.device, ctx.tp_rank, ctx.tp)
+        m = LlamaModel(cfg, w, ctx.device, comm=comm, max_positions=4096)
+        gen = torch.Generator().manual_seed(7)
+        ids = torch.randint(3, cfg.vocab_size, (300,), generator=gen).tolist()
+        local = _prefill_logits(m, ids)  # [1, V/2] this rank's vocab shard
+        full = comm.ipc.all_gather(local.contiguous()).view(WORLD, 1, -1)
+        res["tp_logits"] = torch.cat([full[r] for r in range(WORLD)], 1)[:, :cfg.vocab_size].cpu()
+        if rank == 0:
+            ref = LlamaModel(cfg, LlamaWeights.from_state_dict(cfg, sd, ctx.device), ctx.device, max_positions=4096)
+            res["ref_logits"] = _prefill_logits(ref, ids).cpu()
+            del ref
+        del sd
+        torch.cuda.empty_cache()
+
+        # engine: graph-captured + asynchronous decode vs eager synchronous, sampled and greedy
+        prompts = [torch.randint(3, cfg.vocab_size, (n,), generator=gen).tolist() for n in (100, 260, 37)]
+        sampled = SamplingParams(max_new_tokens=12, temperature=0.7, top_p=0.9, top_k=50, ignore_eos=True)
+        greedy = SamplingParams(max_new_tokens=12, do_sample=False, ignore_eos=True)
+        for graphs in (True, False):
+            eng = LLMEngine(m, num_blocks=64, max_batch=4, max_model_len=1024, use_graphs=graphs,
+                            tp_group=ctx.tp_group, graph_buckets=[1, 2, 4])
+            if graphs:
+                eng.warmup_graphs()
+            res[("sampled", graphs)] = eng.generate(prompts, sampled, seeds=[11, 12, 13])
+            res[("greedy", graphs)] = eng.generate(prompts, greedy)
+            res[("async", graphs)] = eng.async_decode
+            del eng
+            torch.cuda.empty_cache()
+        res["error"] = comm.ipc.error()
+    finally:
+        torch.cuda.synchronize()
+        dist.barrier(group=ctx.tp_cpu_group)
+        if comm is not None and comm.ipc is not None:
+            comm.ipc.close()
+        torch.save(res, os.path.join(d, "r%d.pt" % rank))
+        dist.destroy_process_group()
+
+
+def _spawn(target, timeout=600):
+    port = _free_port()
+    d = tempfile.mkdtemp()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=target, args=(r, port, d)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=timeout)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+            p.join()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return [torch.load(os.path.join(d, "r%d.pt" % r), weights_only=False) for r in range(WORLD)]
+
+
+def test_tp2_llama8b_widths_on_one_gpu(native):
+    out = _spawn(_tp_worker)
+    assert out[0]["ipc"] and out[1]["ipc"], "peer-mapped collectives must pass their self-test"
+    ref = out[0]["ref_logits"]
+    for r in range(WORLD):
+        got = out[r]["tp_logits"]
+        rel = ((got - ref).norm() / ref.norm()).item()
+        assert rel < 2e-2, (r, rel)
+        assert out[r]["error"] is False
+    assert torch.equal(out[0]["tp_logits"], out[1]["tp_logits"])
+    for r in range(WORLD):
+        assert out[r][("async", True)] is True
+        for kind in ("sampled", "greedy"):
+            g, e = out[r][(kind, True)], out[r][(kind, False)]
+            assert [len(x) for x in g] == [12, 12, 12]
+            assert g == e, (r, kind, g, e)  # graph-captured async TP decode == eager synchronous
+    for kind in ("sampled", "greedy"):
+        assert out[0][(kind, True)] == out[1][(kind, True)]  # every rank sampled the same tokens
+
+
+def _fault_worker(rank, port, d):
+    """Rank 1 stops taking part after set-up; rank 0's engine loop must fail its step with
+    CommError within the bounded wait, and the service must report unhealthy."""
+    ctx = _init(rank, port)
+    from types import SimpleNamespace
+
+    from rag_llm_k8s_amd.config import RagConfig
+    from rag_llm_k8s_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights, llama_tiny
+    from rag_llm_k8s_amd.parallel.comm import TPComm
+    from rag_llm_k8s_amd.server.rag_service import RagService
+
+    res = {}
+    comm = None
+    try:
+        cfg = llama_tiny(vocab=1024, layers=2, hidden=512, heads=8, kv_heads=2, inter=1024)
+        comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, ctx.device, ctx.tp_cpu_group, ipc_spin_limit=20000)  # 20 ms
+        res["ipc"] = comm.ipc is not None
+        w = LlamaWeights.random(cfg, ctx.device, ctx.tp_rank, ctx.tp, seed=3)
+        m = LlamaModel(cfg, w, ctx.device, comm=comm, max_positions=1024)
+        eng = LLMEngine(m, num_blocks=16, max_batch=2, max_model_len=512, use_graphs=False, tp_group=ctx.tp_group)
+        if rank == 0:
+            store = SimpleNamespace(index=SimpleNamespace(ntotal=0))
+            svc = RagService(RagConfig(device=ctx.device), eng, None, None, store, start_threads=True)
+            before = svc.health()
+            t0 = time.monotonic()
+            s = svc.loop.submit(list(range(3, 40)), SamplingParams(max_new_tokens=4, do_sample=False), seed=1)
+            s.done.wait(60)
+            res["elapsed"] = time.monotonic() - t0
+            res["finish"] = s.finish_reason
+            res["before"] = before["engine_alive"]
+            h = svc.health()
+            res["after"] = h["engine_alive"]
+            res["comm_ok"] = h["comm_ok"]
+            res["error"] = h["engine_error"]
+            svc.shutdown()
+    finally:
+        torch.cuda.synchronize()
+        dist.barrier(group=ctx.tp_cpu_group)  # rank 1 keeps its mapped region alive until rank 0 is done
+        if comm is not None and comm.ipc is not None:
+            comm.ipc.close()
+        torch.save(res, os.path.join(d, "r%d.pt" % rank))
+        dist.destroy_process_group()
+
+
+def test_tp_comm_fault_fails_step_and_health(native):
+    out = _spawn(_fault_worker, timeout=300)
+    r0 = out[0]
+    assert r0["ipc"]
+    assert r0["before"] is True
+    assert r0["finish"] == "error", r0
+    assert "CommError" in (r0["error"] or ""), r0
+    assert r0["after"] is False and r0["comm_ok"] is False
+    assert r0["elapsed"] < 30, r0["elapsed"]
