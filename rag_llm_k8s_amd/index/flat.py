@@ -111,16 +111,24 @@ class FlatL2Index:
             return self._xb[:self.ntotal].numpy().copy()
 
     # ---------------------------------------------------------------- persistence
-    def write(self, path):
-        from ..runtime import native_rt
-        from .faiss_io import atomic_write, write_flat_l2
-
+    def snapshot_writer(self):
+        """Host copy of the vectors now; the returned callable writes it (faiss IxF2) atomically."""
         xb = self.reconstruct_all()
-        rt = native_rt()
-        if rt is not None:  # C++ writer: temp file + fsync + rename
-            rt.write_flat_index(path, xb.reshape(-1, self.d))
-        else:
-            atomic_write(path, lambda f: write_flat_l2(f, xb))
+        d = self.d
+
+        def write(path):
+            from ..runtime import native_rt
+            from .faiss_io import atomic_write, write_flat_l2
+
+            rt = native_rt()
+            if rt is not None:  # C++ writer: temp file + fsync + rename
+                rt.write_flat_index(path, xb.reshape(-1, d))
+            else:
+                atomic_write(path, lambda f: write_flat_l2(f, xb))
+        return write
+
+    def write(self, path):
+        self.snapshot_writer()(path)
 
     @classmethod
     def read(cls, path, device="cpu"):

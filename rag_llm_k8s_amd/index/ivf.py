@@ -132,11 +132,20 @@ class IVFFlatIndex:
             I[qi, :kk] = ids[order[:kk]]
         return D, I
 
-    def write(self, path):
-        from .faiss_io import atomic_write, write_ivf_flat
+    def snapshot_writer(self):
+        """Consistent copy of centroids + inverted lists now; the callable writes it atomically."""
+        with self._lock:
+            cents = self.centroids.cpu().numpy() if self.centroids is not None else np.zeros((0, self.d), np.float32)
+            lists, ids, nprobe, d = list(self.lists), list(self.ids), self.nprobe, self.d
 
-        cents = self.centroids.cpu().numpy() if self.centroids is not None else np.zeros((0, self.d), np.float32)
-        atomic_write(path, lambda f: write_ivf_flat(f, self.d, cents, self.lists, self.ids, self.nprobe))
+        def write(path):
+            from .faiss_io import atomic_write, write_ivf_flat
+
+            atomic_write(path, lambda f: write_ivf_flat(f, d, cents, lists, ids, nprobe))
+        return write
+
+    def write(self, path):
+        self.snapshot_writer()(path)
 
     @classmethod
     def from_lists(cls, r, device="cpu"):

@@ -5,7 +5,10 @@ Reference behaviour and its fixes:
   * index + metadata re-read from disk on every request    -> kept resident (HBM), reloaded
     only if the files on disk change (mtime check);
   * unlocked read-modify-write of both files               -> single writer lock + atomic
-    os.replace snapshots, so readers never see torn files;
+    os.replace snapshots, so readers never see torn files; an /upload_pdf append returns as soon
+    as the vectors are in HBM and the snapshot is written by a background thread (the state is
+    copied under the lock, the file I/O runs outside it; bursts of appends coalesce into one
+    write), so a 1M x 1024 index (4 GB) is not rewritten on the request path;
   * faiss label -1 mapped to metadata[-1] (last chunk)     -> -1 results are dropped, making the
     "No relevant information found" branch reachable;
   * startup re-ingest duplicates chunks                    -> idempotent by (filename, chunk_id)
@@ -40,9 +43,12 @@ class DocumentStore:
         self.index = self._new_index()
         self.metadata = []
         self._keys = set()
-        self._wlock = threading.Lock()
+        self._wlock = threading.RLock()
         self._mtimes = None
         self.recovered = None
+        self._dirty = False
+        self._persister = None
+        self._persist_error = None
 
     def _new_index(self):
         if self.index_type == "ivf":
@@ -121,10 +127,53 @@ class DocumentStore:
                     log.warning("index on disk changed but is unreadable (%s); keeping the resident copy", e)
                     self._mtimes = m
 
-    def persist(self):
-        self.index.write(self.index_path)
-        save_metadata(self.meta_path, self.metadata)
+    def _snapshot(self):
+        """(index writer, metadata copy) of the current state; caller holds _wlock."""
+        return self.index.snapshot_writer(), list(self.metadata)
+
+    def _write(self, writer, meta):
+        writer(self.index_path)
+        save_metadata(self.meta_path, meta)
         self._mtimes = self._disk_mtimes()
+
+    def persist(self):
+        """Synchronous snapshot (startup / directory ingest / shutdown)."""
+        with self._wlock:
+            writer, meta = self._snapshot()
+            self._dirty = False
+            self._write(writer, meta)
+
+    def persist_async(self):
+        """Schedule a background snapshot; appends made meanwhile are folded into the same write."""
+        with self._wlock:
+            self._dirty = True
+            if self._persister is None or not self._persister.is_alive():
+                self._persister = threading.Thread(target=self._persist_loop, name="index-snapshot", daemon=True)
+                self._persister.start()
+
+    def _persist_loop(self):
+        while True:
+            with self._wlock:
+                if not self._dirty:
+                    return
+                self._dirty = False
+                writer, meta = self._snapshot()  # host copy under the lock (consistent vectors + metadata)
+            try:
+                self._write(writer, meta)  # file I/O outside the lock: searches and appends continue
+            except Exception as e:  # keep serving from HBM; the next append retries the snapshot
+                self._persist_error = e
+                log.error("index snapshot failed: %s", e)
+
+    def flush(self):
+        """Wait until every scheduled snapshot is on disk."""
+        t = self._persister
+        if t is not None:
+            t.join()
+        with self._wlock:
+            if self._dirty:
+                writer, meta = self._snapshot()
+                self._dirty = False
+                self._write(writer, meta)
 
     # ------------------------------------------------------------------ writes
     def add(self, vectors, metadata, dedupe=True, persist=True):
@@ -144,20 +193,23 @@ class DocumentStore:
                     self.metadata.append(metadata[i])
                     self._keys.add((metadata[i]["filename"], metadata[i]["chunk_id"]))
                 if persist:
-                    self.persist()
+                    self.persist_async()
             log.info("Index updated. Total vectors: %d, Dimension: %d", self.index.ntotal, self.dim)
             return len(keep)
 
     # ------------------------------------------------------------------ reads
     def search(self, qvecs, k):
         """Batched search -> list (per query) of [(metadata, squared_l2)] ascending, -1 dropped."""
-        D, I = self.index.search(qvecs, k)
+        with self._wlock:  # consistent (index, metadata) pair: an append cannot land in between
+            D, I = self.index.search(qvecs, k)
+            meta = self.metadata
+            n = len(meta)
         out = []
         for drow, irow in zip(D.tolist(), I.tolist()):
             res = []
             for d, i in zip(drow, irow):
-                if 0 <= i < len(self.metadata):
-                    res.append((self.metadata[i], float(d)))
+                if 0 <= i < n:
+                    res.append((meta[i], float(d)))
             out.append(res)
         return out
 

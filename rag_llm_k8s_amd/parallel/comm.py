@@ -36,6 +36,7 @@ class CommError(RuntimeError):
 
 class TPComm:
     def __init__(self, group, size, rank, device, cpu_group=None, ipc_max_bytes=None, ipc_spin_limit=None):
+        """ipc_spin_limit: bound of one peer wait in microseconds, applied after the self-test."""
         self.group, self.size, self.rank, self.device = group, size, rank, device
         self.cpu_group = cpu_group
         self.ipc = None
@@ -47,9 +48,10 @@ class TPComm:
             try:
                 from .ipc_allreduce import MAX_BYTES, IPCAllReduce
 
-                ipc = IPCAllReduce(group, cpu_group, size, rank, device,
-                                   max_bytes=ipc_max_bytes or MAX_BYTES, spin_limit=ipc_spin_limit)
-                ok = 1 if ipc.self_test(cpu_group) else 0
+                ipc = IPCAllReduce(group, cpu_group, size, rank, device, max_bytes=ipc_max_bytes or MAX_BYTES)
+                ok = 1 if ipc.self_test(cpu_group) else 0  # at the default (long) peer-wait bound
+                if ok and ipc_spin_limit:
+                    ipc.set_timeout_us(ipc_spin_limit)
             except Exception as e:  # fall back to RCCL, loudly
                 log.warning("IPC all-reduce unavailable on rank %d (%s); using RCCL", rank, e)
             flag = torch.tensor([ok], dtype=torch.int32)

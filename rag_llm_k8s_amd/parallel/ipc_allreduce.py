@@ -44,7 +44,7 @@ class IPCAllReduce:
         self.max_bytes = int(L.ragk_ar_max_bytes(self.h))
         spin = SPIN_LIMIT if spin_limit is None else int(spin_limit)
         if spin > 0:
-            check(L.ragk_ar_set_spin_limit(self.h, spin), "ragk_ar_set_spin_limit")
+            self.set_timeout_us(spin)
         ep = L.ragk_ar_error_host_ptr(self.h)
         # pinned host word the kernel sets when a peer wait gives up: polled after every engine step
         self._err_word = ctypes.c_uint.from_address(ep) if ep else None
@@ -74,6 +74,11 @@ class IPCAllReduce:
         ok &= bool(torch.equal(got, torch.cat([torch.arange(64, dtype=torch.int32) + 1000 * r
                                                for r in range(self.size)])))
         return ok
+
+    def set_timeout_us(self, us: int):
+        """Bound of one peer wait inside the kernels (a rank's first launch of a kernel can lag its
+        peers by tens of ms while the code object loads: keep this well above that)."""
+        check(self.L.ragk_ar_set_spin_limit(self.h, int(us)), "ragk_ar_set_spin_limit")
 
     def fits(self, x: torch.Tensor) -> bool:
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0

@@ -112,8 +112,13 @@ class EngineLoop(threading.Thread):
                 self.step_started = None
                 self.steps += 1
                 metrics.set_gauge("kv_free", eng.bm.free_blocks())
+                metrics.set_gauge("batch", len(eng.running))
+                if self.steps % 64 == 1 and torch.cuda.is_available():
+                    metrics.set_gauge("hbm", torch.cuda.memory_allocated())
                 for s in fin:
                     metrics.inc("tokens", len(s.out))
+                    if s.t_first is not None and s.t_done is not None and len(s.out) > 1:
+                        metrics.observe("tpot", (s.t_done - s.t_first) / (len(s.out) - 1))
         except Exception as e:  # surface engine failure to every waiter
             log.exception("engine loop failed")
             self.error = e
@@ -443,3 +448,7 @@ class RagService:
     def shutdown(self):
         self.watchdog.stop_flag = True
         self.loop.stop()
+        try:
+            self.store.flush()
+        except Exception as e:
+            log.error("index snapshot on shutdown failed: %s", e)

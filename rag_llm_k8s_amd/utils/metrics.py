@@ -29,12 +29,15 @@ def registry():
         _M["request"] = prom.Histogram("rag_request_seconds", "end-to-end /generate latency", buckets=b,
                                        registry=_REG)
         _M["ttft"] = prom.Histogram("rag_ttft_seconds", "time to first generated token", buckets=b, registry=_REG)
+        _M["tpot"] = prom.Histogram("rag_tpot_seconds", "time per output token after the first (per request)",
+                                    buckets=(0.001, 0.002, 0.003, 0.005, 0.0075, 0.01, 0.015, 0.02, 0.03, 0.05, 0.1,
+                                             0.25), registry=_REG)
         _M["tokens"] = prom.Counter("rag_generated_tokens_total", "generated tokens", registry=_REG)
         _M["prompt_tokens"] = prom.Counter("rag_prompt_tokens_total", "prompt tokens", registry=_REG)
         _M["timeouts"] = prom.Counter("rag_request_timeouts_total", "requests aborted by request_timeout_s",
                                       registry=_REG)
         _M["requests"] = prom.Counter("rag_requests_total", "requests", ["route", "status"], registry=_REG)
-        _M["batch"] = prom.Gauge("rag_decode_batch", "sequences in the last decode step", registry=_REG)
+        _M["batch"] = prom.Gauge("rag_decode_batch", "running sequences after the last engine step", registry=_REG)
         _M["kv_free"] = prom.Gauge("rag_kv_free_blocks", "free KV-cache blocks", registry=_REG)
         _M["index"] = prom.Gauge("rag_index_vectors", "vectors in the index", registry=_REG)
         _M["hbm"] = prom.Gauge("rag_hbm_bytes_allocated", "HBM allocated by torch", registry=_REG)

@@ -120,6 +120,7 @@ def test_restart_is_idempotent(client, assets):
     _, svc, idx = client
     root, pdfs = assets
     n = svc.store.index.ntotal
+    svc.store.flush()  # /upload_pdf snapshots are written in the background
     svc2 = make_service(make_cfg(root, pdfs, idx))
     try:
         assert svc2.store.index.ntotal == n

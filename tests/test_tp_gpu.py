@@ -207,7 +207,7 @@ def _fault_worker(rank, port, d):
         m = LlamaModel(cfg, w, ctx.device, comm=comm, max_positions=1024)
         eng = LLMEngine(m, num_blocks=16, max_batch=2, max_model_len=512, use_graphs=False, tp_group=ctx.tp_group)
         if rank == 0:
-            store = SimpleNamespace(index=SimpleNamespace(ntotal=0))
+            store = SimpleNamespace(index=SimpleNamespace(ntotal=0), flush=lambda: None)
             svc = RagService(RagConfig(device=ctx.device), eng, None, None, store, start_threads=True)
             before = svc.health()
             t0 = time.monotonic()
