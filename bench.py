@@ -3,7 +3,7 @@
 Llama-3.1-8B (random init, bf16), all-MiniLM-L6-v2-shaped embedder, 10k-chunk FlatL2 index
 resident in HBM, retrieve top-k = 4 (all 4 go into the prompt), 150 new tokens per query.
 
-One "step" = one wave of `--concurrency` concurrent /query requests per data-parallel replica
+One "step" = one wave of `--concurrency` concurrent /query requests per engine (TP group)
 served end to end: batched query embedding -> HBM L2 top-k -> prompt build (reference template) ->
 tokenize -> continuous-batching prefill + hipGraph decode (temperature 0.7, top-p 0.9, top-k 50,
 150 tokens, EOS ignored so every request produces exactly 150 tokens) -> detokenize ->
@@ -17,6 +17,8 @@ scaling: per-GPU work fixed). `--dp` runs N independent data-parallel replicas i
 replicas behind the Service); `--tp T` picks any TP degree dividing N (tp x dp layouts).
 
 value = total generated tokens of all ranks / max-over-ranks wall time of the K timed steps.
+p50_latency_ms is the wave latency of a step; p50_latency_c1_ms the single-query latency (C=1,
+measured after the timed steps: the reference serves one query per /generate call).
 """
 import argparse
 import json
@@ -53,6 +55,8 @@ def parse():
                     help="linear-layer weights: bf16 (headline) or fp8 e4m3 (BASELINE config 5)")
     ap.add_argument("--seq-parallel", action="store_true",
                     help="TP prefill with Megatron sequence parallelism (reduce-scatter/all-gather)")
+    ap.add_argument("--c1", type=int, default=5,
+                    help="after the timed steps: this many single queries one at a time (C=1 latency; untimed)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -128,11 +132,20 @@ def main():
     torch.cuda.synchronize()
     D.barrier(ctx)
     elapsed = time.perf_counter() - t0
+    # single-request latency (the reference serves one query per /generate call): outside the timed
+    # region, same service path, one query at a time
+    c1_lat, c1_ttft = [], []
+    for i in range(a.c1):
+        q = make_queries(wl.wm, 1, seed=777000 + 1000 * ctx.dp_rank + i)
+        o = svc.generate_batch(q, params=params, seeds=[4242 + i])[0]
+        if "_latency_s" in o:
+            c1_lat.append(o["_latency_s"] * 1e3)
+            c1_ttft.append(o["_ttft_s"] * 1e3)
     elapsed_max = D.all_reduce_max(ctx, elapsed)
     my_tokens = sum(gtoks) if ctx.tp_rank == 0 else 0
     total_tokens = D.all_reduce_sum(ctx, float(my_tokens))
     allstats = D.all_gather_object(ctx, dict(lat=lat, ttft=ttft, ptoks=ptoks, eng=svc.engine.stats,
-                                             setup=wl.timings, step_ms=step_ms))
+                                             setup=wl.timings, step_ms=step_ms, c1=c1_lat, c1_ttft=c1_ttft))
     if ctx.rank == 0:
         L = [x for s in allstats for x in s["lat"]]
         T = [x for s in allstats for x in s["ttft"]]
@@ -171,6 +184,8 @@ def main():
             "p50_latency_ms": round(pct(L, 50), 1) if L else None,
             "p90_latency_ms": round(pct(L, 90), 1) if L else None,
             "ttft_p50_ms": round(pct(T, 50), 1) if T else None,
+            "p50_latency_c1_ms": round(pct(allstats[0]["c1"], 50), 1) if allstats[0]["c1"] else None,
+            "ttft_c1_p50_ms": round(pct(allstats[0]["c1_ttft"], 50), 1) if allstats[0]["c1_ttft"] else None,
             "per_gpu_tokens_per_s": round(value / ctx.world, 2),
             "engine": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in eng.items()},
             "setup_s": round(setup_s, 1),

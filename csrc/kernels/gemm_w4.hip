@@ -29,6 +29,8 @@
 // scheduler reorders it (the post-RA one bunched the DMAs at the end of segment 2).
 #include <stdlib.h>
 
+#include <utility>
+
 #include "common.h"
 using namespace ragk;
 
@@ -43,6 +45,16 @@ constexpr int W4_LDS = 2 * W_BUF;  // two K-tile buffers; the epilogue needs no 
 constexpr int WGROUP_M = 8;
 
 __device__ __forceinline__ int wswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <typename F, int... Ms>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Ms...>) {
+  (f(std::integral_constant<int, Ms>{}), ...);
+}
+// f(integral_constant<int, m>) for m = 0..N-1, every m a compile-time constant
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 // 256 rows x 128 B = 32 pieces of 8 rows; wave w stages pieces 8w..8w+7 of each operand. Per-lane
 // byte offsets of those 8 pieces (row clamped to the last valid row, chunk source-swizzled).
@@ -93,13 +105,15 @@ constexpr int W_VM16 = 0x4F70;   // vmcnt(16)
 
 // Vector-memory ops one wave issues in w4_epilogue_reg on a full tile (no row/column guard): the
 // persistent loop's wait for the next tile's first K-tile counts them as younger than its DMA.
+// bf16 outputs of full tiles use the widened store epilogue (w4_epilogue_wide: 16 B per lane),
+// fp32 outputs the 4-column one (w4_epilogue_reg).
 template <int EPI, bool OUT_F32>
 constexpr int w4_epi_vmem() {
-  if constexpr (EPI == EPI_SILU_MUL) return 32;
+  if constexpr (EPI == EPI_SILU_MUL) return 16;
   constexpr bool RES = (EPI == EPI_RESID || EPI == EPI_BIAS_RESID);
   constexpr bool BIAS = (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU ||
                          EPI == EPI_BIAS_GELU_TANH);
-  return 64 + (RES ? 64 : 0) + (BIAS ? 8 : 0);
+  return (OUT_F32 ? 64 : 32) + (RES ? 64 : 0) + (BIAS ? 8 : 0);  // bf16: 32 x 16-B stores
 }
 
 __device__ __forceinline__ void w4_store4(void* C, size_t idx, const float (&o)[4], bool f32) {
@@ -208,6 +222,112 @@ __device__ __forceinline__ void w4_epilogue_reg(const f32x4 (&acc)[8][8], int wr
   }
 }
 
+// Widened full-tile epilogue for bf16 outputs (T21 for the 16x16 layout): lane (fr, fh) of acc[i][j]
+// holds 4 consecutive columns 16j + 4fh.. of row 16i + fr, so the plain store is 64 x 8 B per lane,
+// each instruction touching 16 rows x 32 B -- an issue-bound tail of ~30k cycles per 256x256 tile in
+// which no MFMA runs. Packed to bf16 first (same fp32 epilogue math and single rounding as
+// w4_epilogue_reg), tiles j and j+1 are paired with v_permlane16_swap (odd 16-lane rows of the
+// first operand <-> even rows of the second): afterwards lanes fh = 0 / 2 hold columns 0-7 / 8-15
+// of tile j and lanes fh = 1 / 3 those of tile j+1, so each pair is ONE 16-byte store per lane,
+// half the store instructions for the same bytes.
+__device__ __forceinline__ void w4_swap_store(bf16_t* row, int col_j, int fh, unsigned (&x)[2], unsigned (&y)[2]) {
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    auto r = __builtin_amdgcn_permlane16_swap(x[d], y[d], false, false);
+    x[d] = r[0];
+    y[d] = r[1];
+  }
+  const int col = col_j + 16 * (fh & 1) + 8 * (fh >> 1);
+  *reinterpret_cast<uint4*>(row + col) = make_uint4(x[0], x[1], y[0], y[1]);
+}
+
+template <int EPI>
+__device__ __forceinline__ void w4_epilogue_wide(const f32x4 (&acc)[8][8], int wr, int wc, int fr, int fh, int m0,
+                                                 int n0, void* C, int ldc, const bf16_t* __restrict__ bias,
+                                                 const bf16_t* resid, int ldr) {
+  const int row0 = m0 + wr * 128 + fr;
+  bf16_t* Cb = reinterpret_cast<bf16_t*>(C);
+  if constexpr (EPI == EPI_SILU_MUL) {
+    const int colb = (n0 >> 1) + wc * 64;  // output tiles j = 0..3: gate acc[i][j], up acc[i][j + 4]
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bf16_t* row = Cb + (size_t)(row0 + 16 * i) * ldc;
+#pragma unroll
+      for (int jp = 0; jp < 4; jp += 2) {
+        unsigned x[2], y[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float a[4], b[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            a[r] = silu(acc[i][jp][r]) * acc[i][jp + 4][r];
+            b[r] = silu(acc[i][jp + 1][r]) * acc[i][jp + 5][r];
+          }
+          x[h] = (unsigned)f2bf(a[2 * h]) | ((unsigned)f2bf(a[2 * h + 1]) << 16);
+          y[h] = (unsigned)f2bf(b[2 * h]) | ((unsigned)f2bf(b[2 * h + 1]) << 16);
+        }
+        w4_swap_store(row, colb + 16 * jp, fh, x, y);
+      }
+    }
+  } else {
+    constexpr bool RES = (EPI == EPI_RESID || EPI == EPI_BIAS_RESID);
+    constexpr bool BIAS = (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU ||
+                           EPI == EPI_BIAS_GELU_TANH);
+    const int col0 = n0 + wc * 128 + 4 * fh;  // this lane's pre-swap columns in tile j: col0 + 16j
+    uint2 bv[BIAS ? 8 : 1];
+    if constexpr (BIAS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bv[j] = *reinterpret_cast<const uint2*>(bias + col0 + 16 * j);
+    }
+    uint2 rv[RES ? 64 : 1];
+    if constexpr (RES) {  // whole residual tile of this lane in flight before the first use
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          rv[8 * i + j] = *reinterpret_cast<const uint2*>(resid + (size_t)(row0 + 16 * i) * ldr + col0 + 16 * j);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      bf16_t* row = Cb + (size_t)(row0 + 16 * i) * ldc;
+#pragma unroll
+      for (int jp = 0; jp < 8; jp += 2) {
+        unsigned pk[2][2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int j = jp + q;
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r];
+          if constexpr (BIAS) {
+            float b[4];
+            unpack4(bv[j], b);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] += b[r];
+          }
+          if constexpr (RES) {
+            float rr[4];
+            unpack4(rv[8 * i + j], rr);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] += rr[r];
+          }
+          if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_GELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = gelu_erf(o[r]);
+          }
+          if constexpr (EPI == EPI_BIAS_GELU_TANH) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = gelu_tanh(o[r]);
+          }
+          pk[q][0] = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
+          pk[q][1] = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+        }
+        w4_swap_store(row, n0 + wc * 128 + 16 * jp, fh, pk[0], pk[1]);
+      }
+    }
+  }
+}
+
 // MFMA #m (= 8i + j) of a sub-step. Inline asm with the accumulator tied in an AGPR ("+a"): with the
 // builtin, hipcc picks dst != srcC for the loop-carried accumulators and adds 84-500 v_accvgpr copies
 // per K-tile. volatile + "memory" keep the statement in source order relative to the LDS reads and
@@ -255,6 +375,35 @@ __device__ __forceinline__ void w4_read_frag(const char* buf, int s, int q, int 
 // the 16 DMAs evenly through segment 2, the 16 F0(t+1) reads evenly through segment 3. The split
 // was set from the stamp build's cycle anatomy (tools/gemm_stamps.py).
 constexpr int W4_S1 = 32, W4_S3 = 16;
+constexpr int W4_SCHED = 0;  // production schedule: 0 = w4_iter (S1/S3 split), 2 = w4_iter2
+#ifndef RAGK_W4_WIDE_EPI
+#define RAGK_W4_WIDE_EPI 1
+#endif
+constexpr bool W4_WIDE_EPI = RAGK_W4_WIDE_EPI;  // widened 16-B store epilogue for bf16 outputs
+
+// j-major variants (SCHED 3): MFMA #m of a sub-step is acc[m & 7][m >> 3], so srcA (the weight
+// fragment b[j]) stays the same register quad for 8 consecutive MFMAs (as in hipBLASLt's loop);
+// reads come in consumption order b[0], a[0..7], b[1..7].
+__device__ __forceinline__ void w4_mfma_jm(f32x4 (&acc)[8][8], const bf16x8 (&a)[8], const bf16x8 (&b)[8], int m) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %2, %1, %0"
+               : "+a"(acc[m & 7][m >> 3])
+               : "v"(a[m & 7]), "v"(b[m >> 3])
+               : "memory");
+}
+
+__device__ __forceinline__ void w4_read_frag_jm(const char* buf, int s, int q, int wr, int wc, int fr, int fh,
+                                                bf16x8 (&a)[8], bf16x8 (&b)[8]) {
+  const int c = 4 * s + fh;
+  if (q == 0 || q > 8) {
+    const int j = q == 0 ? 0 : q - 8;
+    const int R = wc * 128 + 16 * j + fr;
+    b[j] = *reinterpret_cast<const bf16x8*>(buf + W_TILE_A + R * 128 + 16 * wswz(R, c));
+  } else {
+    const int i = q - 1;
+    const int R = wr * 128 + 16 * i + fr;
+    a[i] = *reinterpret_cast<const bf16x8*>(buf + R * 128 + 16 * wswz(R, c));
+  }
+}
 
 __device__ __forceinline__ void w4_mfma_m(f32x4 (&acc)[8][8], const bf16x8 (&a0)[8], const bf16x8 (&b0)[8],
                                           const bf16x8 (&a1)[8], const bf16x8 (&b1)[8], int m) {
@@ -380,6 +529,77 @@ __device__ __forceinline__ void w4_iter1(char* smem, int t, i32x4 srd_a, i32x4 s
   }
 }
 
+// Spread two-barrier iteration (SCHED 2), the read/DMA placement of hipBLASLt's gfx950 256x256x64
+// direct-to-LDS kernel (studied from its disassembly: LDS fragment reads ~one per two MFMAs and
+// issued a full sub-step ahead of their use, DMAs one per few MFMAs): the old schedule (w4_iter)
+// bunched its 32 fragment reads into 32 of the 128 MFMAs (one read per 16-cycle MFMA gap: the LDS
+// saturates with 4 waves) and issued F0(t+1) right before the MFMAs that consume it.
+//   m 0..BA-1 : 16 reads of F1(t) (buffer t&1), spread          [F0 MFMAs]
+//   m = BA    : lgkmcnt(0) + barrier A: every wave holds F1(t), buffer t&1 is free
+//   m BA..    : 16 DMAs of tile t+2 -> buffer t&1, one per DS MFMAs
+//   m = 64    : vmcnt(#DMAs issued so far) (= tile t+1 landed) + barrier B
+//   m 64..95  : 16 reads of F0(t+1) (buffer (t+1)&1), one per 2 MFMAs   [F1 MFMAs]
+//   m 96..127 : MFMA only (the F0(t+1) reads land 32+ MFMAs before their use)
+template <bool STAGE, bool READ, bool STAMP, int BA, int DS, bool JM = false, int RW = 2>
+__device__ __forceinline__ void w4_iter2(char* smem, int t, i32x4 srd_a, i32x4 srd_b, const int (&off_a)[8],
+                                         const int (&off_b)[8], int wid, int wr, int wc, int fr, int fh,
+                                         f32x4 (&acc)[8][8], bf16x8 (&a0)[8], bf16x8 (&b0)[8], bf16x8 (&a1)[8],
+                                         bf16x8 (&b1)[8], unsigned long long (&stp)[5]) {
+  static_assert(BA >= 16 && BA <= 64 && BA % 16 == 0, "barrier A position");
+  static_assert(BA + 15 * DS < 128, "DMA window");
+  constexpr int RSA = BA / 16;                         // MFMAs per F1(t) read
+  constexpr int NB = (64 - BA + DS - 1) / DS;         // DMAs issued before barrier B
+  constexpr int VB = NB > 15 ? 15 : NB;
+  char* buf = smem + (t & 1) * W_BUF;
+  const char* nbuf = smem + ((t + 1) & 1) * W_BUF;
+  unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+  if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
+  // compile-time m (a #pragma unroll over this body is not always honoured: a runtime m would put
+  // the accumulator array in scratch)
+  static_for<128>([&](auto mc) __attribute__((always_inline)) {
+    constexpr int m = decltype(mc)::value;
+    if constexpr (m == BA) {
+      if constexpr (STAMP) t1 = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_s_waitcnt(W_LGKM0);  // F1(t) in registers
+      w4_barrier();                         // every wave: buffer t&1 no longer read
+      if constexpr (STAMP) t2 = __builtin_amdgcn_s_memtime();
+    }
+    if constexpr (m == 64) {
+      if constexpr (STAMP) t3 = __builtin_amdgcn_s_memtime();
+      if constexpr (STAGE) __builtin_amdgcn_s_waitcnt((VB & 15) | (0x7 << 4) | (0xF << 8));  // vmcnt(VB)
+      else __builtin_amdgcn_s_waitcnt(W_VM0);
+      w4_barrier();  // tile t+1 landed for every wave
+      if constexpr (STAMP) {
+        const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+        stp[0] += t1 - t0;
+        stp[1] += t2 - t1;
+        stp[2] += t3 - t2;
+        stp[3] += t4 - t3;
+      }
+    }
+    if constexpr (m < BA && m % RSA == 0) {
+      if constexpr (JM) w4_read_frag_jm(buf, 1, m / RSA, wr, wc, fr, fh, a1, b1);
+      else w4_read_frag(buf, 1, m / RSA, wr, wc, fr, fh, a1, b1);
+    }
+    if constexpr (STAGE && m >= BA && (m - BA) % DS == 0 && (m - BA) / DS < 16) {
+      constexpr int q = (m - BA) / DS;
+      if constexpr (q < 8) blds16(srd_a, off_a[q], (t + 2) * WBK * 2, buf + (wid * 8 + q) * 1024);
+      else blds16(srd_b, off_b[q - 8], (t + 2) * WBK * 2, buf + W_TILE_A + (wid * 8 + q - 8) * 1024);
+    }
+    if constexpr (READ && m >= 64 && m < 64 + 16 * RW && (m - 64) % RW == 0) {
+      if constexpr (JM) w4_read_frag_jm(nbuf, 0, (m - 64) / RW, wr, wc, fr, fh, a0, b0);
+      else w4_read_frag(nbuf, 0, (m - 64) / RW, wr, wc, fr, fh, a0, b0);
+    }
+    if constexpr (JM) {
+      if constexpr (m < 64) w4_mfma_jm(acc, a0, b0, m);
+      else w4_mfma_jm(acc, a1, b1, m - 64);
+    } else {
+      w4_mfma_m(acc, a0, b0, a1, b1, m);
+    }
+  });
+  if constexpr (STAMP) stp[4] += __builtin_amdgcn_s_memtime() - t0;
+}
+
 // Output tile `tile` (of nwg) -> origin. Tiles are numbered so that the 8 XCDs each own a contiguous
 // range (xcd_remap; a persistent block keeps its XCD since the grid is a multiple of 8), grouped
 // WGROUP_M M-tiles deep for L2 reuse of the weight tiles.
@@ -404,7 +624,8 @@ __device__ __forceinline__ void w4_zero(f32x4 (&acc)[8][8]) {
 // one-tile-per-block launch). Between two tiles, LDS is free as soon as the K-loop's last barrier has
 // passed, so the next tile's first two K-tiles are DMA'd BEFORE this tile's epilogue runs: the DMA
 // latency that a fresh block pays in its prologue hides behind the epilogue's stores.
-template <int EPI, bool OUT_F32, bool STAMP = false, int S1 = W4_S1, int S3 = W4_S3>
+template <int EPI, bool OUT_F32, bool STAMP = false, int S1 = W4_S1, int S3 = W4_S3, int SCHED = W4_SCHED,
+          bool WIDE = W4_WIDE_EPI>
 __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __restrict__ A, int lda,
                                                                 const bf16_t* __restrict__ B, int ldb, void* C,
                                                                 int ldc, const bf16_t* __restrict__ bias,
@@ -444,7 +665,10 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
   // vector-memory ops issued after the current tile's K-tile-0 DMA: its 16 K-tile-1 DMAs, plus the
   // previous tile's full-tile epilogue (0 = none, or a guarded epilogue that drained itself)
   int younger_epi = 0, done = 0;
+  unsigned long long tl_loop = 0, tl_epi = 0;  // STAMP: per-tile K-loop / epilogue cycles (sums)
   for (;;) {
+    unsigned long long tt0 = 0;
+    if constexpr (STAMP) tt0 = __builtin_amdgcn_s_memtime();
     w4_zero(acc);
     w4_pin_acc(acc);
     if (nk == 1) {
@@ -452,7 +676,7 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
     } else if (younger_epi == 0) {
       __builtin_amdgcn_s_waitcnt(W_VM16);
     } else {
-      constexpr int E = 16 + w4_epi_vmem<EPI, OUT_F32>();
+      constexpr int E = 16 + w4_epi_vmem<EPI, OUT_F32 || !WIDE>() + ((!OUT_F32 && !WIDE && EPI == EPI_SILU_MUL) ? 16 : 0);
       constexpr int V = E > 63 ? 63 : E;
       __builtin_amdgcn_s_waitcnt((V & 15) | (((V >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
     }
@@ -462,7 +686,21 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
     __builtin_amdgcn_sched_barrier(0);
 
     int t = 0;
-    if constexpr (S3 == 0) {
+    if constexpr (SCHED >= 2) {  // S1 = barrier-A position, S3 = MFMAs per DMA
+      constexpr bool JM = SCHED == 3;
+      constexpr int RW = SCHED == 4 ? 4 : 2;  // MFMAs per F0(t+1) read
+      for (; t + 2 < nk; ++t)
+        w4_iter2<true, true, STAMP, S1, S3, JM, RW>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0,
+                                            a1, b1, stp);
+      if (t + 1 < nk) {
+        w4_iter2<false, true, false, S1, S3, JM, RW>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0,
+                                             a1, b1, stp);
+        ++t;
+      }
+      // last K-tile: barrier A retires every wave's last reads, barrier B follows it
+      w4_iter2<false, false, false, S1, S3, JM, RW>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0,
+                                            a1, b1, stp);
+    } else if constexpr (S3 == 0) {
       for (; t + 2 < nk; ++t)
         w4_iter1<true, true, STAMP, S1>(smem, t, srd_a, srd_b, off_a, off_b, wid, wr, wc, fr, fh, acc, a0, b0, a1,
                                         b1, stp);
@@ -491,6 +729,8 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
                                            a1, b1, stp);
     }
 
+    unsigned long long tt1 = 0;
+    if constexpr (STAMP) tt1 = __builtin_amdgcn_s_memtime();
     const int next = tile + (int)gridDim.x;
     if (next < nwg) {
       int nm0, nn0;
@@ -510,7 +750,10 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
     }
     w4_pin_acc(acc);
     if (m0 + WBM <= M && n0 + WBN <= N) {
-      w4_epilogue_reg<EPI, OUT_F32, true>(acc, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr, M, N);
+      if constexpr (OUT_F32 || !WIDE)
+        w4_epilogue_reg<EPI, OUT_F32, true>(acc, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr, M, N);
+      else
+        w4_epilogue_wide<EPI>(acc, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr);
       younger_epi = 1;
     } else {
       w4_epilogue_reg<EPI, OUT_F32, false>(acc, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr, M, N);
@@ -518,16 +761,23 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
       younger_epi = 0;
     }
     ++done;
+    if constexpr (STAMP) {
+      const unsigned long long tt2 = __builtin_amdgcn_s_memtime();
+      tl_loop += tt1 - tt0;
+      tl_epi += tt2 - tt1;
+    }
     if (next >= nwg) break;
     tile = next;
     w4_origin(tile, nwg, tiles_m, tiles_n, m0, n0);
   }
   if constexpr (STAMP) {
     if (lane == 0) {
-      unsigned long long* d = dbg + ((size_t)blockIdx.x * 4 + wid) * 6;
+      unsigned long long* d = dbg + ((size_t)blockIdx.x * 4 + wid) * 8;
 #pragma unroll
       for (int i = 0; i < 5; ++i) d[i] = stp[i];
       d[5] = (unsigned long long)done * (unsigned long long)(nk - 2);  // steady-state iterations
+      d[6] = tl_loop;  // per tile: zero + prologue wait + K-loop
+      d[7] = tl_epi;   // per tile: next tile's staging + epilogue
     }
   }
 }
@@ -602,13 +852,13 @@ RAGK_API int ragk_gemm_w4(const void* A, int lda, const void* B, int ldb, void* 
 
 // Diagnostic / tuning builds of the EPI_NONE kernel (tools/gemm_stamps.py). variant selects the
 // segment split (S1, S3); stamp != 0 adds s_memtime stamps around the K-loop segments, dbg:
-// [nwg][4 waves][6] u64 = seg1, barrier1, seg2, barrier2, whole iteration (sums over the
-// steady-state iterations), iteration count.
-template <bool STAMP, int S1, int S3>
+// [nwg][4 waves][8] u64 = seg1, barrier1, seg2, barrier2, whole iteration (sums over the
+// steady-state iterations), iteration count, per-tile K-loop cycles, per-tile epilogue cycles (sums).
+template <bool STAMP, int S1, int S3, int SCHED = 0, bool WIDE = W4_WIDE_EPI>
 int launch_w4_diag(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int N, int K,
                    unsigned long long* dbg, hipStream_t st) {
   const int nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
-  hipLaunchKernelGGL((gemm_w4_kernel<EPI_NONE, false, STAMP, S1, S3>), dim3(w4_grid(nwg)), dim3(W4_THREADS), 0, st,
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI_NONE, false, STAMP, S1, S3, SCHED, WIDE>), dim3(w4_grid(nwg)), dim3(W4_THREADS), 0, st,
                      (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, nullptr, nullptr, 0, M, N, K, dbg);
   return (int)hipGetLastError();
 }
@@ -622,6 +872,10 @@ RAGK_API int ragk_gemm_w4_diag(int variant, int stamp, const void* A, int lda, c
   case V:                                                                                                    \
     return stamp ? launch_w4_diag<true, S1, S3>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)                    \
                  : launch_w4_diag<false, S1, S3>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);
+#define RAGK_W4D2(V, BA, DS)                                                                               \
+  case V:                                                                                                  \
+    return stamp ? launch_w4_diag<true, BA, DS, 2>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)                \
+                 : launch_w4_diag<false, BA, DS, 2>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);
   switch (variant) {
     RAGK_W4D(0, 32, 16)
     RAGK_W4D(1, 24, 24)
@@ -632,8 +886,38 @@ RAGK_API int ragk_gemm_w4_diag(int variant, int stamp, const void* A, int lda, c
     RAGK_W4D(6, 32, 0)
     RAGK_W4D(7, 24, 0)
     RAGK_W4D(8, 40, 0)
+    RAGK_W4D2(9, 32, 4)
+    RAGK_W4D2(10, 32, 5)
+    RAGK_W4D2(11, 32, 6)
+    RAGK_W4D2(12, 48, 4)
+    RAGK_W4D2(13, 16, 6)
+    case 14:  // production schedule with the 8-byte-store epilogue (A/B of the widened one)
+      return stamp ? launch_w4_diag<true, 32, 16, 0, false>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)
+                   : launch_w4_diag<false, 32, 16, 0, false>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);
+    case 16:  // w4_iter2 (32, 6), j-major MFMA order
+      return stamp ? launch_w4_diag<true, 32, 6, 3, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)
+                   : launch_w4_diag<false, 32, 6, 3, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);
+    case 17:  // w4_iter2 (32, 4), j-major MFMA order
+      return stamp ? launch_w4_diag<true, 32, 4, 3, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)
+                   : launch_w4_diag<false, 32, 4, 3, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);
+    case 18:
+      return stamp ? launch_w4_diag<true, 32, 6, 4, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)
+                   : launch_w4_diag<false, 32, 6, 4, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);
+    case 19:
+      return stamp ? launch_w4_diag<true, 32, 4, 4, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)
+                   : launch_w4_diag<false, 32, 4, 4, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);
+    case 20:
+      return stamp ? launch_w4_diag<true, 16, 7, 4, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)
+                   : launch_w4_diag<false, 16, 7, 4, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);
+    case 21:
+      return stamp ? launch_w4_diag<true, 48, 5, 4, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)
+                   : launch_w4_diag<false, 48, 5, 4, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);
+    case 15:  // w4_iter2 (32, 6) + widened epilogue
+      return stamp ? launch_w4_diag<true, 32, 6, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)
+                   : launch_w4_diag<false, 32, 6, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);
     default:
       return (int)hipErrorInvalidValue;
   }
 #undef RAGK_W4D
+#undef RAGK_W4D2
 }

@@ -65,6 +65,7 @@ class RagConfig:
     step_timeout_s: float = 300.0  # watchdog: an engine step (incl. its collectives) longer than this = hung
     watchdog_exit: bool = True  # hung engine -> dump stacks and exit so k8s restarts the pod
     index_recovery: str = "rebuild"  # rebuild (quarantine unreadable index, re-ingest PDF_DIR) | fail
+    ignore_eos: bool = False  # benchmarks only: every request generates exactly max_new_tokens
     extra: dict = field(default_factory=dict)
 
     @classmethod
@@ -84,7 +85,7 @@ class RagConfig:
             "USE_CUDA_GRAPHS": ("use_cuda_graphs", bool), "LOG_LEVEL": ("log_level", str),
             "TRUNCATE_PROMPT": ("truncate_prompt", str), "REQUEST_TIMEOUT_S": ("request_timeout_s", float),
             "STEP_TIMEOUT_S": ("step_timeout_s", float), "WATCHDOG_EXIT": ("watchdog_exit", bool),
-            "INDEX_RECOVERY": ("index_recovery", str),
+            "INDEX_RECOVERY": ("index_recovery", str), "IGNORE_EOS": ("ignore_eos", bool),
         }
         for env, (attr, cast) in m.items():
             setattr(c, attr, _env(env, getattr(c, attr), cast))

@@ -132,6 +132,9 @@ class LLMEngine:
         # freed only after that step has completed. Under TP every rank samples the same token from
         # the same gathered candidates, so all ranks take the same decisions one step late.
         self.async_decode = self.use_graphs and os.environ.get("RAGK_ASYNC_DECODE", "1") == "1"
+        # Mixed prefill + decode steps (chunked prefill): a step that admits prompt tokens
+        # also advances every decoding sequence by one token through the same forward.
+        self.mixed_steps = os.environ.get("RAGK_MIXED_STEPS", "1") == "1"
         self._inflight = None  # dict(seqs, rows, entry, event, host_out, n)
         self._free_after = []  # seq ids whose blocks are freed once the in-flight step has completed
         self._out_pins = [torch.empty(max(1, max_batch), dtype=torch.int32, pin_memory=self.is_cuda)
@@ -168,10 +171,11 @@ class LLMEngine:
         return bool(self.waiting) or bool(self.running) or self._inflight is not None
 
     # ------------------------------------------------------------------ scheduling
-    def _admit(self):
-        """Pick (seq, start, n) prefill chunks for this step."""
+    def _admit(self, reserve=0):
+        """Pick (seq, start, n) prefill chunks for this step (`reserve` tokens of the budget are taken
+        by decode rows riding along in a mixed step)."""
         chunks = []
-        budget = self.max_prefill_tokens
+        budget = self.max_prefill_tokens - reserve
         # continue partially-prefilled running sequences first
         for s in self.running:
             if s.computed < len(s.prompt) and budget > 0:
@@ -236,10 +240,18 @@ class LLMEngine:
             fin += self._drain()
             self._apply_aborts()
         self._fault_hooks()
-        chunks = self._admit()
+        n_ready = sum(1 for s in self.running if s.computed >= len(s.prompt)) if self.mixed_steps else 0
+        chunks = self._admit(reserve=n_ready)
         if chunks:
             fin += self._drain()
-            return fin + self._prefill(chunks)
+            rows = []
+            if self.mixed_steps:
+                # mixed step: every running sequence past its prompt rides along as a 1-token chunk (its
+                # last sampled token), so a long prefill does not stall the decoding requests
+                inchunk = set(id(c[0]) for c in chunks)
+                rows = [(s, s.length - 1, 1) for s in self.running
+                        if id(s) not in inchunk and s.computed >= len(s.prompt) and s.computed == s.length - 1]
+            return fin + self._prefill(chunks + rows, n_decode=len(rows))
         ready = [s for s in self.running if s.computed >= len(s.prompt)]
         if ready and self._needs_full_vocab(ready):
             fin += self._drain()
@@ -449,7 +461,10 @@ class LLMEngine:
         for ci, (s, start, n) in enumerate(chunks):
             table = np.asarray(self.bm.table(s.id), dtype=np.int32)
             p = np.arange(start, start + n, dtype=np.int32)
-            ids.append(s.prompt_np[start:start + n])
+            if start + n <= len(s.prompt):
+                ids.append(s.prompt_np[start:start + n])
+            else:  # a decode row of a mixed step: the generated tokens past the prompt
+                ids.append(np.asarray([s.token_at(i) for i in range(start, start + n)], dtype=np.int32))
             pos.append(p)
             slots.append(table[p // BLOCK] * BLOCK + p % BLOCK)
             cu.append(cu[-1] + n)
@@ -457,7 +472,7 @@ class LLMEngine:
             qlens.append(n)
             nb = min(len(table), self.max_blocks)
             bts[ci, :nb] = table[:nb]
-            if start + n == len(s.prompt):
+            if start + n == len(s.prompt) or (start + n == s.length and start >= len(s.prompt)):
                 out_rows.append(cu[-1] - 1)
                 out_seqs.append(s)
         from ..ops.native import build_prefill_tiles
@@ -491,7 +506,7 @@ class LLMEngine:
             out.append(cur)
         return out
 
-    def _prefill(self, chunks):
+    def _prefill(self, chunks, n_decode=0):
         t0 = time.perf_counter()
         m = self.model
         ntok = sum(n for _, _, n in chunks)
@@ -527,7 +542,9 @@ class LLMEngine:
                 self._finish(s, r)
                 finished.append(s)
         self.stats["prefill_steps"] += 1
-        self.stats["prefill_tokens"] += ntok
+        self.stats["prefill_tokens"] += ntok - n_decode
+        if n_decode:
+            self.stats["mixed_decode_tokens"] = self.stats.get("mixed_decode_tokens", 0) + n_decode
         self.stats["prefill_s"] += time.perf_counter() - t0
         return finished
 

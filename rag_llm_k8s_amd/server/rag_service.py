@@ -218,7 +218,8 @@ class RagService:
         eos = gen.get("eos_token_id")
         stop = tuple(eos) if isinstance(eos, list) else ((eos,) if eos is not None else ())
         self.params = SamplingParams(max_new_tokens=cfg.max_new_tokens, temperature=cfg.temperature,
-                                     top_p=cfg.top_p, top_k=cfg.top_k, do_sample=do_sample, stop_token_ids=stop)
+                                     top_p=cfg.top_p, top_k=cfg.top_k, do_sample=do_sample, stop_token_ids=stop,
+                                     ignore_eos=bool(getattr(cfg, "ignore_eos", False)))
         self.loop = EngineLoop(llm_engine, control=control)
         self.watchdog = Watchdog(self.loop, cfg.step_timeout_s, cfg.watchdog_exit)
         self.batcher = MicroBatcher(self._retrieve_batch)

@@ -95,7 +95,7 @@ class Workload:
 def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=1000, retrieve_k=4, context_k=4,
                    max_new_tokens=150, max_batch=32, max_model_len=8192, max_prefill_tokens=32768, device="cuda",
                    ctx=None, tp_comm=None, seed=0, use_graphs=True, index_type="flat", kv_blocks=None,
-                   word_vocab=400000, dtype="bf16", index_vectors=0):
+                   word_vocab=400000, dtype="bf16", index_vectors=0, start_threads=False, ignore_eos=False):
     from ..engine.encoder_engine import EmbeddingEngine
     from ..engine.llm_engine import LLMEngine
     from ..index.store import DocumentStore
@@ -140,7 +140,7 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     t0 = time.time()
     cfg = RagConfig(device=device, retrieve_k=retrieve_k, context_k=context_k, max_new_tokens=max_new_tokens,
                     max_batch=max_batch, max_model_len=max_model_len, index_path="/tmp/ragk_bench_index",
-                    index_type=index_type, seed=seed)
+                    index_type=index_type, seed=seed, max_prefill_tokens=max_prefill_tokens, ignore_eos=ignore_eos)
     store = DocumentStore(cfg.index_path, emb.dim, device=device, index_type=index_type)
     vecs = emb.embed(chunks)
     meta = [{"filename": "synthetic_%05d.pdf" % (i // 20), "chunk_id": i % 20, "text": c}
@@ -163,7 +163,8 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     t["ingest_s"] = time.time() - t0
     svc = RagService(cfg, engine, llm_tok, emb, store, gen_config={"do_sample": True,
                                                                    "eos_token_id": lcfg.eos_token_id},
-                     start_threads=False)
+                     start_threads=start_threads)
+    svc.ready = True
     return Workload(svc, wm, llm_tok, t, n_chunks)
 
 

@@ -154,3 +154,31 @@ def test_split_k_decode_path_matches_plain_decode(tiny):
         outs.append(eng.generate(prompts, params))
         assert bool(calls) == part
     assert outs[0] == outs[1]
+
+
+def test_mixed_prefill_decode_steps_match_separate_steps(tiny):
+    """Mixed steps (decoding sequences ride along in a prefill step as 1-token chunks) produce the same
+    tokens as separate prefill / decode steps, for requests that arrive while others decode; a mixed
+    step carries both kinds of rows."""
+    cfg, hf, sd = tiny
+    w = LlamaWeights.from_state_dict(cfg, sd, "cpu")
+    torch.manual_seed(9)
+    prompts = [torch.randint(3, cfg.vocab_size, (n,)).tolist() for n in (30, 45, 12, 60)]
+    params = [SamplingParams(max_new_tokens=8, do_sample=False, ignore_eos=True),
+              SamplingParams(max_new_tokens=8, temperature=0.8, top_p=0.9, top_k=20, ignore_eos=True)]
+    outs, mixed_rows = {}, {}
+    for mixed in (False, True):
+        model = LlamaModel(cfg, w, "cpu", max_positions=512)
+        eng = LLMEngine(model, num_blocks=64, max_batch=4, max_prefill_tokens=32, max_model_len=512,
+                        use_graphs=False)
+        eng.mixed_steps = mixed
+        seqs = []
+        for i, pr in enumerate(prompts):  # staggered arrivals: one new prompt every 3 steps
+            seqs.append(eng.add_request(pr, params[i % 2], seed=100 + i))
+            for _ in range(3):
+                eng.step()
+        eng.run_until_done()
+        outs[mixed] = [s.out for s in seqs]
+        mixed_rows[mixed] = eng.stats.get("mixed_decode_tokens", 0)
+    assert outs[True] == outs[False]
+    assert mixed_rows[True] > 0 and mixed_rows[False] == 0

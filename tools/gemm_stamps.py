@@ -36,7 +36,7 @@ for (M, N, K) in [(16384, 4096, 4096), (16384, 6144, 4096), (16384, 4096, 14336)
     out = torch.empty(M, N, device="cuda").bfloat16()
     ref = x.float() @ w.float().t()
     nwg = (M // 256) * (N // 256)
-    dbg = torch.zeros(nwg * 4 * 6, dtype=torch.int64, device="cuda")
+    dbg = torch.zeros(nwg * 4 * 8, dtype=torch.int64, device="cuda")
     ts = {v: [] for v in VARIANTS}
     for v in VARIANTS:
         run(v, 0, x, w, out, M, N, K, None)
@@ -51,7 +51,7 @@ for (M, N, K) in [(16384, 4096, 4096), (16384, 6144, 4096), (16384, 4096, 14336)
         t = sorted(ts[v])[len(ts[v]) // 2]
         run(v, 1, x, w, out, M, N, K, dbg)
         torch.cuda.synchronize()
-        d = dbg.view(nwg, 4, 6).double().cpu()
+        d = dbg.view(nwg, 4, 8).double().cpu()
         d = d[d[:, 0, 5] > 0]  # persistent grid: only blocks that ran
         it = d[:, :, 5]
         per = (d[:, :, :5] / it.unsqueeze(-1)).reshape(-1, 5).median(0).values.tolist()
