@@ -799,14 +799,31 @@ static int w4_grid(int nwg) {
   return (g_w4_grid == 0 || g_w4_grid >= nwg) ? nwg : g_w4_grid;
 }
 
+// K-loop schedule by K (tools/gemm_sched_ab.py, profiles/gemm_sched_ab_r2.txt): long K (the down
+// projection, K = 14336) runs the spread schedule w4_iter2 (F1 reads in the first 16 MFMAs, one DMA
+// per 7 MFMAs, F0(t+1) reads one per 4 MFMAs; -2.6 %), K = 4096 the S1/S3 split (within 1 %).
+static int g_w4_sched_k = -1;
+static int w4_sched_min_k() {
+  if (g_w4_sched_k < 0) {
+    const char* e = getenv("RAGK_W4_SPREAD_MIN_K");
+    g_w4_sched_k = e ? atoi(e) : 8192;
+  }
+  return g_w4_sched_k;
+}
+
 template <int EPI, bool F32>
 int launch_w4(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias, const void* resid,
               int ldr, int M, int N, int K, hipStream_t st) {
   const int nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
   const int grid = w4_grid(nwg);
-  hipLaunchKernelGGL((gemm_w4_kernel<EPI, F32>), dim3(grid), dim3(W4_THREADS), 0, st, (const bf16_t*)A, lda,
-                     (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K,
-                     nullptr);
+  if (K >= w4_sched_min_k())
+    hipLaunchKernelGGL((gemm_w4_kernel<EPI, F32, false, 16, 7, 4>), dim3(grid), dim3(W4_THREADS), 0, st,
+                       (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid,
+                       ldr, M, N, K, nullptr);
+  else
+    hipLaunchKernelGGL((gemm_w4_kernel<EPI, F32>), dim3(grid), dim3(W4_THREADS), 0, st, (const bf16_t*)A, lda,
+                       (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K,
+                       nullptr);
   return (int)hipGetLastError();
 }
 

@@ -16,6 +16,10 @@ if [ "$STEP" = "all" ] || [ "$STEP" = "suite" ]; then
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider --deselect tests/test_tp_gpu.py > gpurun_out/pytest_gpu.log 2>&1
 echo "suite rc=$?"; tail -15 gpurun_out/pytest_gpu.log
 fi
+if [ "$STEP" = "all" ] || [ "$STEP" = "serve" ]; then
+timeout -k 10 600 python -u tools/bench_serve.py --json-out gpurun_out/serve.json ${SERVE_ARGS:-} > gpurun_out/serve.log 2>&1
+echo "serve rc=$?"; grep -E "^C=1|^Poisson" gpurun_out/serve.log
+fi
 if [ "$STEP" = "all" ] || [ "$STEP" = "bench" ]; then
 timeout -k 10 600 python -u bench.py --steps ${BSTEPS:-3} --warmup 1 --json-out gpurun_out/bench.json > gpurun_out/bench.log 2>&1 &&
 tail -2 gpurun_out/bench.log &&
