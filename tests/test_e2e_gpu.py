@@ -23,16 +23,50 @@ def tiny_llama():
     return cfg, llama_state_dict(cfg, seed=3, std=0.05)
 
 
+def _oracle_logits(cfg, sd, ids):
+    """fp32-accumulating CPU oracle: logits [T, V] of every position of `ids` (one prefill)."""
+    from rag_llm_k8s_amd.models.llama import StepInput
+    from rag_llm_k8s_amd.ops.backend import AttnMeta
+
+    eng = _engine(cfg, sd, "cpu", graphs=False)
+    n = len(ids)
+    eng.bm.ensure(99, n + 1)
+    tbl = eng.bm.table(99)
+    slots = torch.tensor([tbl[q // 64] * 64 + q % 64 for q in range(n)], dtype=torch.int32)
+    bt = torch.tensor([tbl + [0] * (eng.max_blocks - len(tbl))], dtype=torch.int32)
+    meta = AttnMeta("prefill", torch.tensor([n], dtype=torch.int32), bt, cu_q=torch.tensor([0, n], dtype=torch.int32),
+                    host_kv_lens=[n])
+    inp = StepInput(torch.tensor(ids, dtype=torch.int32), torch.arange(n, dtype=torch.int32), slots, meta, None)
+    return eng.model.forward(inp).float()
+
+
+def _check_greedy(cfg, sd, prompts, outs, rel_tol=0.02):
+    """Per-step top-1 margin check (teacher forced on the GPU's own tokens, so one flip does not
+    cascade): every greedy token must be the oracle's argmax, or within rel_tol x the row's logit
+    spread of it (a near-tie that a bf16 reduction order may legitimately flip). Returns the count of
+    exact argmax agreements."""
+    exact = 0
+    for pr, out in zip(prompts, outs):
+        lg = _oracle_logits(cfg, sd, pr + out[:-1])
+        for k, tok in enumerate(out):
+            row = lg[len(pr) - 1 + k]
+            top = float(row.max())
+            gap = top - float(row[tok])
+            spread = top - float(row.min())
+            assert gap <= rel_tol * spread, (k, tok, int(row.argmax()), gap, spread)
+            exact += int(gap == 0.0)
+    return exact
+
+
 def test_gpu_engine_matches_cpu_greedy(native, tiny_llama):
+    """GPU engine (graphs, async decode, mixed steps) greedy tokens vs the fp32 CPU oracle, per step."""
     cfg, sd = tiny_llama
     torch.manual_seed(0)
     prompts = [torch.randint(3, 1000, (n,)).tolist() for n in (5, 77, 130, 300, 513)]
     p = SamplingParams(max_new_tokens=6, do_sample=False, ignore_eos=True)
     gpu = _engine(cfg, sd, "cuda", graphs=True).generate(prompts, p)
-    cpu = _engine(cfg, sd, "cpu", graphs=False).generate(prompts, p)
-    first = sum(int(g[0] == c[0]) for g, c in zip(gpu, cpu))
-    total = sum(int(x == y) for g, c in zip(gpu, cpu) for x, y in zip(g, c))
-    assert first >= 4 and total >= 20, (gpu, cpu)
+    exact = _check_greedy(cfg, sd, prompts, gpu)
+    assert exact >= 0.7 * sum(len(x) for x in gpu), exact
 
 
 def test_graph_decode_equals_eager(native, tiny_llama):
@@ -60,6 +94,10 @@ def test_async_decode_equals_sync(native, tiny_llama):
     for mode in (True, False):
         eng = _engine(cfg, sd, "cuda", graphs=True, mb=4)
         eng.async_decode = mode
+        # mixed prefill+decode steps run a decoding row through the prefill kernels (different bf16
+        # reduction order), and WHICH steps are mixed shifts with the one-step-late acceptance: off here,
+        # so the comparison isolates the pipeline (mixed steps: test_mixed_steps_gpu_close_to_separate)
+        eng.mixed_steps = False
         seqs = [eng.add_request(pr, pa, seed=10 + i) for i, (pr, pa) in enumerate(zip(prompts, params))]
         eng.run_until_done()
         assert eng._inflight is None and not eng.running
@@ -110,3 +148,30 @@ def test_tiny_rag_workload_end_to_end(native):
     from rag_llm_k8s_amd.utils.smoke import run_smoke
 
     run_smoke("cuda:0")
+
+
+def test_mixed_steps_gpu_close_to_separate(native, tiny_llama):
+    """Mixed prefill+decode steps on the GPU: decoding rows computed inside prefill steps (prefill
+    attention / tile GEMM path) still produce (near-)argmax greedy tokens under the fp32 oracle, for
+    staggered arrivals; every KV block comes back."""
+    cfg, sd = tiny_llama
+    torch.manual_seed(6)
+    prompts = [torch.randint(3, 1000, (n,)).tolist() for n in (30, 200, 64, 150)]
+    p = SamplingParams(max_new_tokens=6, do_sample=False, ignore_eos=True)
+    outs, mixed = {}, {}
+    for m in (False, True):
+        eng = _engine(cfg, sd, "cuda", graphs=True, mb=4)
+        eng.mixed_steps = m
+        eng.max_prefill_tokens = 128
+        seqs = []
+        for pr in prompts:  # staggered: each new prompt is prefilled while the earlier ones decode
+            seqs.append(eng.add_request(pr, p, seed=1))
+            for _ in range(2):
+                eng.step()
+        eng.run_until_done()
+        assert eng._inflight is None and not eng.running and eng.bm.free_blocks() == 64 - 1
+        outs[m] = [s.out for s in seqs]
+        mixed[m] = eng.stats.get("mixed_decode_tokens", 0)
+    assert mixed[True] > 0 and mixed[False] == 0
+    for m in (False, True):  # every token of both runs is a (near-)argmax of the fp32 oracle
+        _check_greedy(cfg, sd, prompts, outs[m])

@@ -61,11 +61,23 @@ def test_services_pvcs_secret_upload_web():
 
 
 def test_tp8_variant():
-    (d,) = load("deploy/k8s/ragdeploy-tp8.yaml")
+    pvc, d, svc = load("deploy/k8s/ragdeploy-tp8.yaml")
     c = d["spec"]["template"]["spec"]["containers"][0]
     assert c["resources"]["limits"]["amd.com/gpu"] == 8
     assert "--nproc-per-node" in c["command"]
     assert {e["name"]: e["value"] for e in c["env"]}["TP_SIZE"] == "8"
+    # can run beside llm/ragdeploy.yaml: distinct selector, Service and model PVC; same init container
+    (base,) = load("llm/ragdeploy.yaml")
+    (base_svc,) = load("llm/service.yaml")
+    sel = d["spec"]["selector"]["matchLabels"]
+    assert sel != base["spec"]["selector"]["matchLabels"]
+    assert not set(base_svc["spec"]["selector"].items()) <= set(d["spec"]["template"]["metadata"]["labels"].items())
+    assert set(svc["spec"]["selector"].items()) <= set(d["spec"]["template"]["metadata"]["labels"].items())
+    assert svc["metadata"]["name"] == "llm-service-tp8" and svc["spec"]["ports"][0]["targetPort"] == 5001
+    vols = {v["name"]: v for v in d["spec"]["template"]["spec"]["volumes"]}
+    assert vols["model-storage"]["persistentVolumeClaim"]["claimName"] == pvc["metadata"]["name"] != "llm-model-pvc"
+    assert vols["download-script"]["configMap"]["name"] == "download-script-configmap"
+    assert d["spec"]["template"]["spec"]["initContainers"][0]["name"] == "download-model"
 
 
 def test_dockerfile_has_no_baked_token():

@@ -23,6 +23,8 @@ fi
 if [ "$STEP" = "all" ] || [ "$STEP" = "bench" ]; then
 timeout -k 10 600 python -u bench.py --steps ${BSTEPS:-3} --warmup 1 --json-out gpurun_out/bench.json > gpurun_out/bench.log 2>&1 &&
 tail -2 gpurun_out/bench.log &&
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 1 --warmup 0 > gpurun_out/prof.log 2>&1
-echo "bench rc=$?"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 1 --warmup 0 --c1 0 > gpurun_out/prof.log 2>&1
+rc=$?; echo "bench rc=$rc"
+rm -f gpurun_out/prof/*kernel_trace.csv  # keep the stats (the full trace exceeds the copy-back limit)
+python tools/rocprof_summary.py gpurun_out/prof/run_kernel_stats.csv 40 > gpurun_out/rocprof_summary.txt 2>&1
 fi
