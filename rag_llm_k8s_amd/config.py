@@ -66,6 +66,7 @@ class RagConfig:
     watchdog_exit: bool = True  # hung engine -> dump stacks and exit so k8s restarts the pod
     index_recovery: str = "rebuild"  # rebuild (quarantine unreadable index, re-ingest PDF_DIR) | fail
     ignore_eos: bool = False  # benchmarks only: every request generates exactly max_new_tokens
+    index_sharded: bool = False  # TP server: each rank keeps a row shard of the index, search is collective
     extra: dict = field(default_factory=dict)
 
     @classmethod
@@ -86,6 +87,7 @@ class RagConfig:
             "TRUNCATE_PROMPT": ("truncate_prompt", str), "REQUEST_TIMEOUT_S": ("request_timeout_s", float),
             "STEP_TIMEOUT_S": ("step_timeout_s", float), "WATCHDOG_EXIT": ("watchdog_exit", bool),
             "INDEX_RECOVERY": ("index_recovery", str), "IGNORE_EOS": ("ignore_eos", bool),
+            "INDEX_SHARDED": ("index_sharded", bool),
         }
         for env, (attr, cast) in m.items():
             setattr(c, attr, _env(env, getattr(c, attr), cast))

@@ -32,8 +32,16 @@ log = logging.getLogger(__name__)
 
 class DocumentStore:
     def __init__(self, index_path, dim, device="cpu", index_type="flat", ivf_nlist=1024, ivf_nprobe=32,
-                 recovery="rebuild"):
+                 recovery="rebuild", shard=None):
+        """shard = (group, rank, world): INDEX_SHARDED tensor-parallel mode -- this rank keeps the rows
+        g % world == rank of the index (parallel/dp.py ShardedFlatIndex) in `<index_path>.shard<r>of<W>`
+        (a faiss IxF2 file of its rows); every rank keeps the full metadata list, rank 0 persists it.
+        search() is then a collective (all ranks call it together, followers with no queries)."""
+        self.sharded = shard is not None
+        self.shard = shard
         self.index_path = index_path
+        self.index_file = index_path if shard is None else "%s.shard%dof%d" % (index_path, shard[1], shard[2])
+        self.persist_meta = shard is None or shard[1] == 0
         self.recovery = recovery  # rebuild: quarantine an unreadable index and start empty | fail
         self.meta_path = index_path + ".metadata"
         self.dim = dim
@@ -51,6 +59,12 @@ class DocumentStore:
         self._persist_error = None
 
     def _new_index(self):
+        if self.sharded:
+            if self.index_type != "flat":
+                raise ValueError("INDEX_SHARDED supports the flat index only")
+            from ..parallel.dp import ShardedFlatIndex
+
+            return ShardedFlatIndex(self.dim, device=self.device, group=self.shard[0])
         if self.index_type == "ivf":
             from .ivf import IVFFlatIndex
 
@@ -60,7 +74,7 @@ class DocumentStore:
     # ------------------------------------------------------------------ lifecycle
     def ensure_exists(self):
         """Reference ensure_index_exists(): create an empty index + [] metadata if missing."""
-        if not os.path.exists(self.index_path):
+        if not os.path.exists(self.index_file):
             log.info("Faiss index not found. Creating a new one.")
             self.persist()
         else:
@@ -78,10 +92,10 @@ class DocumentStore:
         """Move an unreadable index (+ metadata) aside and start empty; the startup directory
         ingest then rebuilds it from PDF_DIR. The reference would crash-loop instead."""
         tag = ".corrupt-%d" % int(time.time())
-        for p in (self.index_path, self.meta_path):
+        for p in (self.index_file, self.meta_path) if self.persist_meta else (self.index_file,):
             if os.path.exists(p):
                 os.replace(p, p + tag)
-        log.error("index %s unreadable (%s); moved aside as *%s, starting empty", self.index_path, err, tag)
+        log.error("index %s unreadable (%s); moved aside as *%s, starting empty", self.index_file, err, tag)
         self.index = self._new_index()
         self.metadata = []
         self._keys = set()
@@ -89,19 +103,28 @@ class DocumentStore:
 
     def _disk_mtimes(self):
         try:
-            return (os.path.getmtime(self.index_path), os.path.getmtime(self.meta_path))
+            return (os.path.getmtime(self.index_file), os.path.getmtime(self.meta_path))
         except OSError:
             return None
 
     def load(self):
-        faults.check("index_read_error", self.index_path)
-        r = read_index(self.index_path)
+        faults.check("index_read_error", self.index_file)
+        r = read_index(self.index_file)
         meta = load_metadata(self.meta_path) if os.path.exists(self.meta_path) else []
         if r["d"] != self.dim:
             raise ValueError("index dimension %d != embedder dimension %d" % (r["d"], self.dim))
+        idx = self._new_index()
+        if self.sharded:  # this rank's rows only; the global count comes from the metadata
+            world, rank = self.shard[2], self.shard[1]
+            if r["ntotal"] != len(range(rank, len(meta), world)):
+                raise ValueError("shard has %d vectors, metadata implies %d" % (r["ntotal"], len(range(rank, len(meta), world))))
+            idx.load_local(r["xb"] if r["ntotal"] else None, len(meta))
+            self.index, self.metadata = idx, list(meta)
+            self._keys = {(m.get("filename"), m.get("chunk_id")) for m in self.metadata if isinstance(m, dict)}
+            self._mtimes = self._disk_mtimes()
+            return
         if len(meta) != r["ntotal"]:
             raise ValueError("index has %d vectors but metadata %d entries (torn write?)" % (r["ntotal"], len(meta)))
-        idx = self._new_index()
         if r["type"] == "flat":
             if r["ntotal"]:
                 if self.index_type == "ivf":
@@ -118,6 +141,8 @@ class DocumentStore:
 
     def maybe_reload(self):
         """Pick up index files replaced on disk by another writer (e.g. an offline ingest job)."""
+        if self.sharded:  # a reload would have to be collective; shards change only through ingest jobs
+            return
         m = self._disk_mtimes()
         if m is not None and self._mtimes is not None and m != self._mtimes:
             with self._wlock:
@@ -132,8 +157,9 @@ class DocumentStore:
         return self.index.snapshot_writer(), list(self.metadata)
 
     def _write(self, writer, meta):
-        writer(self.index_path)
-        save_metadata(self.meta_path, meta)
+        writer(self.index_file)
+        if self.persist_meta:
+            save_metadata(self.meta_path, meta)
         self._mtimes = self._disk_mtimes()
 
     def persist(self):

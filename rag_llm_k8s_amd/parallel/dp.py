@@ -54,6 +54,23 @@ class ShardedFlatIndex:
         self.d = d
         self.ntotal = 0
 
+    @property
+    def device(self):
+        return self.local.device
+
+    def load_local(self, xb, ntotal):
+        """This rank's rows (from its shard file) and the global vector count."""
+        if xb is not None and len(xb):
+            self.local.add(torch.as_tensor(xb))
+        self.ntotal = int(ntotal)
+
+    def snapshot_writer(self):
+        """This rank's rows as a faiss IndexFlatL2 file (the store names it <index>.shard<r>of<W>)."""
+        return self.local.snapshot_writer()
+
+    def write(self, path):
+        self.snapshot_writer()(path)
+
     def add(self, x):
         """All ranks pass the same full batch; each keeps its round-robin share."""
         x = torch.as_tensor(x).float().reshape(-1, self.d)

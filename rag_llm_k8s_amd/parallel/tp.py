@@ -38,7 +38,7 @@ from ..utils import faults
 log = logging.getLogger(__name__)
 
 HEARTBEAT_S = 30.0
-K_STEP, K_NOOP, K_SHUTDOWN = 1, 2, 3
+K_STEP, K_NOOP, K_SHUTDOWN, K_JOB = 1, 2, 3, 4
 
 
 class GlooChannel:
@@ -79,27 +79,45 @@ class ShmChannel:
     HDR_WORDS = 64
     POLL_SPIN_S = 0.002
 
-    def __init__(self, cpu_group, rank, world, capacity=1 << 20, src=0, timeout_s=600.0):
+    @classmethod
+    def create(cls, cpu_group, rank, world, capacity=1 << 20, src=0, timeout_s=600.0):
+        """Collective constructor: the channel on every rank, or None on every rank."""
         from multiprocessing import shared_memory
 
-        self.rank, self.world, self.src, self.timeout_s = rank, world, src, timeout_s
-        name = [None]
+        shm, name = None, [None]
         if rank == src:
-            name[0] = "ragk_tp_%s" % uuid.uuid4().hex[:16]
-            self.shm = shared_memory.SharedMemory(name=name[0], create=True,
-                                                  size=self.HDR_WORDS * 8 + capacity)
-            self.shm.buf[:self.HDR_WORDS * 8] = bytes(self.HDR_WORDS * 8)
+            try:
+                name[0] = "ragk_tp_%s" % uuid.uuid4().hex[:16]
+                shm = shared_memory.SharedMemory(name=name[0], create=True, size=cls.HDR_WORDS * 8 + capacity)
+                shm.buf[:cls.HDR_WORDS * 8] = bytes(cls.HDR_WORDS * 8)
+            except Exception as e:
+                log.warning("cannot create the TP control segment: %s", e)
+                name[0] = None
         dist.broadcast_object_list(name, src=src, group=cpu_group)
-        if rank != src:
-            self.shm = shared_memory.SharedMemory(name=name[0], create=False)
-            try:  # the producer owns the segment; followers must not unlink it at exit
-                from multiprocessing import resource_tracker
-                resource_tracker.unregister(self.shm._name, "shared_memory")
-            except Exception:
-                pass
-        dist.barrier(group=cpu_group)
-        if rank == src:  # every rank has mapped it: the name can go (the mapping stays)
-            self.shm.unlink()
+        if rank != src and name[0] is not None:
+            try:
+                shm = shared_memory.SharedMemory(name=name[0], create=False)
+                try:  # the producer owns the segment; followers must not unlink it at exit
+                    from multiprocessing import resource_tracker
+                    resource_tracker.unregister(shm._name, "shared_memory")
+                except Exception:
+                    pass
+            except Exception as e:
+                log.warning("cannot attach the TP control segment: %s", e)
+                shm = None
+        ok = torch.tensor([1 if shm is not None else 0], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=cpu_group)  # every rank mapped it (or none uses it)
+        if rank == src and shm is not None:  # the name can go now (the mappings stay)
+            shm.unlink()
+        if int(ok.item()) == 0:
+            if shm is not None:
+                shm.close()
+            return None
+        return cls(cpu_group, rank, world, shm, src=src, timeout_s=timeout_s)
+
+    def __init__(self, cpu_group, rank, world, shm, src=0, timeout_s=600.0):
+        self.rank, self.world, self.src, self.timeout_s = rank, world, src, timeout_s
+        self.shm = shm
         self.words = np.ndarray((self.HDR_WORDS,), dtype=np.int64, buffer=self.shm.buf)
         self.cap = len(self.shm.buf) - self.HDR_WORDS * 8
         self.seq = 0
@@ -153,16 +171,18 @@ class ShmChannel:
 
 
 def make_channel(cpu_group, rank, world, src=0):
-    """Shared memory when every TP rank runs on this host (RAGK_TP_CONTROL=gloo forces gloo)."""
+    """Shared memory when every TP rank runs on this host (RAGK_TP_CONTROL=gloo forces gloo). Every
+    rank reaches the same choice: a segment that cannot be created or attached on ANY rank (e.g.
+    /dev/shm not writable) falls back to gloo everywhere, loudly."""
     mode = os.environ.get("RAGK_TP_CONTROL", "auto")
     if mode != "gloo":
         hosts = [None] * world
         dist.all_gather_object(hosts, socket.gethostname(), group=cpu_group)
         if len(set(hosts)) == 1:
-            try:
-                return ShmChannel(cpu_group, rank, world, src=src)
-            except Exception as e:  # e.g. /dev/shm not writable: fall back, loudly
-                log.warning("shared-memory TP control channel unavailable (%s); using gloo", e)
+            ch = ShmChannel.create(cpu_group, rank, world, src=src)
+            if ch is not None:
+                return ch
+            log.warning("shared-memory TP control channel unavailable; using gloo")
     return GlooChannel(cpu_group, src)
 
 
@@ -201,6 +221,11 @@ class TPControl:
         for s in new:
             engine.add_sequence(s)
 
+    def publish_job(self, name, args):
+        """A collective job (data-parallel ingest, sharded search) every rank runs before its next step."""
+        self.chan.send(K_JOB, pickle.dumps((name, args), protocol=pickle.HIGHEST_PROTOCOL))
+        self.last_publish = time.time()
+
     def publish_heartbeat(self):
         self.chan.send(K_NOOP)
         self.last_publish = time.time()
@@ -212,8 +237,9 @@ class TPControl:
             pass
 
 
-def follow(engine, cpu_group, src_rank=0, channel=None):
-    """Follower loop (ranks != 0): mirror rank 0's admissions and steps until shutdown."""
+def follow(engine, cpu_group, src_rank=0, channel=None, jobs=None):
+    """Follower loop (ranks != 0): mirror rank 0's admissions, steps and collective jobs until shutdown.
+    `jobs`: name -> callable(args), the same functions rank 0's engine loop runs (RagService.job_fns)."""
     if channel is None:
         channel = make_channel(cpu_group, dist.get_rank(cpu_group), dist.get_world_size(cpu_group), src_rank)
     try:
@@ -222,6 +248,10 @@ def follow(engine, cpu_group, src_rank=0, channel=None):
             if kind == K_SHUTDOWN:
                 return
             if kind == K_NOOP:
+                continue
+            if kind == K_JOB:
+                name, args = pickle.loads(payload)
+                jobs[name](args)
                 continue
             hang = faults.value("comm_hang_s")
             if hang:  # fault injection: this rank stalls, rank 0's collectives wait (watchdog path)
@@ -250,7 +280,9 @@ def run_tp_server(cfg, rank, world):
     svc = build_service(cfg, start_threads=(rank == 0), tp_rank=ctx.tp_rank, tp_size=ctx.tp, comm=comm,
                         tp_group=ctx.tp_group, control=control)
     if rank != 0:
-        follow(svc.engine, ctx.tp_cpu_group, channel=chan)
+        if svc.store.sharded:  # every rank serves (and persists) its own row shard
+            svc.store.ensure_exists()
+        follow(svc.engine, ctx.tp_cpu_group, channel=chan, jobs=svc.job_fns())
         return
     svc.store.ensure_exists()
     svc.ingest_directory()

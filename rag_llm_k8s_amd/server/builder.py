@@ -99,7 +99,12 @@ def build_service(cfg, start_threads=True, tp_rank=0, tp_size=1, comm=None, tp_g
     engine, tok, gen = build_generator(cfg, device, tp_rank, tp_size, comm, tp_group)
     log.info("Model and tokenizer loaded successfully")
     embedder = build_embedder(cfg, device)
+    shard = None
+    if cfg.index_sharded and tp_size > 1:
+        shard = (tp_group, tp_rank, tp_size)  # INDEX_SHARDED=1: row shard per TP rank (parallel/dp.py)
     store = DocumentStore(cfg.index_path, embedder.dim, device=device, index_type=cfg.index_type,
-                          ivf_nlist=cfg.ivf_nlist, ivf_nprobe=cfg.ivf_nprobe, recovery=cfg.index_recovery)
-    svc = RagService(cfg, engine, tok, embedder, store, gen_config=gen, start_threads=start_threads, control=control)
+                          ivf_nlist=cfg.ivf_nlist, ivf_nprobe=cfg.ivf_nprobe, recovery=cfg.index_recovery,
+                          shard=shard)
+    svc = RagService(cfg, engine, tok, embedder, store, gen_config=gen, start_threads=start_threads, control=control,
+                     tp_group=tp_group if tp_size > 1 else None)
     return svc

@@ -64,8 +64,20 @@ def _tp_bcast_prompts(comm, rows, id_lists, seeds):
     return rows, out, seeds
 
 
+class _Job:
+    def __init__(self, name, args):
+        self.name, self.args = name, args
+        self.done = threading.Event()
+        self.result = self.error = None
+
+
 class EngineLoop(threading.Thread):
-    """Drives LLMEngine.step() on one thread; wakes when requests arrive."""
+    """Drives LLMEngine.step() on one thread; wakes when requests arrive.
+
+    Collective jobs (tensor-parallel serving): work that every TP rank must run together -- the
+    data-parallel ingest of an uploaded PDF, a search of a row-sharded index -- is queued here and run
+    by this thread BETWEEN engine steps, after the job record has been published to the follower ranks
+    (parallel/tp.py), so every rank executes the same collectives in the same order as its steps."""
 
     def __init__(self, engine, control=None):
         super().__init__(daemon=True, name="llm-engine-loop")
@@ -76,6 +88,37 @@ class EngineLoop(threading.Thread):
         self.error = None
         self.step_started = None  # monotonic start of the step in flight (watchdog)
         self.steps = 0
+        self.jobs = []
+        self.job_fns = {}
+
+    def run_job(self, name, args, timeout=None):
+        """Run job `name` on every TP rank between two engine steps; returns this rank's result."""
+        if self.error is not None:
+            raise RuntimeError("engine loop failed: %r" % (self.error,))
+        job = _Job(name, args)
+        with self.cv:
+            self.jobs.append(job)
+            self.cv.notify()
+        if not job.done.wait(timeout):
+            raise TimeoutError("collective job %s not run within %ss" % (name, timeout))
+        if job.error is not None:
+            raise job.error
+        return job.result
+
+    def _run_jobs(self):
+        with self.cv:
+            jobs, self.jobs = self.jobs, []
+        for job in jobs:
+            try:
+                if self.control is not None:
+                    self.control.publish_job(job.name, job.args)
+                job.result = self.job_fns[job.name](job.args)
+            except Exception as e:
+                job.error = e
+                if self.control is not None:  # a half-run collective leaves the ranks out of step
+                    raise
+            finally:
+                job.done.set()
 
     def submit(self, prompt_ids, params, seed=None):
         if self.control is not None:  # TP: admission is broadcast to the follower ranks first
@@ -90,7 +133,7 @@ class EngineLoop(threading.Thread):
     def _idle(self):
         eng = self.engine
         pending = self.control.has_pending() if self.control is not None else False
-        return not eng.has_work() and not pending
+        return not eng.has_work() and not pending and not self.jobs
 
     def run(self):
         from ..parallel.tp import HEARTBEAT_S
@@ -105,6 +148,10 @@ class EngineLoop(threading.Thread):
                             self.control.publish_heartbeat()
                 if self.stop_flag:
                     break
+                if self.jobs:
+                    self._run_jobs()
+                    if self._idle():
+                        continue
                 self.step_started = time.monotonic()
                 if self.control is not None:
                     self.control.publish_step(eng)
@@ -125,6 +172,11 @@ class EngineLoop(threading.Thread):
             for s in list(eng.running) + list(eng.waiting):
                 s.finish_reason = "error"
                 s.done.set()
+            with self.cv:
+                jobs, self.jobs = self.jobs, []
+            for job in jobs:
+                job.error = RuntimeError("engine loop failed: %r" % (e,))
+                job.done.set()
         finally:
             if self.control is not None:
                 self.control.publish_shutdown()
@@ -207,7 +259,7 @@ class MicroBatcher(threading.Thread):
 
 class RagService:
     def __init__(self, cfg, llm_engine, llm_tokenizer, embedder, store, gen_config=None, start_threads=True,
-                 control=None):
+                 control=None, tp_group=None):
         self.cfg = cfg
         self.engine = llm_engine
         self.tok = llm_tokenizer
@@ -221,6 +273,11 @@ class RagService:
                                      top_p=cfg.top_p, top_k=cfg.top_k, do_sample=do_sample, stop_token_ids=stop,
                                      ignore_eos=bool(getattr(cfg, "ignore_eos", False)))
         self.loop = EngineLoop(llm_engine, control=control)
+        # tensor-parallel group (set by the TP server): PDF ingest is data-parallel over it and, with
+        # INDEX_SHARDED, every rank holds a row shard of the index (both run as collective jobs)
+        self.tp_group = tp_group
+        self.collective = control is not None
+        self.loop.job_fns.update(self.job_fns())
         self.watchdog = Watchdog(self.loop, cfg.step_timeout_s, cfg.watchdog_exit)
         self.batcher = MicroBatcher(self._retrieve_batch)
         self._seed = cfg.seed
@@ -232,6 +289,34 @@ class RagService:
             self.watchdog.start()
 
     # ------------------------------------------------------------------ retrieval
+    # ------------------------------------------------------------------ collective jobs
+    def job_fns(self):
+        """Jobs every TP rank runs together (rank 0: engine-loop thread; followers: parallel/tp.follow)."""
+        return {"ingest": self._job_ingest, "search": self._job_search}
+
+    def _job_ingest(self, args):
+        """Data-parallel embedding of one upload's chunks: rank r embeds chunks[r::world], the vectors are
+        all-gathered (RCCL on GPUs) and added to the index -- by rank 0 only (replicated-index mode: only
+        rank 0 retrieves), or by every rank for its row shard (INDEX_SHARDED)."""
+        from ..parallel.dp import embed_distributed
+
+        filename, chunks, dedupe, persist = args
+        if self.collective or (self.tp_group is not None and not self.loop.is_alive()):
+            vecs = embed_distributed(self.embedder, chunks, group=self.tp_group)
+        else:  # single process (or a DP replica): never a collective over the default group
+            vecs = self.embedder.embed(chunks)
+        rank0 = self.tp_group is None or torch.distributed.get_rank(self.tp_group) == 0
+        if rank0 or getattr(self.store, "sharded", False):
+            self.store.add(vecs, chunk_metadata(filename, chunks), dedupe=dedupe, persist=persist)
+        return len(chunks)
+
+    def _job_search(self, args):
+        """Row-sharded index: every rank searches its shard for rank 0's queries (followers pass none)."""
+        q, k = args
+        if q is None:
+            q = torch.zeros((0, self.store.dim), dtype=torch.float32)
+        return self.store.search(q, k)
+
     def _retrieve_batch(self, prompts):
         tr = Trace("retrieve")
         with tr.span("embed"):
@@ -239,7 +324,10 @@ class RagService:
             q = self.embedder.embed(list(prompts))
         with tr.span("search"):
             self.store.maybe_reload()
-            res = self.store.search(q, self.cfg.retrieve_k)
+            if self.collective and getattr(self.store, "sharded", False):
+                res = self.loop.run_job("search", (q.cpu(), self.cfg.retrieve_k), timeout=self.cfg.request_timeout_s)
+            else:
+                res = self.store.search(q, self.cfg.retrieve_k)
         return [(r, tr.spans) for r in res]
 
     def retrieve(self, prompt):
@@ -409,9 +497,11 @@ class RagService:
         text = pdfmod.extract_text(data)
         chunks = split_text(text, self.cfg.chunk_words, self.cfg.chunk_overlap)
         if chunks:
-            vecs = self.embedder.embed(chunks)
-            self.store.add(vecs, chunk_metadata(filename, chunks), dedupe=not self.cfg.reingest_append,
-                           persist=persist)
+            args = (filename, chunks, not self.cfg.reingest_append, persist)
+            if self.collective:  # tensor-parallel server: every rank embeds a share (data-parallel ingest)
+                self.loop.run_job("ingest", args, timeout=self.cfg.request_timeout_s)
+            else:
+                self._job_ingest(args)
             metrics.set_gauge("index", self.store.index.ntotal)
         return len(chunks)
 
@@ -428,8 +518,12 @@ class RagService:
         total = 0
         for fn in files:
             with open(os.path.join(d, fn), "rb") as f:
-                total += self.ingest_pdf_bytes(fn, f.read(), persist=False)
-        self.store.persist()
+                # collective (TP) ingest: every rank snapshots what it holds, in the background
+                total += self.ingest_pdf_bytes(fn, f.read(), persist=self.collective)
+        if self.collective:
+            self.store.flush()
+        else:
+            self.store.persist()
         log.info("Processed %d PDFs into %d chunks", len(files), total)
         return len(files)
 

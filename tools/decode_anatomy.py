@@ -1,0 +1,54 @@
+"""Decode-step anatomy of the Llama-3.1-8B engine (random init, bf16) at batch B with ~5.2k-token
+contexts (the bench's RAG prompts): wall ms per decode step from the engine (hipGraph + async
+decode) and, under `rocprofv3 --kernel-trace --stats`, the per-kernel split.
+
+  python tools/decode_anatomy.py 1 32          # batch sizes
+  DA_PROMPT=5200 DA_STEPS=64 ...
+"""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from rag_llm_k8s_amd import _build
+    from rag_llm_k8s_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from rag_llm_k8s_amd.models import llama as L
+
+    _build.build_all()
+    Bs = [int(a) for a in sys.argv[1:]] or [1, 32]
+    plen = int(os.environ.get("DA_PROMPT", "5200"))
+    steps = int(os.environ.get("DA_STEPS", "64"))
+    cfg = L.llama31_8b()
+    dev = "cuda:0"
+    w = L.LlamaWeights.random(cfg, dev, seed=0)
+    m = L.LlamaModel(cfg, w, dev, max_positions=8192)
+    for B in Bs:
+        eng = LLMEngine(m, num_blocks=B * 128 + 16, max_batch=B, max_prefill_tokens=32768, max_model_len=8192,
+                        eos_ids=cfg.eos_token_id, graph_buckets=[B])
+        eng.warmup_graphs([B])
+        g = torch.Generator().manual_seed(B)
+        p = SamplingParams(max_new_tokens=steps + 1, temperature=0.7, top_p=0.9, top_k=50, ignore_eos=True)
+        for i in range(B):
+            eng.add_request(torch.randint(3, cfg.vocab_size, (plen,), generator=g).tolist(), p, seed=i)
+        while any(s.computed < len(s.prompt) for s in eng.running) or eng.waiting:
+            eng.step()
+        torch.cuda.synchronize()
+        d0, n0 = eng.stats["decode_s"], eng.stats["decode_steps"]
+        t0 = time.perf_counter()
+        eng.run_until_done()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        n = eng.stats["decode_steps"] - n0
+        print("B=%d ctx=%d: %d decode steps, %.3f ms/step (engine decode_s %.3f ms/step), %.0f tok/s" % (
+            B, plen, n, dt / n * 1e3, (eng.stats["decode_s"] - d0) / n * 1e3, B * n / dt), flush=True)
+        del eng
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
