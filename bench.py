@@ -168,7 +168,8 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16" if a.dtype == "bf16" else "fp8-weights (bf16 activations/KV)",
             "data": "synthetic (random-init weights of the named architectures; Zipfian pseudo-English corpus "
-                    "of %d x 1000-word chunks; trained 128k BPE + WordPiece tokenizers)" % a.chunks,
+                    "of %d x 1000-word chunks; trained 128k BPE + %s tokenizers)" % (
+                        a.chunks, "XLM-R SentencePiece Unigram" if a.embedder == "bge-m3" else "WordPiece"),
             "config": {
                 "model": {"8b": "Llama-3.1-8B-Instruct", "70b": "Llama-3.1-70B-Instruct", "tiny": "llama-tiny"}[a.model],
                 "embedder": {"minilm": "all-MiniLM-L6-v2", "bge-large": "bge-large-en-v1.5", "bge-m3": "bge-m3",
@@ -189,6 +190,8 @@ def main():
             "per_gpu_tokens_per_s": round(value / ctx.world, 2),
             "engine": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in eng.items()},
             "setup_s": round(setup_s, 1),
+            # ingest throughput of the corpus build (tokenize + batched varlen encoder, one GPU)
+            "ingest_embed_chunks_per_s": round(a.chunks / max(1e-9, allstats[0]["setup"].get("embed_s", 0.0)), 1),
         }
         line = json.dumps(res)
         print(line, flush=True)

@@ -108,6 +108,7 @@ constexpr int IVF_DMAX = 2048;
 __global__ __launch_bounds__(ST) void ivf_scan_kernel(const float* __restrict__ xt, int cap, int d,
                                                       const float* __restrict__ q, const int* __restrict__ probes,
                                                       int nprobe, int chunks, const int* __restrict__ offsets,
+                                                      const int* __restrict__ ends,
                                                       const int* __restrict__ ids_map, int k, float* out_d,
                                                       int* out_i) {
   __shared__ float qs[IVF_DMAX];
@@ -116,7 +117,9 @@ __global__ __launch_bounds__(ST) void ivf_scan_kernel(const float* __restrict__ 
   const int qi = blockIdx.y;
   const int p = blockIdx.x / chunks, c = blockIdx.x % chunks;
   const int list = probes[(size_t)qi * nprobe + p];
-  const int lend = offsets[list + 1];
+  // list rows [offsets[list], ends[list]) -- lists may carry spare capacity after their rows
+  // (incremental appends); without `ends` the lists are packed: end = offsets[list + 1]
+  const int lend = ends ? ends[list] : offsets[list + 1];
   const int r0 = offsets[list] + c * RPB;
   const int r1 = min(lend, r0 + RPB);
   for (int t = threadIdx.x; t < d; t += ST) qs[t] = q[(size_t)qi * d + t];
@@ -192,12 +195,132 @@ __global__ void l2_append_kernel(float* xt, int cap, int d, int n0, const float*
   if (row < n) xt[(size_t)dim * cap + n0 + row] = x[(size_t)row * d + dim];
 }
 
+// scatter row-major rows x[j] into column-major store slots pos[j] (IVF list appends)
+__global__ void l2_scatter_kernel(float* xt, int cap, int d, const int* __restrict__ pos, const float* __restrict__ x,
+                                  int n) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int dim = blockIdx.y;
+  if (j < n) xt[(size_t)dim * cap + pos[j]] = x[(size_t)j * d + dim];
+}
+
 // gather rows (by index) out of the column-major store -> row-major [n][d]
 __global__ void l2_gather_kernel(const float* __restrict__ xt, int cap, int d, const int* __restrict__ idx, int n,
                                  float* out) {
   const int i = blockIdx.x;
   const int row = idx[i];
   for (int t = threadIdx.x; t < d; t += blockDim.x) out[(size_t)i * d + t] = row >= 0 ? xt[(size_t)t * cap + row] : 0.f;
+}
+
+// ---------------------------------------------------------------------------------------------
+// k-means assignment as an MFMA distance GEMM with a fused argmin (index/ivf.py training, IVF
+// list assignment). ||x - c||^2 = ||x||^2 + (||c||^2 - 2 x.c): the x.c products run on the exact
+// fp32-input MFMA (v_mfma_f32_16x16x4_f32: a k-ordered fmaf chain, 1/16 of the bf16 rate but
+// exact like faiss' sgemm path), the argmin over centroids is kept per lane in registers.
+// Block = 32 rows of X resident in LDS (pitch d + 4 floats: 16 distinct 16-B slots for the 16 rows
+// a ds_read_b128 lane group touches) x every centroid, streamed in [64 centroids][64 dims] chunks.
+// Wave w: rows 16*(w >> 1) .. +15 against centroids 32*(w & 1) .. +31 of each 64-centroid tile (two
+// 16x16 accumulator tiles). MFMA k-slot mapping: lane l feeds dims 4*(l >> 4) + s of a 16-dim step
+// in MFMA s = 0..3, so A and B fragments are single ds_read_b128s.
+constexpr int KA_ROWS = 32, KA_CT = 64, KA_DC = 64, KA_DMAX = 1024;
+
+__device__ __forceinline__ void ka_better(float v, int i, float& bv, int& bi) {
+  if (v < bv || (v == bv && i < bi)) {
+    bv = v;
+    bi = i;
+  }
+}
+
+__global__ __launch_bounds__(256) void kmeans_assign_kernel(const float* __restrict__ X, int n, int d,
+                                                            const float* __restrict__ C,
+                                                            const float* __restrict__ cnorm, int k,
+                                                            int* __restrict__ assign, float* __restrict__ dist) {
+  extern __shared__ __attribute__((aligned(16))) float ka_smem[];
+  const int xp = d + 4;
+  float* xs = ka_smem;                          // [KA_ROWS][xp]
+  float* cs = ka_smem + KA_ROWS * xp;           // [KA_CT][KA_DC + 4]
+  __shared__ float s_bv[2][KA_ROWS];
+  __shared__ int s_bi[2][KA_ROWS];
+  __shared__ float s_xn[KA_ROWS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int row0 = blockIdx.x * KA_ROWS;
+  // X tile -> LDS (rows past n are zero)
+  const int d4 = d / 4;
+  for (int e = tid; e < KA_ROWS * d4; e += 256) {
+    const int r = e / d4, c4 = e % d4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row0 + r < n) v = *reinterpret_cast<const f32x4*>(X + (size_t)(row0 + r) * d + 4 * c4);
+    *reinterpret_cast<f32x4*>(xs + r * xp + 4 * c4) = v;
+  }
+  __syncthreads();
+  if (tid < KA_ROWS) {
+    float sq = 0.f;
+    for (int t = 0; t < d; ++t) sq = fmaf(xs[tid * xp + t], xs[tid * xp + t], sq);
+    s_xn[tid] = sq;
+  }
+  const int rg = wid >> 1, ch = wid & 1;  // row group, centroid half
+  const int fr = lane & 15, fg = lane >> 4;
+  const float* xrow = xs + (16 * rg + fr) * xp + 4 * fg;
+  float bv[4] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
+  int bi[4] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+  for (int c0 = 0; c0 < k; c0 += KA_CT) {
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    for (int d0 = 0; d0 < d; d0 += KA_DC) {
+      __syncthreads();  // previous chunk fully consumed
+      for (int e = tid; e < KA_CT * (KA_DC / 4); e += 256) {
+        const int r = e / (KA_DC / 4), c4 = e % (KA_DC / 4);
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (c0 + r < k) v = *reinterpret_cast<const f32x4*>(C + (size_t)(c0 + r) * d + d0 + 4 * c4);
+        *reinterpret_cast<f32x4*>(cs + r * (KA_DC + 4) + 4 * c4) = v;
+      }
+      __syncthreads();
+      const float* c0row = cs + (32 * ch + fr) * (KA_DC + 4) + 4 * fg;
+      const float* c1row = c0row + 16 * (KA_DC + 4);
+#pragma unroll
+      for (int kk = 0; kk < KA_DC; kk += 16) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(xrow + d0 + kk);
+        const f32x4 b0 = *reinterpret_cast<const f32x4*>(c0row + kk);
+        const f32x4 b1 = *reinterpret_cast<const f32x4*>(c1row + kk);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b0[s], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b1[s], acc1, 0, 0, 0);
+        }
+      }
+    }
+    // lane holds rows 4*fg + r (of this wave's 16), centroids c0 + 32*ch + fr (acc0) / + 16 (acc1)
+    const int ca = c0 + 32 * ch + fr, cb = ca + 16;
+    const float na = ca < k ? cnorm[ca] : 0.f, nb = cb < k ? cnorm[cb] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (ca < k) ka_better(na - 2.f * acc0[r], ca, bv[r], bi[r]);
+      if (cb < k) ka_better(nb - 2.f * acc1[r], cb, bv[r], bi[r]);
+    }
+  }
+  // argmin across the 16 lanes of a row group (same fg), then across the two centroid halves
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const float ov = __shfl_xor(bv[r], o, 64);
+      const int oi = __shfl_xor(bi[r], o, 64);
+      ka_better(ov, oi, bv[r], bi[r]);
+    }
+  }
+  if (fr == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s_bv[ch][16 * rg + 4 * fg + r] = bv[r];
+      s_bi[ch][16 * rg + 4 * fg + r] = bi[r];
+    }
+  }
+  __syncthreads();
+  if (tid < KA_ROWS && row0 + tid < n) {
+    float v = s_bv[0][tid];
+    int i = s_bi[0][tid];
+    ka_better(s_bv[1][tid], s_bi[1][tid], v, i);
+    assign[row0 + tid] = i;
+    if (dist) dist[row0 + tid] = fmaxf(s_xn[tid] + v, 0.f);
+  }
 }
 
 }  // namespace
@@ -219,12 +342,31 @@ RAGK_API int ragk_l2_partial(const float* xt, int cap, int d, int row_begin, int
 
 // out buffers: nq * nprobe * chunks * k entries; chunks = ceil(max_list_len / 1024)
 RAGK_API int ragk_ivf_scan(const float* xt, int cap, int d, const float* q, int nq, const int* probes, int nprobe,
-                           int chunks, const int* offsets, const int* ids_map, int k, float* out_d, int* out_i,
-                           hipStream_t st) {
+                           int chunks, const int* offsets, const int* ends, const int* ids_map, int k, float* out_d,
+                           int* out_i, hipStream_t st) {
   if (nq <= 0) return 0;
   if (d > IVF_DMAX || k > RPB || chunks < 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(ivf_scan_kernel, dim3(nprobe * chunks, nq), dim3(ST), 0, st, xt, cap, d, q, probes, nprobe,
-                     chunks, offsets, ids_map, k, out_d, out_i);
+                     chunks, offsets, ends, ids_map, k, out_d, out_i);
+  return (int)hipGetLastError();
+}
+
+// k-means / IVF assignment: a[i] = argmin_c ||x_i - c||^2 over the k centroids (ties -> lower c),
+// dist[i] = that squared distance. X [n][d], C [k][d] fp32 row-major, cnorm[c] = ||c||^2.
+RAGK_API int ragk_kmeans_assign(const float* X, int n, int d, const float* C, const float* cnorm, int k, int* assign,
+                                float* dist, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (d % KA_DC || d > KA_DMAX || k <= 0 || ((uintptr_t)X & 15) || ((uintptr_t)C & 15)) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)KA_ROWS * (d + 4) * 4 + (size_t)KA_CT * (KA_DC + 4) * 4;
+  static bool attr_set = false;  // > 64 KiB of dynamic LDS needs the opt-in (d up to 1024: ~149 KiB)
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kmeans_assign_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       KA_ROWS * (KA_DMAX + 4) * 4 + KA_CT * (KA_DC + 4) * 4);
+    if (e != hipSuccess) return (int)e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kmeans_assign_kernel, dim3((n + KA_ROWS - 1) / KA_ROWS), dim3(256), lds, st, X, n, d, C, cnorm, k,
+                     assign, dist);
   return (int)hipGetLastError();
 }
 
@@ -245,6 +387,14 @@ RAGK_API int ragk_l2_append(float* xt, int cap, int d, int n0, const float* x, i
   if (n0 + n > cap) return (int)hipErrorInvalidValue;
   dim3 grid((n + 255) / 256, d);
   hipLaunchKernelGGL(l2_append_kernel, grid, dim3(256), 0, st, xt, cap, d, n0, x, n);
+  return (int)hipGetLastError();
+}
+
+// x [n][d] row-major -> store slots pos[j] (every pos < cap; the launcher's caller checks)
+RAGK_API int ragk_l2_scatter(float* xt, int cap, int d, const int* pos, const float* x, int n, hipStream_t st) {
+  if (n <= 0) return 0;
+  dim3 grid((n + 255) / 256, d);
+  hipLaunchKernelGGL(l2_scatter_kernel, grid, dim3(256), 0, st, xt, cap, d, pos, x, n);
   return (int)hipGetLastError();
 }
 

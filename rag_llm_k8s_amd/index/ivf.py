@@ -1,11 +1,20 @@
 """IVF-Flat index (faiss IndexIVFFlat semantics; BASELINE config 4: 1M-chunk IVF-Flat in HBM).
 
-Coarse quantizer = k-means centroids (trained on the GPU with MFMA matmuls); each vector
-is stored in the inverted list of its nearest centroid. All lists live in ONE
-list-ordered, column-major HBM store (rows of a list are contiguous), so a probe is a
-contiguous row range. Search: coarse top-nprobe over the centroids, then the gfx950
-``ivf_scan`` kernel scans every (query, probe) range and keeps a per-range top-k, merged by
-``topk_merge``. Exact within the probed lists (nprobe = nlist == brute force).
+The reference only has IndexFlatL2 (/root/reference/llm/rag.py:61,80,116); IVF is the config-4
+extension of SURVEY §2.4 V3.
+
+* Coarse quantizer = k-means centroids. Training runs on the GPU: the assignment step is the MFMA
+  distance-GEMM + argmin kernel (ops/native.kmeans_assign in csrc/kernels/search.hip; exact fp32
+  products), the centroid update a scatter-add. faiss defaults: at most 256 training points per
+  centroid (random subsample), empty clusters re-seeded from the data.
+* Storage: every list lives in ONE column-major HBM store [d][cap] with spare capacity per list
+  (start, size, capacity). An append writes the new rows straight into their lists' free slots (one
+  scatter kernel); only when some list runs out of room is the store regrown (capacities x1.5, so
+  amortised O(1) per vector) -- an append never rebuilds the store from the host lists.
+* Search: coarse top-nprobe over the centroids (HBM flat kernel), then the ``ivf_scan`` kernel scans
+  every (query, probe) row range [start, start + size) with a per-range top-k, merged by
+  ``topk_merge``. Exact within the probed lists (nprobe = nlist == brute force).
+* Host copies of the lists are kept for faiss-format persistence (faiss_io.write_ivf_flat).
 """
 from __future__ import annotations
 
@@ -16,16 +25,38 @@ import torch
 
 from .flat import FLT_MAX, FlatL2Index
 
+MAX_POINTS_PER_CENTROID = 256  # faiss ClusteringParameters default
 
-def kmeans(x: torch.Tensor, k: int, iters: int = 20, seed: int = 0):
-    """Lloyd's k-means (faiss-like: random init from the data, empty clusters re-seeded)."""
+
+def _native_assign_ok(x):
+    return x.is_cuda and x.dtype == torch.float32 and x.shape[1] % 64 == 0 and x.shape[1] <= 1024
+
+
+def assign(x: torch.Tensor, c: torch.Tensor, cnorm=None):
+    """Nearest centroid of every row (ties -> lower id): MFMA kernel on the GPU, torch elsewhere."""
+    if _native_assign_ok(x):
+        from ..ops import native
+
+        a, _ = native.kmeans_assign(x.contiguous(), c.float().contiguous(), cnorm)
+        return a.long()
+    d = (x * x).sum(1, keepdim=True) - 2 * x @ c.t() + (c * c).sum(1)[None]
+    return d.argmin(1)
+
+
+def kmeans(x: torch.Tensor, k: int, iters: int = 20, seed: int = 0,
+           max_points_per_centroid: int = MAX_POINTS_PER_CENTROID):
+    """Lloyd's k-means (faiss-like: training subsample of at most max_points_per_centroid * k points,
+    random init from the data, empty clusters re-seeded)."""
     g = torch.Generator(device="cpu").manual_seed(seed)
+    x = x.float().contiguous()
     n = x.shape[0]
     k = min(k, n)
+    if max_points_per_centroid and n > max_points_per_centroid * k:
+        x = x[torch.randperm(n, generator=g)[:max_points_per_centroid * k].to(x.device)].contiguous()
+        n = x.shape[0]
     c = x[torch.randperm(n, generator=g)[:k].to(x.device)].clone()
     for _ in range(iters):
-        d = (x * x).sum(1, keepdim=True) - 2 * x @ c.t() + (c * c).sum(1)[None]
-        a = d.argmin(1)
+        a = assign(x, c)
         s = torch.zeros_like(c).index_add_(0, a, x)
         cnt = torch.bincount(a, minlength=k).float()
         empty = cnt == 0
@@ -42,27 +73,82 @@ class IVFFlatIndex:
         self.nlist, self.nprobe = int(nlist), int(nprobe)
         self.is_trained = False
         self.centroids = None
+        self._cnorm = None
         self.quant = None
-        self.lists = []  # host: per-list float32 [n_i, d]
+        self.lists = []  # host: per-list float32 [n_i, d] (persistence, CPU search)
         self.ids = []  # host: per-list int64 [n_i]
         self.ntotal = 0
         self.metric = 1
-        self._dirty = True
+        self.regrows = 0
         self._lock = threading.RLock()
-        self._store = None
+        self._reset_store()
 
+    # ------------------------------------------------------------------ device store
+    def _reset_store(self):
+        self._xt, self._cap = None, 0
+        self._start = np.zeros(self.nlist, np.int64)
+        self._size = np.zeros(self.nlist, np.int64)
+        self._lcap = np.zeros(self.nlist, np.int64)
+        self._ids_dev = self._start_dev = self._end_dev = None
+
+    def _regrow(self, need):
+        """New store with max(16, 1.5 x need) slots per list (multiple of 16); live rows move over."""
+        lcap = np.maximum(16, np.ceil(need * 1.5 / 16).astype(np.int64) * 16)
+        start = np.concatenate([[0], np.cumsum(lcap)[:-1]]).astype(np.int64)
+        cap = int(lcap.sum())
+        if cap >= 2 ** 31:
+            raise ValueError("IVF store of %d rows exceeds int32 row addressing" % cap)
+        xt = torch.zeros(self.d, cap, dtype=torch.float32, device=self.device)
+        ids = torch.full((cap,), -1, dtype=torch.int32, device=self.device)
+        live = self._size > 0
+        if live.any():
+            src = np.concatenate([np.arange(s, s + z) for s, z in zip(self._start[live], self._size[live])])
+            dst = np.concatenate([np.arange(s, s + z) for s, z in zip(start[live], self._size[live])])
+            src_d, dst_d = torch.from_numpy(src).to(self.device), torch.from_numpy(dst).to(self.device)
+            xt[:, dst_d] = self._xt[:, src_d]
+            ids[dst_d] = self._ids_dev[src_d]
+        self._xt, self._cap, self._ids_dev = xt, cap, ids
+        self._start, self._lcap = start, lcap
+        self.regrows += 1
+
+    def _append_device(self, x, a, ids):
+        """Rows x [n, d] (fp32, on the device) into lists a [n] (host int64) with original ids [n]."""
+        from ..ops import native
+
+        counts = np.bincount(a, minlength=self.nlist).astype(np.int64)
+        need = self._size + counts
+        if self._xt is None or bool((need > self._lcap).any()):
+            self._regrow(need)
+        order = np.argsort(a, kind="stable")
+        first = np.concatenate([[0], np.cumsum(counts)[:-1]])
+        rank = np.empty(len(a), np.int64)
+        rank[order] = np.arange(len(a)) - first[a[order]]
+        pos = torch.from_numpy((self._start[a] + self._size[a] + rank).astype(np.int32)).to(self.device)
+        native.l2_scatter(self._xt, self._cap, pos, x.contiguous())
+        self._ids_dev[pos.long()] = torch.from_numpy(ids.astype(np.int32)).to(self.device)
+        self._size = need
+        self._start_dev = torch.from_numpy(self._start.astype(np.int32)).to(self.device)
+        self._end_dev = torch.from_numpy((self._start + self._size).astype(np.int32)).to(self.device)
+
+    # ------------------------------------------------------------------ training / adds
     def train(self, x):
-        x = torch.as_tensor(np.asarray(x, dtype=np.float32)).to(self.device)
+        if isinstance(x, torch.Tensor):
+            x = x.detach().float().reshape(-1, self.d).to(self.device)
+        else:
+            x = torch.as_tensor(np.asarray(x, dtype=np.float32)).reshape(-1, self.d).to(self.device)
         c = kmeans(x, self.nlist)
         self.nlist = c.shape[0]
         self._set_centroids(c)
 
     def _set_centroids(self, c):
         self.centroids = c.float().contiguous()
+        self._cnorm = (self.centroids * self.centroids).sum(1)
         self.quant = FlatL2Index(self.d, device=self.device, capacity=self.nlist)
         self.quant.add(self.centroids.cpu())
         self.lists = [np.zeros((0, self.d), np.float32) for _ in range(self.nlist)]
         self.ids = [np.zeros(0, np.int64) for _ in range(self.nlist)]
+        self.ntotal = 0
+        self._reset_store()
         self.is_trained = True
 
     def add(self, x):
@@ -72,66 +158,55 @@ class IVFFlatIndex:
         with self._lock:
             if not self.is_trained:
                 self.train(x)
-            _, a = self.quant.search(torch.from_numpy(x), 1)
-            a = a[:, 0].numpy()
+            xd = torch.from_numpy(x).to(self.device)
+            a = assign(xd, self.centroids, self._cnorm).cpu().numpy().astype(np.int64)
             ids = np.arange(self.ntotal, self.ntotal + len(x), dtype=np.int64)
-            for li in np.unique(a):
-                m = a == li
-                self.lists[li] = np.concatenate([self.lists[li], x[m]])
-                self.ids[li] = np.concatenate([self.ids[li], ids[m]])
+            order = np.argsort(a, kind="stable")
+            bounds = np.searchsorted(a[order], np.arange(self.nlist + 1))
+            for li in np.nonzero(np.diff(bounds))[0]:
+                sel = order[bounds[li]:bounds[li + 1]]
+                self.lists[li] = np.concatenate([self.lists[li], x[sel]])
+                self.ids[li] = np.concatenate([self.ids[li], ids[sel]])
+            if self.device.type == "cuda":
+                self._append_device(xd, a, ids)
             self.ntotal += len(x)
-            self._dirty = True
 
-    def _build(self):
-        sizes = np.array([len(i) for i in self.ids], dtype=np.int64)
-        self._offsets = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-        allx = np.concatenate(self.lists) if self.ntotal else np.zeros((0, self.d), np.float32)
-        allid = np.concatenate(self.ids) if self.ntotal else np.zeros(0, np.int64)
-        self._store = FlatL2Index(self.d, device=self.device, capacity=max(1, self.ntotal))
-        self._store.add(allx)
-        self._ids_dev = torch.from_numpy(allid.astype(np.int32)).to(self.device)
-        self._ids_host = torch.from_numpy(allid)
-        self._off_dev = torch.from_numpy(self._offsets.astype(np.int32)).to(self.device)
-        self._dirty = False
-
+    # ------------------------------------------------------------------ query
     def search(self, q, k):
         q = torch.as_tensor(q).reshape(-1, self.d).float().contiguous()
         nq = q.shape[0]
         with self._lock:
             if self.ntotal == 0:
                 return torch.full((nq, k), FLT_MAX), torch.full((nq, k), -1, dtype=torch.int64)
-            if self._dirty:
-                self._build()
             nprobe = min(self.nprobe, self.nlist)
             _, probes = self.quant.search(q, nprobe)  # [nq, nprobe] host
             if self.device.type == "cuda" and k <= 64:
                 from ..ops import native
 
-                D, I = native.ivf_search(self._store._xt, self._store._cap, q.to(self.device),
-                                         probes.to(self.device).int(), self._off_dev, self._ids_dev, k)
+                D, I = native.ivf_search(self._xt, self._cap, q.to(self.device), probes.to(self.device).int(),
+                                         self._start_dev, self._ids_dev, k, max_list=int(self._size.max()),
+                                         ends=self._end_dev)
                 return D.cpu(), I.cpu()
-            return self._search_torch(q, probes, k)
+            return self._search_host(q, probes, k)
 
-    def _search_torch(self, q, probes, k):
-        xb = self._store.reconstruct_all()
-        xb = torch.from_numpy(xb)
+    def _search_host(self, q, probes, k):
         nq = q.shape[0]
         D = torch.full((nq, k), FLT_MAX)
         I = torch.full((nq, k), -1, dtype=torch.int64)
         for qi in range(nq):
-            rows = [torch.arange(int(self._offsets[p]), int(self._offsets[p + 1])) for p in probes[qi].tolist()]
-            rows = torch.cat(rows) if rows else torch.zeros(0, dtype=torch.int64)
-            if len(rows) == 0:
+            ls = [p for p in probes[qi].tolist() if p >= 0 and len(self.ids[p])]
+            if not ls:
                 continue
-            x = xb[rows]
+            x = torch.from_numpy(np.concatenate([self.lists[p] for p in ls]))
+            ids = torch.from_numpy(np.concatenate([self.ids[p] for p in ls]))
             d = ((x - q[qi][None]) ** 2).sum(1)
-            ids = self._ids_host[rows]
             order = torch.argsort(d, stable=True)
             kk = min(k, len(order))
             D[qi, :kk] = d[order[:kk]]
             I[qi, :kk] = ids[order[:kk]]
         return D, I
 
+    # ------------------------------------------------------------------ persistence
     def snapshot_writer(self):
         """Consistent copy of centroids + inverted lists now; the callable writes it atomically."""
         with self._lock:
@@ -150,9 +225,12 @@ class IVFFlatIndex:
     @classmethod
     def from_lists(cls, r, device="cpu"):
         idx = cls(r["d"], device=device, nlist=r["nlist"], nprobe=max(1, r["nprobe"]))
-        idx._set_centroids(torch.from_numpy(r["centroids"]).to(idx.device))
-        idx.lists = [np.asarray(x, np.float32) for x in r["lists"]]
+        idx._set_centroids(torch.from_numpy(np.asarray(r["centroids"], np.float32)).to(idx.device))
+        idx.lists = [np.asarray(x, np.float32).reshape(-1, idx.d) for x in r["lists"]]
         idx.ids = [np.asarray(x, np.int64) for x in r["ids"]]
         idx.ntotal = int(sum(len(x) for x in idx.ids))
-        idx._dirty = True
+        if idx.device.type == "cuda" and idx.ntotal:
+            a = np.concatenate([np.full(len(i), li, np.int64) for li, i in enumerate(idx.ids)])
+            x = torch.from_numpy(np.concatenate(idx.lists)).to(idx.device)
+            idx._append_device(x, a, np.concatenate(idx.ids))
         return idx

@@ -646,24 +646,50 @@ def _merge_all(pd, pi, nq, G, k):
     return pd.reshape(nq, k), pi.reshape(nq, k).long()
 
 
-def ivf_search(xt, cap, q, probes, offsets, ids_map, k, max_list=None):
-    """IVF-Flat scan of the probed lists. probes int32 [nq, nprobe] (device), offsets int32
-    [nlist+1] (device, list-ordered store), ids_map int32 [ntotal] original ids."""
+def ivf_search(xt, cap, q, probes, offsets, ids_map, k, max_list=None, ends=None):
+    """IVF-Flat scan of the probed lists. probes int32 [nq, nprobe] (device); list i occupies store
+    rows [offsets[i], ends[i]) (ends None: packed lists, offsets has nlist+1 entries); ids_map int32
+    [cap] original id of every store row."""
     _req(xt.dtype == torch.float32 and q.dtype == torch.float32 and q.is_contiguous(), "fp32")
     _req(probes.dtype == torch.int32 and offsets.dtype == torch.int32 and ids_map.dtype == torch.int32, "int32")
+    _req(ends is None or (ends.dtype == torch.int32 and ends.is_cuda), "ends int32")
     d = xt.shape[0]
     nq, nprobe = probes.shape
     _req(1 <= k <= 64 and d <= 2048, "k <= 64, d <= 2048")
     if max_list is None:
-        max_list = int((offsets[1:] - offsets[:-1]).max().item())
+        max_list = int(((ends - offsets[:ends.numel()]) if ends is not None else (offsets[1:] - offsets[:-1])).max())
     chunks = max(1, -(-max_list // 1024))
     G = nprobe * chunks
     pd = torch.empty((nq, G, k), dtype=torch.float32, device=q.device)
     pi = torch.empty((nq, G, k), dtype=torch.int32, device=q.device)
     check(_lib.lib().ragk_ivf_scan(xt.data_ptr(), cap, d, q.data_ptr(), nq, probes.data_ptr(), nprobe, chunks,
-                                   offsets.data_ptr(), ids_map.data_ptr(), k, pd.data_ptr(), pi.data_ptr(),
-                                   stream_ptr()), "ragk_ivf_scan")
+                                   offsets.data_ptr(), ptr(ends), ids_map.data_ptr(), k, pd.data_ptr(),
+                                   pi.data_ptr(), stream_ptr()), "ragk_ivf_scan")
     return _merge_all(pd, pi, nq, G, k)
+
+
+def kmeans_assign(x, c, cnorm=None):
+    """argmin_j ||x_i - c_j||^2 (ties -> lower j) and that squared distance, on the MFMA distance-GEMM
+    kernel (exact fp32 products). x [n, d], c [k, d] fp32 contiguous on the GPU; d % 64 == 0, <= 1024."""
+    _req(x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 2, "x fp32 [n, d]")
+    _req(c.is_cuda and c.dtype == torch.float32 and c.is_contiguous() and c.shape[1] == x.shape[1], "c fp32 [k, d]")
+    n, d = x.shape
+    _req(d % 64 == 0 and d <= 1024, "d % 64 == 0 and d <= 1024")
+    if cnorm is None:
+        cnorm = (c * c).sum(1)
+    a = torch.empty(n, dtype=torch.int32, device=x.device)
+    dist = torch.empty(n, dtype=torch.float32, device=x.device)
+    check(_lib.lib().ragk_kmeans_assign(x.data_ptr(), n, d, c.data_ptr(), cnorm.contiguous().data_ptr(), c.shape[0],
+                                        a.data_ptr(), dist.data_ptr(), stream_ptr()), "ragk_kmeans_assign")
+    return a, dist
+
+
+def l2_scatter(xt, cap, pos, x):
+    """Store rows x [n, d] at slots pos (int32, each < cap) of the column-major store xt[d][cap]."""
+    _req(x.dtype == torch.float32 and x.is_contiguous() and x.shape[1] == xt.shape[0], "x fp32 [n,d]")
+    _req(pos.dtype == torch.int32 and pos.is_cuda and pos.numel() == x.shape[0], "pos int32 [n]")
+    check(_lib.lib().ragk_l2_scatter(xt.data_ptr(), cap, xt.shape[0], pos.data_ptr(), x.data_ptr(), x.shape[0],
+                                     stream_ptr()), "ragk_l2_scatter")
 
 
 def l2_append(xt, cap, n0, x):

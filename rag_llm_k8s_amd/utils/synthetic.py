@@ -149,6 +149,47 @@ def train_wordpiece_tokenizer(out_dir, wm: WordModel = None, corpus_words=1_000_
     return tok
 
 
+def train_xlmr_unigram_tokenizer(out_dir, wm: WordModel = None, corpus_words=600_000, vocab=16000):
+    """XLM-R / bge-m3 style tokenizer.json: SentencePiece Unigram (nmt_nfkc Precompiled charsmap,
+    Metaspace, <s> $A </s>) with XLM-R's special ids <s>=0 <pad>=1 </s>=2 <unk>=3 -- the layout
+    transformers' SpmConverter writes for xlm-roberta. The piece inventory is trained on the synthetic
+    corpus (a real 250k-piece vocabulary needs a real corpus); ids stay < the model's vocab_size."""
+    import tempfile
+
+    import sentencepiece as spm
+    from sentencepiece import sentencepiece_model_pb2 as pb
+    from tokenizers import AddedToken, Regex, Tokenizer, decoders, models, normalizers, pre_tokenizers, processors
+
+    wm = wm or WordModel(seed=11)
+    with tempfile.TemporaryDirectory() as td:
+        corpus = os.path.join(td, "c.txt")
+        with open(corpus, "w", encoding="utf-8") as f:
+            f.write("\n".join(wm.corpus_lines(corpus_words)))
+        spm.SentencePieceTrainer.train(input=corpus, model_prefix=os.path.join(td, "m"), vocab_size=vocab,
+                                       model_type="unigram", normalization_rule_name="nmt_nfkc",
+                                       character_coverage=1.0, bos_id=0, pad_id=1, eos_id=2, unk_id=3,
+                                       hard_vocab_limit=False, minloglevel=2)
+        proto = pb.ModelProto()
+        with open(os.path.join(td, "m.model"), "rb") as f:
+            proto.ParseFromString(f.read())
+    pieces = [(p.piece, p.score) for p in proto.pieces]
+    tok = Tokenizer(models.Unigram(pieces, unk_id=3))
+    tok.normalizer = normalizers.Sequence([normalizers.Precompiled(proto.normalizer_spec.precompiled_charsmap),
+                                           normalizers.Replace(Regex(" {2,}"), " ")])
+    tok.pre_tokenizer = pre_tokenizers.Metaspace()
+    tok.decoder = decoders.Metaspace()
+    tok.add_special_tokens([AddedToken(t, special=True) for t in ("<s>", "<pad>", "</s>", "<unk>")])
+    tok.post_processor = processors.TemplateProcessing(
+        single="<s> $A </s>", pair="<s> $A </s> </s> $B </s>", special_tokens=[("<s>", 0), ("</s>", 2)])
+    os.makedirs(out_dir, exist_ok=True)
+    tok.save(os.path.join(out_dir, "tokenizer.json"))
+    with open(os.path.join(out_dir, "tokenizer_config.json"), "w") as f:
+        json.dump({"bos_token": "<s>", "eos_token": "</s>", "pad_token": "<pad>", "unk_token": "<unk>",
+                   "cls_token": "<s>", "sep_token": "</s>", "model_max_length": 8192,
+                   "tokenizer_class": "XLMRobertaTokenizer"}, f)
+    return tok
+
+
 # --------------------------------------------------------------------------- checkpoints
 def llama_state_dict(cfg, seed=0, std=0.02):
     g = torch.Generator().manual_seed(seed)
@@ -275,7 +316,10 @@ def write_encoder_checkpoint(out_dir, cfg, seed=0, wm=None):
                     "type": "sentence_transformers.models.Normalize"}], f, indent=2)
     save_file(encoder_state_dict(cfg, seed), os.path.join(out_dir, "model.safetensors"), metadata={"format": "pt"})
     if not os.path.exists(os.path.join(out_dir, "tokenizer.json")):
-        train_wordpiece_tokenizer(out_dir, wm, vocab=cfg.vocab_size)
+        if cfg.model_type == "xlm-roberta":
+            train_xlmr_unigram_tokenizer(out_dir, wm, vocab=min(16000, cfg.vocab_size))
+        else:
+            train_wordpiece_tokenizer(out_dir, wm, vocab=cfg.vocab_size)
 
 
 def write_pdf_corpus(out_dir, n_docs, pages=4, words_per_page=600, wm=None, seed=0):

@@ -20,7 +20,8 @@ import numpy as np
 import torch
 
 from ..config import RagConfig
-from .synthetic import WordModel, train_llama3_tokenizer, train_small_bpe, train_wordpiece_tokenizer
+from .synthetic import (WordModel, train_llama3_tokenizer, train_small_bpe, train_wordpiece_tokenizer,
+                        train_xlmr_unigram_tokenizer)
 
 
 def asset_dir(tag):
@@ -48,10 +49,12 @@ def _once(path, build, ctx=None):
             raise TimeoutError("asset %s never appeared" % path)
 
 
-def make_tokenizers(wm, llm_vocab, enc_vocab, ctx=None):
+def make_tokenizers(wm, llm_vocab, enc_vocab, ctx=None, enc_kind="wordpiece"):
+    """LLM BPE + encoder tokenizer: BERT WordPiece (MiniLM / bge-large) or XLM-R SentencePiece
+    Unigram (bge-m3)."""
     from ..runtime.tokenizer import Tokenizer
 
-    tag = "tok_%d_%d" % (llm_vocab, enc_vocab)
+    tag = "tok_%d_%d" % (llm_vocab, enc_vocab) + ("" if enc_kind == "wordpiece" else "_" + enc_kind)
     d = asset_dir(tag)
     llm_d, enc_d = os.path.join(d, "llm"), os.path.join(d, "enc")
 
@@ -60,7 +63,10 @@ def make_tokenizers(wm, llm_vocab, enc_vocab, ctx=None):
             train_llama3_tokenizer(llm_d, wm)
         else:
             train_small_bpe(llm_d, llm_vocab, wm)
-        train_wordpiece_tokenizer(enc_d, wm, corpus_words=600_000, vocab=enc_vocab)
+        if enc_kind == "unigram":
+            train_xlmr_unigram_tokenizer(enc_d, wm, corpus_words=600_000, vocab=enc_vocab)
+        else:
+            train_wordpiece_tokenizer(enc_d, wm, corpus_words=600_000, vocab=enc_vocab)
 
     _once(os.path.join(d, "tok"), build, ctx)
     return Tokenizer(llm_d), Tokenizer(enc_d)
@@ -111,10 +117,9 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     ecfg = {"minilm": E.minilm_l6, "bge-large": E.bge_large_en, "bge-m3": E.bge_m3,
             "tiny": lambda: E.EncoderConfig(vocab_size=2048, hidden_size=128, num_hidden_layers=2,
                                             num_attention_heads=4, intermediate_size=256, max_seq_length=128)}[embedder]()
-    enc_vocab = ecfg.vocab_size if ecfg.model_type == "bert" else 30522
-    llm_tok, enc_tok = make_tokenizers(wm, lcfg.vocab_size, enc_vocab, ctx)
-    if ecfg.model_type != "bert":  # XLM-R shaped: reuse the WordPiece ids (random weights, vocab 250002)
-        ecfg.model_type = "bert"
+    xlmr = ecfg.model_type == "xlm-roberta"  # bge-m3: XLM-R embeddings (position offset) + Unigram ids
+    enc_vocab = min(16000, ecfg.vocab_size) if xlmr else ecfg.vocab_size
+    llm_tok, enc_tok = make_tokenizers(wm, lcfg.vocab_size, enc_vocab, ctx, "unigram" if xlmr else "wordpiece")
     t["tokenizers_s"] = time.time() - t0
 
     t0 = time.time()
@@ -143,6 +148,9 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
                     index_type=index_type, seed=seed, max_prefill_tokens=max_prefill_tokens, ignore_eos=ignore_eos)
     store = DocumentStore(cfg.index_path, emb.dim, device=device, index_type=index_type)
     vecs = emb.embed(chunks)
+    if device.startswith("cuda"):
+        torch.cuda.synchronize()
+    t["embed_s"] = time.time() - t0  # tokenize + encode of the n_chunks corpus (ingest throughput)
     meta = [{"filename": "synthetic_%05d.pdf" % (i // 20), "chunk_id": i % 20, "text": c}
             for i, c in enumerate(chunks)]
     store.add(vecs, meta, dedupe=False, persist=False)

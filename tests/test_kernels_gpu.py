@@ -280,7 +280,10 @@ def _paged_setup(lens, Hkv, D, seed=0):
 
 
 @pytest.mark.parametrize("q_lens,kv_lens,Hq,Hkv", [([37], [37], 8, 2), ([100, 64, 1], [100, 300, 129], 32, 8),
-                                                   ([200], [200], 4, 4), ([5, 70], [513, 70], 8, 1)])
+                                                   ([200], [200], 4, 4), ([5, 70], [513, 70], 8, 1),
+                                                   # 5.2k RAG prompt, chunked prefill at 8B heads: later chunks
+                                                   # have q_len < kv_len, 82 KV blocks (> 80)
+                                                   ([2048, 1104], [4096, 5200], 32, 8)])
 def test_attn_prefill_paged(native, q_lens, kv_lens, Hq, Hkv):
     D = 128
     torch.manual_seed(9)
