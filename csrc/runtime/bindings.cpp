@@ -88,25 +88,59 @@ PYBIND11_MODULE(_ragk_rt, m) {
   py::class_<Tokenizer>(m, "Tokenizer")
       .def(py::init<const std::string&>())
       .def("encode",
-           [](const Tokenizer& t, const std::string& s, bool add_special) {
+           [](const Tokenizer& t, const std::string& s, bool add_special, int max_tokens) {
              std::vector<int> ids;
              {
                py::gil_scoped_release nogil;
-               ids = t.encode(s, add_special);
+               ids = t.encode(s, add_special, max_tokens);
              }
              return ids;
            },
-           py::arg("text"), py::arg("add_special_tokens") = true)
+           py::arg("text"), py::arg("add_special_tokens") = true, py::arg("max_tokens") = -1)
       .def("encode_batch",
-           [](const Tokenizer& t, const std::vector<std::string>& texts, bool add_special, int threads) {
+           [](const Tokenizer& t, const std::vector<std::string>& texts, bool add_special, int threads,
+              int max_tokens) {
              std::vector<std::vector<int>> ids;
              {
                py::gil_scoped_release nogil;
-               ids = t.encode_batch(texts, add_special, threads);
+               ids = t.encode_batch(texts, add_special, threads, max_tokens);
              }
              return ids;
            },
-           py::arg("texts"), py::arg("add_special_tokens") = true, py::arg("threads") = 8)
+           py::arg("texts"), py::arg("add_special_tokens") = true, py::arg("threads") = 8,
+           py::arg("max_tokens") = -1)
+      // ingest path: (ids int32 [sum lens], lens int32 [n]) with right truncation to max_length that
+      // keeps a trailing special token -- no per-token Python objects on the way to the encoder
+      .def("encode_batch_flat",
+           [](const Tokenizer& t, const std::vector<std::string>& texts, bool add_special, int threads,
+              int max_length) {
+             std::vector<int32_t> flat, lens(texts.size());
+             {
+               py::gil_scoped_release nogil;
+               std::vector<std::vector<int>> ids = t.encode_batch(texts, add_special, threads, max_length);
+               size_t tot = 0;
+               for (size_t i = 0; i < ids.size(); ++i) {
+                 std::vector<int>& v = ids[i];
+                 if (max_length > 0 && (int)v.size() > max_length) {
+                   const int last = v.back();
+                   if (add_special && t.is_special(last)) {
+                     v.resize(max_length - 1);
+                     v.push_back(last);
+                   } else {
+                     v.resize(max_length);
+                   }
+                 }
+                 lens[i] = (int32_t)v.size();
+                 tot += v.size();
+               }
+               flat.reserve(tot);
+               for (const auto& v : ids) flat.insert(flat.end(), v.begin(), v.end());
+             }
+             return py::make_tuple(py::array_t<int32_t>(flat.size(), flat.data()),
+                                   py::array_t<int32_t>(lens.size(), lens.data()));
+           },
+           py::arg("texts"), py::arg("add_special_tokens") = true, py::arg("threads") = 8,
+           py::arg("max_length") = -1)
       .def("decode", &Tokenizer::decode, py::arg("ids"), py::arg("skip_special_tokens") = true)
       .def("vocab_size", &Tokenizer::vocab_size)
       .def("token_to_id",

@@ -222,6 +222,8 @@ Tokenizer::Tokenizer(const std::string& path) : uid_(g_tok_uid_next()) {
   load_pre(j.get("pre_tokenizer"));
   load_post(j.get("post_processor"));
   load_decoder(j.get("decoder"));
+  slice_safe_ = pre_ == PRE_BERT || pre_ == PRE_WHITESPACE;
+  for (const auto& st : norm_) slice_safe_ = slice_safe_ && (st.kind == NormStep::BERT || st.kind == NormStep::LOWER);
 }
 
 void Tokenizer::load_model(const Json& m) {
@@ -712,13 +714,14 @@ class EncodePool {
 }  // namespace
 
 std::vector<std::vector<int>> Tokenizer::encode_batch(const std::vector<std::string>& texts, bool add_special,
-                                                      int threads) const {
+                                                      int threads, int max_tokens) const {
   std::vector<std::vector<int>> out(texts.size());
   const int n = (int)texts.size();
+  const size_t budget = max_tokens < 0 ? SIZE_MAX : (size_t)max_tokens;
   EncodePool& pool = EncodePool::get();
   const int nt = std::max(1, std::min({threads, n, pool.size()}));
   if (nt == 1) {
-    for (int i = 0; i < n; ++i) out[i] = encode(texts[i], add_special);
+    for (int i = 0; i < n; ++i) out[i] = encode_impl(texts[i], add_special, nullptr, budget);
     return out;
   }
   std::atomic<int> next{0};
@@ -729,7 +732,7 @@ std::vector<std::vector<int>> Tokenizer::encode_batch(const std::vector<std::str
     thread_local std::unordered_map<unsigned long long, WordCache> caches;
     WordCache& local = caches[uid];
     try {
-      for (int i = next++; i < n; i = next++) out[i] = encode_impl(texts[i], add_special, &local);
+      for (int i = next++; i < n; i = next++) out[i] = encode_impl(texts[i], add_special, &local, budget);
     } catch (...) {
       std::lock_guard<std::mutex> g(err_mu);
       if (!err) err = std::current_exception();
@@ -812,7 +815,25 @@ void Tokenizer::unigram_word(const std::string& word, std::vector<int>& out) con
   }
 }
 
-void Tokenizer::encode_segment(const std::string& seg, std::vector<int>& out, WordCache* local) const {
+void Tokenizer::encode_segment(const std::string& seg, std::vector<int>& out, WordCache* local, size_t budget) const {
+  // Truncated encode of a long text with a per-character normalizer and whitespace-delimited words
+  // (BERT WordPiece: MiniLM / bge-large ingest of 1000-word chunks truncated to 256 / 512 tokens):
+  // normalise and split only as much text as the budget needs, in slices cut at ASCII whitespace (a
+  // word boundary before and after normalisation), instead of the whole chunk.
+  if (budget != SIZE_MAX && slice_safe_ && seg.size() > 2048) {
+    size_t pos = 0;
+    while (pos < seg.size() && out.size() < budget) {
+      size_t end = std::min(seg.size(), pos + std::max<size_t>(1024, (budget - out.size()) * 8));
+      while (end < seg.size() && seg[end] != ' ' && seg[end] != '\t' && seg[end] != '\n' && seg[end] != '\r') ++end;
+      encode_words(seg.substr(pos, end - pos), out, local, budget);
+      pos = end;
+    }
+    return;
+  }
+  encode_words(seg, out, local, budget);
+}
+
+void Tokenizer::encode_words(const std::string& seg, std::vector<int>& out, WordCache* local, size_t budget) const {
   std::vector<uint32_t> cps = utf8_decode(norm_.empty() ? seg : normalize(seg));
   std::vector<std::pair<size_t, size_t>> words;
   const size_t n = cps.size();
@@ -856,6 +877,7 @@ void Tokenizer::encode_segment(const std::string& seg, std::vector<int>& out, Wo
     words.push_back({0, n});
   }
   for (auto& w : words) {
+    if (out.size() >= budget) break;  // truncated encode: later words cannot change this prefix
     std::string piece = utf8_encode(cps, w.first, w.second);
     if (model_ == BPE) {
       if (byte_level_) {
@@ -864,28 +886,40 @@ void Tokenizer::encode_segment(const std::string& seg, std::vector<int>& out, Wo
         piece.swap(mapped);
       }
       bpe_word(piece, out, local);
-    } else if (model_ == WORDPIECE) {
-      wordpiece_word(std::vector<uint32_t>(cps.begin() + w.first, cps.begin() + w.second), out);
     } else {
-      unigram_word(piece, out);
+      // WordPiece / Unigram: memoised per word in the batch worker's private cache (Zipfian text
+      // repeats words; no lock on this path)
+      if (local) {
+        auto c = local->find(piece);
+        if (c != local->end()) {
+          out.insert(out.end(), c->second.begin(), c->second.end());
+          continue;
+        }
+      }
+      std::vector<int> ids;
+      if (model_ == WORDPIECE) wordpiece_word(std::vector<uint32_t>(cps.begin() + w.first, cps.begin() + w.second), ids);
+      else unigram_word(piece, ids);
+      out.insert(out.end(), ids.begin(), ids.end());
+      if (local && local->size() < 200000) local->emplace(std::move(piece), std::move(ids));
     }
   }
 }
 
-std::vector<int> Tokenizer::encode(const std::string& text, bool add_special_tokens) const {
-  return encode_impl(text, add_special_tokens, nullptr);
+std::vector<int> Tokenizer::encode(const std::string& text, bool add_special_tokens, int max_tokens) const {
+  return encode_impl(text, add_special_tokens, nullptr, max_tokens < 0 ? SIZE_MAX : (size_t)max_tokens);
 }
 
-std::vector<int> Tokenizer::encode_impl(const std::string& text, bool add_special_tokens, WordCache* local) const {
+std::vector<int> Tokenizer::encode_impl(const std::string& text, bool add_special_tokens, WordCache* local,
+                                        size_t budget) const {
   std::vector<int> body;
   size_t seg_start = 0, i = 0;
   const size_t n = text.size();
-  while (i < n) {
+  while (i < n && body.size() < budget) {
     if (!added_first_bytes_.empty() && added_first_bytes_.count((unsigned char)text[i])) {
       bool hit = false;
       for (auto& a : added_) {
         if (!a.content.empty() && text.compare(i, a.content.size(), a.content) == 0) {
-          if (i > seg_start) encode_segment(text.substr(seg_start, i - seg_start), body, local);
+          if (i > seg_start) encode_segment(text.substr(seg_start, i - seg_start), body, local, budget);
           body.push_back(a.id);
           i += a.content.size();
           seg_start = i;
@@ -897,7 +931,7 @@ std::vector<int> Tokenizer::encode_impl(const std::string& text, bool add_specia
     }
     ++i;
   }
-  if (seg_start < n) encode_segment(text.substr(seg_start), body, local);
+  if (seg_start < n && body.size() < budget) encode_segment(text.substr(seg_start), body, local, budget);
   if (!add_special_tokens || !has_template_) return body;
   std::vector<int> out;
   for (int t : template_single_) {

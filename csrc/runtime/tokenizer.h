@@ -23,13 +23,16 @@ namespace ragk_rt {
 class Tokenizer {
  public:
   explicit Tokenizer(const std::string& path);
-  std::vector<int> encode(const std::string& text, bool add_special_tokens) const;  // thread-safe
+  // max_tokens >= 0: stop once the body holds max_tokens tokens (every model here tokenizes word by
+  // word, so the result is a prefix of the full encoding: exact under right truncation to max_tokens)
+  std::vector<int> encode(const std::string& text, bool add_special_tokens, int max_tokens = -1) const;  // thread-safe
   // many texts on `threads` worker threads (the per-word BPE cache is shared under a shared_mutex)
   std::vector<std::vector<int>> encode_batch(const std::vector<std::string>& texts, bool add_special_tokens,
-                                             int threads) const;
+                                             int threads, int max_tokens = -1) const;
   std::string decode(const std::vector<int>& ids, bool skip_special_tokens) const;
   int vocab_size() const { return (int)id_to_tok_.size(); }
   int token_to_id(const std::string& t) const;
+  bool is_special(int id) const { return special_ids_.count(id) != 0; }
   std::string model_type() const { return model_name_; }
 
  private:
@@ -92,8 +95,12 @@ class Tokenizer {
   void load_decoder(const Json* d);
   using WordCache = std::unordered_map<std::string, std::vector<int>>;
   // local != null: a caller-owned (per-thread) word cache, used without locking
-  std::vector<int> encode_impl(const std::string& text, bool add_special_tokens, WordCache* local) const;
-  void encode_segment(const std::string& seg, std::vector<int>& out, WordCache* local) const;
+  std::vector<int> encode_impl(const std::string& text, bool add_special_tokens, WordCache* local,
+                               size_t budget = SIZE_MAX) const;
+  void encode_segment(const std::string& seg, std::vector<int>& out, WordCache* local,
+                      size_t budget = SIZE_MAX) const;
+  void encode_words(const std::string& seg, std::vector<int>& out, WordCache* local, size_t budget) const;
+  bool slice_safe_ = false;  // normaliser per character + whitespace pre-tokenizer: slicing at spaces is exact
   std::string normalize(const std::string& s) const;
   bool pc_transform(const char* p, size_t n, std::string& out) const;
   void bpe_word(const std::string& word, std::vector<int>& out, WordCache* local) const;

@@ -179,15 +179,30 @@ class IVFFlatIndex:
             if self.ntotal == 0:
                 return torch.full((nq, k), FLT_MAX), torch.full((nq, k), -1, dtype=torch.int64)
             nprobe = min(self.nprobe, self.nlist)
-            _, probes = self.quant.search(q, nprobe)  # [nq, nprobe] host
             if self.device.type == "cuda" and k <= 64:
                 from ..ops import native
 
-                D, I = native.ivf_search(self._xt, self._cap, q.to(self.device), probes.to(self.device).int(),
-                                         self._start_dev, self._ids_dev, k, max_list=int(self._size.max()),
-                                         ends=self._end_dev)
+                qd = q.to(self.device, non_blocking=True)
+                probes = self._coarse_device(qd, nprobe)  # stays on the device: one host sync per search
+                D, I = native.ivf_search(self._xt, self._cap, qd, probes, self._start_dev, self._ids_dev, k,
+                                         max_list=int(self._size.max()), ends=self._end_dev)
                 return D.cpu(), I.cpu()
+            _, probes = self.quant.search(q, nprobe) if nprobe <= 64 else self._coarse_torch(q, nprobe)
             return self._search_host(q, probes, k)
+
+    def _coarse_device(self, qd, nprobe):
+        """Top-nprobe centroids per query as int32 [nq, nprobe] on the device (HBM flat kernel up to
+        64 probes, a torch distance GEMM + topk beyond)."""
+        if nprobe <= 64:
+            _, I = self.quant.search_device(qd, nprobe)
+            return I.int()
+        return self._coarse_torch(qd, nprobe)[1].int()
+
+    def _coarse_torch(self, q, nprobe):
+        c = self.centroids.to(q.device)
+        d = (c * c).sum(1)[None] - 2 * q @ c.t()
+        D, I = d.topk(nprobe, dim=1, largest=False)
+        return D, I
 
     def _search_host(self, q, probes, k):
         nq = q.shape[0]

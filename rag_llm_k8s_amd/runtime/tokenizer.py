@@ -15,7 +15,17 @@ from __future__ import annotations
 import json
 import os
 
-ENCODE_THREADS = int(os.environ.get("RAGK_TOKENIZER_THREADS", "8"))
+import numpy as np
+
+def _default_threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:
+        n = os.cpu_count() or 8
+    return max(1, min(16, n))
+
+
+ENCODE_THREADS = int(os.environ.get("RAGK_TOKENIZER_THREADS", "0")) or _default_threads()
 
 
 class Tokenizer:
@@ -79,8 +89,8 @@ class Tokenizer:
     def encode(self, text, add_special_tokens=True, max_length=None):
         if self.backend == "hf":
             ids = self.impl.encode(text, add_special_tokens=add_special_tokens).ids
-        else:
-            ids = self.impl.encode(text, add_special_tokens)
+        else:  # native: stops tokenizing once max_length body tokens exist (same prefix, less work)
+            ids = self.impl.encode(text, add_special_tokens, -1 if max_length is None else int(max_length))
         if max_length is not None and len(ids) > max_length:
             ids = self._truncate(ids, max_length, add_special_tokens)
         return list(ids)
@@ -96,13 +106,25 @@ class Tokenizer:
             encs = self.impl.encode_batch(list(texts), add_special_tokens=add_special_tokens)
             out = [e.ids for e in encs]
         elif hasattr(self.impl, "encode_batch"):  # C++ worker threads, GIL released
-            out = self.impl.encode_batch(list(texts), add_special_tokens, ENCODE_THREADS)
+            out = self.impl.encode_batch(list(texts), add_special_tokens, ENCODE_THREADS,
+                                         -1 if max_length is None else int(max_length))
         else:
             out = [self.impl.encode(t, add_special_tokens) for t in texts]
         if max_length is not None:
             out = [self._truncate(list(x), max_length, add_special_tokens) if len(x) > max_length else list(x)
                    for x in out]
         return out
+
+    def encode_batch_flat(self, texts, add_special_tokens=True, max_length=None):
+        """(ids int32 [sum of lengths], lens int32 [n]) numpy arrays: encode_batch + truncation, built in
+        C++ on the native backend (the embedding engine's ingest path)."""
+        if self.backend == "native" and hasattr(self.impl, "encode_batch_flat"):
+            return self.impl.encode_batch_flat(list(texts), add_special_tokens, ENCODE_THREADS,
+                                               -1 if max_length is None else int(max_length))
+        out = self.encode_batch(texts, add_special_tokens, max_length)
+        lens = np.fromiter((len(x) for x in out), dtype=np.int32, count=len(out))
+        ids = np.fromiter((t for x in out for t in x), dtype=np.int32, count=int(lens.sum()))
+        return ids, lens
 
     def decode(self, ids, skip_special_tokens=True):
         ids = [int(i) for i in ids if 0 <= int(i) < self.vocab_size]

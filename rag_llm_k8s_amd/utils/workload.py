@@ -84,6 +84,33 @@ def make_chunks(wm, n_chunks, chunk_words, seed=0):
     return out
 
 
+class TopicCorpus:
+    """Chunks with topical structure, as a real corpus has (documents cluster by subject, which is what
+    makes an IVF index's coarse quantizer useful): topic t owns `topic_words` mid-frequency words; a chunk
+    of topic t draws a `mix` share of its words from them and the rest from the global Zipf law. Queries
+    are drawn the same way from a topic, so their true neighbours are that topic's chunks."""
+
+    def __init__(self, wm, n_topics=2000, topic_words=400, mix=0.5, seed=0):
+        rng = np.random.default_rng(seed + 99)
+        lo, hi = 500, min(len(wm.words), 200000)
+        self.wm, self.mix = wm, mix
+        self.vocab = rng.integers(lo, hi, size=(n_topics, topic_words))
+
+    def _words(self, n, words, rng):
+        topics = rng.integers(0, len(self.vocab), n)
+        glob = np.minimum(np.searchsorted(self.wm.cdf, rng.random((n, words)), side="right"), len(self.wm.words) - 1)
+        top = self.vocab[topics[:, None], rng.integers(0, self.vocab.shape[1], (n, words))]
+        idx = np.where(rng.random((n, words)) < self.mix, top, glob)
+        w = self.wm.words[idx]
+        return [" ".join(r) for r in w], topics
+
+    def chunks(self, n, words, seed):
+        return self._words(n, words, np.random.default_rng(seed))[0]
+
+    def queries(self, n, words, seed):
+        return [q.capitalize() + "?" for q in self._words(n, words, np.random.default_rng(seed + 7))[0]]
+
+
 def make_queries(wm, n, seed, words=12):
     rng = np.random.default_rng(seed)
     qs = []

@@ -239,3 +239,28 @@ def test_unigram_precompiled_charsmap_matches_hf(rt, tmp_path):
         n = rt.Tokenizer(p)
         for t in PC_TEXTS + [wm.text(60) for _ in range(5)]:
             assert n.encode(t, False) == tok.encode(t, add_special_tokens=False).ids, t
+
+
+def test_truncated_encode_equals_full_then_truncate(rt, corpus, tmp_path):
+    """Budgeted native encode (stops once max_length body tokens exist; encoder ingest truncates 1000-word
+    chunks to 256/512 tokens) == full encode + right truncation keeping the trailing special, for
+    WordPiece (BERT), byte-level BPE with specials, and XLM-R Unigram."""
+    from rag_llm_k8s_amd.runtime.tokenizer import Tokenizer
+    from rag_llm_k8s_amd.utils.synthetic import train_wordpiece_tokenizer, train_xlmr_unigram_tokenizer
+
+    wm, lines = corpus
+    dirs = [str(tmp_path / "wp"), str(tmp_path / "uni")]
+    train_wordpiece_tokenizer(dirs[0], wm, corpus_words=60000, vocab=2000)
+    train_xlmr_unigram_tokenizer(dirs[1], wm, corpus_words=60000, vocab=1200)
+    texts = TEXTS + [wm.text(n) for n in (3, 40, 400)]
+    for d in dirs:
+        nat = Tokenizer(d, backend="native")
+        hf = Tokenizer(d, backend="hf")
+        assert nat.backend == "native"
+        for L in (1, 2, 3, 7, 64, 100000):
+            got = nat.encode_batch(texts, add_special_tokens=True, max_length=L)
+            ref = hf.encode_batch(texts, add_special_tokens=True, max_length=L)
+            assert got == ref, (d, L)
+            assert [nat.encode(t, True, max_length=L) for t in texts] == ref
+            assert nat.encode_batch(texts, add_special_tokens=False, max_length=L) == \
+                hf.encode_batch(texts, add_special_tokens=False, max_length=L)
