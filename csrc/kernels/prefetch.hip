@@ -1,0 +1,91 @@
+// Weight prefetch into the MALL (Infinity Cache, 256 MB memory-side cache on MI355X).
+//
+// At decode batch sizes a Llama layer alternates HBM-bound weight GEMMs with latency-bound kernels
+// (rope/KV write, split-K attention, its merge, the residual+norm consumers) during which HBM is
+// nearly idle. A prefetch kernel on a side stream, launched when those latency-bound kernels start,
+// reads the NEXT GEMMs' weights once with the default (allocating) cache policy, so the GEMM then
+// streams part of its matrix from the MALL instead of HBM. Reads only; a result is stored only
+// when the XOR of the data equals a runtime key (keeps the loads live; a hit is a harmless
+// write to a scratch sink) -- vector stores only.
+#include "common.h"
+using namespace ragk;
+
+namespace {
+
+constexpr int PF_THREADS = 256;
+
+__global__ __launch_bounds__(PF_THREADS) void prefetch_kernel(const u32x4* __restrict__ p, size_t n16,
+                                                              unsigned* __restrict__ sink, unsigned key) {
+  // block b reads a contiguous range, 8 independent 16-B loads per lane in flight per round
+  const size_t per = (n16 + gridDim.x - 1) / gridDim.x;
+  const size_t b0 = (size_t)blockIdx.x * per;
+  const size_t b1 = b0 + per < n16 ? b0 + per : n16;
+  unsigned acc = 0;
+  for (size_t i = b0 + threadIdx.x; i < b1; i += (size_t)PF_THREADS * 8) {
+    u32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const size_t k = i + (size_t)j * PF_THREADS;
+      v[j] = k < b1 ? p[k] : (u32x4){0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc ^= v[j][0] ^ v[j][3];
+  }
+  if (acc == key) sink[blockIdx.x] = acc;  // data-dependent (key is a runtime argument): keeps the loads live
+}
+
+// Latency stand-in for experiments: one wave spins `us` microseconds on the 100 MHz real-time counter.
+__global__ void spin_kernel(long long ticks) {
+  const long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+// Experiment: block 0 spins `ticks` (a latency-bound kernel's duration), blocks 1.. prefetch.
+__global__ __launch_bounds__(PF_THREADS) void spin_prefetch_kernel(long long ticks, const u32x4* __restrict__ p,
+                                                                   size_t n16, unsigned* __restrict__ sink,
+                                                                   unsigned key) {
+  if (blockIdx.x == 0) {
+    const long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+    return;
+  }
+  const int nb = gridDim.x - 1, bid = blockIdx.x - 1;
+  const size_t per = (n16 + nb - 1) / nb;
+  const size_t b0 = (size_t)bid * per;
+  const size_t b1 = b0 + per < n16 ? b0 + per : n16;
+  unsigned acc = 0;
+  for (size_t i = b0 + threadIdx.x; i < b1; i += (size_t)PF_THREADS * 8) {
+    u32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const size_t k = i + (size_t)j * PF_THREADS;
+      v[j] = k < b1 ? p[k] : (u32x4){0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc ^= v[j][0] ^ v[j][3];
+  }
+  if (acc == key) sink[blockIdx.x] = acc;
+}
+
+}  // namespace
+
+RAGK_API int ragk_spin_prefetch(int us, const void* p, long long bytes, int blocks, unsigned* sink, hipStream_t st) {
+  if (((uintptr_t)p & 15) || !sink || blocks < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(spin_prefetch_kernel, dim3(1 + (bytes >= 16 ? blocks : 0)), dim3(PF_THREADS), 0, st,
+                     (long long)us * 100, (const u32x4*)p, (size_t)(bytes / 16), sink, 0x9e3779b9u);
+  return (int)hipGetLastError();
+}
+
+RAGK_API int ragk_prefetch(const void* p, long long bytes, int blocks, unsigned* sink, hipStream_t st) {
+  if (bytes < 16 || blocks <= 0) return 0;
+  if (((uintptr_t)p & 15) || !sink) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(prefetch_kernel, dim3(blocks), dim3(PF_THREADS), 0, st, (const u32x4*)p, (size_t)bytes / 16,
+                     sink, 0x9e3779b9u);
+  return (int)hipGetLastError();
+}
+
+RAGK_API int ragk_spin_us(int us, hipStream_t st) {
+  if (us <= 0) return 0;
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, st, (long long)us * 100);
+  return (int)hipGetLastError();
+}

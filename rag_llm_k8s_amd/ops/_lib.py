@@ -59,6 +59,9 @@ _SIGS = {
     "ragk_ivf_scan": [P, I, I, P, I, P, I, I, P, P, P, I, P, P, S],
     "ragk_kmeans_assign": [P, I, I, P, P, I, P, P, S],
     "ragk_l2_scatter": [P, I, I, P, P, I, S],
+    "ragk_prefetch": [P, ctypes.c_longlong, I, P, S],
+    "ragk_spin_us": [I, S],
+    "ragk_spin_prefetch": [I, P, ctypes.c_longlong, I, P, S],
     "ragk_l2_append": [P, I, I, I, P, I, S],
     "ragk_l2_gather": [P, I, I, P, I, P, S],
     "ragk_gemm_stream": [P, I, P, I, P, P, I, P, P, I, I, I, I, I, I, I, P, P, S],

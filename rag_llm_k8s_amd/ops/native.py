@@ -696,3 +696,23 @@ def l2_append(xt, cap, n0, x):
     _req(x.dtype == torch.float32 and x.is_contiguous() and x.shape[1] == xt.shape[0], "x fp32 [n,d]")
     check(_lib.lib().ragk_l2_append(xt.data_ptr(), cap, xt.shape[0], n0, x.data_ptr(), x.shape[0], stream_ptr()),
           "ragk_l2_append")
+
+
+# ----------------------------------------------------------------------------- MALL prefetch
+_pf_sink = {}
+
+
+def prefetch(t, nbytes=None, blocks=64):
+    """Read the first `nbytes` of tensor `t` once with the allocating cache policy (csrc/kernels/
+    prefetch.hip) so a following kernel finds them in the MALL. Reads only."""
+    key = str(t.device)
+    if key not in _pf_sink:
+        _pf_sink[key] = torch.zeros(4096, dtype=torch.int32, device=t.device)
+    nb = t.numel() * t.element_size() if nbytes is None else min(int(nbytes), t.numel() * t.element_size())
+    _req(t.data_ptr() % 16 == 0 and blocks <= 4096, "16-B aligned, <= 4096 blocks")
+    check(_lib.lib().ragk_prefetch(t.data_ptr(), nb, int(blocks), _pf_sink[key].data_ptr(), stream_ptr()),
+          "ragk_prefetch")
+
+
+def spin_us(us):
+    check(_lib.lib().ragk_spin_us(int(us), stream_ptr()), "ragk_spin_us")

@@ -46,6 +46,17 @@ def main():
         n = eng.stats["decode_steps"] - n0
         print("B=%d ctx=%d: %d decode steps, %.3f ms/step (engine decode_s %.3f ms/step), %.0f tok/s" % (
             B, plen, n, dt / n * 1e3, (eng.stats["decode_s"] - d0) / n * 1e3, B * n / dt), flush=True)
+        # pure GPU time of the captured decode step: back-to-back replays of the B-bucket graph
+        # (stale inputs are fine: same shapes and context lengths), no host work in between
+        e = eng.graphs.get(B)
+        if e is not None and e["graph"] is not None:
+            e["graph"].replay()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(20):
+                e["graph"].replay()
+            torch.cuda.synchronize()
+            print("B=%d graph replay only: %.3f ms/step" % (B, (time.perf_counter() - t0) / 20 * 1e3), flush=True)
         del eng
         torch.cuda.empty_cache()
 

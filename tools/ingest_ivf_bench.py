@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--queries", type=int, default=1000)
     ap.add_argument("--topics", type=int, default=2000,
                     help="topical structure of the IVF corpus (0: plain Zipf words, no clusters)")
+    ap.add_argument("--topic-mix", type=float, default=0.5, help="share of a chunk's words drawn from its topic")
+    ap.add_argument("--topic-words", type=int, default=400, help="vocabulary size of one topic")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
 
@@ -103,7 +105,7 @@ def main():
             cfg = E.minilm_l6()
             emb = EmbeddingEngine(E.EncoderModel(cfg, E.EncoderWeights.random(cfg, dev, seed=1), dev), tok)
         M, d = a.ivf_chunks, emb.dim
-        tc = TopicCorpus(wm, n_topics=a.topics) if a.topics else None
+        tc = TopicCorpus(wm, n_topics=a.topics, topic_words=a.topic_words, mix=a.topic_mix) if a.topics else None
         xb = torch.empty((M, d), dtype=torch.float32, device=dev)
         t0 = time.time()
         bs = 50000
@@ -127,6 +129,12 @@ def main():
         sync()
         t_flat = time.time() - t0
         Df, If = flat.search(q, 4)
+        # relative contrast (mean distance to a random base vector / distance to the 4th neighbour): ~1
+        # means the neighbourhoods are barely distinguishable and any partitioned index loses recall
+        ridx = torch.randint(0, M, (256,), device=dev)
+        dmean = torch.cdist(q, xb[ridx]).pow(2).mean(1).cpu()
+        contrast = float((dmean / Df[:, 3].clamp_min(1e-12)).mean())
+        log("relative contrast (mean dist / 4-NN dist): %.3f" % contrast)
 
         t0 = time.time()
         ivf = IVFFlatIndex(d, device=dev, nlist=a.nlist, nprobe=a.nprobe)
@@ -162,7 +170,8 @@ def main():
         fms1, _ = timed(flat, q[:1])
         fms32, _ = timed(flat, q[:32])
         sizes = ivf._size
-        res["ivf"] = {"chunks": M, "words_per_chunk": a.ivf_words, "topics": a.topics, "embedder": "all-MiniLM-L6-v2 (random init)",
+        res["ivf"] = {"chunks": M, "words_per_chunk": a.ivf_words, "topics": a.topics, "topic_mix": a.topic_mix, "topic_words": a.topic_words,
+                      "relative_contrast": round(contrast, 3), "embedder": "all-MiniLM-L6-v2 (random init)",
                       "dim": d, "nlist": ivf.nlist, "queries": a.queries,
                       "embed_s": round(t_emb, 1), "flat_build_s": round(t_flat, 2), "ivf_train_s": round(t_train, 2),
                       "ivf_add_s": round(t_add, 2), "ivf_build_s": round(t_train + t_add, 2),
