@@ -433,10 +433,15 @@ __device__ __forceinline__ int decode_part_tiles(int n_kt, const DecodeArgs& a) 
 }
 
 template <int D, int G, bool NT = false>
-__global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a) {
+__global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArgs pf) {
   using C = Cfg<D>;
   static_assert(G <= 16, "at most 16 query heads per KV head");
   __shared__ __attribute__((aligned(16))) char smem[4 * C::TILEB];  // one V tile per wave
+  if ((int)blockIdx.x >= a.max_parts) {  // MALL prefetch rider (block-uniform): x beyond the partitions
+    const int ex = gridDim.x - a.max_parts;
+    pf_rider(pf, (blockIdx.x - a.max_parts) + ex * (blockIdx.y + gridDim.y * blockIdx.z), ex * gridDim.y * gridDim.z);
+    return;
+  }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
   const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
@@ -751,13 +756,15 @@ RAGK_API int ragk_attn_decode(const void* q, int q_stride, const void* kc, const
                part_o, part_ml, (bf16_t*)out, out_stride, Hq, Hkv, part_tiles, max_parts,
                scale * 1.4426950408889634f};
   const int G = Hq / Hkv;
-  dim3 grid(max_parts, Hkv, B);
+  const PfArgs pf = pf_take();
+  const int ex = (pf.blocks + Hkv * B - 1) / (Hkv * B);  // rider columns (x beyond max_parts)
+  dim3 grid(max_parts + ex, Hkv, B);
 #define RAGK_DC(DD, GG)                                                            \
   if (D == DD && G == GG) {                                                          \
     if (g_decode_nt)                                                                 \
-      hipLaunchKernelGGL((attn_decode_kernel<DD, GG, true>), grid, dim3(256), 0, st, a); \
+      hipLaunchKernelGGL((attn_decode_kernel<DD, GG, true>), grid, dim3(256), 0, st, a, pf); \
     else                                                                             \
-      hipLaunchKernelGGL((attn_decode_kernel<DD, GG, false>), grid, dim3(256), 0, st, a); \
+      hipLaunchKernelGGL((attn_decode_kernel<DD, GG, false>), grid, dim3(256), 0, st, a, pf); \
     if (max_parts > 1)                                                               \
       hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(Hq, B), dim3(DD), 0, st, a, DD); \
     return (int)hipGetLastError();                                                   \

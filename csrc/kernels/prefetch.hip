@@ -89,3 +89,17 @@ RAGK_API int ragk_spin_us(int us, hipStream_t st) {
   hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, st, (long long)us * 100);
   return (int)hipGetLastError();
 }
+
+// Arm the next rider-capable launch on this thread (rope_kv_partials, attn_decode, add_partials_rmsnorm)
+// with up to two byte ranges to prefetch and the number of rider blocks. Ranges are 16-B aligned.
+RAGK_API int ragk_pf_arm(const void* p0, long long b0, const void* p1, long long b1, int blocks, unsigned* sink) {
+  if (((uintptr_t)p0 & 15) || ((uintptr_t)p1 & 15) || blocks < 0 || blocks > 4096) return (int)hipErrorInvalidValue;
+  PfArgs& a = pf_slot();
+  a.p0 = (const u32x4*)p0;
+  a.n0 = p0 ? b0 / 16 : 0;
+  a.p1 = (const u32x4*)p1;
+  a.n1 = p1 ? b1 / 16 : 0;
+  a.sink = sink;
+  a.blocks = blocks;
+  return 0;
+}

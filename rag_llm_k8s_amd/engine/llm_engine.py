@@ -116,6 +116,8 @@ class LLMEngine:
         self.buckets = sorted(set(graph_buckets or [b for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)
                                                     if b <= max_batch] + [max_batch]))
         self.graphs = {}
+        # RAGK_DECODE_TIMING=1: (start, end) CUDA events around every async decode graph replay
+        self._timing = [] if os.environ.get("RAGK_DECODE_TIMING") == "1" else None
         self.stats = dict(prefill_steps=0, decode_steps=0, prefill_tokens=0, decode_tokens=0, prefill_s=0.0,
                           decode_s=0.0)
         # two pinned staging buffers, alternated per step: with the asynchronous decode pipeline a
@@ -684,7 +686,14 @@ class LLMEngine:
                 idx = self._h2d_i32(np.asarray(src + dst, dtype=np.int32)).long()
                 k = len(src)
                 ids.index_copy_(0, idx[k:], prev["out"].index_select(0, idx[:k]))
-        e["graph"].replay()
+        if self._timing is not None:
+            ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ea.record()
+            e["graph"].replay()
+            eb.record()
+            self._timing.append((ea, eb))
+        else:
+            e["graph"].replay()
         self._out_idx ^= 1
         host_out = self._out_pins[self._out_idx]
         host_out[:n].copy_(e["out"][:n], non_blocking=True)

@@ -25,6 +25,13 @@ import torch
 from ..ops.backend import AttnMeta, get_backend
 from ..ops.reference import pack_gate_up, rope_tables
 
+# decode MALL prefetch (LlamaModel._pf_plan): on/off, MB per latency window, rider blocks, and the
+# batch size up to which the split-K attention counts as latency-bound
+DECODE_PF = os.environ.get("RAGK_DECODE_PF", "0") == "1"
+DECODE_PF_MB = int(os.environ.get("RAGK_DECODE_PF_MB", "16"))
+DECODE_PF_BLOCKS = int(os.environ.get("RAGK_DECODE_PF_BLOCKS", "128"))
+DECODE_PF_SMALL_BATCH = int(os.environ.get("RAGK_DECODE_PF_SMALL", "8"))
+
 
 @dataclass
 class LlamaConfig:
@@ -291,6 +298,19 @@ class LlamaModel:
         L, M = self.w.layers[0], h.shape[0]
         return self.be.part_ok(M, L["wqkv"]) and self.be.part_ok(M, L["wo"]) and self.be.part_ok(M, L["wdown"])
 
+    def _pf_plan(self, M):
+        """MALL prefetch plan of a decode step at batch M (csrc/kernels/prefetch.hip, common.h pf_rider):
+        bytes of the next GEMM's weights that rider blocks of each latency-bound kernel pull into the
+        Infinity Cache. At small batch the split-K attention is latency-bound too and carries riders; at
+        large batch it streams the KV cache at full bandwidth (and would evict what was prefetched
+        before it), so only the post-attention consumers carry them. RAGK_DECODE_PF=0 disables."""
+        if not DECODE_PF or self.device.type != "cuda":
+            return None
+        mb = 1 << 20
+        small = M <= DECODE_PF_SMALL_BATCH
+        return dict(rope=DECODE_PF_MB * mb if small else 0, attn=2 * DECODE_PF_MB * mb if small else 0,
+                    post=DECODE_PF_MB * mb, blocks=DECODE_PF_BLOCKS)
+
     def hidden_states_decode_part(self, inp: StepInput, h):
         """Decode step with the split-K partial GEMM (csrc/kernels/gemm_part.hip) for the three
         small-N projections: qkv / o_proj / down write fp32 partial slabs and the following row
@@ -305,17 +325,27 @@ class LlamaModel:
         attn = torch.empty((M, Hq * D), dtype=h.dtype, device=h.device)
         q = torch.empty((M, Hq * D), dtype=h.dtype, device=h.device)
         layers = w.layers
+        pf = self._pf_plan(M)
         xn = be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
             P = be.gemm_part(xn, L["wqkv"])
+            if pf and pf["rope"]:
+                be.pf_arm([(L["wo"], 0, pf["rope"])], pf["blocks"])
             be.rope_kv_partials(P, q, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
+            if pf and pf["attn"]:
+                be.pf_arm([(L["wo"], pf["rope"], pf["attn"] // 2), (L["wgu"], 0, pf["attn"] // 2)], pf["blocks"])
             be.attn_decode(q, kc, vc, inp.meta, attn, Hq, Hkv, D)
             P = be.gemm_part(attn, L["wo"])
+            if pf:
+                be.pf_arm([(L["wgu"], pf["attn"] // 2, pf["post"])], pf["blocks"])
             xn = be.add_partials_rmsnorm(P, h, L["ln_post"], c.rms_norm_eps)
             a = be.gemm(xn, L["wgu"], epi="silu_mul")
             P = be.gemm_part(a, L["wdown"])
             nxt = layers[li + 1]["ln_in"] if li + 1 < len(layers) else w.norm
+            if pf:
+                be.pf_arm([(layers[li + 1]["wqkv"] if li + 1 < len(layers) else w.lm_head, 0, pf["post"])],
+                          pf["blocks"])
             xn = be.add_partials_rmsnorm(P, h, nxt, c.rms_norm_eps)
         if inp.logits_idx is not None:
             xn = be.gather_rows(xn, inp.logits_idx)

@@ -62,6 +62,7 @@ _SIGS = {
     "ragk_prefetch": [P, ctypes.c_longlong, I, P, S],
     "ragk_spin_us": [I, S],
     "ragk_spin_prefetch": [I, P, ctypes.c_longlong, I, P, S],
+    "ragk_pf_arm": [P, ctypes.c_longlong, P, ctypes.c_longlong, I, P],
     "ragk_l2_append": [P, I, I, I, P, I, S],
     "ragk_l2_gather": [P, I, I, P, I, P, S],
     "ragk_gemm_stream": [P, I, P, I, P, P, I, P, P, I, I, I, I, I, I, I, P, P, S],

@@ -114,6 +114,9 @@ class TorchBackend:
     def part_ok(self, M, w):
         return self.enable_part and M <= 64
 
+    def pf_arm(self, ranges, blocks):
+        """MALL prefetch hint for the next decode kernel (GPU only; nothing to do here)."""
+
     def gemm_part(self, x, w):
         wf = w.dequant() if isinstance(w, Fp8Weight) else w.float()
         return (x.float() @ wf.t()).unsqueeze(0)
@@ -229,6 +232,9 @@ class NativeBackend(TorchBackend):
 
     def gemm_part(self, x, w):
         return self.n.gemm_part(x, w)
+
+    def pf_arm(self, ranges, blocks):
+        self.n.pf_arm(ranges, blocks)
 
     def add_partials_rmsnorm(self, P, h, w, eps):
         return self.n.add_partials_rmsnorm(P, h, w, eps)

@@ -714,5 +714,29 @@ def prefetch(t, nbytes=None, blocks=64):
           "ragk_prefetch")
 
 
+def pf_arm(ranges, blocks):
+    """Arm the next rider-capable launch (rope_kv_partials / attn_decode / add_partials_rmsnorm) on this
+    thread with up to two (tensor, byte_offset, nbytes) weight ranges to pull into the MALL with
+    `blocks` extra rider blocks (csrc/kernels/common.h pf_rider). Ranges are clipped to the tensors."""
+    args = []
+    dev = None
+    for t, off, nb in list(ranges)[:2]:
+        if hasattr(t, "w8"):  # Fp8Weight: the e4m3 byte matrix
+            t = t.w8
+        total = t.numel() * t.element_size()
+        off = min(int(off), total) & ~15
+        nb = (min(int(nb), total - off)) & ~15
+        if nb > 0:
+            args.append((t.data_ptr() + off, nb))
+            dev = t.device
+    if not args or blocks <= 0:
+        return
+    key = str(dev)
+    if key not in _pf_sink:
+        _pf_sink[key] = torch.zeros(4096, dtype=torch.int32, device=dev)
+    (p0, b0), (p1, b1) = args[0], (args[1] if len(args) > 1 else (None, 0))
+    check(_lib.lib().ragk_pf_arm(p0, b0, p1, b1, int(blocks), _pf_sink[key].data_ptr()), "ragk_pf_arm")
+
+
 def spin_us(us):
     check(_lib.lib().ragk_spin_us(int(us), stream_ptr()), "ragk_spin_us")

@@ -19,7 +19,7 @@ for n, k, epi in [(6144, 4096, "none"), (4096, 4096, "resid"), (14336, 4096, "si
     h = torch.randn(M, n, device="cuda").bfloat16()
     kw = dict(resid=h, epi="resid", out=h) if epi == "resid" else dict(epi=epi)
     N.gemm(x, w, **kw)
-    t = N._blaslt_times.get((w.shape[0], k, epi))
+    t = N._blaslt_times.get((w.shape[0], k, epi, max(0, M.bit_length() - 1)))
     route = {}
     for name, path in (("auto", None), ("w4", 6)):
         ev = [torch.cuda.Event(True) for _ in range(2)]

@@ -27,7 +27,16 @@ def main():
     dev = "cuda:0"
     w = L.LlamaWeights.random(cfg, dev, seed=0)
     m = L.LlamaModel(cfg, w, dev, max_positions=8192)
-    for B in Bs:
+    # DA_PF="off,16:128,32:255": decode MALL prefetch configs (MB per window : rider blocks) to A/B
+    cfgs = [c for c in os.environ.get("DA_PF", "").split(",") if c] or [None]
+    runs = [(B, c) for c in cfgs for B in Bs]
+    for B, pfc in runs:
+        if pfc is not None:
+            L.DECODE_PF = pfc != "off"
+            if L.DECODE_PF:
+                mbs, blk = pfc.split(":")
+                L.DECODE_PF_MB, L.DECODE_PF_BLOCKS = int(mbs), int(blk)
+            print("-- decode prefetch %s" % pfc, flush=True)
         eng = LLMEngine(m, num_blocks=B * 128 + 16, max_batch=B, max_prefill_tokens=32768, max_model_len=8192,
                         eos_ids=cfg.eos_token_id, graph_buckets=[B])
         eng.warmup_graphs([B])
