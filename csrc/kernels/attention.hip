@@ -421,6 +421,8 @@ struct DecodeArgs {
   bf16_t* out; int out_stride;
   int Hq, Hkv, part_tiles, max_parts;
   float scale_log2;
+  int* counters;                           // [B][Hkv] zeroed tickets: fused split-K merge (null: separate
+                                           // attn_decode_reduce_kernel launch)
 };
 
 // Tiles per partition of one sequence: its KV tiles spread evenly over all max_parts partitions
@@ -571,6 +573,71 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
       }
     }
   }
+  if (nparts == 1 || a.counters == nullptr) return;
+
+  // ---- fused split-K merge: the last of this (b, kvh)'s nparts partition blocks to finish merges
+  // them (same math as attn_decode_reduce_kernel), so the merge costs no extra launch. Agent-scope
+  // release before the ticket / acquire after it: the partition blocks may sit on any XCD.
+  __shared__ int s_last;
+  wait_vmcnt0();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    wait_vmcnt0();
+    const int old = __hip_atomic_fetch_add(a.counters + b * a.Hkv + kvh, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (old == nparts - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    wait_vmcnt0();
+  }
+  __syncthreads();
+  float* s_m = reinterpret_cast<float*>(smem);  // [G][nparts] partition max, then its scale
+  float* s_l = s_m + G * nparts;                 // [G][nparts] partition sum
+  float* s_L = s_l + G * nparts;                 // [G] merged sum
+  const size_t hb = (size_t)b * a.Hq + kvh * G;  // first query head of this KV head
+  for (int e = threadIdx.x; e < G * nparts; e += 256) {
+    const int g = e / nparts, p = e % nparts;
+    const size_t pi = (hb + g) * a.max_parts + p;
+    s_m[e] = a.part_ml[pi * 2];
+    s_l[e] = a.part_ml[pi * 2 + 1];
+  }
+  __syncthreads();
+  if (threadIdx.x < G) {
+    const int g = threadIdx.x;
+    float Mx = -INFINITY;
+    for (int p = 0; p < nparts; ++p) Mx = fmaxf(Mx, s_m[g * nparts + p]);
+    const float Mu = Mx == -INFINITY ? 0.f : Mx;
+    float L = 0.f;
+    for (int p = 0; p < nparts; ++p) {
+      const float sc = exp2f(s_m[g * nparts + p] - Mu);
+      s_m[g * nparts + p] = sc;
+      L += s_l[g * nparts + p] * sc;
+    }
+    s_L[g] = L;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < G * D; e += 256) {
+    const int g = e / D, d = e % D;
+    const float* po = a.part_o + (hb + g) * a.max_parts * D + d;
+    const float* sc = s_m + g * nparts;
+    float O = 0.f;
+    int p = 0;
+    for (; p + 8 <= nparts; p += 8) {  // 8 independent loads in flight
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = po[(size_t)(p + i) * D];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) O += v[i] * sc[p + i];
+    }
+    for (; p < nparts; ++p) O += po[(size_t)p * D] * sc[p];
+    const float L = s_L[g];
+    a.out[(size_t)b * a.out_stride + (kvh * G + g) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(a.counters + b * a.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // merge split-K partitions: grid (Hq, B), block D threads. The partition statistics are loaded by
@@ -749,12 +816,14 @@ RAGK_API int ragk_attn_decode_set_nt(int nt) {
 RAGK_API int ragk_attn_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                               int bt_stride, const int* kv_lens, float* part_o, float* part_ml, void* out,
                               int out_stride, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
-                              float scale, hipStream_t st) {
+                              float scale, int* counters, hipStream_t st) {
   if (B <= 0) return 0;
   if (Hq % Hkv || part_tiles < 1 || max_parts < 1 || max_parts > RED_MAXP) return (int)hipErrorInvalidValue;
+  // fused merge: LDS holds 2 x G x max_parts + G floats of partition statistics (< the 64 KiB V tiles)
+  if (counters && 2 * (Hq / Hkv) * max_parts + 16 > 4 * KT * D * 2 / 4) return (int)hipErrorInvalidValue;
   DecodeArgs a{(const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, bt_stride, kv_lens,
                part_o, part_ml, (bf16_t*)out, out_stride, Hq, Hkv, part_tiles, max_parts,
-               scale * 1.4426950408889634f};
+               scale * 1.4426950408889634f, counters};
   const int G = Hq / Hkv;
   const PfArgs pf = pf_take();
   const int ex = (pf.blocks + Hkv * B - 1) / (Hkv * B);  // rider columns (x beyond max_parts)
@@ -765,7 +834,7 @@ RAGK_API int ragk_attn_decode(const void* q, int q_stride, const void* kc, const
       hipLaunchKernelGGL((attn_decode_kernel<DD, GG, true>), grid, dim3(256), 0, st, a, pf); \
     else                                                                             \
       hipLaunchKernelGGL((attn_decode_kernel<DD, GG, false>), grid, dim3(256), 0, st, a, pf); \
-    if (max_parts > 1)                                                               \
+    if (max_parts > 1 && !counters)                                                  \
       hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(Hq, B), dim3(DD), 0, st, a, DD); \
     return (int)hipGetLastError();                                                   \
   }

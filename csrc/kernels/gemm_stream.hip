@@ -26,6 +26,9 @@ namespace {
 
 constexpr int ST_THREADS = 256;
 constexpr int WROWS = 128;  // weight rows per block
+#ifndef STREAM_LDS_KB
+#define STREAM_LDS_KB 150
+#endif
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
@@ -60,7 +63,10 @@ struct StreamGeom {
   static constexpr int WBYTES = WROWS * 128;        // 16 KB: 128 rows x 128 B
   static constexpr int XBYTES = XROWS * XROW;       // MT x 2 KB (bf16) or MT x 4 KB (fp8 case)
   static constexpr int STAGE = WBYTES + XBYTES;
-  static constexpr int NS = (STAGE * 6 <= 120 * 1024) ? 6 : ((STAGE * 5 <= 124 * 1024) ? 5 : 4);
+  // ring depth: as many stages as ~RAGK_STREAM_LDS_KB of LDS allow (NS - 1 K-steps of weights in flight
+  // per CU; a pure streaming read needs ~128 KB in flight per CU to reach 5.7 TB/s, tools/read_roofline.py)
+  static constexpr int NS_CAP = STREAM_LDS_KB * 1024 / STAGE;
+  static constexpr int NS = NS_CAP >= 8 ? 8 : (NS_CAP < 4 ? 4 : NS_CAP);
   static constexpr int XPIECES = XBYTES / 1024;     // 1 KB glds pieces (64 lanes x 16 B)
   static constexpr int XP = (XPIECES + 3) / 4;      // per wave (duplicates pad the last round)
   static constexpr int LOADS = 4 + XP;              // glds per wave per stage

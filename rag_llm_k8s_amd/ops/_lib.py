@@ -51,7 +51,7 @@ _SIGS = {
     "ragk_gather_rows": [P, I, P, P, I, I, I, S],
     "ragk_attn_prefill_qtile": [I, I],
     "ragk_attn_prefill": [P, I, P, P, I, P, I, P, P, P, P, I, P, I, I, I, I, I, I, F, S],
-    "ragk_attn_decode": [P, I, P, P, P, I, P, P, P, P, I, I, I, I, I, I, I, F, S],
+    "ragk_attn_decode": [P, I, P, P, P, I, P, P, P, P, I, I, I, I, I, I, I, F, P, S],
     "ragk_topk_candidates": [P, I, I, I, I, I, I, P, P, S],
     "ragk_sample_candidates": [P, P, I, I, P, P, P, P, P, P, P, S],
     "ragk_l2_partial": [P, I, I, I, I, P, I, I, P, P, P, P, S],

@@ -563,11 +563,30 @@ def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, par
             ws_ml = torch.empty((B, Hq, max_parts, 2), dtype=torch.float32, device=q.device)
         _req(ws_o.numel() >= B * Hq * max_parts * D and ws_ml.numel() >= B * Hq * max_parts * 2, "workspace")
     scale = 1.0 / math.sqrt(D) if scale is None else scale
+    cnt = None
+    if max_parts > 1 and ATTN_FUSED_MERGE and 2 * G * max_parts + 16 <= 4 * 64 * D * 2 // 4:
+        cnt = _attn_counters(q.device)
+        _req(B * Hkv <= cnt.numel(), "attention ticket buffer too small")
     check(_lib.lib().ragk_attn_decode(
         q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
         block_tables.stride(0), kv_lens.data_ptr(), ptr(ws_o), ptr(ws_ml), out.data_ptr(), out.stride(0), B, Hq, Hkv,
-        D, part_tiles, max_parts, float(scale), stream_ptr()), "ragk_attn_decode")
+        D, part_tiles, max_parts, float(scale), ptr(cnt), stream_ptr()), "ragk_attn_decode")
     return out
+
+
+# split-K decode attention: the last partition block of each (sequence, KV head) merges the partitions
+# (a ticket per pair; zeroed once, reset by the merging block) instead of a separate merge launch
+# Off by default: measured slower at batch 1 (4.41 vs 4.2-4.3 ms per decode step; every partition
+# block's agent-scope release writes back its L2), kept for A/B (tests/test_kernels_gpu.py checks it).
+ATTN_FUSED_MERGE = os.environ.get("RAGK_ATTN_FUSED_MERGE", "0") == "1"
+_attn_cnt = {}
+
+
+def _attn_counters(device):
+    key = str(device)
+    if key not in _attn_cnt:
+        _attn_cnt[key] = torch.zeros(1 << 16, dtype=torch.int32, device=device)
+    return _attn_cnt[key]
 
 
 # ----------------------------------------------------------------------------- sampling

@@ -341,6 +341,37 @@ def test_attn_decode(native, kv_lens, Hq, Hkv, target):
     assert rel_err(out.cpu().reshape(B, Hq, D), ref) < 2e-2
 
 
+def test_attn_decode_fused_merge_matches_separate_and_resets(native):
+    """Split-K decode with the merge fused into the partition kernel (ticket per (sequence, KV head),
+    last block merges) == the separate merge launch, bit for bit, and stays so over repeated launches
+    (the merging block resets its ticket, as a replayed hipGraph needs)."""
+    D, Hq, Hkv = 128, 32, 8
+    kv_lens = [5200, 1, 64, 65, 3000, 700]
+    torch.manual_seed(13)
+    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=4)
+    B = len(kv_lens)
+    q = torch.randn(B, Hq * D).bfloat16().to(DEV)
+    kc, vc, bt = kc.to(DEV), vc.to(DEV), bt.to(DEV)
+    kvl = torch.tensor(kv_lens, dtype=torch.int32).to(DEV)
+    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv, target_blocks=1024)
+    assert mp > 1
+    outs = {}
+    for fused in (False, True):
+        native.ATTN_FUSED_MERGE = fused
+        try:
+            runs = []
+            for _ in range(3):
+                out = torch.empty(B, Hq * D, device=DEV).bfloat16()
+                native.attn_decode(q, kc, vc, bt, kvl, out, Hq, Hkv, D, pt, mp)
+                runs.append(out.cpu())
+        finally:
+            native.ATTN_FUSED_MERGE = False
+        assert all(torch.equal(runs[0], r) for r in runs[1:])
+        outs[fused] = runs[0]
+    assert torch.equal(outs[True], outs[False])
+    assert int(native._attn_counters(DEV)[:B * Hkv].abs().sum()) == 0
+
+
 def test_pool_l2norm(native):
     torch.manual_seed(12)
     h = torch.randn(50, 384, device=DEV).bfloat16()
