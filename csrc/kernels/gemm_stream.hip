@@ -55,23 +55,40 @@ __device__ __forceinline__ bf16x8 fp8x8_to_bf16(uint2 w) {
   return __builtin_bit_cast(bf16x8, r);
 }
 
-template <int MT, bool FP8>
+template <int MT, bool FP8, int ROWS = WROWS>
 struct StreamGeom {
   static constexpr int KSTEP = FP8 ? 128 : 64;      // k elements per pipeline step
   static constexpr int XROW = 2 * KSTEP;            // activation row bytes per step (bf16)
   static constexpr int XROWS = 16 * MT;
-  static constexpr int WBYTES = WROWS * 128;        // 16 KB: 128 rows x 128 B
+  static constexpr int WBYTES = ROWS * 128;         // ROWS rows x 128 B
   static constexpr int XBYTES = XROWS * XROW;       // MT x 2 KB (bf16) or MT x 4 KB (fp8 case)
   static constexpr int STAGE = WBYTES + XBYTES;
-  // ring depth: as many stages as ~RAGK_STREAM_LDS_KB of LDS allow (NS - 1 K-steps of weights in flight
-  // per CU; a pure streaming read needs ~128 KB in flight per CU to reach 5.7 TB/s, tools/read_roofline.py)
-  static constexpr int NS_CAP = STREAM_LDS_KB * 1024 / STAGE;
+  // ring depth: as many stages as ~STREAM_LDS_KB of LDS per CU allow (NS - 1 K-steps of weights in
+  // flight; a pure streaming read needs ~128 KB in flight per CU for 5.7 TB/s, tools/read_roofline.py).
+  // 64-row tiles run two blocks per CU, each with half the LDS.
+  static constexpr int BPC = ROWS == 64 ? 2 : 1;
+  static constexpr int NS_CAP = STREAM_LDS_KB * 1024 / BPC / STAGE;
   static constexpr int NS = NS_CAP >= 8 ? 8 : (NS_CAP < 4 ? 4 : NS_CAP);
   static constexpr int XPIECES = XBYTES / 1024;     // 1 KB glds pieces (64 lanes x 16 B)
   static constexpr int XP = (XPIECES + 3) / 4;      // per wave (duplicates pad the last round)
-  static constexpr int LOADS = 4 + XP;              // glds per wave per stage
-  static constexpr int EPI_LD = WROWS + 4;
+  static constexpr int WPW = ROWS / 32;             // weight pieces (8 rows) per wave per stage
+  static constexpr int LOADS = WPW + XP;            // glds per wave per stage
+  static constexpr int EPI_LD = ROWS + 4;
+  static constexpr int J = ROWS / 64;               // 16-row weight fragments per wave
 };
+
+// Packed weight row of local tile row r. The SiLU*up weights are packed [64 gate | 64 up] per 128
+// rows; a 64-row tile of a pair GEMM takes gate rows h*32..h*32+31 and the matching up rows of
+// group g (tile = 2g + h), so every tile still holds whole (gate, up) pairs.
+template <int ROWS, bool PAIR>
+__device__ __forceinline__ int stream_row(int tile, int r) {
+  if constexpr (ROWS == 64 && PAIR) {
+    const int g = tile >> 1, h = tile & 1;
+    return g * 128 + (r < 32 ? h * 32 + r : 64 + h * 32 + (r - 32));
+  } else {
+    return tile * ROWS + r;
+  }
+}
 
 // Weight-stream LDS-DMA with the non-temporal policy (aux = 2): each weight row is read by exactly
 // one block once per decode step, from a stream far larger than the Infinity Cache.
@@ -80,19 +97,19 @@ __device__ __forceinline__ void glds16_nt(const void* gsrc, void* lds_wave_base)
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 2);
 }
 
-template <int MT, bool FP8, bool NT = false>
+template <int MT, bool FP8, bool NT, int ROWS, bool PAIR>
 __device__ __forceinline__ void stage_load(const bf16_t* __restrict__ X, int ldx, int M,
-                                           const unsigned char* __restrict__ Wb, int ldw_bytes, int Nrows, int n0,
+                                           const unsigned char* __restrict__ Wb, int ldw_bytes, int Nrows, int tile,
                                            int kel, char* st, int wid, int lane) {
-  using G = StreamGeom<MT, FP8>;
-  // weights: 128 rows x 128 B; wave w issues pieces 4w..4w+3 (8 rows each)
+  using G = StreamGeom<MT, FP8, ROWS>;
+  // weights: ROWS rows x 128 B; wave w issues pieces WPW*w .. WPW*w + WPW-1 (8 rows each)
   const size_t kbyte = FP8 ? (size_t)kel : (size_t)kel * 2;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = wid * 4 + i;
+  for (int i = 0; i < G::WPW; ++i) {
+    const int q = wid * G::WPW + i;
     const int r = q * 8 + (lane >> 3);
     const int c = swz(r, lane & 7);
-    const int gr = min(n0 + r, Nrows - 1);
+    const int gr = min(stream_row<ROWS, PAIR>(tile, r), Nrows - 1);
     if constexpr (NT) glds16_nt(Wb + (size_t)gr * ldw_bytes + kbyte + c * 16, st + q * 1024);
     else glds16(Wb + (size_t)gr * ldw_bytes + kbyte + c * 16, st + q * 1024);
   }
@@ -118,38 +135,40 @@ __device__ __forceinline__ void stage_load(const bf16_t* __restrict__ X, int ldx
   }
 }
 
-template <int MT, int EPI, bool OUT_F32, bool FP8, bool NT = false>
-__global__ __launch_bounds__(ST_THREADS, 1) void gemm_stream_kernel(
+template <int MT, int EPI, bool OUT_F32, bool FP8, bool NT = false, int ROWS = WROWS>
+__global__ __launch_bounds__(ST_THREADS, ROWS == 64 ? 2 : 1) void gemm_stream_kernel(
     const bf16_t* __restrict__ X, int ldx, const void* __restrict__ Wv, int ldw, const float* __restrict__ wscale,
     void* C, int ldc, const bf16_t* __restrict__ bias, const bf16_t* resid, int ldr, int M, int N, int K, int S,
     float* ws, int* counters) {
-  using G = StreamGeom<MT, FP8>;
+  using G = StreamGeom<MT, FP8, ROWS>;
   constexpr bool PAIR = (EPI == EPI_SILU_MUL);
-  constexpr int NS = G::NS;
+  constexpr int NS = G::NS, J = G::J;
   __shared__ __attribute__((aligned(16))) char smem[NS * G::STAGE + 16];  // one object: see trap (a)
   int& s_flag = *reinterpret_cast<int*>(smem + NS * G::STAGE);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
   const int fr = lane & 15, fh = lane >> 4;
-  const int ntile = blockIdx.x, slice = blockIdx.y;
+  const int ntile = blockIdx.x, slice = blockIdx.y, ntiles = gridDim.x;
   const int Nrows = PAIR ? 2 * N : N;
-  const int n0 = ntile * WROWS;
   const unsigned char* Wb = reinterpret_cast<const unsigned char*>(Wv);
   const int ldw_bytes = FP8 ? ldw : ldw * 2;
   const int steps_total = K / G::KSTEP;
   const int nst = steps_total / S;
   const int k0 = slice * nst * G::KSTEP;
 
-  f32x4 acc[MT][2];
+  f32x4 acc[MT][J];
 #pragma unroll
-  for (int t = 0; t < MT; ++t) acc[t][0] = acc[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   // prologue: NS-1 stages in flight
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
-    if (p < nst) stage_load<MT, FP8, NT>(X, ldx, M, Wb, ldw_bytes, Nrows, n0, k0 + p * G::KSTEP, smem + p * G::STAGE,
-                                     wid_u, lane);
+    if (p < nst)
+      stage_load<MT, FP8, NT, ROWS, PAIR>(X, ldx, M, Wb, ldw_bytes, Nrows, ntile, k0 + p * G::KSTEP,
+                                          smem + p * G::STAGE, wid_u, lane);
 
   for (int t = 0; t < nst; ++t) {
     // stage t landed (this wave's part): at most the later stages' loads still outstanding
@@ -159,35 +178,35 @@ __global__ __launch_bounds__(ST_THREADS, 1) void gemm_stream_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier_raw();  // every wave's part of stage t landed; every wave finished reading stage t-1
     if (t + NS - 1 < nst)
-      stage_load<MT, FP8, NT>(X, ldx, M, Wb, ldw_bytes, Nrows, n0, k0 + (t + NS - 1) * G::KSTEP,
-                          smem + ((t + NS - 1) % NS) * G::STAGE, wid_u, lane);
+      stage_load<MT, FP8, NT, ROWS, PAIR>(X, ldx, M, Wb, ldw_bytes, Nrows, ntile, k0 + (t + NS - 1) * G::KSTEP,
+                                          smem + ((t + NS - 1) % NS) * G::STAGE, wid_u, lane);
     const char* wt = smem + (t % NS) * G::STAGE;
     const char* xt = wt + G::WBYTES;
     if constexpr (!FP8) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int c = 4 * s + fh;
-        bf16x8 wf[2];
+        bf16x8 wf[J];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int R = wid * 32 + 16 * j + fr;
+        for (int j = 0; j < J; ++j) {
+          const int R = wid * (ROWS / 4) + 16 * j + fr;
           wf[j] = *reinterpret_cast<const bf16x8*>(wt + R * 128 + 16 * swz(R, c));
         }
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           const int R = 16 * m + fr;
           const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xt + R * 128 + 16 * swz(R, c));
-          acc[m][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[0], acc[m][0], 0, 0, 0);
-          acc[m][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[1], acc[m][1], 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < J; ++j) acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[j], acc[m][j], 0, 0, 0);
         }
       }
     } else {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {  // k = 32 s + 8 fh + j
-        bf16x8 wf[2];
+        bf16x8 wf[J];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int R = wid * 32 + 16 * j + fr;
+        for (int j = 0; j < J; ++j) {
+          const int R = wid * (ROWS / 4) + 16 * j + fr;
           const uint2 raw = *reinterpret_cast<const uint2*>(wt + R * 128 + 16 * swz(R, 2 * s + (fh >> 1)) +
                                                             8 * (fh & 1));
           wf[j] = fp8x8_to_bf16(raw);
@@ -198,14 +217,14 @@ __global__ __launch_bounds__(ST_THREADS, 1) void gemm_stream_kernel(
         for (int m = 0; m < MT; ++m) {
           const int R = 16 * m + fr;
           const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xh + R * 128 + 16 * swz(R, c));
-          acc[m][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[0], acc[m][0], 0, 0, 0);
-          acc[m][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[1], acc[m][1], 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < J; ++j) acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[j], acc[m][j], 0, 0, 0);
         }
       }
     }
   }
 
-  // ---------------- epilogue: partial tile -> LDS [16 MT][128] f32 ----------------------
+  // ---------------- epilogue: partial tile -> LDS [16 MT][ROWS] f32 ----------------------
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   wait_vm<0>();
   barrier_raw();
@@ -213,9 +232,10 @@ __global__ __launch_bounds__(ST_THREADS, 1) void gemm_stream_kernel(
 #pragma unroll
   for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < J; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sC[(16 * m + 4 * fh + r) * G::EPI_LD + wid * 32 + 16 * j + fr] = acc[m][j][r];
+      for (int r = 0; r < 4; ++r)
+        sC[(16 * m + 4 * fh + r) * G::EPI_LD + wid * (ROWS / 4) + 16 * j + fr] = acc[m][j][r];
   __syncthreads();
 
   auto finish = [&](int row, int c, float v) {  // c = output column
@@ -229,44 +249,37 @@ __global__ __launch_bounds__(ST_THREADS, 1) void gemm_stream_kernel(
     else
       reinterpret_cast<bf16_t*>(C)[(size_t)row * ldc + c] = f2bf(v);
   };
-  // final value of packed row pr for activation row `row` from the full-K sum `v`
-  auto emit = [&](int row, int pr, float v, float u) {
+  constexpr int OUTC = PAIR ? ROWS / 2 : ROWS;
+  // final value of local column cc (pair: gate cc with up cc + ROWS/2) for activation row `row`
+  auto emit = [&](int row, int cc) {
+    const int gp = stream_row<ROWS, PAIR>(ntile, cc);  // packed weight row (the gate row of a pair)
+    if (gp >= Nrows) return;
+    float v = sC[row * G::EPI_LD + cc];
     if constexpr (PAIR) {
+      float u = sC[row * G::EPI_LD + cc + ROWS / 2];
       if constexpr (FP8) {
-        v *= wscale[pr];
-        u *= wscale[pr + 64];
+        v *= wscale[gp];
+        u *= wscale[gp + 64];
       }
-      const int c = (pr >> 7) * 64 + (pr & 63);
-      finish(row, c, silu(v) * u);
+      finish(row, (gp >> 7) * 64 + (gp & 63), silu(v) * u);
     } else {
-      if constexpr (FP8) v *= wscale[pr];
-      finish(row, pr, v);
+      if constexpr (FP8) v *= wscale[gp];
+      finish(row, gp, v);
     }
   };
-  constexpr int OUTC = PAIR ? 64 : 128;
 
   if (S == 1) {
-    for (int e = tid; e < M * OUTC; e += ST_THREADS) {
-      const int row = e / OUTC, cc = e % OUTC;
-      const int pr = n0 + cc;
-      if (pr >= Nrows) continue;
-      emit(row, pr, sC[row * G::EPI_LD + cc], PAIR ? sC[row * G::EPI_LD + cc + 64] : 0.f);
-    }
+    for (int e = tid; e < M * OUTC; e += ST_THREADS) emit(e / OUTC, e % OUTC);
     return;
   }
-  // split-K: slab ws[slice][row][Nrows] fp32 (16-B stores), then the last-arriving block reduces
-  const size_t slab = (size_t)M * Nrows;
-  const bool full = n0 + WROWS <= Nrows;  // Nrows % 128 == 0 for every real layer; tails go scalar
-  for (int e = tid; e < M * 32; e += ST_THREADS) {
-    const int row = e >> 5, c4 = (e & 31) * 4;
+  // split-K: slab ws[slice][tile][row][ROWS] fp32 (16-B stores), then the last-arriving block reduces
+  const size_t slab = (size_t)ntiles * M * ROWS;
+  const size_t tbase = (size_t)ntile * M * ROWS;
+  for (int e = tid; e < M * (ROWS / 4); e += ST_THREADS) {
+    const int row = e / (ROWS / 4), c4 = (e % (ROWS / 4)) * 4;
     const float* src = sC + row * G::EPI_LD + c4;
-    float* dst = ws + slice * slab + (size_t)row * Nrows + n0 + c4;
-    if (full) {
-      *reinterpret_cast<f32x4*>(dst) = (f32x4){src[0], src[1], src[2], src[3]};
-    } else {
-      for (int q = 0; q < 4; ++q)
-        if (n0 + c4 + q < Nrows) dst[q] = src[q];
-    }
+    *reinterpret_cast<f32x4*>(ws + slice * slab + tbase + (size_t)row * ROWS + c4) =
+        (f32x4){src[0], src[1], src[2], src[3]};
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -286,54 +299,55 @@ __global__ __launch_bounds__(ST_THREADS, 1) void gemm_stream_kernel(
   // reduce the S slabs of this tile into sC (all loads of a round issued before any use), then
   // run the epilogue from LDS exactly as the S == 1 path
   const float* __restrict__ wsr = ws;
-  for (int e = tid; e < M * 32; e += ST_THREADS) {
-    const int row = e >> 5, c4 = (e & 31) * 4;
-    const size_t off = (size_t)row * Nrows + n0 + c4;
+  for (int e = tid; e < M * (ROWS / 4); e += ST_THREADS) {
+    const int row = e / (ROWS / 4), c4 = (e % (ROWS / 4)) * 4;
+    const size_t off = tbase + (size_t)row * ROWS + c4;
     f32x4 a = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if (full) {
-      f32x4 v[8];
+    f32x4 v[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (q < S) v[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(wsr + q * slab + off));
+    for (int q = 0; q < 8; ++q)
+      if (q < S) v[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(wsr + q * slab + off));
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (q < S) a += v[q];
-      for (int q = 8; q < S; ++q) a += *reinterpret_cast<const f32x4*>(wsr + q * slab + off);
-    } else {
-      for (int q = 0; q < S; ++q)
-        for (int j = 0; j < 4; ++j)
-          if (n0 + c4 + j < Nrows) a[j] += wsr[q * slab + off + j];
-    }
+    for (int q = 0; q < 8; ++q)
+      if (q < S) a += v[q];
+    for (int q = 8; q < S; ++q) a += *reinterpret_cast<const f32x4*>(wsr + q * slab + off);
     float* d = sC + row * G::EPI_LD + c4;
     d[0] = a[0]; d[1] = a[1]; d[2] = a[2]; d[3] = a[3];
   }
   __syncthreads();
-  for (int e = tid; e < M * OUTC; e += ST_THREADS) {
-    const int row = e / OUTC, cc = e % OUTC;
-    const int pr = n0 + cc;
-    if (pr >= Nrows) continue;
-    emit(row, pr, sC[row * G::EPI_LD + cc], PAIR ? sC[row * G::EPI_LD + cc + 64] : 0.f);
-  }
+  for (int e = tid; e < M * OUTC; e += ST_THREADS) emit(e / OUTC, e % OUTC);
   if (tid == 0) __hip_atomic_store(counters + ntile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Weight-stream cache policy for the SiLU*up (gate/up) instantiations: 1 = non-temporal.
 int g_stream_nt = 1;
+// Tile rows for the SiLU*up GEMM: 64 = two blocks per CU over 64-row (32 gate + 32 up) tiles, so the
+// 28672-row Llama gate/up grid (448 tiles) occupies all 256 CUs; 128 = one block per CU, 224 tiles.
+int g_stream_pair_rows = 64;
+
+inline int stream_rows(int epi) { return (epi == EPI_SILU_MUL && g_stream_pair_rows == 64) ? 64 : WROWS; }
 
 template <int MT, int EPI, bool F32, bool FP8>
 int launch_stream(const void* X, int ldx, const void* W, int ldw, const float* wscale, void* C, int ldc,
                   const void* bias, const void* resid, int ldr, int M, int N, int K, int S, float* ws, int* cnt,
                   hipStream_t st) {
   const int Nrows = EPI == EPI_SILU_MUL ? 2 * N : N;
-  const dim3 grid((Nrows + WROWS - 1) / WROWS, S);
   if constexpr (EPI == EPI_SILU_MUL) {
-    if (g_stream_nt) {
-      hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI, F32, FP8, true>), grid, dim3(ST_THREADS), 0, st,
-                         (const bf16_t*)X, ldx, W, ldw, wscale, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid,
-                         ldr, M, N, K, S, ws, cnt);
-      return (int)hipGetLastError();
+#define RAGK_ST_PAIR(NTV, R)                                                                                         \
+  hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI, F32, FP8, NTV, R>), dim3((Nrows + R - 1) / R, S), dim3(ST_THREADS), \
+                     0, st, (const bf16_t*)X, ldx, W, ldw, wscale, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid,  \
+                     ldr, M, N, K, S, ws, cnt)
+    if (g_stream_pair_rows == 64) {
+      if (g_stream_nt) RAGK_ST_PAIR(true, 64);
+      else RAGK_ST_PAIR(false, 64);
+    } else {
+      if (g_stream_nt) RAGK_ST_PAIR(true, 128);
+      else RAGK_ST_PAIR(false, 128);
     }
+#undef RAGK_ST_PAIR
+    return (int)hipGetLastError();
   }
+  const dim3 grid((Nrows + WROWS - 1) / WROWS, S);
   hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI, F32, FP8>), grid, dim3(ST_THREADS), 0, st, (const bf16_t*)X, ldx,
                      W, ldw, wscale, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K, S, ws, cnt);
   return (int)hipGetLastError();
@@ -361,13 +375,20 @@ RAGK_API int ragk_gemm_stream_set_nt(int nt) {
   return 0;
 }
 
+RAGK_API int ragk_gemm_stream_set_pair_rows(int rows) {
+  if (rows != 64 && rows != 128) return (int)hipErrorInvalidValue;
+  g_stream_pair_rows = rows;
+  return 0;
+}
+
 RAGK_API int ragk_gemm_stream_splits(int N, int K, int epi, int fp8) {
   static const int s_env = [] {
     const char* v = getenv("RAGK_STREAM_S");
     return v ? atoi(v) : 0;
   }();
   const int Nrows = epi == EPI_SILU_MUL ? 2 * N : N;
-  const int tiles = (Nrows + WROWS - 1) / WROWS;
+  const int rows = stream_rows(epi);
+  const int tiles = (Nrows + rows - 1) / rows;
   const int steps = K / (fp8 ? 128 : 64);
   if (s_env > 0) {
     int S = s_env;
@@ -375,12 +396,14 @@ RAGK_API int ragk_gemm_stream_splits(int N, int K, int epi, int fp8) {
     return S;
   }
   int S = 1;
-  while (tiles * S * 2 <= 320 && steps % (S * 2) == 0 && steps / (S * 2) >= 8) S *= 2;
+  const int slots = rows == 64 ? 640 : 320;  // 64-row tiles: two blocks per CU
+  while (tiles * S * 2 <= slots && steps % (S * 2) == 0 && steps / (S * 2) >= 8) S *= 2;
   return S;
 }
 
 // C[M,N] = epi(X[M,K] . W^T): W bf16 [Nrows, K] (wscale == null) or fp8 e4m3 [Nrows, K] with per-row
-// fp32 scales. M <= 64. ws/counters: split-K workspace (S * M * Nrows floats, Nrows/128 zeroed ints).
+// fp32 scales. M <= 64. ws/counters: split-K workspace (S * M * ceil(Nrows/128)*128 floats, Nrows/64
+// zeroed ints).
 RAGK_API int ragk_gemm_stream(const void* X, int ldx, const void* W, int ldw, const float* wscale, void* C, int ldc,
                               const void* bias, const void* resid, int ldr, int M, int N, int K, int epi, int out_f32,
                               int S, float* ws, int* counters, hipStream_t st) {

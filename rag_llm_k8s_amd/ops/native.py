@@ -283,8 +283,8 @@ def _gemm_stream(x, w, wscale, out, bias, resid, ldr, M, N, K, epi, e, out_f32):
     S = STREAM_S_OVERRIDE or L.ragk_gemm_stream_splits(N, K, e, int(fp8))
     ws, cnt = dec_workspace(x.device)
     rows = 2 * N if epi == "silu_mul" else N
-    _req(S == 1 or S * M * rows <= ws.numel(), "stream GEMM workspace too small")
-    _req(-(-rows // 128) <= cnt.numel(), "too many n-tiles for the counter buffer")
+    _req(S == 1 or S * M * (-(-rows // 128) * 128) <= ws.numel(), "stream GEMM workspace too small")
+    _req(-(-rows // 64) <= cnt.numel(), "too many n-tiles for the counter buffer")
     return L.ragk_gemm_stream(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), ptr(wscale), out.data_ptr(),
                               out.stride(0), ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), S, ws.data_ptr(),
                               cnt.data_ptr(), stream_ptr())
