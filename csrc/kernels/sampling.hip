@@ -119,6 +119,125 @@ __global__ __launch_bounds__(TK_THREADS) void topk_candidates_kernel(const float
   }
 }
 
+// LDS-resident variant (chunks of up to TK_VMAX entries, i.e. every chunk of a 128k vocab split 7
+// ways): the chunk's keys are read from HBM once into LDS, the four 8-bit radix passes count into 16
+// per-wave histograms (no single hot LDS counter for the common exponent byte), and wave 0 finds the
+// bin with a shuffle scan instead of a serial 256-step walk by one thread. Ties at the K-th value take
+// the lowest vocabulary ids (deterministic).
+constexpr int TK_VMAX = 24576;
+constexpr int TK_WAVES = TK_THREADS / 64;
+
+__global__ __launch_bounds__(TK_THREADS) void topk_lds_kernel(const float* __restrict__ logits, int ld, int Vtot,
+                                                              int K, int vocab_offset, int chunks,
+                                                              float* cand_v, int* cand_i) {
+  extern __shared__ __attribute__((aligned(16))) unsigned tk_smem[];
+  unsigned* whist = tk_smem;                   // [TK_WAVES][256]
+  unsigned* skey = tk_smem + TK_WAVES * 256;   // [Vc] order-preserving keys
+  __shared__ unsigned hist[256];
+  __shared__ unsigned s_prefix, s_krem, s_eqtot, s_cnt_gt, s_cnt_eq;
+  __shared__ float sv[MAXK];
+  __shared__ int si[MAXK];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int b = blockIdx.x / chunks, chunk = blockIdx.x % chunks;
+  const int Vc = ((Vtot + chunks - 1) / chunks + 7) & ~7;
+  const int c0 = min(chunk * Vc, Vtot);
+  const int V = min(Vtot - c0, Vc);
+  const size_t obase = ((size_t)b * chunks + chunk) * K;
+  if (V <= 0) {  // block-uniform: an empty chunk of a short row
+    for (int i = tid; i < K; i += TK_THREADS) {
+      cand_v[obase + i] = -INFINITY;
+      cand_i[obase + i] = -1;
+    }
+    return;
+  }
+  const float* row = logits + (size_t)b * ld + c0;
+  for (int i = tid; i < V; i += TK_THREADS) skey[i] = fkey(row[i]);
+  unsigned prefix = 0, mask = 0, krem = (unsigned)min(K, V);
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = tid; i < TK_WAVES * 256; i += TK_THREADS) whist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < V; i += TK_THREADS) {
+      const unsigned k = skey[i];
+      if ((k & mask) == prefix) atomicAdd(&whist[wid * 256 + ((k >> shift) & 255)], 1u);
+    }
+    __syncthreads();
+    if (tid < 256) {
+      unsigned h = 0;
+#pragma unroll
+      for (int w = 0; w < TK_WAVES; ++w) h += whist[w * 256 + tid];
+      hist[tid] = h;
+    }
+    __syncthreads();
+    if (wid == 0) {  // lane l owns bins 255-4l .. 252-4l; scan from the top
+      unsigned c[4], tot = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = hist[255 - 4 * lane - j];
+        tot += c[j];
+      }
+      unsigned incl = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      const unsigned excl = incl - tot;
+      if (excl < krem && krem <= incl) {  // exactly one lane
+        unsigned above = excl;
+        int d = 255 - 4 * lane - 3;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (above + c[j] >= krem) {
+            d = 255 - 4 * lane - j;
+            break;
+          }
+          above += c[j];
+        }
+        s_prefix = prefix | ((unsigned)d << shift);
+        s_krem = krem - above;
+        s_eqtot = hist[d];
+      }
+    }
+    __syncthreads();
+    prefix = s_prefix;
+    krem = s_krem;
+    mask |= 255u << shift;
+  }
+  // prefix = key of the K-th largest: every key > prefix, plus the krem lowest-id keys == prefix
+  const int kk = min(K, V);
+  const unsigned n_gt = (unsigned)kk - krem;
+  if (tid == 0) { s_cnt_gt = 0; s_cnt_eq = 0; }
+  for (int i = tid; i < MAXK; i += TK_THREADS) { sv[i] = -INFINITY; si[i] = 0x7fffffff; }
+  __syncthreads();
+  const bool all_eq = s_eqtot == krem;
+  for (int i = tid; i < V; i += TK_THREADS) {
+    const unsigned k = skey[i];
+    if (k > prefix) {
+      const unsigned slot = atomicAdd(&s_cnt_gt, 1u);
+      if (slot < (unsigned)MAXK) { sv[slot] = unkey(k); si[slot] = i + vocab_offset + c0; }
+    } else if (k == prefix && all_eq) {
+      const unsigned slot = n_gt + atomicAdd(&s_cnt_eq, 1u);
+      if (slot < (unsigned)MAXK) { sv[slot] = unkey(k); si[slot] = i + vocab_offset + c0; }
+    }
+  }
+  if (!all_eq && tid == 0) {  // ties beyond the K-th value (rare): the lowest ids, in order
+    unsigned e = 0;
+    for (int i = 0; i < V && e < krem; ++i)
+      if (skey[i] == prefix) {
+        const unsigned slot = n_gt + e++;
+        if (slot < (unsigned)MAXK) { sv[slot] = unkey(prefix); si[slot] = i + vocab_offset + c0; }
+      }
+  }
+  __syncthreads();
+  int n = 1;
+  while (n < kk) n <<= 1;
+  bitonic_desc(sv, si, n);
+  for (int i = tid; i < K; i += TK_THREADS) {
+    cand_v[obase + i] = i < kk ? sv[i] : -INFINITY;
+    cand_i[obase + i] = i < kk ? si[i] : -1;
+  }
+}
+
 __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -145,45 +264,89 @@ __global__ __launch_bounds__(SC_THREADS) void sample_candidates_kernel(
   }
   __syncthreads();
   bitonic_desc(sv, si, n);
-  if (threadIdx.x != 0) return;
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
   const float T = temps[b];
   int K = top_ks[b];
   if (K <= 0 || K > n_cand) K = n_cand;
-  // drop -inf / invalid tail
-  int valid = 0;
-  while (valid < K && sv[valid] > -INFINITY && si[valid] >= 0) ++valid;
-  if (valid == 0) { out_tok[b] = 0; if (out_logprob) out_logprob[b] = -INFINITY; return; }
+  const unsigned long long r = splitmix64(seeds[b] ^ splitmix64((unsigned long long)steps[b] + 0x51ED270Bull));
+  const float top_p = top_ps[b];
+  if (K > 64) {  // wide top-k (or top_k disabled): the serial tail
+    if (lane != 0) return;
+    int valid = 0;
+    while (valid < K && sv[valid] > -INFINITY && si[valid] >= 0) ++valid;
+    if (valid == 0) { out_tok[b] = 0; if (out_logprob) out_logprob[b] = -INFINITY; return; }
+    if (!(T > 0.f)) { out_tok[b] = si[0]; if (out_logprob) out_logprob[b] = 0.f; return; }
+    const float inv_t = 1.f / T;
+    const float m = sv[0] * inv_t;
+    float Z = 0.f;
+    for (int i = 0; i < valid; ++i) Z += __expf(sv[i] * inv_t - m);
+    // top-p: keep token i iff the probability mass ranked strictly above it is < top_p
+    int keep = valid;
+    if (top_p < 1.f) {
+      float cum = 0.f;
+      for (int i = 0; i < valid; ++i) {
+        if (i > 0 && cum >= top_p) { keep = i; break; }
+        cum += __expf(sv[i] * inv_t - m) / Z;
+      }
+    }
+    float Zk = 0.f;
+    for (int i = 0; i < keep; ++i) Zk += __expf(sv[i] * inv_t - m);
+    const float u = (float)((r >> 40) * (1.0 / 16777216.0)) * Zk;
+    float c = 0.f;
+    int pick = keep - 1;
+    for (int i = 0; i < keep; ++i) {
+      c += __expf(sv[i] * inv_t - m);
+      if (u < c) { pick = i; break; }
+    }
+    out_tok[b] = si[pick];
+    if (out_logprob) out_logprob[b] = (sv[pick] * inv_t - m) - __logf(Zk);
+    return;
+  }
+  // K <= 64: one candidate per lane of wave 0, reductions and scans by shuffles
+  const float v = lane < K ? sv[lane] : -INFINITY;
+  const int ix = lane < K ? si[lane] : -1;
+  const bool ok = lane < K && v > -INFINITY && ix >= 0;  // sorted: the valid ones lead
+  const unsigned long long okm = __ballot(ok);
+  const int valid = okm == ~0ull ? 64 : __builtin_ctzll(~okm);
+  if (valid == 0) {
+    if (lane == 0) { out_tok[b] = 0; if (out_logprob) out_logprob[b] = -INFINITY; }
+    return;
+  }
   if (!(T > 0.f)) {  // greedy
-    out_tok[b] = si[0];
-    if (out_logprob) out_logprob[b] = 0.f;
+    if (lane == 0) { out_tok[b] = ix; if (out_logprob) out_logprob[b] = 0.f; }
     return;
   }
   const float inv_t = 1.f / T;
-  const float m = sv[0] * inv_t;
-  float Z = 0.f;
-  for (int i = 0; i < valid; ++i) Z += __expf(sv[i] * inv_t - m);
+  const float m = __shfl(v, 0, 64) * inv_t;
+  const float e = lane < valid ? __expf(v * inv_t - m) : 0.f;
+  const float Z = wave_sum(e);
+  float incl = e;  // inclusive prefix of e over lanes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
   // top-p: keep token i iff the probability mass ranked strictly above it is < top_p
-  const float top_p = top_ps[b];
-  int keep = valid;
-  if (top_p < 1.f) {
-    float cum = 0.f;
-    for (int i = 0; i < valid; ++i) {
-      if (i > 0 && cum >= top_p) { keep = i; break; }
-      cum += __expf(sv[i] * inv_t - m) / Z;
-    }
-  }
-  float Zk = 0.f;
-  for (int i = 0; i < keep; ++i) Zk += __expf(sv[i] * inv_t - m);
-  const unsigned long long r = splitmix64(seeds[b] ^ splitmix64((unsigned long long)steps[b] + 0x51ED270Bull));
+  const bool kept = lane < valid && (top_p >= 1.f || lane == 0 || (incl - e) / Z < top_p);
+  const float ek = kept ? e : 0.f;
+  const float Zk = wave_sum(ek);
   const float u = (float)((r >> 40) * (1.0 / 16777216.0)) * Zk;
-  float c = 0.f;
-  int pick = keep - 1;
-  for (int i = 0; i < keep; ++i) {
-    c += __expf(sv[i] * inv_t - m);
-    if (u < c) { pick = i; break; }
+  float ck = ek;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(ck, o, 64);
+    if (lane >= o) ck += t;
   }
-  out_tok[b] = si[pick];
-  if (out_logprob) out_logprob[b] = (sv[pick] * inv_t - m) - __logf(Zk);
+  const unsigned long long hit = __ballot(kept && u < ck);
+  const unsigned long long keptm = __ballot(kept);
+  const int pick = hit ? __builtin_ctzll(hit) : 63 - __builtin_clzll(keptm);
+  const float pv = __shfl(v, pick, 64);
+  const int pix = __shfl(ix, pick, 64);
+  if (lane == 0) {
+    out_tok[b] = pix;
+    if (out_logprob) out_logprob[b] = (pv * inv_t - m) - __logf(Zk);
+  }
 }
 
 }  // namespace
@@ -193,6 +356,19 @@ RAGK_API int ragk_topk_candidates(const float* logits, int ld, int B, int V, int
                                   float* cand_v, int* cand_i, hipStream_t st) {
   if (B <= 0) return 0;
   if (K < 1 || K > MAXK || chunks < 1 || chunks > 64) return (int)hipErrorInvalidValue;
+  const int Vc = ((V + chunks - 1) / chunks + 7) & ~7;
+  if (Vc <= TK_VMAX) {
+    static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in
+    if (!attr) {
+      const hipError_t e = hipFuncSetAttribute((const void*)topk_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (TK_WAVES * 256 + TK_VMAX) * 4);
+      if (e != hipSuccess) return (int)e;
+      attr = true;
+    }
+    hipLaunchKernelGGL(topk_lds_kernel, dim3(B * chunks), dim3(TK_THREADS), (TK_WAVES * 256 + Vc) * 4, st, logits, ld,
+                       V, K, vocab_offset, chunks, cand_v, cand_i);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(topk_candidates_kernel, dim3(B * chunks), dim3(TK_THREADS), 0, st, logits, ld, V, K, vocab_offset,
                      chunks, cand_v, cand_i);
   return (int)hipGetLastError();

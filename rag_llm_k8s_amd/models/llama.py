@@ -31,6 +31,8 @@ DECODE_PF = os.environ.get("RAGK_DECODE_PF", "0") == "1"
 DECODE_PF_MB = int(os.environ.get("RAGK_DECODE_PF_MB", "16"))
 DECODE_PF_BLOCKS = int(os.environ.get("RAGK_DECODE_PF_BLOCKS", "128"))
 DECODE_PF_SMALL_BATCH = int(os.environ.get("RAGK_DECODE_PF_SMALL", "8"))
+# decode batches up to this size run the down projection on the register-streaming GEMM (fused residual)
+DECODE_DOWN_SKINNY_MAX_M = int(os.environ.get("RAGK_DECODE_DOWN_SKINNY_MAX_M", "4"))
 
 
 @dataclass
@@ -341,8 +343,14 @@ class LlamaModel:
                 be.pf_arm([(L["wgu"], pf["attn"] // 2, pf["post"])], pf["blocks"])
             xn = be.add_partials_rmsnorm(P, h, L["ln_post"], c.rms_norm_eps)
             a = be.gemm(xn, L["wgu"], epi="silu_mul")
-            P = be.gemm_part(a, L["wdown"])
             nxt = layers[li + 1]["ln_in"] if li + 1 < len(layers) else w.norm
+            if M <= DECODE_DOWN_SKINNY_MAX_M:
+                # tiny batch: the register-streaming GEMM with the fused residual + a plain norm beats
+                # the split-K partials + consumer by ~2 us (profiles/decode_gemm_graph_ab_M_r2.log)
+                be.gemm(a, L["wdown"], resid=h, epi="resid", out=h)
+                xn = be.rmsnorm(h, nxt, c.rms_norm_eps)
+                continue
+            P = be.gemm_part(a, L["wdown"])
             if pf:
                 be.pf_arm([(layers[li + 1]["wqkv"] if li + 1 < len(layers) else w.lm_head, 0, pf["post"])],
                           pf["blocks"])

@@ -121,14 +121,6 @@ def test_gemm_decode_v3(native, M, N, K):
         y = native.gemm(x, R.pack_gate_up(g, u), epi="silu_mul", path=4)
         ref2 = torch.nn.functional.silu(x.float() @ g.float().t()) * (x.float() @ u.float().t())
         assert rel_err(y, ref2) < 1e-2
-        # 128-row tiles (one block per CU) == 64-row pair tiles (two per CU): same k order per output
-        L = native._lib.lib()
-        try:
-            L.ragk_gemm_stream_set_pair_rows(128)
-            y128 = native.gemm(x, R.pack_gate_up(g, u), epi="silu_mul", path=5)
-        finally:
-            L.ragk_gemm_stream_set_pair_rows(64)
-        assert torch.equal(y, y128)
 
 
 @pytest.mark.parametrize("path", [0, 1])

@@ -42,11 +42,14 @@ def timed_graph(body, reps=5):
 def main():
     torch.manual_seed(0)
     res = []
-    for (name, n, k) in [("o_proj", 4096, 4096), ("down", 4096, 14336), ("qkv", 6144, 4096)]:
+    shapes = [("o_proj", 4096, 4096), ("down", 4096, 14336), ("qkv", 6144, 4096)]
+    ms = [int(v) for v in os.environ.get("AB_M", "1,32").split(",")]
+    only = os.environ.get("AB_VARIANTS", "")
+    for (name, n, k) in shapes:
         ws = [(torch.randn(n, k, device="cuda") / math.sqrt(k)).bfloat16() for _ in range(LAYERS)]
         nw = (torch.ones(H, device="cuda")).bfloat16()
         mb = n * k * 2 / 2 ** 20
-        for M in (1, 32):
+        for M in ms:
             x = torch.randn(M, k, device="cuda").bfloat16()
             h = torch.randn(M, H, device="cuda").bfloat16()
             out = torch.empty(M, n, device="cuda").bfloat16()
@@ -75,6 +78,8 @@ def main():
                         N.rmsnorm(h, nw, 1e-5)
                 variants["default+rmsnorm"] = default_pair
             for vname, v in variants.items():
+                if only and not any(vname.startswith(o) for o in only.split(",")):
+                    continue
                 S = 0
                 if isinstance(v, tuple):
                     v, S = v
