@@ -535,6 +535,11 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
     }
   }
 
+  // partition-statistics buffers as write-through (sc1) buffer resources for the fused merge
+  const unsigned pbytes = (unsigned)((size_t)gridDim.z * a.Hq * a.max_parts * 4);
+  const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(a.part_o, (short)0, (int)(pbytes * D), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_ml = __builtin_amdgcn_make_buffer_rsrc(a.part_ml, (short)0, (int)(pbytes * 2), 0x00020000);
+
   // ---- combine the 4 waves in LDS ----
   __syncthreads();
   float* sm = reinterpret_cast<float*>(smem);    // [4][16] max
@@ -566,35 +571,39 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
       a.out[(size_t)b * a.out_stride + hq * D + d] = f2bf(L > 0.f ? O / L : 0.f);
     } else {
       const size_t pi = ((size_t)b * a.Hq + hq) * a.max_parts + part;
-      a.part_o[pi * D + d] = O;
-      if (d == 0) {
-        a.part_ml[pi * 2] = M;
-        a.part_ml[pi * 2 + 1] = L;
+      if (a.counters) {  // fused merge: write-through (sc1) stores, read back by another CU below
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(O), rs_o, (int)((pi * D + d) * 4), 0, 16);
+        if (d == 0) {
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(M), rs_ml, (int)(pi * 8), 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(L), rs_ml, (int)(pi * 8 + 4), 0, 16);
+        }
+      } else {
+        a.part_o[pi * D + d] = O;
+        if (d == 0) {
+          a.part_ml[pi * 2] = M;
+          a.part_ml[pi * 2 + 1] = L;
+        }
       }
     }
   }
   if (nparts == 1 || a.counters == nullptr) return;
 
   // ---- fused split-K merge: the last of this (b, kvh)'s nparts partition blocks to finish merges
-  // them (same math as attn_decode_reduce_kernel), so the merge costs no extra launch. Agent-scope
-  // release before the ticket / acquire after it: the partition blocks may sit on any XCD.
+  // them (same math as attn_decode_reduce_kernel), so the merge costs no extra launch. The partials
+  // were stored write-through (sc1) and are read back with sc1 loads, so no agent-scope release or
+  // acquire fence is needed for any block -> XCD placement (an L2 write-back per block cost more than
+  // the merge launch it saved).
   __shared__ int s_last;
-  wait_vmcnt0();
+  wait_vmcnt0();  // every storing wave drains its sc1 stores
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    wait_vmcnt0();
     const int old = __hip_atomic_fetch_add(a.counters + b * a.Hkv + kvh, 1, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
     s_last = (old == nparts - 1);
   }
   __syncthreads();
   if (!s_last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    wait_vmcnt0();
-  }
-  __syncthreads();
+  asm volatile("" ::: "memory");  // the sc1 loads below stay after the ticket
   float* s_m = reinterpret_cast<float*>(smem);  // [G][nparts] partition max, then its scale
   float* s_l = s_m + G * nparts;                 // [G][nparts] partition sum
   float* s_L = s_l + G * nparts;                 // [G] merged sum
@@ -602,8 +611,8 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
   for (int e = threadIdx.x; e < G * nparts; e += 256) {
     const int g = e / nparts, p = e % nparts;
     const size_t pi = (hb + g) * a.max_parts + p;
-    s_m[e] = a.part_ml[pi * 2];
-    s_l[e] = a.part_ml[pi * 2 + 1];
+    s_m[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ml, (int)(pi * 8), 0, 16));
+    s_l[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ml, (int)(pi * 8 + 4), 0, 16));
   }
   __syncthreads();
   if (threadIdx.x < G) {
@@ -622,18 +631,18 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
   __syncthreads();
   for (int e = threadIdx.x; e < G * D; e += 256) {
     const int g = e / D, d = e % D;
-    const float* po = a.part_o + (hb + g) * a.max_parts * D + d;
+    const int po = (int)(((hb + g) * a.max_parts * D + d) * 4);  // byte offset of partition 0
     const float* sc = s_m + g * nparts;
     float O = 0.f;
     int p = 0;
     for (; p + 8 <= nparts; p += 8) {  // 8 independent loads in flight
       float v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = po[(size_t)(p + i) * D];
+      for (int i = 0; i < 8; ++i) v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_o, po + (p + i) * D * 4, 0, 16));
 #pragma unroll
       for (int i = 0; i < 8; ++i) O += v[i] * sc[p + i];
     }
-    for (; p < nparts; ++p) O += po[(size_t)p * D] * sc[p];
+    for (; p < nparts; ++p) O += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_o, po + p * D * 4, 0, 16)) * sc[p];
     const float L = s_L[g];
     a.out[(size_t)b * a.out_stride + (kvh * G + g) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
   }
