@@ -168,8 +168,10 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16" if a.dtype == "bf16" else "fp8-weights (bf16 activations/KV)",
             "data": "synthetic (random-init weights of the named architectures; Zipfian pseudo-English corpus "
-                    "of %d x 1000-word chunks; trained 128k BPE + %s tokenizers)" % (
-                        a.chunks, "XLM-R SentencePiece Unigram" if a.embedder == "bge-m3" else "WordPiece"),
+                    "of %d x 1000-word chunks%s; trained 128k BPE + %s tokenizers)" % (
+                        a.chunks, (" + %d embedded 100-word topical chunks" % (a.index_vectors - a.chunks)
+                                   if a.index_vectors > a.chunks else ""),
+                        "XLM-R SentencePiece Unigram" if a.embedder == "bge-m3" else "WordPiece"),
             "config": {
                 "model": {"8b": "Llama-3.1-8B-Instruct", "70b": "Llama-3.1-70B-Instruct", "tiny": "llama-tiny"}[a.model],
                 "embedder": {"minilm": "all-MiniLM-L6-v2", "bge-large": "bge-large-en-v1.5", "bge-m3": "bge-m3",

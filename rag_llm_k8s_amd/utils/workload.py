@@ -173,26 +173,34 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     cfg = RagConfig(device=device, retrieve_k=retrieve_k, context_k=context_k, max_new_tokens=max_new_tokens,
                     max_batch=max_batch, max_model_len=max_model_len, index_path="/tmp/ragk_bench_index",
                     index_type=index_type, seed=seed, max_prefill_tokens=max_prefill_tokens, ignore_eos=ignore_eos)
-    store = DocumentStore(cfg.index_path, emb.dim, device=device, index_type=index_type)
+    n_index = max(n_chunks, index_vectors)
+    store = DocumentStore(cfg.index_path, emb.dim, device=device, index_type=index_type,
+                          ivf_nlist=4096 if n_index >= 500_000 else 1024)
     vecs = emb.embed(chunks)
     if device.startswith("cuda"):
         torch.cuda.synchronize()
     t["embed_s"] = time.time() - t0  # tokenize + encode of the n_chunks corpus (ingest throughput)
     meta = [{"filename": "synthetic_%05d.pdf" % (i // 20), "chunk_id": i % 20, "text": c}
             for i, c in enumerate(chunks)]
+    # BASELINE config 4 scale (1M-chunk index): the rest of the index is a second corpus of short
+    # (100-word) chunks with topical structure, EMBEDDED by the same encoder (a real corpus, not random
+    # vectors; ~30 s for 1M chunks with MiniLM). Their text is real, so retrieval may pick them.
+    pads = []
+    if index_vectors > len(meta):
+        tc = TopicCorpus(wm, n_topics=2000, topic_words=40, mix=0.5, seed=seed)
+        bs, done = 65536, len(meta)
+        while done < index_vectors:
+            nb = min(bs, index_vectors - done)
+            texts = tc.chunks(nb, 100, seed=seed + 17 + done // bs)
+            pads.append((emb.embed(texts), [{"filename": "synthetic_pad_%04d.pdf" % ((done + i) // 1000),
+                                             "chunk_id": (done + i) % 1000, "text": x}
+                                            for i, x in enumerate(texts)]))
+            done += nb
+    if index_type == "ivf":  # train the coarse quantizer on the whole corpus (faiss subsample rule)
+        store.index.train(torch.cat([vecs] + [v for v, _ in pads]))
     store.add(vecs, meta, dedupe=False, persist=False)
-    # BASELINE config 4 scale (1M-chunk index): pad the index with random unit vectors after the
-    # embedded corpus (embedding 1M x 1000-word chunks is hours of encoder time; search cost depends
-    # only on the index size). Padding rows carry empty text.
-    g = torch.Generator(device=device).manual_seed(seed + 7)
-    done = len(meta)
-    while done < index_vectors:
-        nb = min(131072, index_vectors - done)
-        pad = torch.randn(nb, emb.dim, device=device, generator=g)
-        pad = torch.nn.functional.normalize(pad, dim=1).cpu().numpy()
-        store.add(pad, [{"filename": "synthetic_pad", "chunk_id": done + i, "text": ""} for i in range(nb)],
-                  dedupe=False, persist=False)
-        done += nb
+    for v, m in pads:
+        store.add(v, m, dedupe=False, persist=False)
     if device.startswith("cuda"):
         torch.cuda.synchronize()
     t["ingest_s"] = time.time() - t0
