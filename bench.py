@@ -169,7 +169,7 @@ def main():
             "dtype": "bf16" if a.dtype == "bf16" else "fp8-weights (bf16 activations/KV)",
             "data": "synthetic (random-init weights of the named architectures; Zipfian pseudo-English corpus "
                     "of %d x 1000-word chunks%s; trained 128k BPE + %s tokenizers)" % (
-                        a.chunks, (" + %d embedded 100-word topical chunks" % (a.index_vectors - a.chunks)
+                        a.chunks, (" + %d embedded 1000-word topical chunks" % (a.index_vectors - a.chunks)
                                    if a.index_vectors > a.chunks else ""),
                         "XLM-R SentencePiece Unigram" if a.embedder == "bge-m3" else "WordPiece"),
             "config": {

@@ -107,6 +107,20 @@ class TopicCorpus:
     def chunks(self, n, words, seed):
         return self._words(n, words, np.random.default_rng(seed))[0]
 
+    def paragraph_chunks(self, n, words, seed, para_words=100, paras_per_topic=64):
+        """Fast path for index-scale corpora (1M x 1000 words): each topic owns a pool of
+        `paras_per_topic` topical paragraphs and a chunk is `words // para_words` of its topic's
+        paragraphs in random order, so chunks of one topic share vocabulary but (almost) never text."""
+        rng = np.random.default_rng(seed)
+        if getattr(self, "_paras", None) is None:
+            prng = np.random.default_rng(4242)
+            self._paras = self._words(len(self.vocab) * paras_per_topic, para_words, prng)[0]
+        per = max(1, words // para_words)
+        topics = rng.integers(0, len(self.vocab), n)
+        pick = topics[:, None] * paras_per_topic + rng.integers(0, paras_per_topic, (n, per))
+        P = self._paras
+        return [" ".join([P[j] for j in row]) for row in pick.tolist()]
+
     def queries(self, n, words, seed):
         return [q.capitalize() + "?" for q in self._words(n, words, np.random.default_rng(seed + 7))[0]]
 
@@ -182,16 +196,17 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     t["embed_s"] = time.time() - t0  # tokenize + encode of the n_chunks corpus (ingest throughput)
     meta = [{"filename": "synthetic_%05d.pdf" % (i // 20), "chunk_id": i % 20, "text": c}
             for i, c in enumerate(chunks)]
-    # BASELINE config 4 scale (1M-chunk index): the rest of the index is a second corpus of short
-    # (100-word) chunks with topical structure, EMBEDDED by the same encoder (a real corpus, not random
-    # vectors; ~30 s for 1M chunks with MiniLM). Their text is real, so retrieval may pick them.
+    # BASELINE config 4 scale (1M-chunk index): the rest of the index is a second corpus of
+    # `chunk_words`-word chunks with topical structure, EMBEDDED by the same encoder (a real corpus, not
+    # random vectors; ~1 min for 1M chunks with MiniLM, ~7 GB of host text). Their text is real, so
+    # retrieval picks them and the prompts keep the reference chunker's size.
     pads = []
     if index_vectors > len(meta):
         tc = TopicCorpus(wm, n_topics=2000, topic_words=40, mix=0.5, seed=seed)
         bs, done = 65536, len(meta)
         while done < index_vectors:
             nb = min(bs, index_vectors - done)
-            texts = tc.chunks(nb, 100, seed=seed + 17 + done // bs)
+            texts = tc.paragraph_chunks(nb, chunk_words, seed=seed + 17 + done // bs)
             pads.append((emb.embed(texts), [{"filename": "synthetic_pad_%04d.pdf" % ((done + i) // 1000),
                                              "chunk_id": (done + i) % 1000, "text": x}
                                             for i, x in enumerate(texts)]))
