@@ -400,8 +400,8 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_prefill_kernel(Prefill
 #pragma unroll
       for (int dt = 0; dt < C::DT; ++dt) {
         const f32x4 v = o[dt][qt] * inv;
-        const unsigned lo = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-        const unsigned hi = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+        const unsigned lo = pk2bf(v[0], v[1]);
+        const unsigned hi = pk2bf(v[2], v[3]);
         *reinterpret_cast<uint2*>(op + 16 * dt) = make_uint2(lo, hi);
       }
     }

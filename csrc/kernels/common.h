@@ -33,6 +33,12 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, h);
 }
 __device__ __forceinline__ short f2bf_s(float f) { return (short)f2bf(f); }
+// two floats -> packed bf16x2 (lo = a) in ONE v_cvt_pk_bf16_f32 (two scalar f2bf + shift/or is 3-4)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pk2bf(float a, float b) {
+  const bf16x2_t h = __builtin_convertvector((f32x2){a, b}, bf16x2_t);
+  return __builtin_bit_cast(unsigned, h);
+}
 
 // 16-byte vector of 8 bf16 <-> 8 floats
 __device__ __forceinline__ void unpack8(const u32x4 v, float* f) {
@@ -46,7 +52,7 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   u32x4 v;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    v[i] = (unsigned)f2bf(f[2 * i]) | ((unsigned)f2bf(f[2 * i + 1]) << 16);
+    v[i] = pk2bf(f[2 * i], f[2 * i + 1]);
   return v;
 }
 

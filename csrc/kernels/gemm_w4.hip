@@ -120,8 +120,8 @@ __device__ __forceinline__ void w4_store4(void* C, size_t idx, const float (&o)[
   if (f32) {
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + idx) = (f32x4){o[0], o[1], o[2], o[3]};
   } else {
-    const unsigned lo = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
-    const unsigned hi = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+    const unsigned lo = pk2bf(o[0], o[1]);
+    const unsigned hi = pk2bf(o[2], o[3]);
     *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(C) + idx) = make_uint2(lo, hi);
   }
 }
@@ -263,8 +263,8 @@ __device__ __forceinline__ void w4_epilogue_wide(const f32x4 (&acc)[8][8], int w
             a[r] = silu(acc[i][jp][r]) * acc[i][jp + 4][r];
             b[r] = silu(acc[i][jp + 1][r]) * acc[i][jp + 5][r];
           }
-          x[h] = (unsigned)f2bf(a[2 * h]) | ((unsigned)f2bf(a[2 * h + 1]) << 16);
-          y[h] = (unsigned)f2bf(b[2 * h]) | ((unsigned)f2bf(b[2 * h + 1]) << 16);
+          x[h] = pk2bf(a[2 * h], a[2 * h + 1]);
+          y[h] = pk2bf(b[2 * h], b[2 * h + 1]);
         }
         w4_swap_store(row, colb + 16 * jp, fh, x, y);
       }
@@ -319,8 +319,8 @@ __device__ __forceinline__ void w4_epilogue_wide(const f32x4 (&acc)[8][8], int w
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[r] = gelu_tanh(o[r]);
           }
-          pk[q][0] = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
-          pk[q][1] = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+          pk[q][0] = pk2bf(o[0], o[1]);
+          pk[q][1] = pk2bf(o[2], o[3]);
         }
         w4_swap_store(row, n0 + wc * 128 + 16 * jp, fh, pk[0], pk[1]);
       }
@@ -782,6 +782,193 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Continuous K-stream variant (gemm_w4c_kernel). The persistent kernel above pays, per output tile,
+// ~7.5k cycles of prologue (acc zeroing, waiting for the new tile's first K-tile, reading its first
+// fragments with no MFMA to hide behind) plus the next tile's 32 DMA issues inside the ~13k-cycle
+// epilogue window (tools/gemm_epi_probe.py: 12-13k cycles per tile at any grid size, so it is issue /
+// latency, not the store burst). Here the block's K-tiles form ONE stream across its tiles: the last two
+// iterations of tile i stage K-tiles 0 and 1 of tile i+1 (with that tile's row offsets) into the ring
+// slots the stream would have used, the last iteration's segment 3 reads tile i+1's first fragments,
+// and the first iteration of a tile writes its accumulators with srcC = 0 (no zeroing pass). Between
+// the tiles only the register epilogue remains; its stores are counted into the first iteration's
+// vmcnt. Ring slot = running K-tile index g & 1 (not t & 1: K-tile counts may be odd).
+__device__ __forceinline__ void w4_mfma0(f32x4 (&acc)[8][8], const bf16x8 (&a)[8], const bf16x8 (&b)[8], int m) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %2, %1, 0"
+               : "=a"(acc[m >> 3][m & 7])
+               : "v"(a[m >> 3]), "v"(b[m & 7])
+               : "memory");
+}
+
+template <bool ZERO>
+__device__ __forceinline__ void w4_mfma_z(f32x4 (&acc)[8][8], const bf16x8 (&a0)[8], const bf16x8 (&b0)[8],
+                                          const bf16x8 (&a1)[8], const bf16x8 (&b1)[8], int m) {
+  if (m < 64) {
+    if (ZERO) w4_mfma0(acc, a0, b0, m);
+    else w4_mfma(acc, a0, b0, m);
+  } else {
+    w4_mfma(acc, a1, b1, m - 64);
+  }
+}
+
+// w4_iter with: ring slot from g, DMA source offsets / K-tile passed in (sa/sb at K-tile kst: this
+// tile's t+2 or the next tile's 0 / 1), ZERO = F0 MFMAs start the accumulators, VMW = vmcnt bound at
+// the end of segment 2 when a DMA was issued (16 + vector-memory ops issued after the slot's DMA).
+template <bool STAGE, bool READ, bool ZERO, int VMW, bool STAMP>
+__device__ __forceinline__ void w4_iter_c(char* smem, int g, i32x4 srd_a, i32x4 srd_b, const int (&sa)[8],
+                                          const int (&sb)[8], int kst, int wid, int wr, int wc, int fr, int fh,
+                                          f32x4 (&acc)[8][8], bf16x8 (&a0)[8], bf16x8 (&b0)[8], bf16x8 (&a1)[8],
+                                          bf16x8 (&b1)[8], unsigned long long (&stp)[5]) {
+  constexpr int S1 = W4_S1, S3 = W4_S3, N2 = 128 - S1 - S3, DSTEP = N2 / 16;
+  static_assert(S1 == 32 && S3 == 16, "continuous schedule uses the production split");
+  static_assert(VMW >= 16 && VMW <= 63, "vmcnt bound");
+  char* buf = smem + (g & 1) * W_BUF;
+  unsigned long long t0 = 0;
+  if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+  for (int m = 0; m < S1; ++m) {
+    if (m < 16) w4_read_frag(buf, 1, m, wr, wc, fr, fh, a1, b1);
+    w4_mfma_z<ZERO>(acc, a0, b0, a1, b1, m);
+  }
+  __builtin_amdgcn_s_waitcnt(W_LGKM0);
+  w4_barrier();
+#pragma unroll
+  for (int i = 0; i < N2; ++i) {
+    if constexpr (STAGE) {
+      if (i % DSTEP == 0) {
+        const int q = i / DSTEP;
+        if (q < 8) blds16(srd_a, sa[q], kst * WBK * 2, buf + (wid * 8 + q) * 1024);
+        else blds16(srd_b, sb[q - 8], kst * WBK * 2, buf + W_TILE_A + (wid * 8 + q - 8) * 1024);
+      }
+    }
+    w4_mfma_z<ZERO>(acc, a0, b0, a1, b1, S1 + i);
+  }
+  if constexpr (STAGE) __builtin_amdgcn_s_waitcnt((VMW & 15) | (((VMW >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
+  else __builtin_amdgcn_s_waitcnt(W_VM0);
+  w4_barrier();
+  const char* nbuf = smem + ((g + 1) & 1) * W_BUF;
+#pragma unroll
+  for (int i = 0; i < S3; ++i) {
+    if constexpr (READ) w4_read_frag(nbuf, 0, i, wr, wc, fr, fh, a0, b0);
+    w4_mfma_z<false>(acc, a0, b0, a1, b1, 128 - S3 + i);
+  }
+  if constexpr (STAMP) stp[4] += __builtin_amdgcn_s_memtime() - t0;
+}
+
+// Requires K / 64 >= 4 (the launcher falls back to gemm_w4_kernel below that).
+template <int EPI, bool OUT_F32, bool STAMP = false>
+__global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4c_kernel(const bf16_t* __restrict__ A, int lda,
+                                                                 const bf16_t* __restrict__ B, int ldb, void* C,
+                                                                 int ldc, const bf16_t* __restrict__ bias,
+                                                                 const bf16_t* resid, int ldr, int M, int N, int K,
+                                                                 unsigned long long* dbg) {
+  __shared__ __attribute__((aligned(16))) char smem[W4_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int fr = lane & 15, fh = lane >> 4;
+  const int tiles_m = (M + WBM - 1) / WBM, tiles_n = (N + WBN - 1) / WBN;
+  const int nwg = tiles_m * tiles_n;
+  const int nk = K / WBK;
+  const i32x4 srd_a = make_srd(A, (unsigned)M * (unsigned)lda * 2u);
+  const i32x4 srd_b = make_srd(B, (unsigned)N * (unsigned)ldb * 2u);
+
+  // epilogue vector-memory ops younger than the next tile's K-tile-1 DMA at its first vmcnt
+  constexpr int EV = w4_epi_vmem<EPI, OUT_F32 || !W4_WIDE_EPI>() +
+                     ((!OUT_F32 && !W4_WIDE_EPI && EPI == EPI_SILU_MUL) ? 16 : 0);
+  constexpr int VMW0 = 16 + EV > 63 ? 63 : 16 + EV;
+
+  int tile = blockIdx.x;
+  int m0, n0;
+  w4_origin(tile, nwg, tiles_m, tiles_n, m0, n0);
+  int off_a[8], off_b[8];
+  w4_offsets(lda, m0, M, wid, lane, off_a);
+  w4_offsets(ldb, n0, N, wid, lane, off_b);
+  w4_stage(srd_a, off_a, 0, smem, wid);
+  w4_stage(srd_b, off_b, 0, smem + W_TILE_A, wid);
+  w4_stage(srd_a, off_a, WBK, smem + W_BUF, wid);
+  w4_stage(srd_b, off_b, WBK, smem + W_BUF + W_TILE_A, wid);
+  __builtin_amdgcn_s_waitcnt(W_VM0);  // K-tiles 0 and 1: the first iteration's vmcnt then only covers K-tile 2
+  w4_barrier();
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+  w4_read(smem, 0, wr, wc, fr, fh, a0, b0);
+  __builtin_amdgcn_s_waitcnt(W_LGKM0);
+  __builtin_amdgcn_sched_barrier(0);
+
+  f32x4 acc[8][8];
+  unsigned long long stp[5] = {0, 0, 0, 0, 0};
+  unsigned long long tl_loop = 0, tl_epi = 0;
+  int g = 0, done = 0;
+  for (;;) {
+    unsigned long long tt0 = 0;
+    if constexpr (STAMP) tt0 = __builtin_amdgcn_s_memtime();
+    const int next = tile + (int)gridDim.x;
+    const bool has_next = next < nwg;
+    w4_iter_c<true, true, true, VMW0, false>(smem, g, srd_a, srd_b, off_a, off_b, 2, wid, wr, wc, fr, fh, acc, a0,
+                                             b0, a1, b1, stp);
+    ++g;
+    for (int t = 1; t + 2 < nk; ++t, ++g)
+      w4_iter_c<true, true, false, 16, STAMP>(smem, g, srd_a, srd_b, off_a, off_b, t + 2, wid, wr, wc, fr, fh, acc,
+                                              a0, b0, a1, b1, stp);
+    // The last two iterations stage (and read the first fragments of) the next tile; on the block's
+    // last tile they re-stage this tile's K-tiles 0 / 1 instead (valid addresses, never read), so both
+    // cases run the same straight-line code: a branch around the MFMA iterations made the register
+    // allocator split the accumulators across the two paths and spill them.
+    int nm0, nn0;
+    w4_origin(has_next ? next : tile, nwg, tiles_m, tiles_n, nm0, nn0);
+    {
+      int ln;  // == lane; opaque so the lane-only offset math is not hoisted out of the loop
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      // this tile's DMAs are all issued: its offset registers take the next tile's
+      w4_offsets(lda, nm0, M, wid, ln, off_a);
+      w4_offsets(ldb, nn0, N, wid, ln, off_b);
+    }
+    w4_iter_c<true, true, false, 16, false>(smem, g, srd_a, srd_b, off_a, off_b, 0, wid, wr, wc, fr, fh, acc, a0, b0,
+                                            a1, b1, stp);
+    ++g;
+    w4_iter_c<true, true, false, 16, false>(smem, g, srd_a, srd_b, off_a, off_b, 1, wid, wr, wc, fr, fh, acc, a0, b0,
+                                            a1, b1, stp);
+    ++g;
+    unsigned long long tt1 = 0;
+    if constexpr (STAMP) tt1 = __builtin_amdgcn_s_memtime();
+    w4_pin_acc(acc);
+    if (m0 + WBM <= M && n0 + WBN <= N) {
+      if constexpr (OUT_F32 || !W4_WIDE_EPI)
+        w4_epilogue_reg<EPI, OUT_F32, true>(acc, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr, M, N);
+      else
+        w4_epilogue_wide<EPI>(acc, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr);
+    } else {
+      w4_epilogue_reg<EPI, OUT_F32, false>(acc, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr, M, N);
+      __builtin_amdgcn_s_waitcnt(W_VM0);  // guarded: count unknown, drain (the next K-tile 1 lands too)
+    }
+    // epilogue accumulator reads -> the next tile's srcC = 0 MFMA writes
+    asm volatile("s_nop 7" ::: "memory");
+    ++done;
+    if constexpr (STAMP) {
+      const unsigned long long tt2 = __builtin_amdgcn_s_memtime();
+      tl_loop += tt1 - tt0;
+      tl_epi += tt2 - tt1;
+    }
+    if (!has_next) {
+      __builtin_amdgcn_s_waitcnt(W_VM0);  // the re-staged K-tiles land before the block's LDS is released
+      break;
+    }
+    tile = next;
+    m0 = nm0;
+    n0 = nn0;
+  }
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      unsigned long long* d = dbg + ((size_t)blockIdx.x * 4 + wid) * 8;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) d[i] = stp[i];
+      d[5] = (unsigned long long)done * (unsigned long long)(nk - 3);  // stamped steady-state iterations
+      d[6] = tl_loop;
+      d[7] = tl_epi;
+    }
+  }
+}
+
 // Persistent grid: one block per CU (the kernel holds 128 KiB of LDS and 4 waves x 512 registers,
 // so a CU never runs two), rounded down to a multiple of 8 so a block keeps its XCD across tiles.
 // RAGK_W4_GRID=0 launches one block per tile instead (A/B), N > 0 caps the grid at N.
@@ -811,12 +998,26 @@ static int w4_sched_min_k() {
   return g_w4_sched_k;
 }
 
+// Continuous K-stream kernel for K < the spread-schedule threshold (RAGK_W4_CONT=0 -> gemm_w4_kernel).
+static int g_w4_cont = -1;
+static bool w4_cont() {
+  if (g_w4_cont < 0) {
+    const char* e = getenv("RAGK_W4_CONT");
+    g_w4_cont = e ? (atoi(e) != 0) : 1;
+  }
+  return g_w4_cont != 0;
+}
+
 template <int EPI, bool F32>
 int launch_w4(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias, const void* resid,
               int ldr, int M, int N, int K, hipStream_t st) {
   const int nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
   const int grid = w4_grid(nwg);
-  if (K >= w4_sched_min_k())
+  if (K < w4_sched_min_k() && K / WBK >= 4 && w4_cont())
+    hipLaunchKernelGGL((gemm_w4c_kernel<EPI, F32>), dim3(grid), dim3(W4_THREADS), 0, st, (const bf16_t*)A, lda,
+                       (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K,
+                       nullptr);
+  else if (K >= w4_sched_min_k())
     hipLaunchKernelGGL((gemm_w4_kernel<EPI, F32, false, 16, 7, 4>), dim3(grid), dim3(W4_THREADS), 0, st,
                        (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid,
                        ldr, M, N, K, nullptr);
@@ -833,6 +1034,13 @@ int launch_w4(const void* A, int lda, const void* B, int ldb, void* C, int ldc, 
 // multiple of 8 keeps each block on one XCD), < 0 = back to the CU count.
 RAGK_API int ragk_gemm_w4_set_grid(int g) {
   g_w4_grid = g < 0 ? -1 : g;
+  return 0;
+}
+
+// Continuous-K-stream override (tests / A/B): 1 = gemm_w4c_kernel for K < the spread threshold, 0 = off,
+// < 0 = back to RAGK_W4_CONT / the default (on).
+RAGK_API int ragk_gemm_w4_set_cont(int on) {
+  g_w4_cont = on < 0 ? -1 : (on != 0);
   return 0;
 }
 
@@ -929,6 +1137,18 @@ RAGK_API int ragk_gemm_w4_diag(int variant, int stamp, const void* A, int lda, c
     case 21:
       return stamp ? launch_w4_diag<true, 48, 5, 4, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)
                    : launch_w4_diag<false, 48, 5, 4, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);
+    case 22:  // continuous K-stream kernel (production for K < 8192)
+    {
+      if (K / WBK < 4) return (int)hipErrorInvalidValue;
+      const dim3 grid(w4_grid(((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN)));
+      if (stamp)
+        hipLaunchKernelGGL((gemm_w4c_kernel<EPI_NONE, false, true>), grid, dim3(W4_THREADS), 0, st, (const bf16_t*)A,
+                           lda, (const bf16_t*)B, ldb, C, ldc, nullptr, nullptr, 0, M, N, K, dbg);
+      else
+        hipLaunchKernelGGL((gemm_w4c_kernel<EPI_NONE, false, false>), grid, dim3(W4_THREADS), 0, st,
+                           (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, nullptr, nullptr, 0, M, N, K, dbg);
+      return (int)hipGetLastError();
+    }
     case 15:  // w4_iter2 (32, 6) + widened epilogue
       return stamp ? launch_w4_diag<true, 32, 6, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st)
                    : launch_w4_diag<false, 32, 6, 2, true>(A, lda, B, ldb, C, ldc, M, N, K, dbg, st);

@@ -29,7 +29,7 @@ HIP_LIB = os.path.join(LIB_DIR, "libragk_hip.so")
 
 
 # per-file flags: gemm_w4.hip is written in its final instruction order (see its header)
-EXTRA_FLAGS = {"gemm_w4.hip": ["-mllvm", "-enable-misched=0", "-mllvm", "-disable-post-ra"]}
+EXTRA_FLAGS = {"gemm_w4.hip": ["-mllvm", "-disable-post-ra"]}
 
 
 def _newer(src_files, target):

@@ -25,6 +25,7 @@ _SIGS = {
     "ragk_gemm_pp": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_pp_set_variant": [I],
     "ragk_gemm_w4_set_grid": [I],
+    "ragk_gemm_w4_set_cont": [I],
     "ragk_attn_prefill_set_prio": [I],
     "ragk_attn_prefill_set_buf": [I],
     "ragk_gemm_stream_set_nt": [I],

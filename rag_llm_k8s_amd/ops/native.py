@@ -53,6 +53,12 @@ def set_w4_grid(g):
     check(_lib.lib().ragk_gemm_w4_set_grid(int(g)), "ragk_gemm_w4_set_grid")
 
 
+def set_w4_cont(on):
+    """gemm_w4 continuous K-stream kernel (K < 8192): 1 = on (default), 0 = the per-tile-prologue
+    kernel, -1 = back to RAGK_W4_CONT / the default."""
+    check(_lib.lib().ragk_gemm_w4_set_cont(int(on)), "ragk_gemm_w4_set_cont")
+
+
 DEC_DEFAULT = os.environ.get("RAGK_DEC_GEMM", "1") == "1"
 DEC_WS_BYTES = int(os.environ.get("RAGK_DEC_WS_MB", "96")) << 20
 _dec_ws = {}
