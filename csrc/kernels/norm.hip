@@ -121,10 +121,22 @@ __global__ __launch_bounds__(NT) void layernorm_kernel(const bf16_t* x, int ldx,
 }
 
 // token embedding gather: out[t] = table[ids[t]]
-__global__ __launch_bounds__(NT) void embed_kernel(const int* __restrict__ ids, const bf16_t* __restrict__ table,
-                                                   bf16_t* out, int H, int vocab) {
+// carry (optional, asynchronous decode): carry[t] >= 0 takes the token id from prev[carry[t]] (the
+// previous decode step's sampled tokens, still on the device) instead of ids[t]; the resolved id is
+// written back to ids[t] so the step's inputs stay self-describing.
+__global__ __launch_bounds__(NT) void embed_kernel(int* __restrict__ ids, const bf16_t* __restrict__ table,
+                                                   bf16_t* out, int H, int vocab, const int* __restrict__ carry,
+                                                   const int* __restrict__ prev) {
   const int t = blockIdx.x;
   int id = ids[t];
+  if (carry != nullptr) {
+    const int c = carry[t];
+    if (c >= 0) {
+      id = prev[c];
+      __syncthreads();  // every lane has read ids[t] before lane 0 overwrites it
+      if (threadIdx.x == 0) ids[t] = id;
+    }
+  }
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);
   const u32x4* src = reinterpret_cast<const u32x4*>(table + (size_t)id * H);
   u32x4* dst = reinterpret_cast<u32x4*>(out + (size_t)t * H);
@@ -498,7 +510,19 @@ RAGK_API int ragk_layernorm(const void* x, int ldx, const void* resid, int ldr, 
 RAGK_API int ragk_embed(const int* ids, const void* table, void* out, int T, int H, int vocab, hipStream_t st) {
   if (T <= 0) return 0;
   if (H % 8) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(NT), 0, st, ids, (const bf16_t*)table, (bf16_t*)out, H, vocab);
+  hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(NT), 0, st, const_cast<int*>(ids), (const bf16_t*)table,
+                     (bf16_t*)out, H, vocab, (const int*)nullptr, (const int*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// Embedding gather whose token ids may come from the previous step's device-side sampler output:
+// carry[t] >= 0 -> id = prev[carry[t]] (also stored to ids[t]); carry[t] < 0 -> ids[t].
+RAGK_API int ragk_embed_carry(int* ids, const int* carry, const int* prev, const void* table, void* out, int T,
+                              int H, int vocab, hipStream_t st) {
+  if (T <= 0) return 0;
+  if (H % 8 || !carry || !prev) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(NT), 0, st, ids, (const bf16_t*)table, (bf16_t*)out, H, vocab,
+                     carry, prev);
   return (int)hipGetLastError();
 }
 

@@ -142,6 +142,10 @@ class LLMEngine:
         self._out_pins = [torch.empty(max(1, max_batch), dtype=torch.int32, pin_memory=self.is_cuda)
                           for _ in range(2)]
         self._out_idx = 0
+        # sampled tokens of every decode graph land in this one device buffer: the next step's graph
+        # (any bucket) reads its carried ids from it inside the embedding kernel (packed "carry" map)
+        self._tok_out = torch.zeros(max(self.buckets + [max_batch, 1]), dtype=torch.int32,
+                                    device=self.device) if self.is_cuda else None
 
     # ------------------------------------------------------------------ requests
     def add_request(self, prompt_ids, params: SamplingParams, seed: Optional[int] = None) -> Sequence:
@@ -596,17 +600,19 @@ class LLMEngine:
         dev = self.device
         mb = self.max_blocks
         meta_n = 4 * B + B * mb + (4 * B + B * mb) % 2  # even: the sampling block holds int64 seeds
-        packed = torch.zeros(meta_n + 6 * B, dtype=torch.int32, device=dev)  # ONE H2D copy per step
+        # ONE H2D copy per step: [decode metadata | sampling params (6B) | carry map (B)]
+        packed = torch.zeros(meta_n + 7 * B, dtype=torch.int32, device=dev)
         ids, pos, slots, kvl = (packed[i * B:(i + 1) * B] for i in range(4))
+        carry = packed[meta_n + 6 * B:meta_n + 7 * B]
         bt = packed[4 * B:4 * B + B * mb].view(B, mb)
         pt, mp = decode_partitions(self.max_model_len, B, m.Hkv)
         ws_o = torch.empty((B, m.Hq, mp, m.D), dtype=torch.float32, device=dev) if mp > 1 else None
         ws_ml = torch.empty((B, m.Hq, mp, 2), dtype=torch.float32, device=dev) if mp > 1 else None
         meta = AttnMeta("decode", kvl, bt, part_tiles=pt, max_parts=mp, ws_o=ws_o, ws_ml=ws_ml)
-        temps, ks, ps, seeds, steps = self._sampling_views(packed[meta_n:], B)
+        temps, ks, ps, seeds, steps = self._sampling_views(packed[meta_n:meta_n + 6 * B], B)
         samp = dict(temps=temps, ks=ks, ps=ps, seeds=seeds, steps=steps)
-        out_tok = torch.zeros(B, dtype=torch.int32, device=dev)
-        inp = StepInput(ids, pos, slots, meta, None)
+        out_tok = self._tok_out[:B]
+        inp = StepInput(ids, pos, slots, meta, None, carry=carry, carry_src=self._tok_out)
 
         def run():
             logits = m.forward(inp)
@@ -616,6 +622,10 @@ class LLMEngine:
         entry = dict(packed=packed, samp=samp, out=out_tok, run=run, graph=None, meta=meta, inp=inp)
         if self.use_graphs:
             kvl.fill_(1)  # scratch-only rows while capturing
+            carry.fill_(-1)
+            # the eager warm-up runs below sample into the shared _tok_out, which may hold the in-flight
+            # step's tokens that the next step carries (a graph captured lazily mid-pipeline): restore it
+            saved = self._tok_out.clone()
             s = torch.cuda.Stream(device=dev)
             s.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(s):
@@ -625,6 +635,7 @@ class LLMEngine:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 run()
+            self._tok_out.copy_(saved)
             entry["graph"] = g
         self.graphs[B] = entry
         return entry
@@ -674,18 +685,12 @@ class LLMEngine:
         samp = self._sampling_host(seqs, pad_to=B)
         steps = samp[5 * B:5 * B + n]
         steps += np.asarray(carried, dtype=np.int32)  # sampling step index of the token being produced
-        host = np.concatenate([self._decode_inputs_async(seqs, B, carried), samp])
+        # carried rows read their id from the previous step's sampled tokens (the shared device buffer
+        # _tok_out, row = that step's row) inside the graph's embedding kernel: no extra copy / gather
+        carry = np.full(B, -1, dtype=np.int32)
+        carry[:n] = [prev_row[id(s)] if c else -1 for s, c in zip(seqs, carried)]
+        host = np.concatenate([self._decode_inputs_async(seqs, B, carried), samp, carry])
         e["packed"].copy_(self._h2d_i32(host), non_blocking=True)
-        if any(carried):
-            ids = e["packed"][:B]
-            src = [prev_row[id(s)] for s, c in zip(seqs, carried) if c]
-            if all(carried) and src == list(range(n)):
-                ids[:n].copy_(prev["out"][:n])
-            else:
-                dst = [i for i, c in enumerate(carried) if c]
-                idx = self._h2d_i32(np.asarray(src + dst, dtype=np.int32)).long()
-                k = len(src)
-                ids.index_copy_(0, idx[k:], prev["out"].index_select(0, idx[:k]))
         if self._timing is not None:
             ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ea.record()
@@ -750,7 +755,8 @@ class LLMEngine:
         if self.is_cuda:
             B = self._bucket(n)
             e = self._decode_graph(B)
-            host = np.concatenate([self._decode_inputs_host(seqs, B), self._sampling_host(seqs, pad_to=B)])
+            host = np.concatenate([self._decode_inputs_host(seqs, B), self._sampling_host(seqs, pad_to=B),
+                                   np.full(B, -1, dtype=np.int32)])
             e["packed"].copy_(self._h2d_i32(host), non_blocking=True)
             if full_vocab:  # eager forward, exact sampler over the whole vocabulary
                 tok = self._sample_full_vocab(self.model.forward(e["inp"])[:n], seqs)

@@ -232,6 +232,10 @@ class StepInput:
     slots: torch.Tensor  # int32 [T]
     meta: AttnMeta
     logits_idx: Optional[torch.Tensor] = None  # int32 [n] rows that need logits (None = all)
+    # asynchronous decode: carry[i] >= 0 -> ids[i] = carry_src[carry[i]] (previous step's sampled token,
+    # resolved on the device by the embedding kernel)
+    carry: Optional[torch.Tensor] = None
+    carry_src: Optional[torch.Tensor] = None
 
 
 class LlamaModel:
@@ -362,7 +366,7 @@ class LlamaModel:
     def hidden_states(self, inp: StepInput):
         """Run the decoder stack; returns the final-norm'ed rows selected by logits_idx."""
         be, w = self.be, self.w
-        h = be.embed(inp.ids, w.embed)
+        h = be.embed(inp.ids, w.embed, carry=inp.carry, prev=inp.carry_src)
         if self._decode_part_ok(inp, h):
             return self.hidden_states_decode_part(inp, h)
         attn = torch.empty((h.shape[0], self.Hq * self.D), dtype=h.dtype, device=h.device)

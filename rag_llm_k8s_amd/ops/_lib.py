@@ -46,6 +46,7 @@ _SIGS = {
     "ragk_rmsnorm": [P, I, P, I, P, P, I, I, I, F, S],
     "ragk_layernorm": [P, I, P, I, P, P, P, I, I, I, F, S],
     "ragk_embed": [P, P, P, I, I, I, S],
+    "ragk_embed_carry": [P, P, P, P, P, I, I, I, S],
     "ragk_embed_ln": [P, P, P, P, P, P, P, P, I, I, F, I, S],
     "ragk_rope_kv": [P, I, P, P, P, P, P, P, I, I, I, I, I, I, S],
     "ragk_pool_l2norm": [P, I, P, P, I, I, I, I, S],

@@ -70,7 +70,10 @@ class TorchBackend:
             return out
         return y
 
-    def embed(self, ids, table, out=None):
+    def embed(self, ids, table, out=None, carry=None, prev=None):
+        if carry is not None:
+            c = carry[:ids.numel()].long()
+            ids.copy_(torch.where(c >= 0, prev.long()[c.clamp(min=0)], ids.long()).to(ids.dtype))
         y = table[ids.long()]
         if out is not None:
             out.copy_(y)
@@ -208,8 +211,8 @@ class NativeBackend(TorchBackend):
     def layernorm(self, x, g, b, eps, out=None, resid=None):
         return self.n.layernorm(x, g, b, eps, out=out, resid=resid)
 
-    def embed(self, ids, table, out=None):
-        return self.n.embed(ids, table, out=out)
+    def embed(self, ids, table, out=None, carry=None, prev=None):
+        return self.n.embed(ids, table, out=out, carry=carry, prev=prev)
 
     def embed_ln(self, ids, pos_ids, word, pos, type_row, g, b, eps, do_ln=True):
         return self.n.embed_ln(ids, pos_ids, word, pos, type_row, g, b, eps, do_ln=do_ln)

@@ -383,12 +383,19 @@ def layernorm(x, g, b, eps, out=None, resid=None):
     return out
 
 
-def embed(ids, table, out=None):
+def embed(ids, table, out=None, carry=None, prev=None):
+    """Embedding gather. carry/prev (asynchronous decode): rows with carry[t] >= 0 take their token id
+    from prev[carry[t]] (the previous step's sampled tokens on the device) and store it into ids[t]."""
     _req(ids.dtype == torch.int32 and ids.is_cuda and ids.is_contiguous(), "ids int32")
     V, H = table.shape
     out = torch.empty((ids.numel(), H), dtype=table.dtype, device=table.device) if out is None else out
-    check(_lib.lib().ragk_embed(ids.data_ptr(), table.data_ptr(), out.data_ptr(), ids.numel(), H, V, stream_ptr()),
-          "ragk_embed")
+    if carry is None:
+        check(_lib.lib().ragk_embed(ids.data_ptr(), table.data_ptr(), out.data_ptr(), ids.numel(), H, V,
+                                    stream_ptr()), "ragk_embed")
+        return out
+    _req(carry.dtype == torch.int32 and prev.dtype == torch.int32 and carry.numel() >= ids.numel(), "carry int32")
+    check(_lib.lib().ragk_embed_carry(ids.data_ptr(), carry.data_ptr(), prev.data_ptr(), table.data_ptr(),
+                                      out.data_ptr(), ids.numel(), H, V, stream_ptr()), "ragk_embed_carry")
     return out
 
 

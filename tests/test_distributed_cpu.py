@@ -121,9 +121,10 @@ def test_tp2_sequence_parallel_matches_allreduce_path(n):
         for sp in (False, True):
             rel = ((out[r][sp] - ref).norm() / ref.norm()).item()
             assert rel < 2e-2, (sp, rel)
-        # bf16 activations, different reduction order (reduce-scatter + all-gather vs all-reduce)
+        # bf16 activations, different reduction order (reduce-scatter + all-gather vs all-reduce).
+        # Measured with these seeded ids: 7.9e-3 (n=40) and 9.1e-3 (n=41); bound ~1.5x that.
         rel = ((out[r][True] - out[r][False]).norm() / out[r][False].norm()).item()
-        assert rel < 2e-2, rel
+        assert rel < 1.4e-2, rel
     assert torch.equal(out[0][True], out[1][True])
 
 

@@ -55,6 +55,10 @@ def main():
         n = eng.stats["decode_steps"] - n0
         print("B=%d ctx=%d: %d decode steps, %.3f ms/step (engine decode_s %.3f ms/step), %.0f tok/s" % (
             B, plen, n, dt / n * 1e3, (eng.stats["decode_s"] - d0) / n * 1e3, B * n / dt), flush=True)
+        if eng._timing:  # RAGK_DECODE_TIMING=1: GPU time of each captured step, in situ
+            ts = sorted(a.elapsed_time(b) for a, b in eng._timing[-n:])
+            print("B=%d in-situ graph time: median %.3f ms, min %.3f, max %.3f" % (
+                B, ts[len(ts) // 2], ts[0], ts[-1]), flush=True)
         # pure GPU time of the captured decode step: back-to-back replays of the B-bucket graph
         # (stale inputs are fine: same shapes and context lengths), no host work in between
         e = eng.graphs.get(B)

@@ -9,7 +9,7 @@ import sys
 
 
 def short(name):
-    for key in ("gemm_w4_kernel", "gemm_pp_kernel", "gemm_pp4_kernel", "attn_prefill_kernel", "attn_decode_kernel",
+    for key in ("gemm_w4c_kernel", "gemm_w4_kernel", "gemm_pp_kernel", "gemm_pp4_kernel", "attn_prefill_kernel", "attn_decode_kernel",
                 "Cijk"):
         if key in name:
             i = name.find("<")
