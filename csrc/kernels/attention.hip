@@ -423,6 +423,13 @@ struct DecodeArgs {
   float scale_log2;
   int* counters;                           // [B][Hkv] zeroed tickets: fused split-K merge (null: separate
                                            // attn_decode_reduce_kernel launch)
+  // Fused RoPE + KV append (null qkv_p: q is read from `q` and the cache already holds the new token).
+  // The qkv projection arrives as fp32 split-K partial slabs P[S][B][ldp] (gemm_part.hip); every
+  // block sums + rotates its G query heads itself, and the block owning the last KV tile also sums,
+  // rotates and appends the new token's k / v before reading that tile.
+  const float* qkv_p; long long p_slab; int ldp, S;
+  const int* positions; const int* slots;
+  const float* cos_t; const float* sin_t;
 };
 
 // Tiles per partition of one sequence: its KV tiles spread evenly over all max_parts partitions
@@ -458,7 +465,52 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
   const int* bt = a.block_tables + (size_t)b * a.bt_stride;
 
   bf16x8 qf[C::KS];
-  {
+  if (a.qkv_p != nullptr) {
+    // q = RoPE(bf16(sum_s P[s][b])) for this KV head's G query heads, one (d, d + D/2) rotate_half
+    // pair of 8-vectors per thread (G * D/16 threads, all slab loads of a thread in flight together),
+    // staged through LDS; in the block owning the last KV tile, other threads append the new
+    // token's k (rotated) and v meanwhile. One barrier covers both.
+    __shared__ __attribute__((aligned(16))) bf16_t s_q[G * D];
+    constexpr int NV = D / 16;  // pairs per head
+    const int pos = a.positions[b];
+    const float* prow = a.qkv_p + (size_t)b * a.ldp;
+    const float* ct = a.cos_t + (size_t)pos * (D / 2);
+    const float* st = a.sin_t + (size_t)pos * (D / 2);
+    const int tid = threadIdx.x;
+    const bool append = kt1 == n_kt;  // block-uniform
+    constexpr int KV0 = (G * NV + 63) / 64 * 64;  // append threads start on a fresh wave
+    if (tid < G * NV) {
+      const int g = tid / NV, v = tid % NV;
+      const float* ph = prow + (size_t)(kvh * G + g) * D + 8 * v;
+      float x1[8], x2[8], o1[8], o2[8];
+      sum_partials8x2(ph, ph + D / 2, a.S, (size_t)a.p_slab, x1, x2);
+      rope8(x1, x2, ct + 8 * v, st + 8 * v, o1, o2);
+      *reinterpret_cast<u32x4*>(s_q + g * D + 8 * v) = pack8(o1);
+      *reinterpret_cast<u32x4*>(s_q + g * D + D / 2 + 8 * v) = pack8(o2);
+    } else if (append && tid >= KV0 && tid < KV0 + 2 * NV) {  // [KV0, KV0+NV): k, [KV0+NV, KV0+2NV): v
+      const int isv = tid - KV0 >= NV, v = (tid - KV0) % NV;
+      const int slot = a.slots[b];
+      const size_t kvo = (((size_t)(slot / KT) * a.Hkv + kvh) * KT + (slot % KT)) * D;
+      const float* ph = prow + (size_t)(a.Hq + (isv ? a.Hkv : 0) + kvh) * D + 8 * v;
+      float x1[8], x2[8];
+      sum_partials8x2(ph, ph + D / 2, a.S, (size_t)a.p_slab, x1, x2);
+      bf16_t* dst = (isv ? const_cast<bf16_t*>(a.vc) : const_cast<bf16_t*>(a.kc)) + kvo;
+      if (isv) {
+        *reinterpret_cast<u32x4*>(dst + 8 * v) = pack8(x1);
+        *reinterpret_cast<u32x4*>(dst + D / 2 + 8 * v) = pack8(x2);
+      } else {
+        float o1[8], o2[8];
+        rope8(x1, x2, ct + 8 * v, st + 8 * v, o1, o2);
+        *reinterpret_cast<u32x4*>(dst + 8 * v) = pack8(o1);
+        *reinterpret_cast<u32x4*>(dst + D / 2 + 8 * v) = pack8(o2);
+      }
+    }
+    __syncthreads();  // q in LDS; the appended row visible to every wave of this block (same CU)
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s)
+      qf[s] = fr < G ? *reinterpret_cast<const bf16x8*>(s_q + fr * D + 32 * s + 8 * fh)
+                     : (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
+  } else {
     const int g = fr < G ? fr : 0;
     const bf16_t* qp = a.q + (size_t)b * a.q_stride + (kvh * G + g) * D + 8 * fh;
 #pragma unroll
@@ -822,6 +874,8 @@ RAGK_API int ragk_attn_decode_set_nt(int nt) {
   return 0;
 }
 
+static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* counters, hipStream_t st);
+
 RAGK_API int ragk_attn_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                               int bt_stride, const int* kv_lens, float* part_o, float* part_ml, void* out,
                               int out_stride, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
@@ -833,6 +887,30 @@ RAGK_API int ragk_attn_decode(const void* q, int q_stride, const void* kc, const
   DecodeArgs a{(const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, bt_stride, kv_lens,
                part_o, part_ml, (bf16_t*)out, out_stride, Hq, Hkv, part_tiles, max_parts,
                scale * 1.4426950408889634f, counters};
+  return launch_attn_decode(a, B, D, max_parts, counters, st);
+}
+
+// Decode attention fed by the qkv projection's split-K partial slabs P[S][B][ldp] (gemm_part.hip):
+// RoPE of q and k, the KV append at slots[b] and the attention in one launch (replaces
+// rope_kv_partials + attn_decode). Cache blocks hold KT tokens.
+RAGK_API int ragk_attn_decode_rope(const float* P, int S, int ldp, const int* positions, const int* slots,
+                                   const float* cos_t, const float* sin_t, void* kc, void* vc,
+                                   const int* block_tables, int bt_stride, const int* kv_lens, float* part_o,
+                                   float* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D,
+                                   int part_tiles, int max_parts, float scale, int* counters, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (Hq % Hkv || part_tiles < 1 || max_parts < 1 || max_parts > RED_MAXP || S < 1 || D % 64 ||
+      ldp < (Hq + 2 * Hkv) * D || !P || !positions || !slots || !cos_t || !sin_t)
+    return (int)hipErrorInvalidValue;
+  if (counters && 2 * (Hq / Hkv) * max_parts + 16 > 4 * KT * D * 2 / 4) return (int)hipErrorInvalidValue;
+  DecodeArgs a{nullptr, 0, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, bt_stride, kv_lens,
+               part_o, part_ml, (bf16_t*)out, out_stride, Hq, Hkv, part_tiles, max_parts,
+               scale * 1.4426950408889634f, counters, P, (long long)B * ldp, ldp, S, positions, slots, cos_t, sin_t};
+  return launch_attn_decode(a, B, D, max_parts, counters, st);
+}
+
+static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* counters, hipStream_t st) {
+  const int Hq = a.Hq, Hkv = a.Hkv;
   const int G = Hq / Hkv;
   const PfArgs pf = pf_take();
   const int ex = (pf.blocks + Hkv * B - 1) / (Hkv * B);  // rider columns (x beyond max_parts)

@@ -56,6 +56,89 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return v;
 }
 
+// Sum of S fp32 slabs of 8 consecutive floats (slab stride in floats), added in slab order 0..S-1.
+// Loads go out in unrolled groups of PSU slabs (index clamped, the excess not added), so a thread
+// has 2 x PSU loads in flight instead of one slab's pair per memory latency (a runtime-S loop made
+// hipcc wait on every slab: 7.7 us for the qkv slabs at S = 8).
+constexpr int PSU = 8;
+__device__ __forceinline__ void sum_slabs8(const float* P, int S, size_t slab, float* a) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = 0.f;
+  for (int s0 = 0; s0 < S; s0 += PSU) {
+    f32x4 p[PSU][2];
+#pragma unroll
+    for (int u = 0; u < PSU; ++u) {
+      const f32x4* ps = reinterpret_cast<const f32x4*>(P + (size_t)min(s0 + u, S - 1) * slab);
+      p[u][0] = ps[0];
+      p[u][1] = ps[1];
+    }
+#pragma unroll
+    for (int u = 0; u < PSU; ++u) {
+      if (s0 + u < S) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] += p[u][0][e];
+          a[4 + e] += p[u][1][e];
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void sum_partials8(const float* P, int S, size_t slab, float* a) {
+  sum_slabs8(P, S, slab, a);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = bf2f(f2bf(a[e]));
+}
+
+// sum_partials8 of two 8-float vectors at once (their 4 x PSU slab loads in flight together; each
+// element summed in slab order 0..S-1, so the results equal two sum_partials8 calls)
+__device__ __forceinline__ void sum_partials8x2(const float* P1, const float* P2, int S, size_t slab, float* a,
+                                                float* b) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = b[e] = 0.f;
+  for (int s0 = 0; s0 < S; s0 += PSU) {
+    f32x4 p[PSU][4];
+#pragma unroll
+    for (int u = 0; u < PSU; ++u) {
+      const size_t o = (size_t)min(s0 + u, S - 1) * slab;
+      p[u][0] = reinterpret_cast<const f32x4*>(P1 + o)[0];
+      p[u][1] = reinterpret_cast<const f32x4*>(P1 + o)[1];
+      p[u][2] = reinterpret_cast<const f32x4*>(P2 + o)[0];
+      p[u][3] = reinterpret_cast<const f32x4*>(P2 + o)[1];
+    }
+#pragma unroll
+    for (int u = 0; u < PSU; ++u) {
+      if (s0 + u < S) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] += p[u][0][e];
+          a[4 + e] += p[u][1][e];
+          b[e] += p[u][2][e];
+          b[4 + e] += p[u][3][e];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    a[e] = bf2f(f2bf(a[e]));
+    b[e] = bf2f(f2bf(b[e]));
+  }
+}
+
+// HF rotate_half RoPE on one pair of 8-element half-vectors (x1 = d in [0, D/2), x2 = d + D/2) with
+// the bf16 rounding of every torch op (q*cos, rotate_half(q)*sin, their sum).
+__device__ __forceinline__ void rope8(const float* x1, const float* x2, const float* ct, const float* st, float* o1,
+                                      float* o2) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float c = ct[e], sn = st[e];
+    o1[e] = bf2f(f2bf(bf2f(f2bf(x1[e] * c)) + bf2f(f2bf(-x2[e] * sn))));
+    o2[e] = bf2f(f2bf(bf2f(f2bf(x2[e] * c)) + bf2f(f2bf(x1[e] * sn))));
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

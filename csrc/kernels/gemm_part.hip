@@ -46,16 +46,29 @@ __device__ __forceinline__ bf16x8 p_fp8x8_bf16(unsigned lo, unsigned hi) {
 // fragments are read from LDS at the same k (chunks 8j + 2fh and 8j + 2fh + 1), so both operands
 // see the same permutation of K and the dot product is unchanged. Half the weight bytes of bf16 per
 // K-slice; the row scale is applied to the partial before it is written.
-template <int MT, int NKS, bool FP8 = false>
+// NORM (decode batch <= 4): X is the un-normalised residual stream h and the block applies the
+// following RMSNorm itself -- out = bf16(gamma * bf16(h * rsqrt(mean(h^2) + eps))), exactly
+// rmsnorm_kernel's math and reduction order (threads 0..255 sum their row vectors in the same order,
+// the wave partials are added in the same order; waves 4..7 add zeros) -- so the separate norm
+// launch before the qkv projection disappears. Every block reads the full rows (8 KiB each at
+// K = 4096, L2-resident) for the sum of squares; its weight stream is already in flight.
+// NR = rows (M), NV = 16-B row vectors per thread (threads 0..255: K = 2048 NV); NR = 0: no norm.
+constexpr int NORM_MAXR = 4;
+
+template <int MT, int NKS, bool FP8 = false, int NR = 0, int NV = 1>
 __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* __restrict__ X, int ldx,
                                                                   const bf16_t* __restrict__ W, int ldw,
                                                                   float* __restrict__ P, int M, int N, int K,
-                                                                  const float* __restrict__ wscale = nullptr) {
+                                                                  const float* __restrict__ wscale = nullptr,
+                                                                  const bf16_t* __restrict__ gamma = nullptr,
+                                                                  float eps = 0.f) {
   constexpr int KS = NKS * 64;          // K-slice of the block (two halves of NKS k-steps of 32)
   constexpr int XROWS = 16 * MT;
   constexpr int ROWB = KS * 2;          // bytes per LDS row
   constexpr int XBYTES = XROWS * ROWB;
   __shared__ __attribute__((aligned(16))) char smem[XBYTES > 16384 ? XBYTES : 16384];
+  constexpr bool NORM = NR > 0;
+  __shared__ float s_red[NORM ? NR * (PT_THREADS / 64) : 1];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -71,14 +84,33 @@ __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* 
   constexpr int PIECES = XBYTES / 1024;          // 1-KiB pieces (64 lanes x 16 B)
   constexpr int PPW = PIECES / (PT_THREADS / 64);
   static_assert(PIECES % (PT_THREADS / 64) == 0 && CPR >= 64, "activation slice shape");
+  u32x4 hv[NORM ? NR : 1][NV];  // NORM: raw row vectors (tid & 255) + 256 i
+  u32x4 gv[NV];
+  if constexpr (NORM) {
+    // full rows (vectors tid + 256 i, threads < 256) and gamma for the slice's vectors, issued before
+    // the weight stream so the counted wait below retires them first
+    // branch-free: every load is issued (addresses clamped into range) and masked afterwards, so the
+    // compiler keeps them all in flight (predicated loads behind branches got a vmcnt(0) each)
+    // (waves 4..7 repeat waves 0..3's addresses -- L1 hits -- and are masked at use, after the weight
+    // loads are issued)
 #pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int p = wid * PPW + i;
-    const int e = p * 64 + lane;                 // destination chunk index (lane-linear)
-    const int r = e / CPR, slot = e % CPR;
-    const int c = (slot & ~15) | ((slot & 15) ^ (r & 15));
-    const int gr = min(r, M - 1);
-    glds16(X + (size_t)gr * ldx + kbase + c * 8, smem + p * 1024);
+    for (int i = 0; i < NV; ++i) {
+      const int vi = (tid & 255) + 256 * i;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) hv[r][i] = *reinterpret_cast<const u32x4*>(X + (size_t)r * ldx + vi * 8);
+      const int gi = min(max(vi * 8, kbase), kbase + KS - 8);
+      gv[i] = *reinterpret_cast<const u32x4*>(gamma + gi);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int p = wid * PPW + i;
+      const int e = p * 64 + lane;                 // destination chunk index (lane-linear)
+      const int r = e / CPR, slot = e % CPR;
+      const int c = (slot & ~15) | ((slot & 15) ^ (r & 15));
+      const int gr = min(r, M - 1);
+      glds16(X + (size_t)gr * ldx + kbase + c * 8, smem + p * 1024);
+    }
   }
 
   __builtin_amdgcn_sched_barrier(0);
@@ -98,9 +130,53 @@ __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* 
 #pragma unroll
     for (int ks = 0; ks < NLD; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
   }
-  // vmcnt(NLD): the DMA (older than the NLD weight loads) has landed
+  // vmcnt(NLD): the DMA / row loads (older than the NLD weight loads) have landed
   __builtin_amdgcn_s_waitcnt((NLD & 15) | (((NLD >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (NORM) {
+    // RMSNorm statistics (rmsnorm_kernel order), then the normalised slice -> LDS (rows >= M are
+    // left as they are: their accumulator rows are never stored)
+    float ss[NR];
+    const u32x4 z = {0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      ss[r] = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        hv[r][i] = tid < 256 ? hv[r][i] : z;
+        float f[8];
+        unpack8(hv[r][i], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ss[r] += f[e] * f[e];
+      }
+      ss[r] = wave_sum(ss[r]);
+      if (lane == 0) s_red[r * (PT_THREADS / 64) + wid] = ss[r];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < PT_THREADS / 64; ++w) t += s_red[r * (PT_THREADS / 64) + w];
+      const float inv = rsqrtf(t / (float)K + eps);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int vi = tid + 256 * i;
+        if (tid < 256 && vi * 8 >= kbase && vi * 8 < kbase + KS) {
+          float f[8], g[8], o[8];
+          unpack8(hv[r][i], f);
+          unpack8(gv[i], g);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = g[e] * bf2f(f2bf(f[e] * inv));
+          const int c = vi - kbase / 8;
+          *reinterpret_cast<u32x4*>(smem + r * ROWB + 16 * ((c & ~15) | ((c & 15) ^ (r & 15)))) = pack8(o);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();  // raw: __syncthreads() would drain the weight loads too (vmcnt(0))
   __builtin_amdgcn_sched_barrier(0);
 
@@ -157,16 +233,17 @@ __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* 
   }
 }
 
-template <int MT, bool FP8 = false>
+template <int MT, bool FP8 = false, int NR = 0, int NV = 1>
 int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K, int ks_steps,
-                   hipStream_t st, const float* wscale = nullptr) {
+                   hipStream_t st, const float* wscale = nullptr, const void* gamma = nullptr, float eps = 0.f) {
   const int KS = ks_steps * 64;
   const dim3 grid((N + PT_NB - 1) / PT_NB, K / KS);
 #define RAGK_PART(NK)                                                                                       \
   case NK:                                                                                                  \
-    if constexpr (16 * MT * NK * 64 * 2 <= 128 * 1024 && (16 * MT * NK * 64 * 2) % 8192 == 0) {           \
-      hipLaunchKernelGGL((gemm_part_kernel<MT, NK, FP8>), grid, dim3(PT_THREADS), 0, st, (const bf16_t*)X, ldx, \
-                         (const bf16_t*)W, ldw, P, M, N, K, wscale);                                        \
+    if constexpr (16 * MT * NK * 64 * 2 <= 128 * 1024 && (16 * MT * NK * 64 * 2) % 8192 == 0 &&           \
+                  (NR == 0 || NK == 8 || NK == 16)) {                                                       \
+      hipLaunchKernelGGL((gemm_part_kernel<MT, NK, FP8, NR, NV>), grid, dim3(PT_THREADS), 0, st, (const bf16_t*)X, \
+                         ldx, (const bf16_t*)W, ldw, P, M, N, K, wscale, (const bf16_t*)gamma, eps);         \
       break;                                                                                                \
     } else {                                                                                                \
       return (int)hipErrorInvalidValue;                                                                     \
@@ -224,6 +301,22 @@ RAGK_API int ragk_gemm_part(const void* X, int ldx, const void* W, int ldw, floa
     case 4: return launch_part_mt<4>(X, ldx, W, ldw, P, M, N, K, ks_steps, st);
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+// X = un-normalised rows h (M <= 4, K <= 8192); the block applies RMSNorm(h) * gamma (rmsnorm_kernel's
+// exact math) before the product: P = partials of rmsnorm(h) . W^T. bf16 weights.
+RAGK_API int ragk_gemm_part_norm(const void* X, int ldx, const void* gamma, float eps, const void* W, int ldw,
+                                 float* P, int M, int N, int K, int ks_steps, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (M > NORM_MAXR || (K != 4096 && K != 8192) || !gamma || (ks_steps != 8 && ks_steps != 16) ||
+      K % (64 * ks_steps) != 0)
+    return (int)hipErrorInvalidValue;
+#define RAGK_PN(R, V) return launch_part_mt<1, false, R, V>(X, ldx, W, ldw, P, M, N, K, ks_steps, st, nullptr, gamma, eps)
+  if (K == 4096) {
+    switch (M) { case 1: RAGK_PN(1, 2); case 2: RAGK_PN(2, 2); case 3: RAGK_PN(3, 2); default: RAGK_PN(4, 2); }
+  }
+  switch (M) { case 1: RAGK_PN(1, 4); case 2: RAGK_PN(2, 4); case 3: RAGK_PN(3, 4); default: RAGK_PN(4, 4); }
+#undef RAGK_PN
 }
 
 // W8A16 variant: W = e4m3fn [N][K] bytes (ldw in bytes), wscale = fp32 [N]; same slabs / slices.

@@ -348,35 +348,6 @@ __global__ __launch_bounds__(NT) void gather_rows_kernel(const bf16_t* x, int ld
 // ---- consumers of the split-K decode GEMM (gemm_part.hip): they sum the S fp32 partial slabs
 // P[S][M][ldp] while doing their own row work, so the reduction needs no extra launch.
 
-// Sum of S fp32 slabs of 8 consecutive floats (slab stride in floats), added in slab order 0..S-1.
-// Loads go out in unrolled groups of PSU slabs (index clamped, the excess not added), so a thread
-// has 2 x PSU loads in flight instead of one slab's pair per memory latency (a runtime-S loop made
-// hipcc wait on every slab: 7.7 us for the qkv slabs at S = 8).
-constexpr int PSU = 8;
-__device__ __forceinline__ void sum_slabs8(const float* P, int S, size_t slab, float* a) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) a[e] = 0.f;
-  for (int s0 = 0; s0 < S; s0 += PSU) {
-    f32x4 p[PSU][2];
-#pragma unroll
-    for (int u = 0; u < PSU; ++u) {
-      const f32x4* ps = reinterpret_cast<const f32x4*>(P + (size_t)min(s0 + u, S - 1) * slab);
-      p[u][0] = ps[0];
-      p[u][1] = ps[1];
-    }
-#pragma unroll
-    for (int u = 0; u < PSU; ++u) {
-      if (s0 + u < S) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          a[e] += p[u][0][e];
-          a[4 + e] += p[u][1][e];
-        }
-      }
-    }
-  }
-}
-
 // h = bf16(h + bf16(sum_s P[s][row]))  (HF: bf16 linear output, then the bf16 residual add), written
 // back to h; out = rmsnorm(h) * w exactly as rmsnorm_kernel. One block of 512 threads per row.
 constexpr int PNT = 512;
@@ -427,11 +398,6 @@ __global__ __launch_bounds__(PNT) void add_partials_rmsnorm_kernel(const float* 
 // rope_kv_kernel fed by qkv partial slabs: qkv = bf16(sum_s P[s][t]) (the bf16 linear output), then
 // the same rotate_half RoPE (HF bf16 op rounding) and paged-KV write. Rotated q goes to q_out
 // (row stride ldq); k / v go to the cache only. grid = (T, HG): head groups split over blocks.
-__device__ __forceinline__ void sum_partials8(const float* P, int S, size_t slab, float* a) {
-  sum_slabs8(P, S, slab, a);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) a[e] = bf2f(f2bf(a[e]));
-}
 
 __global__ __launch_bounds__(NT) void rope_kv_partials_kernel(const float* __restrict__ P, int S, int T, int ldp,
                                                               bf16_t* q_out, int ldq,
@@ -469,12 +435,7 @@ __global__ __launch_bounds__(NT) void rope_kv_partials_kernel(const float* __res
       continue;
     }
     float o1[8], o2[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float c = ct[v * 8 + e], sn = st[v * 8 + e];
-      o1[e] = bf2f(f2bf(bf2f(f2bf(x1[e] * c)) + bf2f(f2bf(-x2[e] * sn))));
-      o2[e] = bf2f(f2bf(bf2f(f2bf(x2[e] * c)) + bf2f(f2bf(x1[e] * sn))));
-    }
+    rope8(x1, x2, ct + v * 8, st + v * 8, o1, o2);
     if (hd < Hq) {
       bf16_t* qp = q_out + (size_t)t * ldq + hd * D;
       *reinterpret_cast<u32x4*>(qp + v * 8) = pack8(o1);

@@ -33,6 +33,10 @@ DECODE_PF_BLOCKS = int(os.environ.get("RAGK_DECODE_PF_BLOCKS", "128"))
 DECODE_PF_SMALL_BATCH = int(os.environ.get("RAGK_DECODE_PF_SMALL", "8"))
 # decode batches up to this size run the down projection on the register-streaming GEMM (fused residual)
 DECODE_DOWN_SKINNY_MAX_M = int(os.environ.get("RAGK_DECODE_DOWN_SKINNY_MAX_M", "4"))
+# decode: RoPE + KV append done by the attention kernel from the qkv partial slabs (attn_decode_rope)
+DECODE_ROPE_FUSED = os.environ.get("RAGK_DECODE_ROPE_FUSED", "1") == "1"
+# decode batch <= DECODE_DOWN_SKINNY_MAX_M: input RMSNorm inside the qkv split-K GEMM (gemm_part_norm)
+DECODE_NORM_FUSED = os.environ.get("RAGK_DECODE_NORM_FUSED", "1") == "1"
 
 
 @dataclass
@@ -332,16 +336,28 @@ class LlamaModel:
         q = torch.empty((M, Hq * D), dtype=h.dtype, device=h.device)
         layers = w.layers
         pf = self._pf_plan(M)
-        xn = be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
+        # batch <= 4: the input norm runs inside the qkv GEMM (gemm_part_norm) -- one launch fewer per layer
+        fuse_norm = (DECODE_NORM_FUSED and M <= DECODE_DOWN_SKINNY_MAX_M and not pf
+                     and be.part_norm_ok(M, layers[0]["wqkv"]))
+        xn = None if fuse_norm else be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
-            P = be.gemm_part(xn, L["wqkv"])
-            if pf and pf["rope"]:
-                be.pf_arm([(L["wo"], 0, pf["rope"])], pf["blocks"])
-            be.rope_kv_partials(P, q, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
-            if pf and pf["attn"]:
-                be.pf_arm([(L["wo"], pf["rope"], pf["attn"] // 2), (L["wgu"], 0, pf["attn"] // 2)], pf["blocks"])
-            be.attn_decode(q, kc, vc, inp.meta, attn, Hq, Hkv, D)
+            if fuse_norm:
+                P = be.gemm_part_norm(h, L["ln_in"], c.rms_norm_eps, L["wqkv"])
+            else:
+                P = be.gemm_part(xn, L["wqkv"])
+            if DECODE_ROPE_FUSED and not pf:
+                # RoPE + KV append inside the attention kernel (one launch fewer per layer)
+                be.attn_decode_rope(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, attn,
+                                    Hq, Hkv, D)
+            else:
+                if pf and pf["rope"]:
+                    be.pf_arm([(L["wo"], 0, pf["rope"])], pf["blocks"])
+                be.rope_kv_partials(P, q, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
+                if pf and pf["attn"]:
+                    be.pf_arm([(L["wo"], pf["rope"], pf["attn"] // 2), (L["wgu"], 0, pf["attn"] // 2)],
+                              pf["blocks"])
+                be.attn_decode(q, kc, vc, inp.meta, attn, Hq, Hkv, D)
             P = be.gemm_part(attn, L["wo"])
             if pf:
                 be.pf_arm([(L["wgu"], pf["attn"] // 2, pf["post"])], pf["blocks"])
@@ -352,7 +368,8 @@ class LlamaModel:
                 # tiny batch: the register-streaming GEMM with the fused residual + a plain norm beats
                 # the split-K partials + consumer by ~2 us (profiles/decode_gemm_graph_ab_M_r2.log)
                 be.gemm(a, L["wdown"], resid=h, epi="resid", out=h)
-                xn = be.rmsnorm(h, nxt, c.rms_norm_eps)
+                if not fuse_norm or li + 1 == len(layers):
+                    xn = be.rmsnorm(h, nxt, c.rms_norm_eps)
                 continue
             P = be.gemm_part(a, L["wdown"])
             if pf:

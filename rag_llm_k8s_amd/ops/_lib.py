@@ -32,6 +32,7 @@ _SIGS = {
     "ragk_gemm_stream_set_pair_rows": [I],
     "ragk_gemm_w4": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_part": [P, I, P, I, P, I, I, I, I, S],
+    "ragk_gemm_part_norm": [P, I, P, F, P, I, P, I, I, I, I, S],
     "ragk_gemm_part_fp8": [P, I, P, I, P, P, I, I, I, I, S],
     "ragk_attn_decode_set_nt": [I],
     "ragk_attn_prefill_set_waves": [I],
@@ -55,6 +56,7 @@ _SIGS = {
     "ragk_attn_prefill_qtile": [I, I],
     "ragk_attn_prefill": [P, I, P, P, I, P, I, P, P, P, P, I, P, I, I, I, I, I, I, F, S],
     "ragk_attn_decode": [P, I, P, P, P, I, P, P, P, P, I, I, I, I, I, I, I, F, P, S],
+    "ragk_attn_decode_rope": [P, I, I, P, P, P, P, P, P, P, I, P, P, P, P, I, I, I, I, I, I, I, F, P, S],
     "ragk_topk_candidates": [P, I, I, I, I, I, I, P, P, S],
     "ragk_sample_candidates": [P, P, I, I, P, P, P, P, P, P, P, S],
     "ragk_l2_partial": [P, I, I, I, I, P, I, I, P, P, P, P, S],

@@ -124,6 +124,12 @@ class TorchBackend:
         wf = w.dequant() if isinstance(w, Fp8Weight) else w.float()
         return (x.float() @ wf.t()).unsqueeze(0)
 
+    def part_norm_ok(self, M, w):
+        return self.enable_part and M <= 4 and not isinstance(w, Fp8Weight) and w.shape[1] <= 8192
+
+    def gemm_part_norm(self, h, gamma, eps, w):
+        return self.gemm_part(R.rmsnorm(h, gamma, eps), w)
+
     def add_partials_rmsnorm(self, P, h, w, eps):
         h.copy_((h.float() + P.sum(0).to(h.dtype).float()).to(h.dtype))
         return R.rmsnorm(h, w, eps)
@@ -143,6 +149,11 @@ class TorchBackend:
                                v_full=lambda s: R.paged_kv_view(vc, bt[s], lens[s], KV_BLOCK))
         out.copy_(o.reshape(T, Hq * D))
         return out
+
+    def attn_decode_rope(self, P, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
+        q = torch.empty((P.shape[1], Hq * D), dtype=out.dtype, device=out.device)
+        self.rope_kv_partials(P, q, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)
+        return self.attn_decode(q, kc, vc, meta, out, Hq, Hkv, D)
 
     def attn_decode(self, q, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
         B = q.shape[0]
@@ -236,6 +247,12 @@ class NativeBackend(TorchBackend):
     def gemm_part(self, x, w):
         return self.n.gemm_part(x, w)
 
+    def part_norm_ok(self, M, w):
+        return self.enable_part and M <= 4 and not isinstance(w, Fp8Weight) and w.shape[1] in (4096, 8192)
+
+    def gemm_part_norm(self, h, gamma, eps, w):
+        return self.n.gemm_part_norm(h, gamma, eps, w)
+
     def pf_arm(self, ranges, blocks):
         self.n.pf_arm(ranges, blocks)
 
@@ -248,6 +265,10 @@ class NativeBackend(TorchBackend):
     def attn_prefill(self, q, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
         return self.n.attn_prefill(q, kc, vc, meta.cu_q, meta.kv_lens, meta.tiles, out, Hq, Hkv, D, causal=True,
                                    paged=True, block_tables=meta.block_tables)
+
+    def attn_decode_rope(self, P, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
+        return self.n.attn_decode_rope(P, positions, cos_t, sin_t, slots, kc, vc, meta.block_tables, meta.kv_lens, out,
+                                       Hq, Hkv, D, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml)
 
     def attn_decode(self, q, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
         return self.n.attn_decode(q, kc, vc, meta.block_tables, meta.kv_lens, out, Hq, Hkv, D, meta.part_tiles,

@@ -246,6 +246,27 @@ def gemm_part_slabs(M, N, K, ks=None):
     return ks, K // (64 * ks)
 
 
+def gemm_part_norm(h, gamma, eps, w, out=None, ks=None):
+    """gemm_part of rmsnorm(h) * gamma (the norm applied inside the GEMM's activation staging, same
+    math as rmsnorm): decode batches <= 4, bf16 weights, K <= 8192."""
+    _bf16_2d(h, "h")
+    _bf16_2d(w, "w")
+    M, K = h.shape
+    N = w.shape[0]
+    _req(w.shape[1] == K and M <= 4 and K <= 8192 and gamma.numel() == K and gamma.dtype == torch.bfloat16
+         and gamma.is_contiguous(), "gemm_part_norm shape")
+    ks, S = gemm_part_slabs(1, N, K, ks)
+    if ks not in (8, 16):  # the norm variant is built for 8- and 16-step K-slices
+        ks, S = gemm_part_slabs(1, N, K, 16)
+    _req(S > 0 and K in (4096, 8192), "gemm_part_norm: unsupported K=%d" % K)
+    if out is None:
+        out = torch.empty((S, M, N), dtype=torch.float32, device=h.device)
+    check(_lib.lib().ragk_gemm_part_norm(h.data_ptr(), h.stride(0), gamma.data_ptr(), float(eps), w.data_ptr(),
+                                         w.stride(0), out.data_ptr(), M, N, K, ks, stream_ptr()),
+          "ragk_gemm_part_norm")
+    return out
+
+
 def gemm_part(x, w, out=None, ks=None):
     """Decode GEMM v5 (csrc/kernels/gemm_part.hip): fp32 split-K partials P[S, M, N] with
     P.sum(0) = x @ w^T. The consumer (add_partials_rmsnorm / rope_kv_partials) does the reduction.
@@ -584,6 +605,40 @@ def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, par
         q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
         block_tables.stride(0), kv_lens.data_ptr(), ptr(ws_o), ptr(ws_ml), out.data_ptr(), out.stride(0), B, Hq, Hkv,
         D, part_tiles, max_parts, float(scale), ptr(cnt), stream_ptr()), "ragk_attn_decode")
+    return out
+
+
+def attn_decode_rope(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D,
+                     part_tiles, max_parts, ws_o=None, ws_ml=None, scale=None):
+    """Decode attention straight from the qkv projection's split-K partial slabs P [S, B, ldp] (fp32):
+    q / k RoPE, the KV append at `slots` and the attention in one launch -- the same result as
+    rope_kv_partials followed by attn_decode (bit-identical), one kernel fewer per layer."""
+    _req(P.dtype == torch.float32 and P.is_contiguous() and P.dim() == 3, "partials")
+    S, B, ldp = P.shape
+    _req(ldp >= (Hq + 2 * Hkv) * D and D % 64 == 0, "qkv width")
+    _req(kv_lens.numel() == B, "one partial row per sequence")
+    _req(positions.dtype == torch.int32 and positions.numel() == B, "positions")
+    _req(slots is not None and slots.dtype == torch.int32 and slots.numel() == B, "slots")
+    _req(k_cache.dim() == 4 and k_cache.shape[1] == Hkv and k_cache.shape[2] == 64 and k_cache.shape[3] == D,
+         "paged cache")
+    _req(block_tables.dtype == torch.int32 and block_tables.shape[0] >= B, "block_tables")
+    _req(kv_lens.dtype == torch.int32, "kv_lens int32")
+    _req(Hq // Hkv <= 16, "G <= 16")
+    if max_parts > 1:
+        if ws_o is None:
+            ws_o = torch.empty((B, Hq, max_parts, D), dtype=torch.float32, device=P.device)
+            ws_ml = torch.empty((B, Hq, max_parts, 2), dtype=torch.float32, device=P.device)
+        _req(ws_o.numel() >= B * Hq * max_parts * D and ws_ml.numel() >= B * Hq * max_parts * 2, "workspace")
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    cnt = None
+    if max_parts > 1 and ATTN_FUSED_MERGE and 2 * (Hq // Hkv) * max_parts + 16 <= 4 * 64 * D * 2 // 4:
+        cnt = _attn_counters(P.device)
+        _req(B * Hkv <= cnt.numel(), "attention ticket buffer too small")
+    check(_lib.lib().ragk_attn_decode_rope(
+        P.data_ptr(), S, ldp, positions.data_ptr(), slots.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(),
+        k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0), kv_lens.data_ptr(),
+        ptr(ws_o), ptr(ws_ml), out.data_ptr(), out.stride(0), B, Hq, Hkv, D, part_tiles, max_parts, float(scale),
+        ptr(cnt), stream_ptr()), "ragk_attn_decode_rope")
     return out
 
 

@@ -396,6 +396,50 @@ def test_attn_decode_fused_merge_matches_separate_and_resets(native):
     assert int(native._attn_counters(DEV)[:B * Hkv].abs().sum()) == 0
 
 
+@pytest.mark.parametrize("kv_lens,target", [([1], 1024), ([5200, 1, 64, 65, 3000, 700], 1024), ([777, 129], 8)])
+def test_attn_decode_rope_matches_unfused(native, kv_lens, target):
+    """attn_decode_rope (q/k RoPE + KV append from the qkv partial slabs inside the attention kernel)
+    == rope_kv_partials + attn_decode: same attention output and same cache contents, bit for bit
+    (new token at the end of a block, at a block start, and as the only token)."""
+    D, Hq, Hkv, S = 128, 32, 8, 8
+    torch.manual_seed(14)
+    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=5)
+    B = len(kv_lens)
+    kc, vc, bt = kc.to(DEV), vc.to(DEV), bt.to(DEV)
+    kvl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    pos = kvl - 1
+    slots = (bt[torch.arange(B, device=DEV), (pos // 64).long()] * 64 + pos % 64).int()
+    P = torch.randn(S, B, (Hq + 2 * Hkv) * D, device=DEV)
+    cos, sin = R.rope_tables(D, 8192, theta=500000.0,
+                             scaling={"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                      "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv, target_blocks=target)
+    kc2, vc2 = kc.clone(), vc.clone()
+    q = torch.empty(B, Hq * D, device=DEV).bfloat16()
+    ref = torch.empty(B, Hq * D, device=DEV).bfloat16()
+    native.rope_kv_partials(P, q, pos, cos, sin, slots, kc2, vc2, Hq, Hkv, D)
+    native.attn_decode(q, kc2, vc2, bt, kvl, ref, Hq, Hkv, D, pt, mp)
+    out = torch.empty(B, Hq * D, device=DEV).bfloat16()
+    native.attn_decode_rope(P, pos, cos, sin, slots, kc, vc, bt, kvl, out, Hq, Hkv, D, pt, mp)
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (3, 6144, 4096), (4, 1280, 8192), (2, 10240, 8192)])
+def test_gemm_part_norm_matches_rmsnorm_then_part(native, M, N, K):
+    """gemm_part_norm (RMSNorm applied while staging the activation slice) == rmsnorm_kernel followed
+    by gemm_part, bit for bit (same reduction order and rounding points)."""
+    torch.manual_seed(15)
+    h = (torch.randn(M, K, device=DEV) * 3).bfloat16()
+    g = (1 + 0.1 * torch.randn(K, device=DEV)).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    out = native.gemm_part_norm(h, g, 1e-5, w)
+    ref = native.gemm_part(native.rmsnorm(h, g, 1e-5), w, ks=K // (64 * out.shape[0]))  # same K-slices
+    assert out.shape == ref.shape
+    assert torch.equal(out, ref)
+
+
 def test_pool_l2norm(native):
     torch.manual_seed(12)
     h = torch.randn(50, 384, device=DEV).bfloat16()
