@@ -252,23 +252,73 @@ constexpr int SC_MAX = 2048;  // R * K candidates
 __global__ __launch_bounds__(SC_THREADS) void sample_candidates_kernel(
     const float* __restrict__ cand_v, const int* __restrict__ cand_i, int n_cand, const float* __restrict__ temps,
     const int* __restrict__ top_ks, const float* __restrict__ top_ps, const unsigned long long* __restrict__ seeds,
-    const int* __restrict__ steps, int* out_tok, float* out_logprob) {
+    const int* __restrict__ steps, int* out_tok, float* out_logprob, int list_len) {
   __shared__ float sv[SC_MAX];
   __shared__ int si[SC_MAX];
+  __shared__ float mv[64];
+  __shared__ int mi[64];
   const int b = blockIdx.x;
-  int n = 1;
-  while (n < n_cand) n <<= 1;
-  for (int i = threadIdx.x; i < n; i += SC_THREADS) {
-    sv[i] = i < n_cand ? cand_v[(size_t)b * n_cand + i] : -INFINITY;
-    si[i] = i < n_cand ? cand_i[(size_t)b * n_cand + i] : 0x7fffffff;
+  int K = top_ks[b];
+  if (K <= 0 || K > n_cand) K = n_cand;
+  if (K <= 64 && list_len > 0) {
+    // The candidate lists (R = n_cand / list_len of them) are each sorted in the total order
+    // (value desc, vocabulary id asc as unsigned, position asc): the global top-64 is found by
+    // ranking every candidate -- its position in its own list plus a binary search per other list --
+    // and scattering the ones ranked < 64 (one barrier instead of a 512-entry bitonic sort's 45).
+    for (int i = threadIdx.x; i < n_cand; i += SC_THREADS) {
+      sv[i] = cand_v[(size_t)b * n_cand + i];
+      si[i] = cand_i[(size_t)b * n_cand + i];
+    }
+    if (threadIdx.x < 64) {
+      mv[threadIdx.x] = -INFINITY;
+      mi[threadIdx.x] = -1;
+    }
+    __syncthreads();
+    const int R = n_cand / list_len;
+    for (int c = threadIdx.x; c < n_cand; c += SC_THREADS) {
+      const float v = sv[c];
+      const unsigned ix = (unsigned)si[c];
+      const int own = c / list_len;
+      int rank = c - own * list_len;
+      for (int j = 0; j < R; ++j) {
+        if (j == own) continue;
+        // count of list j's entries that precede c: (v' > v) or (v' == v and (ix' < ix or (ix' == ix and j < own)))
+        int lo = 0, hi = list_len;
+        const int base = j * list_len;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          const float w = sv[base + mid];
+          const unsigned iw = (unsigned)si[base + mid];
+          const bool before = w > v || (w == v && (iw < ix || (iw == ix && j < own)));
+          if (before) lo = mid + 1; else hi = mid;
+        }
+        rank += lo;
+        if (rank >= 64) break;
+      }
+      if (rank < 64) {
+        mv[rank] = v;
+        mi[rank] = (int)ix;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      sv[threadIdx.x] = mv[threadIdx.x];
+      si[threadIdx.x] = mi[threadIdx.x];
+    }
+    __syncthreads();
+  } else {
+    int n = 1;
+    while (n < n_cand) n <<= 1;
+    for (int i = threadIdx.x; i < n; i += SC_THREADS) {
+      sv[i] = i < n_cand ? cand_v[(size_t)b * n_cand + i] : -INFINITY;
+      si[i] = i < n_cand ? cand_i[(size_t)b * n_cand + i] : 0x7fffffff;
+    }
+    __syncthreads();
+    bitonic_desc(sv, si, n);
   }
-  __syncthreads();
-  bitonic_desc(sv, si, n);
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
   const float T = temps[b];
-  int K = top_ks[b];
-  if (K <= 0 || K > n_cand) K = n_cand;
   const unsigned long long r = splitmix64(seeds[b] ^ splitmix64((unsigned long long)steps[b] + 0x51ED270Bull));
   const float top_p = top_ps[b];
   if (K > 64) {  // wide top-k (or top_k disabled): the serial tail
@@ -380,6 +430,20 @@ RAGK_API int ragk_sample_candidates(const float* cand_v, const int* cand_i, int 
   if (B <= 0) return 0;
   if (n_cand < 1 || n_cand > SC_MAX) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(sample_candidates_kernel, dim3(B), dim3(SC_THREADS), 0, st, cand_v, cand_i, n_cand, temps, top_ks,
-                     top_ps, seeds, steps, out_tok, out_logprob);
+                     top_ps, seeds, steps, out_tok, out_logprob, 0);
+  return (int)hipGetLastError();
+}
+
+// As ragk_sample_candidates for candidates that arrive as n_cand / list_len lists of list_len, each
+// sorted (topk_candidates output, all-gathered per TP rank): rows with top_k <= 64 rank-merge the
+// lists instead of sorting all candidates.
+RAGK_API int ragk_sample_candidates_lists(const float* cand_v, const int* cand_i, int B, int n_cand, int list_len,
+                                          const float* temps, const int* top_ks, const float* top_ps,
+                                          const unsigned long long* seeds, const int* steps, int* out_tok,
+                                          float* out_logprob, hipStream_t st) {
+  if (B <= 0) return 0;
+  if (n_cand < 1 || n_cand > SC_MAX || list_len < 1 || n_cand % list_len) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(sample_candidates_kernel, dim3(B), dim3(SC_THREADS), 0, st, cand_v, cand_i, n_cand, temps, top_ks,
+                     top_ps, seeds, steps, out_tok, out_logprob, list_len);
   return (int)hipGetLastError();
 }

@@ -432,7 +432,7 @@ class LLMEngine:
                                     vocab_offset=w.vocab_offset, chunks=chunks)
         if self.tp_size > 1:
             cv, ci = self._gather_candidates(cv, ci)
-        tok = be.sample_candidates(cv, ci, temps, ks, ps, seeds, steps)
+        tok = be.sample_candidates(cv, ci, temps, ks, ps, seeds, steps, list_len=self.K)
         if out is not None:
             out.copy_(tok)
             return out

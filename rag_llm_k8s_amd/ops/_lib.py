@@ -59,6 +59,7 @@ _SIGS = {
     "ragk_attn_decode_rope": [P, I, I, P, P, P, P, P, P, P, I, P, P, P, P, I, I, I, I, I, I, I, F, P, S],
     "ragk_topk_candidates": [P, I, I, I, I, I, I, P, P, S],
     "ragk_sample_candidates": [P, P, I, I, P, P, P, P, P, P, P, S],
+    "ragk_sample_candidates_lists": [P, P, I, I, I, P, P, P, P, P, P, P, S],
     "ragk_l2_partial": [P, I, I, I, I, P, I, I, P, P, P, P, S],
     "ragk_topk_merge": [P, P, I, I, I, P, P, S],
     "ragk_ivf_scan": [P, I, I, P, I, P, I, I, P, P, P, I, P, P, S],

@@ -182,7 +182,7 @@ class TorchBackend:
             i = torch.cat([i, torch.full((i.shape[0], K - k), -1)], 1)
         return v, (i + vocab_offset).int()
 
-    def sample_candidates(self, cand_v, cand_i, temps, top_ks, top_ps, seeds, steps):
+    def sample_candidates(self, cand_v, cand_i, temps, top_ks, top_ps, seeds, steps, list_len=None):
         out = torch.empty(cand_v.shape[0], dtype=torch.int32)
         for b in range(cand_v.shape[0]):
             order = torch.argsort(cand_v[b], descending=True, stable=True)
@@ -284,8 +284,8 @@ class NativeBackend(TorchBackend):
     def topk_candidates(self, logits, K, vocab_offset=0, max_cand=512, chunks=None):
         return self.n.topk_candidates(logits, K, vocab_offset=vocab_offset, max_cand=max_cand, chunks=chunks)
 
-    def sample_candidates(self, cand_v, cand_i, temps, top_ks, top_ps, seeds, steps):
-        return self.n.sample_candidates(cand_v, cand_i, temps, top_ks, top_ps, seeds, steps)
+    def sample_candidates(self, cand_v, cand_i, temps, top_ks, top_ps, seeds, steps, list_len=None):
+        return self.n.sample_candidates(cand_v, cand_i, temps, top_ks, top_ps, seeds, steps, list_len=list_len)
 
 
 def _lens_dev(cu):

@@ -684,12 +684,25 @@ def topk_candidates(logits, K, vocab_offset=0, max_cand=512, chunks=None, cand_v
     return cand_v, cand_i
 
 
-def sample_candidates(cand_v, cand_i, temps, top_ks, top_ps, seeds, steps, out_tok=None, out_lp=None):
+# candidate lists rank-merged in the sampler (no full sort) when rows ask for top_k <= 64
+SAMPLE_LIST_MERGE = os.environ.get("RAGK_SAMPLE_LIST_MERGE", "1") == "1"
+
+
+def sample_candidates(cand_v, cand_i, temps, top_ks, top_ps, seeds, steps, out_tok=None, out_lp=None, list_len=None):
+    """list_len: the candidates are n / list_len sorted lists of list_len (topk_candidates output);
+    lets rows with top_k <= 64 merge the lists by rank instead of sorting every candidate."""
     B, n = cand_v.shape
     _req(n <= 2048, "<= 2048 candidates")
     _req(temps.dtype == torch.float32 and top_ks.dtype == torch.int32 and top_ps.dtype == torch.float32, "param dtypes")
     _req(seeds.dtype == torch.int64 and steps.dtype == torch.int32, "seeds int64 / steps int32")
     out_tok = torch.empty(B, dtype=torch.int32, device=cand_v.device) if out_tok is None else out_tok
+    if list_len and SAMPLE_LIST_MERGE:
+        _req(n % list_len == 0, "candidate lists")
+        check(_lib.lib().ragk_sample_candidates_lists(cand_v.data_ptr(), cand_i.data_ptr(), B, n, int(list_len),
+                                                      temps.data_ptr(), top_ks.data_ptr(), top_ps.data_ptr(),
+                                                      seeds.data_ptr(), steps.data_ptr(), out_tok.data_ptr(),
+                                                      ptr(out_lp), stream_ptr()), "ragk_sample_candidates_lists")
+        return out_tok
     check(_lib.lib().ragk_sample_candidates(cand_v.data_ptr(), cand_i.data_ptr(), B, n, temps.data_ptr(),
                                             top_ks.data_ptr(), top_ps.data_ptr(), seeds.data_ptr(), steps.data_ptr(),
                                             out_tok.data_ptr(), ptr(out_lp), stream_ptr()), "ragk_sample_candidates")

@@ -495,6 +495,26 @@ def test_topk_and_greedy(native):
     assert torch.equal(tok.long(), logits.argmax(-1))
 
 
+@pytest.mark.parametrize("V,K,chunks,topk", [(128256, 64, 7, 50), (4000, 50, 3, 50), (30000, 64, 16, 64),
+                                              (37, 50, 3, 40)])
+def test_sample_list_merge_matches_sort(native, V, K, chunks, topk):
+    """Rank-merging the sorted per-chunk candidate lists (top_k <= 64) samples exactly the same tokens
+    as the full bitonic sort of all candidates: sampled (many seeds), greedy, and with -inf padding
+    (a 37-entry row spread over 3 chunks of 50)."""
+    torch.manual_seed(16)
+    B = 64
+    logits = (torch.randn(B, V, device=DEV) * 3).contiguous()
+    logits[:, 5] = logits[:, 9]  # an exact tie across ids
+    cv, ci = native.topk_candidates(logits, K, chunks=chunks)
+    for temp in (0.7, 0.0):
+        args = (torch.full((B,), temp, device=DEV), torch.full((B,), topk, dtype=torch.int32, device=DEV),
+                torch.full((B,), 0.9, device=DEV), torch.arange(B, dtype=torch.int64, device=DEV) * 31 + 7,
+                torch.arange(B, dtype=torch.int32, device=DEV))
+        a = native.sample_candidates(cv, ci, *args)
+        b = native.sample_candidates(cv, ci, *args, list_len=K)
+        assert torch.equal(a, b)
+
+
 def test_sampling_support_matches_hf_rules(native):
     """Sampled tokens always lie in the HF temperature->top-k->top-p kept set, and the
     empirical distribution matches the renormalised kept probabilities."""
