@@ -18,6 +18,8 @@
 // Replaces reference ops K3/K7/K8/K9/K10/K11 (the reference
 // runs them as fp32 ATen CPU matmuls inside transformers' LlamaForCausalLM,
 // /root/reference/llm/rag.py:24,172) and encoder ops E2/E4/E5/E6.
+#include <stdlib.h>
+
 #include "common.h"
 using namespace ragk;
 
@@ -200,13 +202,16 @@ __global__ __launch_bounds__(TILE_THREADS, 2) void gemm_tile_kernel(
 // ------------------------------------------------------------------------------------
 constexpr int SK_WAVES = 8;
 
-template <int MT, int EPI, bool OUT_F32>
-__global__ __launch_bounds__(SK_WAVES * 64) void gemm_skinny_kernel(
+// WV waves per block (default 8; 16 is an A/B option for long-K / few-column shapes such as the
+// batch-1 down projection -- measured slower there: more waves per block lengthen the LDS reduction
+// and the per-block tail more than the extra loads in flight gain).
+template <int MT, int EPI, bool OUT_F32, int WV = SK_WAVES>
+__global__ __launch_bounds__(WV * 64) void gemm_skinny_kernel(
     const bf16_t* __restrict__ X, int ldx, const bf16_t* __restrict__ W, int ldw, void* C, int ldc,
     const bf16_t* __restrict__ bias, const bf16_t* resid, int ldr, int M, int N, int K) {
   constexpr bool PAIR = (EPI == EPI_SILU_MUL);
   constexpr int NACC = PAIR ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) f32x4 red[SK_WAVES][NACC * MT][64];
+  __shared__ __attribute__((aligned(16))) f32x4 red[WV][NACC * MT][64];
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int fr = lane & 15, fh = lane >> 4;
@@ -240,7 +245,7 @@ __global__ __launch_bounds__(SK_WAVES * 64) void gemm_skinny_kernel(
 
   const int nkb = K >> 7;  // 128-deep K blocks
   const bf16x8 zero = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  for (int kb = wid; kb < nkb; kb += SK_WAVES) {
+  for (int kb = wid; kb < nkb; kb += WV) {
     const int k = kb * 128;
     bf16x8 wf[NACC][4];
 #pragma unroll
@@ -270,14 +275,14 @@ __global__ __launch_bounds__(SK_WAVES * 64) void gemm_skinny_kernel(
   __syncthreads();
 
   // reduce over waves; element e = (t, lane, r): row = 16t + 4*(lane>>4) + r, col = n0 + (lane&15)
-  for (int e = threadIdx.x; e < MT * 64 * 4; e += SK_WAVES * 64) {
+  for (int e = threadIdx.x; e < MT * 64 * 4; e += WV * 64) {
     const int t = e >> 8, ln = (e >> 2) & 63, r = e & 3;
     const int row = t * 16 + 4 * (ln >> 4) + r;
     const int col = n0 + (ln & 15);
     if (row >= M || col >= N) continue;
     float v = 0.f, u = 0.f;
 #pragma unroll
-    for (int w = 0; w < SK_WAVES; ++w) {
+    for (int w = 0; w < WV; ++w) {
       v += red[w][t][ln][r];
       if constexpr (PAIR) u += red[w][MT + t][ln][r];
     }
@@ -460,9 +465,28 @@ hipError_t launch_tile(const void* A, int lda, const void* B, int ldb, void* C, 
   return hipGetLastError();
 }
 
+static int g_skinny_waves = -1;  // -1: auto (RAGK_SKINNY_WAVES env, else by shape)
+RAGK_API int ragk_gemm_skinny_set_waves(int w) {
+  g_skinny_waves = (w == 8 || w == 16) ? w : -1;
+  return 0;
+}
+
 template <int MT, int EPI, bool F32>
 hipError_t launch_skinny(const void* X, int ldx, const void* W, int ldw, void* C, int ldc, const void* bias,
                          const void* resid, int ldr, int M, int N, int K, hipStream_t st) {
+  static const int s_env = [] {
+    const char* v = getenv("RAGK_SKINNY_WAVES");
+    return v ? atoi(v) : 0;
+  }();
+  int wv = g_skinny_waves > 0 ? g_skinny_waves : (s_env == 8 || s_env == 16 ? s_env : 0);
+  // auto = 8: 16 waves measured slower on the batch-1 down projection (decode step 3.66 -> 3.74 ms)
+  if (wv == 0) wv = 8;
+  if (wv == 16 && MT == 1) {
+    hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, 16>), dim3((N + 15) / 16), dim3(16 * 64), 0, st,
+                       (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
+                       (const bf16_t*)resid, ldr, M, N, K);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0, st,
                      (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
                      (const bf16_t*)resid, ldr, M, N, K);

@@ -29,6 +29,7 @@ _SIGS = {
     "ragk_attn_prefill_set_prio": [I],
     "ragk_attn_prefill_set_buf": [I],
     "ragk_gemm_stream_set_nt": [I],
+    "ragk_gemm_skinny_set_waves": [I],
     "ragk_gemm_stream_set_pair_rows": [I],
     "ragk_gemm_w4": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_part": [P, I, P, I, P, I, I, I, I, S],

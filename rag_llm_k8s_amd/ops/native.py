@@ -53,6 +53,12 @@ def set_w4_grid(g):
     check(_lib.lib().ragk_gemm_w4_set_grid(int(g)), "ragk_gemm_w4_set_grid")
 
 
+def set_skinny_waves(w):
+    """Waves per block of the skinny decode GEMM (one row tile): 8, 16, or -1 = auto (8;
+    RAGK_SKINNY_WAVES overrides). 16 measured slower on the batch-1 down projection."""
+    check(_lib.lib().ragk_gemm_skinny_set_waves(int(w)), "ragk_gemm_skinny_set_waves")
+
+
 def set_w4_cont(on):
     """gemm_w4 continuous K-stream kernel (K < 8192): 1 = on (default), 0 = the per-tile-prologue
     kernel, -1 = back to RAGK_W4_CONT / the default."""

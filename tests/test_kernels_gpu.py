@@ -147,6 +147,26 @@ def test_gemm_decode_v3(native, M, N, K):
         assert rel_err(y, ref2) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1, 4, 13])
+def test_gemm_skinny_wave_variants(native, M):
+    """Skinny decode GEMM (ragk_gemm routing at M <= 16) with 8 and 16 waves per block: same result
+    (K-blocks strided over the waves; the 16-wave variant serves long-K shapes like down_proj)."""
+    torch.manual_seed(22)
+    N, K = 4096, 14336
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    ref = x.float() @ w.float().t() + r.float()
+    outs = []
+    for wv in (8, 16):
+        native.set_skinny_waves(wv)
+        try:
+            outs.append(native.gemm(x, w, resid=r, epi="resid"))
+        finally:
+            native.set_skinny_waves(-1)
+        assert rel_err(outs[-1], ref) < 1e-2
+
+
 @pytest.mark.parametrize("path", [0, 1])
 @pytest.mark.parametrize("M", [1, 16, 33, 64])
 def test_gemm_paths_agree(native, path, M):
