@@ -876,6 +876,15 @@ RAGK_API int ragk_attn_decode_set_nt(int nt) {
 
 static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* counters, hipStream_t st);
 
+// Deferred merge: the next decode-attention launches leave the split-K partitions unmerged (no
+// attn_decode_reduce launch) for a consumer that merges them itself (gemm_part.hip MergeArgs: the
+// o_proj GEMM). The host sets it around one launch.
+static int g_decode_defer = 0;
+RAGK_API int ragk_attn_decode_set_defer(int on) {
+  g_decode_defer = on ? 1 : 0;
+  return 0;
+}
+
 RAGK_API int ragk_attn_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                               int bt_stride, const int* kv_lens, float* part_o, float* part_ml, void* out,
                               int out_stride, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
@@ -921,7 +930,7 @@ static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* co
       hipLaunchKernelGGL((attn_decode_kernel<DD, GG, true>), grid, dim3(256), 0, st, a, pf); \
     else                                                                             \
       hipLaunchKernelGGL((attn_decode_kernel<DD, GG, false>), grid, dim3(256), 0, st, a, pf); \
-    if (max_parts > 1 && !counters)                                                  \
+    if (max_parts > 1 && !counters && !g_decode_defer)                               \
       hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(Hq, B), dim3(DD), 0, st, a, DD); \
     return (int)hipGetLastError();                                                   \
   }

@@ -55,13 +55,45 @@ __device__ __forceinline__ bf16x8 p_fp8x8_bf16(unsigned lo, unsigned hi) {
 // NR = rows (M), NV = 16-B row vectors per thread (threads 0..255: K = 2048 NV); NR = 0: no norm.
 constexpr int NORM_MAXR = 4;
 
-template <int MT, int NKS, bool FP8 = false, int NR = 0, int NV = 1>
-__global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* __restrict__ X, int ldx,
+// MG (o_proj at decode batch <= 4): the activation is the split-K decode attention's UNMERGED output
+// -- per (sequence, query head) max_parts partial (O, max, sum) records (attention.hip, written with the
+// separate merge launch deferred) -- and every block merges the heads of its own K-slice while its
+// weight stream is in flight: the attn_decode_reduce launch (~5 us of pure latency per layer at batch
+// 1) disappears. The merge math is attn_decode_reduce_kernel's (max-rescaled sums, bf16(O / L)); only
+// the fp32 summation order differs. Rows whose sequence used a single partition were written as bf16
+// by the attention kernel itself and are read from there.
+struct MergeArgs {
+  const float* part_o;   // [B][Hq][max_parts][MG_D]
+  const float* part_ml;  // [B][Hq][max_parts][2] (max, sum)
+  const bf16_t* out;     // [B][out_stride] bf16: rows with a single partition
+  int out_stride;
+  const int* kv_lens;    // [B]
+  int Hq, part_tiles, max_parts;
+};
+constexpr int MG_D = 128;    // head dim
+constexpr int MG_KT = 64;    // keys per KV tile (attention.hip KT)
+constexpr int MG_MAXPP = 16; // partition records loaded per thread
+constexpr int MG_MAXR = 4;   // rows
+// The merge runs on 4 EXTRA waves (threads 512..767) that issue no weight loads: vmcnt is per wave, so
+// the 8 weight-streaming waves issue their whole stream at once as before and never wait behind the
+// partition-record loads (merging in the weight waves themselves, ahead of their stream, was slower
+// than the separate reduce launch).
+constexpr int MG_THREADS = 256;
+// partition groups per (row, head, 4-column) task: the merge threads split the partitions of a task
+__host__ __device__ inline int mg_groups(int M, int KS) {
+  const int tasks = M * (KS / MG_D) * (MG_D / 4);
+  int pg = 1;
+  while (pg < 8 && tasks * pg * 2 <= MG_THREADS) pg *= 2;
+  return pg;
+}
+
+template <int MT, int NKS, bool FP8 = false, int NR = 0, int NV = 1, bool MG = false>
+__global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), 1) void gemm_part_kernel(const bf16_t* __restrict__ X, int ldx,
                                                                   const bf16_t* __restrict__ W, int ldw,
                                                                   float* __restrict__ P, int M, int N, int K,
                                                                   const float* __restrict__ wscale = nullptr,
                                                                   const bf16_t* __restrict__ gamma = nullptr,
-                                                                  float eps = 0.f) {
+                                                                  float eps = 0.f, MergeArgs mg = {}) {
   constexpr int KS = NKS * 64;          // K-slice of the block (two halves of NKS k-steps of 32)
   constexpr int XROWS = 16 * MT;
   constexpr int ROWB = KS * 2;          // bytes per LDS row
@@ -86,6 +118,11 @@ __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* 
   static_assert(PIECES % (PT_THREADS / 64) == 0 && CPR >= 64, "activation slice shape");
   u32x4 hv[NORM ? NR : 1][NV];  // NORM: raw row vectors (tid & 255) + 256 i
   u32x4 gv[NV];
+  f32x4 mg_o[MG ? MG_MAXPP : 1];   // MG: partition records
+  f32x2 mg_ml[MG ? MG_MAXPP : 1];
+  uint2 mg_one;
+  int mg_pg = 0, mg_r = 0, mg_c = 0, mg_half = 0, mg_np = 1;
+  bool mg_act = false;
   if constexpr (NORM) {
     // full rows (vectors tid + 256 i, threads < 256) and gamma for the slice's vectors, issued before
     // the weight stream so the counted wait below retires them first
@@ -100,6 +137,39 @@ __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* 
       for (int r = 0; r < NR; ++r) hv[r][i] = *reinterpret_cast<const u32x4*>(X + (size_t)r * ldx + vi * 8);
       const int gi = min(max(vi * 8, kbase), kbase + KS - 8);
       gv[i] = *reinterpret_cast<const u32x4*>(gamma + gi);
+    }
+  } else if constexpr (MG) {
+    // merge waves: partition records of this thread's task (row r, head j of the slice, columns
+    // 4 d4 .. 4 d4 + 3), partitions pg, pg + npg, ... (indices clamped, all loads in flight)
+    if (wid >= PT_THREADS / 64) {
+    const int npg = mg_groups(M, KS);
+    const int task = (tid - PT_THREADS) / npg;
+    mg_pg = (tid - PT_THREADS) % npg;
+    mg_act = task < M * (KS / MG_D) * (MG_D / 4);
+    const int tk = mg_act ? task : 0;
+    mg_r = tk / (KS / 4);
+    const int j = (tk / (MG_D / 4)) % (KS / MG_D), d4 = tk % (MG_D / 4);
+    mg_c = j * (MG_D / 8) + d4 / 2;  // 16-B chunk of the slice row; 8-B half d4 & 1
+    mg_half = d4 & 1;
+    const int hq = kbase / MG_D + j;
+    // kv_len of row r: uniform scalar loads (lgkmcnt, not the vector counter), selected per lane
+    int kvl = mg.kv_lens[0];
+#pragma unroll
+    for (int rr = 1; rr < MG_MAXR; ++rr) {
+      const int v = mg.kv_lens[min(rr, M - 1)];
+      kvl = mg_r == rr ? v : kvl;
+    }
+    const int n_kt = (kvl + MG_KT - 1) / MG_KT;
+    const int pt = max(mg.part_tiles, (n_kt + mg.max_parts - 1) / mg.max_parts);
+    mg_np = (n_kt + pt - 1) / pt;
+    const size_t pb = ((size_t)mg_r * mg.Hq + hq) * mg.max_parts;
+#pragma unroll
+    for (int i = 0; i < MG_MAXPP; ++i) {
+      const int p = min(mg_pg + i * npg, max(mg_np, 1) - 1);
+      mg_o[i] = *reinterpret_cast<const f32x4*>(mg.part_o + (pb + p) * MG_D + 4 * d4);
+      mg_ml[i] = *reinterpret_cast<const f32x2*>(mg.part_ml + (pb + p) * 2);
+    }
+    mg_one = *reinterpret_cast<const uint2*>(mg.out + (size_t)mg_r * mg.out_stride + hq * MG_D + 4 * d4);
     }
   } else {
 #pragma unroll
@@ -119,8 +189,10 @@ __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* 
   constexpr int NLD = FP8 ? NKS / 2 : NKS;  // 16-B loads per lane
   static_assert(!FP8 || NKS % 2 == 0, "fp8 slices cover whole 64-k blocks");
   const int wrow = min(n0 + 16 * nt + fr, N - 1);
+  const bool wwave = !MG || wid < PT_THREADS / 64;  // wave-uniform: MG's merge waves stream no weights
   bf16x8 wf[NLD];
-  if constexpr (FP8) {
+  if (!wwave) {
+  } else if constexpr (FP8) {
     const unsigned char* wp = reinterpret_cast<const unsigned char*>(W) + (size_t)wrow * ldw + kbase + kh * (KS / 2) +
                               fh * 16;
 #pragma unroll
@@ -177,6 +249,44 @@ __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* 
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  if (MG && !wwave) {
+    // online max-rescaled merge of this thread's partitions, then of the npg threads of the task
+    // (adjacent lanes); lane pg 0 writes bf16(O / L) into the swizzled activation slice
+    const int npg = mg_groups(M, KS);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < MG_MAXPP; ++i) mx = mg_pg + i * npg < mg_np ? fmaxf(mx, mg_ml[i][0]) : mx;
+    const float mu = mx == -INFINITY ? 0.f : mx;
+    float l = 0.f;
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < MG_MAXPP; ++i) {
+      const float sc = mg_pg + i * npg < mg_np ? exp2f(mg_ml[i][0] - mu) : 0.f;
+      l += mg_ml[i][1] * sc;
+      o += mg_o[i] * sc;
+    }
+    for (int off = 1; off < npg; off <<= 1) {
+      const float mo = __shfl_xor(mx, off, 64), lo = __shfl_xor(l, off, 64);
+      f32x4 oo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) oo[e] = __shfl_xor(o[e], off, 64);
+      const float mn = fmaxf(mx, mo);
+      const float sa = mx == -INFINITY ? 0.f : exp2f(mx - mn), sb = mo == -INFINITY ? 0.f : exp2f(mo - mn);
+      l = l * sa + lo * sb;
+      o = o * sa + oo * sb;
+      mx = mn;
+    }
+    if (mg_act && mg_pg == 0) {
+      uint2 v = mg_one;
+      if (mg_np > 1) {
+        v.x = pk2bf(l > 0.f ? o[0] / l : 0.f, l > 0.f ? o[1] / l : 0.f);
+        v.y = pk2bf(l > 0.f ? o[2] / l : 0.f, l > 0.f ? o[3] / l : 0.f);
+      }
+      const int c = (mg_c & ~15) | ((mg_c & 15) ^ (mg_r & 15));
+      *reinterpret_cast<uint2*>(smem + mg_r * ROWB + 16 * c + 8 * mg_half) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();  // raw: __syncthreads() would drain the weight loads too (vmcnt(0))
   __builtin_amdgcn_sched_barrier(0);
 
@@ -188,7 +298,8 @@ __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* 
     const int r = 16 * t + fr;
     return *reinterpret_cast<const bf16x8*>(smem + r * ROWB + 16 * ((chunk & ~15) | ((chunk & 15) ^ (r & 15))));
   };
-  if constexpr (FP8) {
+  if (!wwave) {
+  } else if constexpr (FP8) {
 #pragma unroll
     for (int j = 0; j < NLD; ++j) {
       const u32x4 raw = __builtin_bit_cast(u32x4, wf[j]);
@@ -233,17 +344,20 @@ __global__ __launch_bounds__(PT_THREADS, 1) void gemm_part_kernel(const bf16_t* 
   }
 }
 
-template <int MT, bool FP8 = false, int NR = 0, int NV = 1>
+template <int MT, bool FP8 = false, int NR = 0, int NV = 1, bool MG = false>
 int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K, int ks_steps,
-                   hipStream_t st, const float* wscale = nullptr, const void* gamma = nullptr, float eps = 0.f) {
+                   hipStream_t st, const float* wscale = nullptr, const void* gamma = nullptr, float eps = 0.f,
+                   MergeArgs mg = {}) {
   const int KS = ks_steps * 64;
   const dim3 grid((N + PT_NB - 1) / PT_NB, K / KS);
 #define RAGK_PART(NK)                                                                                       \
   case NK:                                                                                                  \
     if constexpr (16 * MT * NK * 64 * 2 <= 128 * 1024 && (16 * MT * NK * 64 * 2) % 8192 == 0 &&           \
-                  (NR == 0 || NK == 8 || NK == 16)) {                                                       \
-      hipLaunchKernelGGL((gemm_part_kernel<MT, NK, FP8, NR, NV>), grid, dim3(PT_THREADS), 0, st, (const bf16_t*)X, \
-                         ldx, (const bf16_t*)W, ldw, P, M, N, K, wscale, (const bf16_t*)gamma, eps);         \
+                  (NR == 0 || NK == 8 || NK == 16) && (!MG || NK == 8)) {                                   \
+      hipLaunchKernelGGL((gemm_part_kernel<MT, NK, FP8, NR, NV, MG>), grid, dim3(PT_THREADS + (MG ? MG_THREADS : 0)), \
+                         0, st,                                                                             \
+                         (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, P, M, N, K, wscale, (const bf16_t*)gamma, \
+                         eps, mg);                                                                          \
       break;                                                                                                \
     } else {                                                                                                \
       return (int)hipErrorInvalidValue;                                                                     \
@@ -334,4 +448,30 @@ RAGK_API int ragk_gemm_part_fp8(const void* X, int ldx, const void* W8, int ldw,
     case 4: return launch_part_mt<4, true>(X, ldx, W8, ldw, P, M, N, K, ks_steps, st, wscale);
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+// o_proj fed by the decode attention's unmerged partitions (MG above; the attention launched with its
+// merge deferred, ragk_attn_decode_set_defer). X (bf16 rows, out_stride) is the attention output buffer:
+// rows whose sequence used one partition are read from it. M <= 4, head dim 128, K = Hq * 128, 8-step
+// K-slices (a 16-step slice spills), at most MG_MAXPP partitions per thread. w8 / wscale: fp8 weights (ldw in bytes).
+RAGK_API int ragk_gemm_part_merge(const float* part_o, const float* part_ml, const void* out, int out_stride,
+                                  const int* kv_lens, int Hq, int part_tiles, int max_parts, const void* W, int ldw,
+                                  const float* wscale, float* P, int M, int N, int K, int ks_steps, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (M > MG_MAXR || K != Hq * MG_D || ks_steps != 8 || K % (64 * ks_steps) || max_parts < 2 ||
+      !part_o || !part_ml || !out || !kv_lens || part_tiles < 1)
+    return (int)hipErrorInvalidValue;
+  const int npg = mg_groups(M, ks_steps * 64);
+  if ((max_parts + npg - 1) / npg > MG_MAXPP) return (int)hipErrorInvalidValue;
+  const MergeArgs mg{part_o, part_ml, (const bf16_t*)out, out_stride, kv_lens, Hq, part_tiles, max_parts};
+  if (wscale) return launch_part_mt<1, true, 0, 1, true>(out, out_stride, W, ldw, P, M, N, K, ks_steps, st, wscale,
+                                                          nullptr, 0.f, mg);
+  return launch_part_mt<1, false, 0, 1, true>(out, out_stride, W, ldw, P, M, N, K, ks_steps, st, nullptr, nullptr,
+                                              0.f, mg);
+}
+
+RAGK_API int ragk_gemm_part_merge_ok(int M, int K, int Hq, int max_parts, int ks_steps) {
+  if (M <= 0 || M > MG_MAXR || K != Hq * MG_D || ks_steps != 8 || max_parts < 2) return 0;
+  const int npg = mg_groups(M, ks_steps * 64);
+  return (max_parts + npg - 1) / npg <= MG_MAXPP;
 }

@@ -856,12 +856,16 @@ __device__ __forceinline__ void w4_iter_c(char* smem, int g, i32x4 srd_a, i32x4 
 }
 
 // Requires K / 64 >= 4 (the launcher falls back to gemm_w4_kernel below that).
-template <int EPI, bool OUT_F32, bool STAMP = false>
+// KSPLIT: split-K over nsplit K-slabs of K columns each in ONE persistent launch -- work item
+// t = z * tiles + tile writes the fp32 partial tile of slab z to C + z * M * ldc (the consumer, e.g.
+// add_partials_rmsnorm, sums the slabs). For prefill shapes whose 256x256 tile count fills only
+// ~1.3 waves of the CUs (o_proj / down at M ~ 5k: 336 tiles on 256 CUs), two slabs make 2.6 waves.
+template <int EPI, bool OUT_F32, bool STAMP = false, bool KSPLIT = false>
 __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4c_kernel(const bf16_t* __restrict__ A, int lda,
                                                                  const bf16_t* __restrict__ B, int ldb, void* C,
                                                                  int ldc, const bf16_t* __restrict__ bias,
                                                                  const bf16_t* resid, int ldr, int M, int N, int K,
-                                                                 unsigned long long* dbg) {
+                                                                 unsigned long long* dbg, int nsplit = 1) {
   __shared__ __attribute__((aligned(16))) char smem[W4_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -869,6 +873,7 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4c_kernel(const bf16_t* _
   const int fr = lane & 15, fh = lane >> 4;
   const int tiles_m = (M + WBM - 1) / WBM, tiles_n = (N + WBN - 1) / WBN;
   const int nwg = tiles_m * tiles_n;
+  const int nwt = KSPLIT ? nwg * nsplit : nwg;  // work items
   const int nk = K / WBK;
   const i32x4 srd_a = make_srd(A, (unsigned)M * (unsigned)lda * 2u);
   const i32x4 srd_b = make_srd(B, (unsigned)N * (unsigned)ldb * 2u);
@@ -879,11 +884,19 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4c_kernel(const bf16_t* _
   constexpr int VMW0 = 16 + EV > 63 ? 63 : 16 + EV;
 
   int tile = blockIdx.x;
+  int z = KSPLIT ? tile / nwg : 0;
   int m0, n0;
-  w4_origin(tile, nwg, tiles_m, tiles_n, m0, n0);
+  w4_origin(tile - z * nwg, nwg, tiles_m, tiles_n, m0, n0);
   int off_a[8], off_b[8];
   w4_offsets(lda, m0, M, wid, lane, off_a);
   w4_offsets(ldb, n0, N, wid, lane, off_b);
+  if constexpr (KSPLIT) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      off_a[i] += z * K * 2;
+      off_b[i] += z * K * 2;
+    }
+  }
   w4_stage(srd_a, off_a, 0, smem, wid);
   w4_stage(srd_b, off_b, 0, smem + W_TILE_A, wid);
   w4_stage(srd_a, off_a, WBK, smem + W_BUF, wid);
@@ -903,7 +916,7 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4c_kernel(const bf16_t* _
     unsigned long long tt0 = 0;
     if constexpr (STAMP) tt0 = __builtin_amdgcn_s_memtime();
     const int next = tile + (int)gridDim.x;
-    const bool has_next = next < nwg;
+    const bool has_next = next < nwt;
     w4_iter_c<true, true, true, VMW0, false>(smem, g, srd_a, srd_b, off_a, off_b, 2, wid, wr, wc, fr, fh, acc, a0,
                                              b0, a1, b1, stp);
     ++g;
@@ -915,13 +928,22 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4c_kernel(const bf16_t* _
     // cases run the same straight-line code: a branch around the MFMA iterations made the register
     // allocator split the accumulators across the two paths and spill them.
     int nm0, nn0;
-    w4_origin(has_next ? next : tile, nwg, tiles_m, tiles_n, nm0, nn0);
+    const int ntile = has_next ? next : tile;
+    const int nz = KSPLIT ? ntile / nwg : 0;
+    w4_origin(ntile - nz * nwg, nwg, tiles_m, tiles_n, nm0, nn0);
     {
       int ln;  // == lane; opaque so the lane-only offset math is not hoisted out of the loop
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
       // this tile's DMAs are all issued: its offset registers take the next tile's
       w4_offsets(lda, nm0, M, wid, ln, off_a);
       w4_offsets(ldb, nn0, N, wid, ln, off_b);
+      if constexpr (KSPLIT) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          off_a[i] += nz * K * 2;
+          off_b[i] += nz * K * 2;
+        }
+      }
     }
     w4_iter_c<true, true, false, 16, false>(smem, g, srd_a, srd_b, off_a, off_b, 0, wid, wr, wc, fr, fh, acc, a0, b0,
                                             a1, b1, stp);
@@ -932,13 +954,14 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4c_kernel(const bf16_t* _
     unsigned long long tt1 = 0;
     if constexpr (STAMP) tt1 = __builtin_amdgcn_s_memtime();
     w4_pin_acc(acc);
+    void* Cz = KSPLIT ? (void*)(reinterpret_cast<float*>(C) + (size_t)z * M * ldc) : C;
     if (m0 + WBM <= M && n0 + WBN <= N) {
       if constexpr (OUT_F32 || !W4_WIDE_EPI)
-        w4_epilogue_reg<EPI, OUT_F32, true>(acc, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr, M, N);
+        w4_epilogue_reg<EPI, OUT_F32, true>(acc, wr, wc, fr, fh, m0, n0, Cz, ldc, bias, resid, ldr, M, N);
       else
-        w4_epilogue_wide<EPI>(acc, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr);
+        w4_epilogue_wide<EPI>(acc, wr, wc, fr, fh, m0, n0, Cz, ldc, bias, resid, ldr);
     } else {
-      w4_epilogue_reg<EPI, OUT_F32, false>(acc, wr, wc, fr, fh, m0, n0, C, ldc, bias, resid, ldr, M, N);
+      w4_epilogue_reg<EPI, OUT_F32, false>(acc, wr, wc, fr, fh, m0, n0, Cz, ldc, bias, resid, ldr, M, N);
       __builtin_amdgcn_s_waitcnt(W_VM0);  // guarded: count unknown, drain (the next K-tile 1 lands too)
     }
     // epilogue accumulator reads -> the next tile's srcC = 0 MFMA writes
@@ -956,6 +979,7 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4c_kernel(const bf16_t* _
     tile = next;
     m0 = nm0;
     n0 = nn0;
+    z = nz;
   }
   if constexpr (STAMP) {
     if (lane == 0) {
@@ -1073,6 +1097,21 @@ RAGK_API int ragk_gemm_w4(const void* A, int lda, const void* B, int ldb, void* 
       return (int)hipErrorInvalidValue;
   }
 #undef RAGK_W4_CASE
+}
+
+// Split-K prefill GEMM into fp32 slabs: P[z][M][N] = A[:, z*Ks:(z+1)*Ks] . B[:, z*Ks:(z+1)*Ks]^T,
+// Ks = K / nsplit, one persistent gemm_w4c launch over nsplit x tiles work items (see KSPLIT).
+RAGK_API int ragk_gemm_w4_splitk(const void* A, int lda, const void* B, int ldb, float* P, int M, int N, int K,
+                                 int nsplit, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (nsplit < 1 || K % nsplit || (K / nsplit) % WBK || (K / nsplit) / WBK < 4 || N % 8 || !P)
+    return (int)hipErrorInvalidValue;
+  if ((long long)M * lda * 2 >= (1LL << 31) || (long long)N * ldb * 2 >= (1LL << 31)) return (int)hipErrorInvalidValue;
+  const int nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
+  hipLaunchKernelGGL((gemm_w4c_kernel<EPI_NONE, true, false, true>), dim3(w4_grid(nwg * nsplit)), dim3(W4_THREADS), 0,
+                     st, (const bf16_t*)A, lda, (const bf16_t*)B, ldb, (void*)P, N, nullptr, nullptr, 0, M, N,
+                     K / nsplit, nullptr, nsplit);
+  return (int)hipGetLastError();
 }
 
 // Diagnostic / tuning builds of the EPI_NONE kernel (tools/gemm_stamps.py). variant selects the

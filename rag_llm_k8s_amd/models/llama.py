@@ -37,6 +37,9 @@ DECODE_DOWN_SKINNY_MAX_M = int(os.environ.get("RAGK_DECODE_DOWN_SKINNY_MAX_M", "
 DECODE_ROPE_FUSED = os.environ.get("RAGK_DECODE_ROPE_FUSED", "1") == "1"
 # decode batch <= DECODE_DOWN_SKINNY_MAX_M: input RMSNorm inside the qkv split-K GEMM (gemm_part_norm)
 DECODE_NORM_FUSED = os.environ.get("RAGK_DECODE_NORM_FUSED", "1") == "1"
+# decode batch <= 4: the o_proj split-K GEMM merges the attention's split-K partitions itself
+# (gemm_part_merge), so the attention's separate merge launch disappears
+DECODE_OPROJ_MERGE = os.environ.get("RAGK_DECODE_OPROJ_MERGE", "1") == "1"
 
 
 @dataclass
@@ -340,13 +343,19 @@ class LlamaModel:
         fuse_norm = (DECODE_NORM_FUSED and M <= DECODE_DOWN_SKINNY_MAX_M and not pf
                      and be.part_norm_ok(M, layers[0]["wqkv"]))
         xn = None if fuse_norm else be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
+        merge = (DECODE_OPROJ_MERGE and DECODE_ROPE_FUSED and not pf
+                 and be.part_merge_ok(M, inp.meta, layers[0]["wo"], Hq, D))
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
             if fuse_norm:
                 P = be.gemm_part_norm(h, L["ln_in"], c.rms_norm_eps, L["wqkv"])
             else:
                 P = be.gemm_part(xn, L["wqkv"])
-            if DECODE_ROPE_FUSED and not pf:
+            if merge:
+                # RoPE + KV append inside the attention kernel, its split-K merge inside the o_proj GEMM
+                be.attn_decode_rope(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, attn,
+                                    Hq, Hkv, D, defer_merge=True)
+            elif DECODE_ROPE_FUSED and not pf:
                 # RoPE + KV append inside the attention kernel (one launch fewer per layer)
                 be.attn_decode_rope(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, attn,
                                     Hq, Hkv, D)
@@ -358,7 +367,7 @@ class LlamaModel:
                     be.pf_arm([(L["wo"], pf["rope"], pf["attn"] // 2), (L["wgu"], 0, pf["attn"] // 2)],
                               pf["blocks"])
                 be.attn_decode(q, kc, vc, inp.meta, attn, Hq, Hkv, D)
-            P = be.gemm_part(attn, L["wo"])
+            P = be.gemm_part_merge(attn, inp.meta, L["wo"], Hq) if merge else be.gemm_part(attn, L["wo"])
             if pf:
                 be.pf_arm([(L["wgu"], pf["attn"] // 2, pf["post"])], pf["blocks"])
             xn = be.add_partials_rmsnorm(P, h, L["ln_post"], c.rms_norm_eps)
@@ -387,12 +396,48 @@ class LlamaModel:
         if self._decode_part_ok(inp, h):
             return self.hidden_states_decode_part(inp, h)
         attn = torch.empty((h.shape[0], self.Hq * self.D), dtype=h.dtype, device=h.device)
+        if self.comm is None and inp.meta is not None and inp.meta.kind != "decode":
+            L0 = w.layers[0]
+            ns = (be.prefill_nsplit(h.shape[0], L0["wo"]), be.prefill_nsplit(h.shape[0], L0["wdown"]))
+            if max(ns) > 1:
+                return self.hidden_states_splitk(inp, h, attn, *ns)
         for li, L in enumerate(w.layers):
             self._attn_block(li, L, h, inp, attn)
             self._allreduce(h)
             self._mlp_block(L, h)
             self._allreduce(h)
         return self._final(h, inp)
+
+    def hidden_states_splitk(self, inp: StepInput, h, attn, ns_o, ns_d):
+        """TP=1 prefill of a step too small to fill the CUs with 256x256 output tiles (a single ~5k-token
+        RAG prompt): o_proj / down run as split-K GEMMs into fp32 slabs (ops/native.py:prefill_nsplit,
+        gemm_w4c KSPLIT) and the residual add moves into the following RMSNorm kernel
+        (add_partials_rmsnorm), which the layer needs anyway -- same rounding points as the residual
+        epilogue path (bf16 projection output, bf16 residual add)."""
+        be, w, c = self.be, self.w, self.cfg
+        Hq, Hkv, D = self.Hq, self.Hkv, self.D
+        layers = w.layers
+        xn = be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
+        for li, L in enumerate(layers):
+            kc, vc = self.kv_cache[li]
+            qkv = be.gemm(xn, L["wqkv"])
+            be.rope_kv(qkv, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
+            be.attn_prefill(qkv, kc, vc, inp.meta, attn, Hq, Hkv, D)
+            if ns_o > 1:
+                xn = be.add_partials_rmsnorm(be.gemm_splitk(attn, L["wo"], ns_o), h, L["ln_post"], c.rms_norm_eps)
+            else:
+                be.gemm(attn, L["wo"], resid=h, epi="resid", out=h)
+                xn = be.rmsnorm(h, L["ln_post"], c.rms_norm_eps)
+            a = be.gemm(xn, L["wgu"], epi="silu_mul")
+            nxt = layers[li + 1]["ln_in"] if li + 1 < len(layers) else w.norm
+            if ns_d > 1:
+                xn = be.add_partials_rmsnorm(be.gemm_splitk(a, L["wdown"], ns_d), h, nxt, c.rms_norm_eps)
+            else:
+                be.gemm(a, L["wdown"], resid=h, epi="resid", out=h)
+                xn = be.rmsnorm(h, nxt, c.rms_norm_eps)
+        if inp.logits_idx is not None:
+            xn = be.gather_rows(xn, inp.logits_idx)
+        return xn
 
     def hidden_states_sp(self, inp: StepInput):
         """Tensor-parallel prefill with Megatron sequence parallelism: the residual

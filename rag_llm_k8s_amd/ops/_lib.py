@@ -32,10 +32,14 @@ _SIGS = {
     "ragk_gemm_skinny_set_waves": [I],
     "ragk_gemm_stream_set_pair_rows": [I],
     "ragk_gemm_w4": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
+    "ragk_gemm_w4_splitk": [P, I, P, I, P, I, I, I, I, S],
     "ragk_gemm_part": [P, I, P, I, P, I, I, I, I, S],
     "ragk_gemm_part_norm": [P, I, P, F, P, I, P, I, I, I, I, S],
     "ragk_gemm_part_fp8": [P, I, P, I, P, P, I, I, I, I, S],
     "ragk_attn_decode_set_nt": [I],
+    "ragk_attn_decode_set_defer": [I],
+    "ragk_gemm_part_merge": [P, P, P, I, P, I, I, I, P, I, P, P, I, I, I, I, S],
+    "ragk_gemm_part_merge_ok": [I, I, I, I, I],
     "ragk_attn_prefill_set_waves": [I],
     "ragk_attn_prefill_stamp": [P, I, P, P, P, I, P, P, P, I, P, I, I, I, F, P, S],
     "ragk_gemm_w4_diag": [I, I, P, I, P, I, P, I, I, I, I, P, S],

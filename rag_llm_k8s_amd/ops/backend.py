@@ -155,6 +155,12 @@ class TorchBackend:
         self.rope_kv_partials(P, q, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)
         return self.attn_decode(q, kc, vc, meta, out, Hq, Hkv, D)
 
+    def part_merge_ok(self, M, meta: AttnMeta, w, Hq, D):
+        return False
+
+    def prefill_nsplit(self, M, w):
+        return 1
+
     def attn_decode(self, q, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
         B = q.shape[0]
         cu = torch.arange(B + 1, dtype=torch.int32)
@@ -266,9 +272,27 @@ class NativeBackend(TorchBackend):
         return self.n.attn_prefill(q, kc, vc, meta.cu_q, meta.kv_lens, meta.tiles, out, Hq, Hkv, D, causal=True,
                                    paged=True, block_tables=meta.block_tables)
 
-    def attn_decode_rope(self, P, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
+    def attn_decode_rope(self, P, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, out, Hq, Hkv, D,
+                         defer_merge=False):
         return self.n.attn_decode_rope(P, positions, cos_t, sin_t, slots, kc, vc, meta.block_tables, meta.kv_lens, out,
-                                       Hq, Hkv, D, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml)
+                                       Hq, Hkv, D, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml,
+                                       defer_merge=defer_merge)
+
+    def prefill_nsplit(self, M, w):
+        if isinstance(w, Fp8Weight):
+            return 1
+        return self.n.prefill_nsplit(M, w.shape[0], w.shape[1])
+
+    def gemm_splitk(self, x, w, nsplit):
+        return self.n.gemm_splitk(x, w, nsplit)
+
+    def part_merge_ok(self, M, meta: AttnMeta, w, Hq, D):
+        return (self.enable_part and D == 128 and not self.n.ATTN_FUSED_MERGE
+                and self.n.gemm_part_merge_ok(M, w, Hq, meta.max_parts, meta.ws_o))
+
+    def gemm_part_merge(self, attn_out, meta: AttnMeta, w, Hq):
+        return self.n.gemm_part_merge(attn_out, meta.kv_lens, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml,
+                                      Hq, w)
 
     def attn_decode(self, q, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
         return self.n.attn_decode(q, kc, vc, meta.block_tables, meta.kv_lens, out, Hq, Hkv, D, meta.part_tiles,

@@ -306,6 +306,94 @@ def gemm_part(x, w, out=None, ks=None):
     return out[:S] if out.dim() == 3 else out
 
 
+PREFILL_SPLITK = os.environ.get("RAGK_PREFILL_SPLITK", "1") == "1"
+_n_cus = [0]
+
+
+def _cu_count():
+    if not _n_cus[0]:
+        try:
+            _n_cus[0] = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+        except Exception:
+            _n_cus[0] = 256
+    return _n_cus[0]
+
+
+def prefill_nsplit(M, N, K):
+    """K-slabs for a prefill GEMM whose 256x256 tile grid fills the CUs poorly (gemm_w4c KSPLIT):
+    the split with the best wave efficiency (tiles / (waves * CUs)), 2 % charged per extra slab for
+    the fp32 slab traffic; 1 = no split. M = 5.2k (a C=1 RAG prompt), N = 4096: 336 tiles = 1.31 waves
+    (66 %) -> 2 slabs = 2.6 waves (88 %). The 32k-token bench steps (2048 tiles) never split."""
+    if not PREFILL_SPLITK or M < 256:
+        return 1
+    cus = _cu_count()
+    tiles = -(-M // 256) * -(-N // 256)
+    best, best_s = 0.0, 1
+    for s in (1, 2, 4):
+        if K % (64 * s) or K // s < 4 * 64:
+            continue
+        wt = tiles * s
+        eff = wt / (-(-wt // cus) * cus) - 0.02 * (s - 1)
+        if eff > best + 1e-9:
+            best, best_s = eff, s
+    return best_s
+
+
+def gemm_splitk(x, w, nsplit, out=None):
+    """fp32 split-K slabs P[nsplit, M, N] with P.sum(0) = x @ w^T, one persistent gemm_w4c launch
+    (csrc/kernels/gemm_w4.hip KSPLIT); consumed by add_partials_rmsnorm (residual add + norm)."""
+    _bf16_2d(x, "x")
+    _bf16_2d(w, "w")
+    M, K = x.shape
+    N = w.shape[0]
+    _req(w.shape[1] == K and K % (64 * nsplit) == 0 and K // nsplit >= 256 and N % 8 == 0, "gemm_splitk shape")
+    if out is None:
+        out = torch.empty((nsplit, M, N), dtype=torch.float32, device=x.device)
+    _req(out.dtype == torch.float32 and out.is_contiguous() and out.numel() >= nsplit * M * N, "gemm_splitk out")
+    check(_lib.lib().ragk_gemm_w4_splitk(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), M, N, K,
+                                         nsplit, stream_ptr()), "ragk_gemm_w4_splitk")
+    return out
+
+
+def gemm_part_merge_ok(M, w, Hq, max_parts, ws_o):
+    """Whether the o_proj split-K GEMM can merge the decode attention's partitions itself
+    (gemm_part.hip MergeArgs): batch <= 4, head dim 128, a partition workspace present."""
+    from .fp8 import Fp8Weight
+
+    if ws_o is None or max_parts < 2:
+        return False
+    wt = w.w8 if isinstance(w, Fp8Weight) else w
+    N, K = wt.shape
+    ks, S = gemm_part_slabs(M, N, K)
+    return S > 0 and bool(_lib.lib().ragk_gemm_part_merge_ok(M, K, Hq, max_parts, ks))
+
+
+def gemm_part_merge(attn_out, kv_lens, part_tiles, max_parts, ws_o, ws_ml, Hq, w, out=None):
+    """o_proj partials P[S, M, N] = merge(attention partitions) @ w^T: the decode attention ran with its
+    split-K merge deferred (attn_decode_rope(..., defer_merge=True)) and every GEMM block merges the
+    heads of its K-slice from ws_o / ws_ml (attn_decode_reduce's math); rows with a single partition
+    are read from attn_out, where the attention kernel wrote them. Replaces the reduce launch."""
+    from .fp8 import Fp8Weight
+
+    fp8 = isinstance(w, Fp8Weight)
+    wt = w.w8 if fp8 else w
+    M = kv_lens.numel()
+    N, K = wt.shape
+    _req(attn_out.dtype == torch.bfloat16 and attn_out.stride(1) == 1 and attn_out.shape[0] >= M
+         and attn_out.shape[1] == K, "attention output rows")
+    _req(ws_o is not None and ws_o.dtype == torch.float32 and ws_o.numel() >= M * Hq * max_parts * 128
+         and ws_ml.numel() >= M * Hq * max_parts * 2, "partition workspace")
+    ks, S = gemm_part_slabs(M, N, K)
+    _req(S > 0 and _lib.lib().ragk_gemm_part_merge_ok(M, K, Hq, max_parts, ks), "gemm_part_merge shape")
+    if out is None:
+        out = torch.empty((S, M, N), dtype=torch.float32, device=attn_out.device)
+    check(_lib.lib().ragk_gemm_part_merge(
+        ws_o.data_ptr(), ws_ml.data_ptr(), attn_out.data_ptr(), attn_out.stride(0), kv_lens.data_ptr(), Hq,
+        part_tiles, max_parts, wt.data_ptr(), wt.stride(0), w.scale.data_ptr() if fp8 else None, out.data_ptr(), M, N,
+        K, ks, stream_ptr()), "ragk_gemm_part_merge")
+    return out
+
+
 STREAM_S_OVERRIDE = 0  # tuning hook (tools/tune_stream.py)
 
 
@@ -615,7 +703,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, par
 
 
 def attn_decode_rope(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D,
-                     part_tiles, max_parts, ws_o=None, ws_ml=None, scale=None):
+                     part_tiles, max_parts, ws_o=None, ws_ml=None, scale=None, defer_merge=False):
     """Decode attention straight from the qkv projection's split-K partial slabs P [S, B, ldp] (fp32):
     q / k RoPE, the KV append at `slots` and the attention in one launch -- the same result as
     rope_kv_partials followed by attn_decode (bit-identical), one kernel fewer per layer."""
@@ -637,14 +725,23 @@ def attn_decode_rope(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_
         _req(ws_o.numel() >= B * Hq * max_parts * D and ws_ml.numel() >= B * Hq * max_parts * 2, "workspace")
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     cnt = None
-    if max_parts > 1 and ATTN_FUSED_MERGE and 2 * (Hq // Hkv) * max_parts + 16 <= 4 * 64 * D * 2 // 4:
+    if defer_merge:  # the partitions stay unmerged for gemm_part_merge (no reduce launch, no fused merge)
+        _req(max_parts > 1 and ws_o is not None, "deferred merge needs a partition workspace")
+    elif max_parts > 1 and ATTN_FUSED_MERGE and 2 * (Hq // Hkv) * max_parts + 16 <= 4 * 64 * D * 2 // 4:
         cnt = _attn_counters(P.device)
         _req(B * Hkv <= cnt.numel(), "attention ticket buffer too small")
-    check(_lib.lib().ragk_attn_decode_rope(
-        P.data_ptr(), S, ldp, positions.data_ptr(), slots.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(),
-        k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0), kv_lens.data_ptr(),
-        ptr(ws_o), ptr(ws_ml), out.data_ptr(), out.stride(0), B, Hq, Hkv, D, part_tiles, max_parts, float(scale),
-        ptr(cnt), stream_ptr()), "ragk_attn_decode_rope")
+    lib = _lib.lib()
+    if defer_merge:
+        lib.ragk_attn_decode_set_defer(1)
+    try:
+        check(lib.ragk_attn_decode_rope(
+            P.data_ptr(), S, ldp, positions.data_ptr(), slots.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(),
+            k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0),
+            kv_lens.data_ptr(), ptr(ws_o), ptr(ws_ml), out.data_ptr(), out.stride(0), B, Hq, Hkv, D, part_tiles,
+            max_parts, float(scale), ptr(cnt), stream_ptr()), "ragk_attn_decode_rope")
+    finally:
+        if defer_merge:
+            lib.ragk_attn_decode_set_defer(0)
     return out
 
 

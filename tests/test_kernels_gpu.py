@@ -446,6 +446,108 @@ def test_attn_decode_rope_matches_unfused(native, kv_lens, target):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("M,N,K,ns", [(5207, 4096, 4096, 2), (5207, 4096, 14336, 2), (300, 4096, 4096, 4),
+                                       (1000, 1024, 2048, 2), (256, 520, 1024, 4)])
+def test_gemm_splitk_slabs(native, M, N, K, ns):
+    """gemm_w4c KSPLIT (one persistent launch over ns K-slabs x tiles): slab z == x[:, z-th K range]
+    @ w[:, z-th K range]^T in fp32, and the slab sum vs the fp32 oracle of the whole product."""
+    torch.manual_seed(23)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    P = native.gemm_splitk(x, w, ns)
+    Ks = K // ns
+    for z in (0, ns - 1):
+        ref = x[:, z * Ks:(z + 1) * Ks].float() @ w[:, z * Ks:(z + 1) * Ks].float().t()
+        assert rel_err(P[z].cpu(), ref.cpu()) < 1e-5, z
+    assert rel_err(P.sum(0).cpu(), (x.float() @ w.float().t()).cpu()) < 1e-5
+
+
+def _run_prefill_logits(m, T):
+    from rag_llm_k8s_amd.models.llama import StepInput
+    from rag_llm_k8s_amd.ops.backend import AttnMeta
+    from rag_llm_k8s_amd.ops.native import build_prefill_tiles
+
+    nb = (T + 63) // 64
+    m.allocate_kv_cache(nb + 1)
+    bt = torch.arange(1, nb + 1, dtype=torch.int32).view(1, nb)
+    slots = torch.arange(64, 64 + T, dtype=torch.int32)
+    meta = AttnMeta("prefill", torch.tensor([T], dtype=torch.int32).to(DEV), bt.to(DEV),
+                    cu_q=torch.tensor([0, T], dtype=torch.int32).to(DEV),
+                    tiles=build_prefill_tiles([T], 4, 1).to(DEV), host_kv_lens=[T])
+    g = torch.Generator().manual_seed(4)
+    ids = torch.randint(0, m.cfg.vocab_size, (T,), generator=g, dtype=torch.int32)
+    inp = StepInput(ids.to(DEV), torch.arange(T, dtype=torch.int32).to(DEV), slots.to(DEV), meta, None)
+    return m.forward(inp).float().cpu()
+
+
+def test_prefill_splitk_model_matches_resid_path(native):
+    """Llama prefill with the split-K o_proj / down (fp32 slabs -> add_partials_rmsnorm) == the
+    residual-epilogue path within bf16 rounding (one ~5k-token prompt at 8B widths, 2 layers)."""
+    from rag_llm_k8s_amd.models import llama as L
+    from rag_llm_k8s_amd.ops.backend import AttnMeta, NativeBackend  # noqa: F401
+
+    cfg = L.llama31_8b()
+    cfg.num_hidden_layers = 2
+    cfg.vocab_size = 1024
+    w = L.LlamaWeights.random(cfg, DEV, seed=3)
+    m = L.LlamaModel(cfg, w, DEV, max_positions=8192)
+    T = 5207
+    assert native.prefill_nsplit(T, 4096, 4096) == 2 and native.prefill_nsplit(32768, 4096, 14336) == 1
+    outs = []
+    for split in (False, True):
+        native.PREFILL_SPLITK = split
+        try:
+            outs.append(_run_prefill_logits(m, T))
+        finally:
+            native.PREFILL_SPLITK = True
+    assert rel_err(outs[1], outs[0]) < 2e-2, rel_err(outs[1], outs[0])
+
+
+@pytest.mark.parametrize("kv_lens,target,fp8", [([5200], 512, False), ([70, 3000], 512, False), ([5200, 64], 512, False),
+                                                ([777, 5300, 65, 2000], 512, False), ([4100], 1024, True),
+                                                ([8100], 512, False)])
+def test_gemm_part_merge_matches_reduce_then_part(native, kv_lens, target, fp8):
+    """o_proj fed by the UNMERGED split-K decode attention (attn_decode_rope with defer_merge, the
+    partitions merged per K-slice inside gemm_part_merge) == attn_decode_rope (reduce launch) followed
+    by gemm_part: same slabs up to fp32 summation order (bf16 activation may differ by 1 ulp), and vs an
+    fp32 oracle of the attention output. Covers single-partition rows, mixed lengths, M = 1..4, fp8."""
+    from rag_llm_k8s_amd.ops.fp8 import quantize_weight
+
+    D, Hq, Hkv, S = 128, 32, 8, 8
+    torch.manual_seed(21)
+    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=7)
+    B = len(kv_lens)
+    kc, vc, bt = kc.to(DEV), vc.to(DEV), bt.to(DEV)
+    kvl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    pos = kvl - 1
+    slots = (bt[torch.arange(B, device=DEV), (pos // 64).long()] * 64 + pos % 64).int()
+    P = torch.randn(S, B, (Hq + 2 * Hkv) * D, device=DEV)
+    cos, sin = R.rope_tables(D, 131072, theta=500000.0)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv, target_blocks=target)
+    assert mp > 1
+    w = (torch.randn(4096, Hq * D, device=DEV) / math.sqrt(Hq * D)).bfloat16()
+    wq = quantize_weight(w) if fp8 else w
+    assert native.gemm_part_merge_ok(B, wq, Hq, mp, torch.empty(1))
+    ws_o = torch.empty((B, Hq, mp, D), dtype=torch.float32, device=DEV)
+    ws_ml = torch.empty((B, Hq, mp, 2), dtype=torch.float32, device=DEV)
+    kc2, vc2 = kc.clone(), vc.clone()
+    ref_attn = torch.empty(B, Hq * D, device=DEV).bfloat16()
+    native.attn_decode_rope(P, pos, cos, sin, slots, kc2, vc2, bt, kvl, ref_attn, Hq, Hkv, D, pt, mp)
+    ref = native.gemm_part(ref_attn, wq).sum(0)
+    attn = torch.zeros(B, Hq * D, device=DEV).bfloat16()
+    native.attn_decode_rope(P, pos, cos, sin, slots, kc, vc, bt, kvl, attn, Hq, Hkv, D, pt, mp, ws_o=ws_o,
+                            ws_ml=ws_ml, defer_merge=True)
+    out = native.gemm_part_merge(attn, kvl, pt, mp, ws_o, ws_ml, Hq, wq).sum(0)
+    torch.cuda.synchronize()
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    # the deferred launch leaves multi-partition rows of attn unwritten (zeros here)
+    wd = wq.dequant() if fp8 else w.float()
+    oracle = ref_attn.float() @ wd.t()
+    assert rel_err(ref.cpu(), oracle.cpu()) < 1e-4
+    assert rel_err(out.cpu(), oracle.cpu()) < 2e-3, rel_err(out.cpu(), oracle.cpu())
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (3, 6144, 4096), (4, 1280, 8192), (2, 10240, 8192)])
 def test_gemm_part_norm_matches_rmsnorm_then_part(native, M, N, K):
     """gemm_part_norm (RMSNorm applied while staging the activation slice) == rmsnorm_kernel followed
