@@ -465,6 +465,26 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
   const int* bt = a.block_tables + (size_t)b * a.bt_stride;
 
   bf16x8 qf[C::KS];
+  // Fused-RoPE path: this wave's first KV tile is requested BEFORE the q prologue (K straight to
+  // registers, V to the wave's LDS tile), so its HBM latency overlaps the qkv partial-slab loads instead
+  // of following them -- at batch 1 a wave handles a single tile and the two latencies were in series.
+  // Not for the sequence's last tile: the new token's k / v is appended into it during the prologue.
+  char* sV = smem + wid * C::TILEB;
+  const bool pre = a.qkv_p != nullptr && kt0 + wid_u < kt1 && kt0 + wid_u != n_kt - 1;  // wave-uniform
+  bf16x8 kf0[4][C::KS];
+  if (pre) {
+    const size_t base = ((size_t)bt[kt0 + wid_u] * a.Hkv + kvh) * KT * D;
+    const bf16_t* kb = a.kc + base;
+    const bf16_t* vb = a.vc + base;
+    stage_kv<D, true, NT, 1>(sV, 0, 1, lane, [&](int r) { return vb + (size_t)r * D; });
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s)
+        kf0[t][s] = NT ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D +
+                                                                                   32 * s + 8 * fh))
+                       : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
+  }
   if (a.qkv_p != nullptr) {
     // q = RoPE(bf16(sum_s P[s][b])) for this KV head's G query heads, one (d, d + D/2) rotate_half
     // pair of 8-vectors per thread (G * D/16 threads, all slab loads of a thread in flight together),
@@ -523,24 +543,30 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
 #pragma unroll
   for (int dt = 0; dt < C::DT; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float m_i = -INFINITY, l_i = 0.f;
-  char* sV = smem + wid * C::TILEB;
 
   for (int kt = kt0 + wid_u; kt < kt1; kt += 4) {
-    const size_t base = ((size_t)bt[kt] * a.Hkv + kvh) * KT * D;
-    const bf16_t* kb = a.kc + base;
-    const bf16_t* vb = a.vc + base;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous tile's V reads retired
-    // V tile -> wave-private LDS (transposed reads later)
-    stage_kv<D, true, NT, 1>(sV, 0, 1, lane, [&](int r) { return vb + (size_t)r * D; });
-    // K fragments straight to VGPRs
     bf16x8 kf[4][C::KS];
+    if (pre && kt == kt0 + wid_u) {  // requested before the prologue
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int s = 0; s < C::KS; ++s)
-        kf[t][s] = NT ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D +
-                                                                                  32 * s + 8 * fh))
-                      : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
+        for (int s = 0; s < C::KS; ++s) kf[t][s] = kf0[t][s];
+    } else {
+      const size_t base = ((size_t)bt[kt] * a.Hkv + kvh) * KT * D;
+      const bf16_t* kb = a.kc + base;
+      const bf16_t* vb = a.vc + base;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous tile's V reads retired
+      // V tile -> wave-private LDS (transposed reads later)
+      stage_kv<D, true, NT, 1>(sV, 0, 1, lane, [&](int r) { return vb + (size_t)r * D; });
+      // K fragments straight to VGPRs
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int s = 0; s < C::KS; ++s)
+          kf[t][s] = NT ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D +
+                                                                                    32 * s + 8 * fh))
+                        : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
+    }
     f32x4 s4[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {

@@ -118,11 +118,6 @@ __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), 1) void gemm_pa
   static_assert(PIECES % (PT_THREADS / 64) == 0 && CPR >= 64, "activation slice shape");
   u32x4 hv[NORM ? NR : 1][NV];  // NORM: raw row vectors (tid & 255) + 256 i
   u32x4 gv[NV];
-  f32x4 mg_o[MG ? MG_MAXPP : 1];   // MG: partition records
-  f32x2 mg_ml[MG ? MG_MAXPP : 1];
-  uint2 mg_one;
-  int mg_pg = 0, mg_r = 0, mg_c = 0, mg_half = 0, mg_np = 1;
-  bool mg_act = false;
   if constexpr (NORM) {
     // full rows (vectors tid + 256 i, threads < 256) and gamma for the slice's vectors, issued before
     // the weight stream so the counted wait below retires them first
@@ -139,37 +134,76 @@ __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), 1) void gemm_pa
       gv[i] = *reinterpret_cast<const u32x4*>(gamma + gi);
     }
   } else if constexpr (MG) {
-    // merge waves: partition records of this thread's task (row r, head j of the slice, columns
-    // 4 d4 .. 4 d4 + 3), partitions pg, pg + npg, ... (indices clamped, all loads in flight)
+    // merge waves: the whole merge happens here (these waves stream no weights); tasks (row r, head j
+    // of the slice, columns 4 d4 .. 4 d4 + 3) in rounds of MG_THREADS / npg, partitions pg, pg + npg, ...
+    // of a task on npg adjacent lanes (indices clamped, all loads of a round in flight)
     if (wid >= PT_THREADS / 64) {
-    const int npg = mg_groups(M, KS);
-    const int task = (tid - PT_THREADS) / npg;
-    mg_pg = (tid - PT_THREADS) % npg;
-    mg_act = task < M * (KS / MG_D) * (MG_D / 4);
-    const int tk = mg_act ? task : 0;
-    mg_r = tk / (KS / 4);
-    const int j = (tk / (MG_D / 4)) % (KS / MG_D), d4 = tk % (MG_D / 4);
-    mg_c = j * (MG_D / 8) + d4 / 2;  // 16-B chunk of the slice row; 8-B half d4 & 1
-    mg_half = d4 & 1;
-    const int hq = kbase / MG_D + j;
-    // kv_len of row r: uniform scalar loads (lgkmcnt, not the vector counter), selected per lane
-    int kvl = mg.kv_lens[0];
+      const int npg = mg_groups(M, KS);
+      const int per = MG_THREADS / npg, ntask = M * (KS / 4);
+      const int pg = (tid - PT_THREADS) % npg;
+      for (int t0 = 0; t0 < ntask; t0 += per) {
+        const int task = t0 + (tid - PT_THREADS) / npg;
+        const bool act = task < ntask;
+        const int tk = act ? task : 0;
+        const int r = tk / (KS / 4);
+        const int j = (tk / (MG_D / 4)) % (KS / MG_D), d4 = tk % (MG_D / 4);
+        const int hq = kbase / MG_D + j;
+        // kv_len of row r: uniform scalar loads, selected per lane
+        int kvl = mg.kv_lens[0];
 #pragma unroll
-    for (int rr = 1; rr < MG_MAXR; ++rr) {
-      const int v = mg.kv_lens[min(rr, M - 1)];
-      kvl = mg_r == rr ? v : kvl;
-    }
-    const int n_kt = (kvl + MG_KT - 1) / MG_KT;
-    const int pt = max(mg.part_tiles, (n_kt + mg.max_parts - 1) / mg.max_parts);
-    mg_np = (n_kt + pt - 1) / pt;
-    const size_t pb = ((size_t)mg_r * mg.Hq + hq) * mg.max_parts;
+        for (int rr = 1; rr < MG_MAXR; ++rr) {
+          const int v = mg.kv_lens[min(rr, M - 1)];
+          kvl = r == rr ? v : kvl;
+        }
+        const int n_kt = (kvl + MG_KT - 1) / MG_KT;
+        const int pt = max(mg.part_tiles, (n_kt + mg.max_parts - 1) / mg.max_parts);
+        const int np = (n_kt + pt - 1) / pt;
+        const size_t pb = ((size_t)r * mg.Hq + hq) * mg.max_parts;
+        f32x4 po[MG_MAXPP];
+        f32x2 pml[MG_MAXPP];
 #pragma unroll
-    for (int i = 0; i < MG_MAXPP; ++i) {
-      const int p = min(mg_pg + i * npg, max(mg_np, 1) - 1);
-      mg_o[i] = *reinterpret_cast<const f32x4*>(mg.part_o + (pb + p) * MG_D + 4 * d4);
-      mg_ml[i] = *reinterpret_cast<const f32x2*>(mg.part_ml + (pb + p) * 2);
-    }
-    mg_one = *reinterpret_cast<const uint2*>(mg.out + (size_t)mg_r * mg.out_stride + hq * MG_D + 4 * d4);
+        for (int i = 0; i < MG_MAXPP; ++i) {
+          const int p = min(pg + i * npg, max(np, 1) - 1);
+          po[i] = *reinterpret_cast<const f32x4*>(mg.part_o + (pb + p) * MG_D + 4 * d4);
+          pml[i] = *reinterpret_cast<const f32x2*>(mg.part_ml + (pb + p) * 2);
+        }
+        const uint2 one = *reinterpret_cast<const uint2*>(mg.out + (size_t)r * mg.out_stride + hq * MG_D + 4 * d4);
+        // max-rescaled merge of this lane's partitions, then across the task's npg lanes
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < MG_MAXPP; ++i) mx = pg + i * npg < np ? fmaxf(mx, pml[i][0]) : mx;
+        const float mu = mx == -INFINITY ? 0.f : mx;
+        float l = 0.f;
+        f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < MG_MAXPP; ++i) {
+          const float sc = pg + i * npg < np ? exp2f(pml[i][0] - mu) : 0.f;
+          l += pml[i][1] * sc;
+          o += po[i] * sc;
+        }
+        for (int off = 1; off < npg; off <<= 1) {
+          const float mo = __shfl_xor(mx, off, 64), lo = __shfl_xor(l, off, 64);
+          f32x4 oo;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) oo[e] = __shfl_xor(o[e], off, 64);
+          const float mn = fmaxf(mx, mo);
+          const float sa = mx == -INFINITY ? 0.f : exp2f(mx - mn), sb = mo == -INFINITY ? 0.f : exp2f(mo - mn);
+          l = l * sa + lo * sb;
+          o = o * sa + oo * sb;
+          mx = mn;
+        }
+        if (act && pg == 0) {
+          uint2 v = one;  // single partition: the attention kernel wrote the row itself
+          if (np > 1) {
+            v.x = pk2bf(l > 0.f ? o[0] / l : 0.f, l > 0.f ? o[1] / l : 0.f);
+            v.y = pk2bf(l > 0.f ? o[2] / l : 0.f, l > 0.f ? o[3] / l : 0.f);
+          }
+          const int cc = j * (MG_D / 8) + d4 / 2;  // 16-B chunk of the slice row; 8-B half d4 & 1
+          const int c = (cc & ~15) | ((cc & 15) ^ (r & 15));
+          *reinterpret_cast<uint2*>(smem + r * ROWB + 16 * c + 8 * (d4 & 1)) = v;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
   } else {
 #pragma unroll
@@ -246,44 +280,6 @@ __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), 1) void gemm_pa
           *reinterpret_cast<u32x4*>(smem + r * ROWB + 16 * ((c & ~15) | ((c & 15) ^ (r & 15)))) = pack8(o);
         }
       }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-  if (MG && !wwave) {
-    // online max-rescaled merge of this thread's partitions, then of the npg threads of the task
-    // (adjacent lanes); lane pg 0 writes bf16(O / L) into the swizzled activation slice
-    const int npg = mg_groups(M, KS);
-    float mx = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < MG_MAXPP; ++i) mx = mg_pg + i * npg < mg_np ? fmaxf(mx, mg_ml[i][0]) : mx;
-    const float mu = mx == -INFINITY ? 0.f : mx;
-    float l = 0.f;
-    f32x4 o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int i = 0; i < MG_MAXPP; ++i) {
-      const float sc = mg_pg + i * npg < mg_np ? exp2f(mg_ml[i][0] - mu) : 0.f;
-      l += mg_ml[i][1] * sc;
-      o += mg_o[i] * sc;
-    }
-    for (int off = 1; off < npg; off <<= 1) {
-      const float mo = __shfl_xor(mx, off, 64), lo = __shfl_xor(l, off, 64);
-      f32x4 oo;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) oo[e] = __shfl_xor(o[e], off, 64);
-      const float mn = fmaxf(mx, mo);
-      const float sa = mx == -INFINITY ? 0.f : exp2f(mx - mn), sb = mo == -INFINITY ? 0.f : exp2f(mo - mn);
-      l = l * sa + lo * sb;
-      o = o * sa + oo * sb;
-      mx = mn;
-    }
-    if (mg_act && mg_pg == 0) {
-      uint2 v = mg_one;
-      if (mg_np > 1) {
-        v.x = pk2bf(l > 0.f ? o[0] / l : 0.f, l > 0.f ? o[1] / l : 0.f);
-        v.y = pk2bf(l > 0.f ? o[2] / l : 0.f, l > 0.f ? o[3] / l : 0.f);
-      }
-      const int c = (mg_c & ~15) | ((mg_c & 15) ^ (mg_r & 15));
-      *reinterpret_cast<uint2*>(smem + mg_r * ROWB + 16 * c + 8 * mg_half) = v;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }

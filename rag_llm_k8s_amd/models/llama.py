@@ -40,6 +40,7 @@ DECODE_NORM_FUSED = os.environ.get("RAGK_DECODE_NORM_FUSED", "1") == "1"
 # decode batch <= 4: the o_proj split-K GEMM merges the attention's split-K partitions itself
 # (gemm_part_merge), so the attention's separate merge launch disappears
 DECODE_OPROJ_MERGE = os.environ.get("RAGK_DECODE_OPROJ_MERGE", "1") == "1"
+DECODE_OPROJ_MERGE_MAX_M = int(os.environ.get("RAGK_DECODE_OPROJ_MERGE_MAX_M", "2"))  # batch 4: 2 merge rounds, slower
 
 
 @dataclass
@@ -343,7 +344,7 @@ class LlamaModel:
         fuse_norm = (DECODE_NORM_FUSED and M <= DECODE_DOWN_SKINNY_MAX_M and not pf
                      and be.part_norm_ok(M, layers[0]["wqkv"]))
         xn = None if fuse_norm else be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
-        merge = (DECODE_OPROJ_MERGE and DECODE_ROPE_FUSED and not pf
+        merge = (DECODE_OPROJ_MERGE and DECODE_ROPE_FUSED and not pf and M <= DECODE_OPROJ_MERGE_MAX_M
                  and be.part_merge_ok(M, inp.meta, layers[0]["wo"], Hq, D))
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]

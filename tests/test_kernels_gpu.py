@@ -503,7 +503,7 @@ def test_prefill_splitk_model_matches_resid_path(native):
     assert rel_err(outs[1], outs[0]) < 2e-2, rel_err(outs[1], outs[0])
 
 
-@pytest.mark.parametrize("kv_lens,target,fp8", [([5200], 512, False), ([70, 3000], 512, False), ([5200, 64], 512, False),
+@pytest.mark.parametrize("kv_lens,target,fp8", [([5200], 512, False), ([70, 3000], 256, False), ([5200, 64], 256, False),
                                                 ([777, 5300, 65, 2000], 512, False), ([4100], 1024, True),
                                                 ([8100], 512, False)])
 def test_gemm_part_merge_matches_reduce_then_part(native, kv_lens, target, fp8):
