@@ -88,6 +88,17 @@ def test_bpe_llama3_split_regex_with_specials(rt, corpus, tmp_path):
     texts = TEXTS + [wm.text(200) + " <|eot_id|> tail" for _ in range(10)] + ["<|begin_of_text|>x<|eot_id|>"]
     _check(rt, tok, p, texts)
     _check(rt, tok, p, texts, add_special=False)
+    # long prompts: the front end cuts them at pre-token boundaries and encodes the pieces in parallel
+    from rag_llm_k8s_amd.runtime.tokenizer import Tokenizer as FrontTok
+
+    ft = FrontTok(p, backend="native")
+    longs = [" ".join(TEXTS) * 12, "\n\n".join(wm.text(400) for _ in range(12)) + " <|eot_id|> Question: why?",
+             "x" * 9000, " ".join(["word"] * 3000), "Ünïcödé café " * 700]
+    for t in longs:
+        assert len(t) >= ft.SPLIT_MIN_CHARS
+        for sp in (True, False):
+            assert ft.encode(t, add_special_tokens=sp) == tok.encode(t, add_special_tokens=sp).ids, (t[:40], sp)
+    assert ft._split_ok()
 
 
 def test_wordpiece_bert(rt, corpus, tmp_path):
