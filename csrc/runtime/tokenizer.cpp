@@ -657,8 +657,11 @@ class EncodePool {
     return p;
   }
   int size() const { return (int)threads_.size(); }
-  // run fn(worker_index) on `n` workers and wait
+  // run fn(worker_index) on `n` workers and wait. One job at a time: concurrent callers (server
+  // threads tokenizing long prompts while the batcher encodes) queue on call_mu_ -- the job slot
+  // (job_ / want_ / started_ / done_) is shared by all workers.
   void run(int n, const std::function<void(int)>& fn) {
+    std::lock_guard<std::mutex> one(call_mu_);
     std::unique_lock<std::mutex> lk(mu_);
     job_ = &fn;
     want_ = std::min(n, size());
@@ -703,6 +706,7 @@ class EncodePool {
     }
   }
   std::vector<std::thread> threads_;
+  std::mutex call_mu_;
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(int)>* job_ = nullptr;

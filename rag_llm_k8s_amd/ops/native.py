@@ -307,6 +307,9 @@ def gemm_part(x, w, out=None, ks=None):
 
 
 PREFILL_SPLITK = os.environ.get("RAGK_PREFILL_SPLITK", "1") == "1"
+# measured: M = 5.2k (one RAG prompt) 2 slabs win (o_proj + down 760 -> 656 us per layer); a ~2.2k-token
+# tail step with 4 slabs was no faster than unsplit in the bench profile -> split only M >= 4096, 2 slabs
+PREFILL_SPLITK_MIN_M = int(os.environ.get("RAGK_PREFILL_SPLITK_MIN_M", "4096"))
 _n_cus = [0]
 
 
@@ -324,12 +327,12 @@ def prefill_nsplit(M, N, K):
     the split with the best wave efficiency (tiles / (waves * CUs)), 2 % charged per extra slab for
     the fp32 slab traffic; 1 = no split. M = 5.2k (a C=1 RAG prompt), N = 4096: 336 tiles = 1.31 waves
     (66 %) -> 2 slabs = 2.6 waves (88 %). The 32k-token bench steps (2048 tiles) never split."""
-    if not PREFILL_SPLITK or M < 256:
+    if not PREFILL_SPLITK or M < PREFILL_SPLITK_MIN_M:
         return 1
     cus = _cu_count()
     tiles = -(-M // 256) * -(-N // 256)
     best, best_s = 0.0, 1
-    for s in (1, 2, 4):
+    for s in (1, 2):
         if K % (64 * s) or K // s < 4 * 64:
             continue
         wt = tiles * s

@@ -101,6 +101,43 @@ def test_bpe_llama3_split_regex_with_specials(rt, corpus, tmp_path):
     assert ft._split_ok()
 
 
+def test_encode_batch_concurrent_callers(rt, corpus, tmp_path):
+    """Several Python threads in encode_batch at once (the server tokenizes long prompts on the shared
+    C++ worker pool while the batcher encodes): every caller gets its own correct result."""
+    import threading
+
+    from tokenizers import Tokenizer, decoders, models, pre_tokenizers, trainers
+
+    wm, lines = corpus
+    tok = Tokenizer(models.BPE())
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    tok.train_from_iterator(lines[:20000], trainers.BpeTrainer(vocab_size=2000, show_progress=False,
+                                                               initial_alphabet=pre_tokenizers.ByteLevel.alphabet()))
+    p = str(tmp_path / "bpe.json")
+    tok.save(p)
+    n = rt.Tokenizer(p)
+    batches = [[wm.text(50 + 7 * i + j) for j in range(24)] for i in range(6)]
+    refs = [[e.ids for e in tok.encode_batch(b)] for b in batches]
+    errs = []
+
+    def worker(i):
+        try:
+            for _ in range(20):
+                if n.encode_batch(batches[i], True, 8, -1) != refs[i]:
+                    errs.append(i)
+                    return
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+
+
 def test_wordpiece_bert(rt, corpus, tmp_path):
     from rag_llm_k8s_amd.utils.synthetic import train_wordpiece_tokenizer
 
