@@ -72,7 +72,8 @@ struct MergeArgs {
 };
 constexpr int MG_D = 128;    // head dim
 constexpr int MG_KT = 64;    // keys per KV tile (attention.hip KT)
-constexpr int MG_MAXPP = 16; // partition records loaded per thread
+constexpr int MG_MAXPP = 32; // partition records merged per thread (host check)
+constexpr int MG_CHUNK = 4;  // records in flight per thread
 constexpr int MG_MAXR = 4;   // rows
 // The merge runs on 4 EXTRA waves (threads 512..767) that issue no weight loads: vmcnt is per wave, so
 // the 8 weight-streaming waves issue their whole stream at once as before and never wait behind the
@@ -88,7 +89,7 @@ __host__ __device__ inline int mg_groups(int M, int KS) {
 }
 
 template <int MT, int NKS, bool FP8 = false, int NR = 0, int NV = 1, bool MG = false>
-__global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), 1) void gemm_part_kernel(const bf16_t* __restrict__ X, int ldx,
+__global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), MG ? 2 : 1) void gemm_part_kernel(const bf16_t* __restrict__ X, int ldx,
                                                                   const bf16_t* __restrict__ W, int ldw,
                                                                   float* __restrict__ P, int M, int N, int K,
                                                                   const float* __restrict__ wscale = nullptr,
@@ -159,27 +160,35 @@ __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), 1) void gemm_pa
         const int pt = max(mg.part_tiles, (n_kt + mg.max_parts - 1) / mg.max_parts);
         const int np = (n_kt + pt - 1) / pt;
         const size_t pb = ((size_t)r * mg.Hq + hq) * mg.max_parts;
-        f32x4 po[MG_MAXPP];
-        f32x2 pml[MG_MAXPP];
-#pragma unroll
-        for (int i = 0; i < MG_MAXPP; ++i) {
-          const int p = min(pg + i * npg, max(np, 1) - 1);
-          po[i] = *reinterpret_cast<const f32x4*>(mg.part_o + (pb + p) * MG_D + 4 * d4);
-          pml[i] = *reinterpret_cast<const f32x2*>(mg.part_ml + (pb + p) * 2);
-        }
         const uint2 one = *reinterpret_cast<const uint2*>(mg.out + (size_t)r * mg.out_stride + hq * MG_D + 4 * d4);
-        // max-rescaled merge of this lane's partitions, then across the task's npg lanes
-        float mx = -INFINITY;
-#pragma unroll
-        for (int i = 0; i < MG_MAXPP; ++i) mx = pg + i * npg < np ? fmaxf(mx, pml[i][0]) : mx;
-        const float mu = mx == -INFINITY ? 0.f : mx;
-        float l = 0.f;
+        // online max-rescaled merge of this lane's partitions pg, pg + npg, ... in chunks of MG_CHUNK
+        // records (a chunk's loads in flight together; few registers, so two blocks fit per CU), then
+        // across the task's npg lanes
+        float mx = -INFINITY, l = 0.f;
         f32x4 o = {0.f, 0.f, 0.f, 0.f};
+        const int mine = (np - pg + npg - 1) / npg;  // partitions of this lane
+        for (int c0 = 0; c0 < mine; c0 += MG_CHUNK) {
+          f32x4 po[MG_CHUNK];
+          f32x2 pml[MG_CHUNK];
 #pragma unroll
-        for (int i = 0; i < MG_MAXPP; ++i) {
-          const float sc = pg + i * npg < np ? exp2f(pml[i][0] - mu) : 0.f;
-          l += pml[i][1] * sc;
-          o += po[i] * sc;
+          for (int i = 0; i < MG_CHUNK; ++i) {
+            const int p = min(pg + (c0 + i) * npg, np - 1);
+            po[i] = *reinterpret_cast<const f32x4*>(mg.part_o + (pb + p) * MG_D + 4 * d4);
+            pml[i] = *reinterpret_cast<const f32x2*>(mg.part_ml + (pb + p) * 2);
+          }
+          float cm = mx;
+#pragma unroll
+          for (int i = 0; i < MG_CHUNK; ++i) cm = c0 + i < mine ? fmaxf(cm, pml[i][0]) : cm;
+          const float sa = mx == -INFINITY ? 0.f : exp2f(mx - cm);  // cm finite: chunk has a valid record
+          l *= sa;
+          o *= sa;
+#pragma unroll
+          for (int i = 0; i < MG_CHUNK; ++i) {
+            const float sc = c0 + i < mine ? exp2f(pml[i][0] - cm) : 0.f;
+            l += pml[i][1] * sc;
+            o += po[i] * sc;
+          }
+          mx = cm;
         }
         for (int off = 1; off < npg; off <<= 1) {
           const float mo = __shfl_xor(mx, off, 64), lo = __shfl_xor(l, off, 64);
