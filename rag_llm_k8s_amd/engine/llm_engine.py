@@ -20,8 +20,8 @@ Here:
 from __future__ import annotations
 
 import itertools
-import os
 import logging
+import os
 import threading
 import time
 from collections import deque
@@ -35,6 +35,9 @@ from ..models.llama import StepInput
 from ..ops.backend import AttnMeta
 from ..utils import faults
 from .kv_manager import BLOCK, make_block_manager
+
+SMALL_BATCH_TOPK_MAX_B = int(os.environ.get("RAGK_TOPK_SMALL_B", "0"))  # off: see docs/PERF_NOTES.md
+SMALL_BATCH_TOPK_CHUNK = int(os.environ.get("RAGK_TOPK_SMALL_CHUNK", "4096"))
 
 log = logging.getLogger(__name__)
 
@@ -428,6 +431,10 @@ class LLMEngine:
         # and all ranks' candidates together fit the sampler's 2048-entry merge
         from ..ops.native import topk_chunks
         chunks = topk_chunks(logits.shape[1], self.K, min(512, 2048 // self.tp_size))
+        if logits.shape[0] <= SMALL_BATCH_TOPK_MAX_B:
+            # small decode batch: 7 workgroups of ~18k logits each left the top-k latency-bound (25 us
+            # at batch 1); ~4k-entry chunks use ~31 CUs and the sampler merges up to 2048 candidates
+            chunks = max(1, min(logits.shape[1] // SMALL_BATCH_TOPK_CHUNK, (2048 // self.tp_size) // self.K, 64))
         cv, ci = be.topk_candidates(lg.contiguous() if not lg.is_contiguous() else lg, self.K,
                                     vocab_offset=w.vocab_offset, chunks=chunks)
         if self.tp_size > 1:
