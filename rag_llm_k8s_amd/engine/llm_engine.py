@@ -62,8 +62,12 @@ class Sequence:
 
     def __init__(self, prompt_ids, params: SamplingParams, seed: int):
         self.id = next(Sequence._ids)
-        self.prompt = list(prompt_ids)
-        self.prompt_np = np.asarray(self.prompt, dtype=np.int32)  # vectorised prefill input building
+        if isinstance(prompt_ids, np.ndarray):  # int32 buffers (TP admission broadcast)
+            self.prompt_np = np.ascontiguousarray(prompt_ids, dtype=np.int32)
+            self.prompt = self.prompt_np.tolist()
+        else:
+            self.prompt = list(prompt_ids)
+            self.prompt_np = np.asarray(self.prompt, dtype=np.int32)  # vectorised prefill input building
         self.out: List[int] = []
         self.params = params
         self.seed = seed
@@ -386,16 +390,19 @@ class LLMEngine:
         w = self.model.w
         lg = logits[:, :w.vocab_valid].float().contiguous()
         if self.tp_size > 1:
-            parts = [torch.empty_like(lg) for _ in range(self.tp_size)]
+            import torch.distributed as dist
+
+            # every rank contributes its FULL (padded) shard width -- the last shard is narrower when
+            # vocab_size % tp != 0, and collectives need equal sizes -- with -inf in the pad columns;
+            # the concatenation is then cut back to vocab_size
+            lp = logits.float().clone()
+            lp[:, w.vocab_valid:] = float("-inf")
             if lg.is_cuda and self.comm is not None and self.comm.ipc is None:
-                import torch.distributed as dist
-                dist.all_gather(parts, lg, group=self.tp_group)
-            else:  # pad shards to equal width host-side (gloo / peer-mapped ranks)
-                import torch.distributed as dist
+                parts = [torch.empty_like(lp) for _ in range(self.tp_size)]
+                dist.all_gather(parts, lp.contiguous(), group=self.tp_group)
+            else:  # host-side over the gloo group (CPU / peer-mapped ranks)
                 grp = getattr(self.comm, "cpu_group", None) or self.tp_group
-                full_w = logits.shape[1]
-                lp = torch.full((lg.shape[0], full_w), float("-inf"))
-                lp[:, :lg.shape[1]] = lg.cpu()
+                lp = lp.cpu()
                 parts = [torch.empty_like(lp) for _ in range(self.tp_size)]
                 dist.all_gather(parts, lp, group=grp)
             lg = torch.cat([p.cpu() for p in parts], 1)[:, :self.model.cfg.vocab_size]

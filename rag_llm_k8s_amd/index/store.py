@@ -55,6 +55,7 @@ class DocumentStore:
         self._mtimes = None
         self.recovered = None
         self._dirty = False
+        self._writing = 0  # snapshot writes in flight (their file replacements are not "other writers")
         self._persister = None
         self._persist_error = None
 
@@ -144,36 +145,52 @@ class DocumentStore:
         if self.sharded:  # a reload would have to be collective; shards change only through ingest jobs
             return
         m = self._disk_mtimes()
-        if m is not None and self._mtimes is not None and m != self._mtimes:
-            with self._wlock:
-                try:
-                    self.load()
-                except Exception as e:  # keep serving the resident snapshot; retry on the next change
-                    log.warning("index on disk changed but is unreadable (%s); keeping the resident copy", e)
-                    self._mtimes = m
+        if m is None or self._mtimes is None or m == self._mtimes:
+            return
+        with self._wlock:
+            # Our own snapshot writer replaces the files outside the lock: while it runs (or while
+            # appends are waiting for it) the disk lags HBM, and reloading would drop those appends.
+            if self._writing or self._dirty:
+                return
+            m = self._disk_mtimes()  # re-check under the lock: a write may have finished meanwhile
+            if m is None or m == self._mtimes:
+                return
+            try:
+                self.load()
+            except Exception as e:  # keep serving the resident snapshot; retry on the next change
+                log.warning("index on disk changed but is unreadable (%s); keeping the resident copy", e)
+                self._mtimes = m
 
     def _snapshot(self):
         """(index writer, metadata copy) of the current state; caller holds _wlock."""
         return self.index.snapshot_writer(), list(self.metadata)
 
     def _write(self, writer, meta):
-        writer(self.index_file)
-        if self.persist_meta:
-            save_metadata(self.meta_path, meta)
-        self._mtimes = self._disk_mtimes()
+        """Write a snapshot. The caller registered it in _writing under _wlock; the mtimes the store
+        itself produced are recorded under the lock, so maybe_reload never mistakes them for another
+        writer's files."""
+        try:
+            writer(self.index_file)
+            if self.persist_meta:
+                save_metadata(self.meta_path, meta)
+        finally:
+            with self._wlock:
+                self._mtimes = self._disk_mtimes()
+                self._writing -= 1
 
     def persist(self):
         """Synchronous snapshot (startup / directory ingest / shutdown)."""
         with self._wlock:
             writer, meta = self._snapshot()
             self._dirty = False
+            self._writing += 1
             self._write(writer, meta)
 
     def persist_async(self):
         """Schedule a background snapshot; appends made meanwhile are folded into the same write."""
         with self._wlock:
             self._dirty = True
-            if self._persister is None or not self._persister.is_alive():
+            if self._persister is None:  # cleared under the lock by the writer when it exits
                 self._persister = threading.Thread(target=self._persist_loop, name="index-snapshot", daemon=True)
                 self._persister.start()
 
@@ -181,9 +198,13 @@ class DocumentStore:
         while True:
             with self._wlock:
                 if not self._dirty:
+                    # deregister while still holding the lock: an add() after this point sees
+                    # _persister None and starts a new writer (no lost wake-up)
+                    self._persister = None
                     return
                 self._dirty = False
                 writer, meta = self._snapshot()  # host copy under the lock (consistent vectors + metadata)
+                self._writing += 1
             try:
                 self._write(writer, meta)  # file I/O outside the lock: searches and appends continue
             except Exception as e:  # keep serving from HBM; the next append retries the snapshot
@@ -199,6 +220,7 @@ class DocumentStore:
             if self._dirty:
                 writer, meta = self._snapshot()
                 self._dirty = False
+                self._writing += 1
                 self._write(writer, meta)
 
     # ------------------------------------------------------------------ writes

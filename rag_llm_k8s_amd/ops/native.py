@@ -30,14 +30,9 @@ def _bf16_2d(t, name):
 PP_MIN_M = int(os.environ.get("RAGK_PP_MIN_M", "1024"))
 PP_VARIANT = int(os.environ.get("RAGK_PP_VARIANT", "2"))
 # large-M kernel: "w4" (default) = 4-wave 128x128-per-wave (gemm_w4.hip, path 6), "pp" = 8-wave
-# ping-pong (path 2). hipBLASLt is a yardstick only, never on the default path: "auto" (A/B tooling)
-# sends a plain (epi none) or residual-add GEMM to hipBLASLt (path 7) when it measured faster, timed
-# once per (N, K, epi, M bucket) at the first call with M >= BLASLT_MIN_M; "blaslt" always does.
+# ping-pong (path 2). Library GEMMs (hipBLASLt) are never dispatched from here: they are the
+# yardstick of tools/gemm_probe.py / tools/blaslt_choice.py only.
 PREFILL_GEMM = os.environ.get("RAGK_PREFILL_GEMM", "w4")
-BLASLT_MIN_M = int(os.environ.get("RAGK_BLASLT_MIN_M", "8192"))
-BLASLT_MARGIN = float(os.environ.get("RAGK_BLASLT_MARGIN", "0.03"))  # required relative win
-_blaslt_choice = {}  # (N, K, epi) -> bool (hipBLASLt measured faster)
-_blaslt_times = {}  # (N, K, epi) -> (M, w4 ms, hipBLASLt ms) of that measurement
 _pp_variant_set = [None]
 
 
@@ -140,17 +135,11 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
         rows = w.shape[0]
         # gemm_w4 addresses operands with 32-bit buffer offsets
         fits = x.stride(0) * M * 2 < 2 ** 31 and w.stride(0) * rows * 2 < 2 ** 31
-        path = 6 if (PREFILL_GEMM in ("w4", "auto", "blaslt") and fits) else 2
-        if (PREFILL_GEMM in ("auto", "blaslt") and epi in ("none", "resid") and not out_f32 and M >= BLASLT_MIN_M
-                and _prefer_blaslt(x, w, resid, epi, out, fits)):
-            path = 7
+        path = 6 if (PREFILL_GEMM == "w4" and fits) else 2
     if path is None and STREAM_DEFAULT and use_stream(M, N, K, epi):
         path = 5
     if path is None and DEC_DEFAULT and use_dec(M, N, K, epi):
         path = 4
-    if path == 7:
-        _gemm_blaslt(x, w, resid, epi, out)
-        return out
     if path == 5:
         rc = _gemm_stream(x, w, None, out, bias, resid, ldr, M, N, K, epi, e, out_f32)
     elif path == 4:
@@ -178,63 +167,6 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
                               out.stride(0), ptr(bias), ptr(resid), ldr, M, N, K, e, stream_ptr())
     check(rc, "ragk_gemm")
     return out
-
-
-def _gemm_blaslt(x, w, resid, epi, out):
-    """Plain library GEMM through hipBLASLt (torch.mm / addmm on ROCm): out = x @ w^T (+ resid with
-    beta = 1, in place when out is resid). fp32 accumulation, one bf16 rounding, as the w4 epilogue."""
-    if epi == "resid":
-        torch.addmm(resid, x, w.t(), out=out)
-    else:
-        torch.mm(x, w.t(), out=out)
-
-
-def _prefer_blaslt(x, w, resid, epi, out, w4_ok):
-    """Measured once per (N, K, epi) on this GPU: is hipBLASLt faster than gemm_w4 on this shape by
-    more than BLASLT_MARGIN? Timed on scratch outputs (an in-place residual GEMM must not run twice),
-    interleaved, median of 5 (`tools/blaslt_choice.py` prints the choice on the Llama-8B shapes)."""
-    if PREFILL_GEMM == "blaslt":
-        return True
-    if not w4_ok:
-        return True
-    key = (w.shape[0], w.shape[1], epi, max(0, int(x.shape[0]).bit_length() - 1))  # M bucket: power of 2
-    hit = _blaslt_choice.get(key)
-    if hit is not None:
-        return hit
-    M, N = x.shape[0], out.shape[1]
-    o = torch.empty((M, N), dtype=out.dtype, device=out.device)
-    r = resid.clone() if epi == "resid" else None
-    L = _lib.lib()
-
-    def w4():
-        check(L.ragk_gemm_w4(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), o.data_ptr(), o.stride(0), 0,
-                             ptr(r), r.stride(0) if r is not None else 0, M, N, x.shape[1], EPI[epi], 0,
-                             stream_ptr()), "ragk_gemm_w4")
-
-    def lt():
-        _gemm_blaslt(x, w, r, epi, o)
-
-    ts = {0: [], 1: []}
-    for _ in range(2):
-        for fn in (w4, lt):
-            fn()
-    for _ in range(5):
-        for i, fn in enumerate((w4, lt)):
-            a, b = torch.cuda.Event(True), torch.cuda.Event(True)
-            a.record()
-            fn()
-            b.record()
-            b.synchronize()
-            ts[i].append(a.elapsed_time(b))
-    t4, tl = sorted(ts[0])[2], sorted(ts[1])[2]
-    _blaslt_choice[key] = tl < t4 * (1.0 - BLASLT_MARGIN)
-    _blaslt_times[key] = (M, t4, tl)
-    import logging
-
-    logging.getLogger(__name__).info("prefill GEMM N=%d K=%d epi=%s M=%d: gemm_w4 %.1f us, hipBLASLt %.1f us -> %s",
-                                     N, x.shape[1], epi, M, t4 * 1e3, tl * 1e3,
-                                     "hipBLASLt" if _blaslt_choice[key] else "gemm_w4")
-    return _blaslt_choice[key]
 
 
 PART_MIN_BLOCKS = int(os.environ.get("RAGK_PART_MIN_BLOCKS", "512"))

@@ -7,7 +7,11 @@ the same record, add the same sequences in the same order and step. All GPU-side
 all-reduces per layer, top-k candidate all-gather) runs over xGMI inside the step.
 
 Control record = fixed 16-byte header (kind, payload bytes) + a payload only when there is
-something to admit (the pickled request list). Two transports:
+something to admit or to abort: the new requests (prompt ids as one int32 buffer, params, seed,
+and rank 0's key of the sequence) and the keys of sequences to abort. Every rank applies the
+aborts at the start of the same step, so a timed-out request frees its KV blocks everywhere
+(the reference fails such a request with a 500, /root/reference/llm/rag.py:179-181). Two
+transports:
 * ``ShmChannel`` (default when every TP rank is on this host, i.e. one xGMI node): a POSIX
   shared-memory mailbox; rank 0 writes payload then header then bumps a sequence word, followers
   poll it (spin briefly, then back off) and acknowledge. A step with nothing to admit costs a few
@@ -186,9 +190,23 @@ def make_channel(cpu_group, rank, world, src=0):
     return GlooChannel(cpu_group, src)
 
 
-def _encode(seqs):
-    return pickle.dumps([(s.prompt, dataclasses.asdict(s.params), s.seed) for s in seqs],
-                        protocol=pickle.HIGHEST_PROTOCOL)
+def _encode(seqs, aborts=()):
+    """Step record payload: new sequences (key, int32 prompt buffer, params, seed) + abort keys."""
+    new = [(s.id, np.asarray(s.prompt, dtype=np.int32).tobytes(), dataclasses.asdict(s.params), s.seed)
+           for s in seqs]
+    return pickle.dumps((new, list(aborts)), protocol=pickle.HIGHEST_PROTOCOL)
+
+
+def _decode(payload):
+    if not payload:
+        return [], []
+    new, aborts = pickle.loads(payload)
+    out = []
+    for key, ids, params, seed in new:
+        p = dict(params)
+        p["stop_token_ids"] = tuple(p.get("stop_token_ids", ()))
+        out.append((key, np.frombuffer(ids, dtype=np.int32), SamplingParams(**p), seed))
+    return out, aborts
 
 
 class TPControl:
@@ -202,6 +220,7 @@ class TPControl:
             channel = make_channel(cpu_group, dist.get_rank(cpu_group), world, src_rank)
         self.chan = channel
         self.pending = []
+        self.aborts = []
         self.lock = threading.Lock()
         self.last_publish = time.time()
 
@@ -209,15 +228,29 @@ class TPControl:
         with self.lock:
             self.pending.append(seq)
 
+    def abort(self, seq: Sequence):
+        """Cancel a sequence on every TP rank (request timeout). Not yet published: dropped here;
+        published: its key rides on the next step record and every rank aborts it at that step."""
+        with self.lock:
+            if seq in self.pending:
+                self.pending.remove(seq)
+                seq.status, seq.finish_reason, seq.t_done = 2, "abort", time.perf_counter()
+                seq.done.set()
+                return
+            self.aborts.append(seq)
+
     def has_pending(self):
         with self.lock:
-            return bool(self.pending)
+            return bool(self.pending) or bool(self.aborts)
 
     def publish_step(self, engine):
         with self.lock:
             new, self.pending = self.pending, []
-        self.chan.send(K_STEP, _encode(new) if new else b"")
+            ab, self.aborts = self.aborts, []
+        self.chan.send(K_STEP, _encode(new, [s.id for s in ab]) if (new or ab) else b"")
         self.last_publish = time.time()
+        for s in ab:
+            engine.abort(s)
         for s in new:
             engine.add_sequence(s)
 
@@ -242,6 +275,7 @@ def follow(engine, cpu_group, src_rank=0, channel=None, jobs=None):
     `jobs`: name -> callable(args), the same functions rank 0's engine loop runs (RagService.job_fns)."""
     if channel is None:
         channel = make_channel(cpu_group, dist.get_rank(cpu_group), dist.get_world_size(cpu_group), src_rank)
+    live, key_of = {}, {}  # rank 0's sequence key <-> this rank's mirror (for aborts)
     try:
         while True:
             kind, payload = channel.recv()
@@ -256,11 +290,17 @@ def follow(engine, cpu_group, src_rank=0, channel=None, jobs=None):
             hang = faults.value("comm_hang_s")
             if hang:  # fault injection: this rank stalls, rank 0's collectives wait (watchdog path)
                 time.sleep(float(hang))
-            for prompt, params, seed in (pickle.loads(payload) if payload else []):
-                p = dict(params)
-                p["stop_token_ids"] = tuple(p.get("stop_token_ids", ()))
-                engine.add_request(prompt, SamplingParams(**p), seed=seed)
-            engine.step()
+            new, aborts = _decode(payload)
+            for key in aborts:
+                s = live.pop(key, None)
+                if s is not None:
+                    key_of.pop(id(s), None)
+                    engine.abort(s)
+            for key, prompt, params, seed in new:
+                s = engine.add_request(prompt.tolist(), params, seed=seed)
+                live[key], key_of[id(s)] = s, key
+            for s in engine.step():
+                live.pop(key_of.pop(id(s), None), None)
     finally:
         channel.close()
 

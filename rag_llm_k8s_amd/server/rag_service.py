@@ -21,6 +21,7 @@ import sys
 import threading
 import time
 
+import numpy as np
 import torch
 
 from ..engine.llm_engine import SamplingParams
@@ -32,36 +33,33 @@ from ..utils.metrics import Trace
 log = logging.getLogger(__name__)
 
 
-def _tp_bcast_prompts(comm, rows, id_lists, seeds):
-    """TP leader -> every TP rank: row indices, token ids and seeds of the prompts to queue
-    (int tensors over the TP gloo group; no pickling)."""
+def _tp_bcast_prompts(comm, rows, flat_ids, lens, seeds):
+    """TP leader -> every TP rank: row indices, token ids and seeds of the prompts to queue, as int
+    buffers over the TP gloo group (no pickling, no per-token Python). flat_ids / lens: the leader's
+    encode_batch_flat() output. Returns (rows, [int32 prompt arrays], seeds)."""
     import torch.distributed as dist
 
     grp = comm.cpu_group if comm.cpu_group is not None else comm.group
     src = dist.get_global_rank(grp, 0) if grp is not None else 0
     if comm.rank == 0:
-        lens = [len(x) for x in id_lists]
-        hdr = torch.tensor([len(rows), sum(lens)], dtype=torch.int64)
+        hdr = torch.tensor([len(rows), int(flat_ids.shape[0])], dtype=torch.int64)
     else:
         hdr = torch.zeros(2, dtype=torch.int64)
     dist.broadcast(hdr, src=src, group=grp)
     nr, nt = int(hdr[0]), int(hdr[1])
     if comm.rank == 0:
-        meta = torch.tensor([rows, lens, seeds], dtype=torch.int64).reshape(3, nr)
-        flat = torch.tensor([t for x in id_lists for t in x], dtype=torch.int32)
+        meta = torch.from_numpy(np.stack([np.asarray(rows, dtype=np.int64), np.asarray(lens, dtype=np.int64),
+                                          np.asarray(seeds, dtype=np.int64)]).reshape(3, nr))
+        flat = torch.from_numpy(np.ascontiguousarray(flat_ids, dtype=np.int32))
     else:
         meta = torch.zeros((3, nr), dtype=torch.int64)
         flat = torch.zeros(nt, dtype=torch.int32)
     dist.broadcast(meta, src=src, group=grp)
     if nt:
         dist.broadcast(flat, src=src, group=grp)
-    rows, lens, seeds = (meta[i].tolist() for i in range(3))
-    out, off = [], 0
-    fl = flat.tolist()
-    for n_ in lens:
-        out.append(fl[off:off + n_])
-        off += n_
-    return rows, out, seeds
+    m = meta.numpy()
+    out = np.split(flat.numpy(), np.cumsum(m[1])[:-1]) if nr else []
+    return m[0].tolist(), out, m[2].tolist()
 
 
 class _Job:
@@ -100,7 +98,11 @@ class EngineLoop(threading.Thread):
             self.jobs.append(job)
             self.cv.notify()
         if not job.done.wait(timeout):
-            raise TimeoutError("collective job %s not run within %ss" % (name, timeout))
+            with self.cv:  # not started yet: withdraw it, so the client's failure means "not done"
+                if job in self.jobs:
+                    self.jobs.remove(job)
+                    raise TimeoutError("collective job %s not run within %ss (withdrawn)" % (name, timeout))
+            raise TimeoutError("collective job %s still running after %ss" % (name, timeout))
         if job.error is not None:
             raise job.error
         return job.result
@@ -350,7 +352,10 @@ class RagService:
         return self.tok.decode(list(prompt_ids) + list(out_ids), skip_special_tokens=True)
 
     def _prompt_ids(self, full_prompt, ids=None):
-        ids = self.tok.encode(full_prompt, add_special_tokens=True) if ids is None else list(ids)
+        if ids is None:
+            ids = self.tok.encode(full_prompt, add_special_tokens=True)
+        elif not isinstance(ids, np.ndarray):
+            ids = list(ids)
         limit = self.engine.max_model_len - self.params.max_new_tokens
         if len(ids) > limit:
             if self.cfg.truncate_prompt != "left":
@@ -375,10 +380,14 @@ class RagService:
         metrics.inc("prompt_tokens", len(ids))
         s = self.loop.submit(ids, params or self.params, seed=self._next_seed())
         if not s.done.wait(timeout=self.cfg.request_timeout_s):
-            if self.loop.control is None:  # TP: followers mirror admissions only; the sequence runs out
+            if self.loop.control is None:
                 self.engine.abort(s)
+            else:  # TP: every rank aborts it at the same step boundary
+                self.loop.control.abort(s)
+                with self.loop.cv:
+                    self.loop.cv.notify()
             metrics.inc("timeouts")
-            raise TimeoutError("generation timed out after %.0fs" % self.cfg.request_timeout_s)
+            raise TimeoutError("generation timed out after %gs" % self.cfg.request_timeout_s)
         if s.finish_reason == "error":
             raise RuntimeError("generation engine failed: %r" % (self.loop.error,))
         tr.add("queue+prefill", (s.t_first or s.t_done) - s.t_arrive)
@@ -434,8 +443,10 @@ class RagService:
 
         rest, err = None, []
         if tp:
-            id_lists = self.tok.encode_batch([fulls[i] for i in rows], add_special_tokens=True) if lead else None
-            rows, id_lists, sd = _tp_bcast_prompts(comm, rows, id_lists, [seed_of[i] for i in rows] if lead else None)
+            flat, lens = (self.tok.encode_batch_flat([fulls[i] for i in rows], add_special_tokens=True)
+                          if lead else (None, None))
+            rows, id_lists, sd = _tp_bcast_prompts(comm, rows, flat, lens,
+                                                   [seed_of[i] for i in rows] if lead else None)
             seed_of = dict(zip(rows, sd))
             submit(rows, id_lists)
         else:

@@ -76,33 +76,20 @@ def test_gemm_w4_cont_matches_tile_kernel(native):
         assert torch.equal(a, b)
 
 
-def test_gemm_blaslt_path_and_auto_choice(native):
-    """Path 7 (hipBLASLt for plain / residual prefill GEMMs), in place on the residual as the model
-    calls it, and the measured w4-vs-hipBLASLt choice: correct whichever kernel wins."""
+def test_gemm_large_m_routes_to_w4(native):
+    """Large-M prefill GEMMs run on the hand-written gemm_w4 (no library GEMM in the product dispatch):
+    the default route equals an explicit path-6 call bit for bit."""
     torch.manual_seed(21)
     M, N, K = 8192 + 17, 1024, 512
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
     r = torch.randn(M, N, device=DEV).bfloat16()
-    ref = x.float() @ w.float().t()
-    assert rel_err(native.gemm(x, w, path=7), ref) < 1e-2
+    assert native.PREFILL_GEMM == "w4"
+    assert not hasattr(native, "_gemm_blaslt")
     h = r.clone()
-    native.gemm(x, w, resid=h, epi="resid", out=h, path=7)
-    assert rel_err(h, ref + r.float()) < 1e-2
-    assert native.PREFILL_GEMM == "w4"  # default route: hand-written kernel only, never hipBLASLt
-    native._blaslt_choice.clear()
-    native.gemm(x, w, resid=r.clone(), epi="resid", out=torch.empty_like(r))
-    assert not native._blaslt_choice
-    old = native.PREFILL_GEMM
-    native.PREFILL_GEMM = "auto"  # A/B tooling: measured choice
-    try:
-        h = r.clone()
-        native.gemm(x, w, resid=h, epi="resid", out=h)  # times both on scratch, then runs the winner once
-        assert (N, K, "resid", 13) in native._blaslt_choice
-        assert rel_err(h, ref + r.float()) < 1e-2
-        assert rel_err(native.gemm(x, w), ref) < 1e-2
-    finally:
-        native.PREFILL_GEMM = old
+    native.gemm(x, w, resid=h, epi="resid", out=h)
+    assert torch.equal(h, native.gemm(x, w, resid=r, epi="resid", path=6))
+    assert rel_err(h, x.float() @ w.float().t() + r.float()) < 1e-2
 
 
 def _check_pingpong(native, M, N, K, path=2):

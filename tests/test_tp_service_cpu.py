@@ -143,3 +143,76 @@ def test_tp_service_dp_ingest_and_sharded_index(assets, sharded):
 
 
 test_tp_service_dp_ingest_and_sharded_index.contexts = {}
+
+
+def _abort_worker(rank, port, d, root, pdfs):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    import time
+
+    from rag_llm_k8s_amd.config import RagConfig
+    from rag_llm_k8s_amd.parallel.comm import TPComm
+    from rag_llm_k8s_amd.parallel.dist import init_distributed
+    from rag_llm_k8s_amd.parallel.tp import TPControl, follow, make_channel
+    from rag_llm_k8s_amd.server.app import create_app
+    from rag_llm_k8s_amd.server.builder import build_service
+    from rag_llm_k8s_amd.utils import faults
+
+    ctx = init_distributed(tp=WORLD, backend="gloo")
+    res = {}
+    try:
+        cfg = RagConfig(model_path=root, index_path=os.path.join(d, "faiss_index"), pdf_dir=pdfs,
+                        embed_model=os.path.join(root, "minilm"), device="cpu", max_new_tokens=300, max_model_len=1024,
+                        max_batch=4, use_cuda_graphs=False, kv_cache_blocks=64, seed=1, retrieve_k=3, context_k=2,
+                        request_timeout_s=0.5, ignore_eos=True)
+        comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, "cpu", ctx.tp_cpu_group)
+        chan = make_channel(ctx.tp_cpu_group, ctx.tp_rank, ctx.tp)
+        control = TPControl(ctx.tp_cpu_group, channel=chan) if rank == 0 else None
+        svc = build_service(cfg, start_threads=(rank == 0), tp_rank=ctx.tp_rank, tp_size=ctx.tp, comm=comm,
+                            tp_group=ctx.tp_group, control=control)
+        free0 = svc.engine.bm.free_blocks()
+        if rank != 0:
+            follow(svc.engine, ctx.tp_cpu_group, channel=chan, jobs=svc.job_fns())
+        else:
+            svc.store.ensure_exists()
+            svc.ingest_directory()
+            svc.ready = True
+            c = create_app(svc).test_client()
+            faults.set_faults("step_delay_ms=50")
+            r = c.post("/generate", json={"prompt": "what do the documents say about w17"})
+            res["status"], res["body"] = r.status_code, r.get_json()
+            # steps stay slow: running the sequence out (300 x 50 ms) would miss this deadline
+            deadline = time.time() + 8
+            while time.time() < deadline and (svc.engine.has_work() or svc.engine.bm.free_blocks() != free0):
+                time.sleep(0.05)
+            faults.set_faults("")
+            res["health"] = c.get("/healthz").status_code
+            from rag_llm_k8s_amd.engine.llm_engine import SamplingParams
+
+            # the server still serves after the abort
+            out = svc.generate("w3", params=SamplingParams(max_new_tokens=2, ignore_eos=True))
+            res["after"] = 200 if "generated_text" in out else 500
+            svc.shutdown()
+            svc.loop.join(30)
+        res["free"] = (svc.engine.bm.free_blocks(), free0)
+        res["has_work"] = svc.engine.has_work()
+        res["decode_tokens"] = svc.engine.stats["decode_tokens"]
+    finally:
+        torch.save(res, os.path.join(d, "a%d.pt" % rank))
+        dist.destroy_process_group()
+
+
+def test_tp_request_timeout_aborts_on_every_rank(assets):
+    """A timed-out TP request is aborted on every rank at the same step boundary (control-channel
+    abort record) and both ranks' KV block managers return to full."""
+    root, pdfs = assets
+    port = _free_port()
+    d = tempfile.mkdtemp()
+    mp.spawn(_abort_worker, args=(port, d, root, pdfs), nprocs=WORLD, join=True)
+    r0, r1 = [torch.load(os.path.join(d, "a%d.pt" % r), weights_only=False) for r in range(WORLD)]
+    assert r0["status"] == 500 and "timed out" in r0["body"]["error"]
+    assert r0["health"] == 200 and r0["after"] == 200
+    for r in (r0, r1):
+        assert r["free"][0] == r["free"][1] and not r["has_work"]
+        assert r["decode_tokens"] < 150  # aborted, not run out to max_new_tokens
