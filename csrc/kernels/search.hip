@@ -1,190 +1,285 @@
 // Exact squared-L2 k-nearest-neighbour search for gfx950 (faiss IndexFlatL2
-// semantics: squared distances, ascending, missing results = (-1, FLT_MAX)).
+// semantics: squared distances, ascending, ties -> lower id, missing results = (-1, FLT_MAX)).
 // Reference: faiss index.search at /root/reference/llm/rag.py:116.
 //
-// The database stays resident in HBM in a COLUMN-major layout xt[d][cap]
-// (cap = row capacity), so a block's 256 threads read 256 consecutive rows of one
-// dimension per load: fully coalesced, no LDS for the data. Queries are staged in
-// LDS and broadcast. Distances are computed directly as sum((x - q)^2) in fp32
-// (faiss' exact path for small query batches), then:
-//   1. l2_block_topk: per (row block, query group) -> top-k per query (bitonic in LDS)
-//   2. topk_merge:    repeatedly merges 64 partial lists per query until one remains.
-// IVF-Flat scans reuse the same kernels over an inverted-list ordered layout
-// (list rows are contiguous) with per-(query, probe) row ranges.
+// The database stays resident in HBM in a COLUMN-major layout xt[d][cap] (cap = row
+// capacity): lane l of a wave reads row r0 + l of one dimension per load, 256 contiguous
+// bytes per wave instruction, no LDS for the data. Queries are staged in LDS in 256-dim
+// chunks and read as broadcasts. Distances are sum((x - q)^2) in fp32 (faiss' exact path).
+//
+// Top-k without sorting the scanned rows: every wave keeps a RUNNING sorted top-64 list per
+// query in its lanes (lane j = j-th best). A tile of 64 fresh distances (one per lane) is
+// skipped outright when none beats the current k-th best (after the first few tiles almost
+// all of them); otherwise it is bitonic-sorted across the lanes (21 shuffle steps) and merged
+// into the running list (min against the reversed list + 6 bitonic-merge steps).
+//   l2_scan:   grid (row-tile groups, query groups); each block loops over its row tiles and
+//              emits one sorted top-k per query -> partial lists [nq][G][k]
+//   ivf_scan:  the same per (query, probe): the probed inverted list's row range
+//   topk_lists_merge: one block per query merges the G sorted lists with the same wave
+//              machinery (64 candidates per step, skip test first).
+// Small indexes split each row tile's dimensions over S waves (S = 4 below 64k rows) so that
+// a 10k-row index still spreads over ~160 blocks; the partial sums are added in slice order.
 #include "common.h"
 #include <float.h>
 using namespace ragk;
 
 namespace {
 
-constexpr int ST = 256;      // threads
-constexpr int RPT = 4;       // rows per thread
-constexpr int RPB = ST * RPT;  // rows per block (1024)
-constexpr int QC = 8;        // queries per block
-constexpr int DCH = 256;     // query dims staged per LDS chunk
+constexpr int ST = 256;   // threads per block (4 waves)
+constexpr int DCH = 256;  // query dims staged per LDS chunk
+constexpr int UNR = 16;   // dims (independent loads) in flight per lane
 
-// sort `n` (power of 2) pairs ascending by (dist, idx) in LDS
-__device__ void bitonic_asc(float* v, int* ix, int n) {
-  for (int k = 2; k <= n; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int p = i ^ j;
-        if (p > i) {
-          const bool up = (i & k) == 0;
-          const float a = v[i], b = v[p];
-          const int ia = ix[i], ib = ix[p];
-          const bool a_first = (a < b) || (a == b && (unsigned)ia < (unsigned)ib);
-          if (a_first != up) { v[i] = b; v[p] = a; ix[i] = ib; ix[p] = ia; }
-        }
+__device__ __forceinline__ bool cand_lt(float av, int ai, float bv, int bi) {
+  return av < bv || (av == bv && (unsigned)ai < (unsigned)bi);
+}
+
+// one compare-exchange step of a lane-level bitonic network (partner = lane ^ j)
+__device__ __forceinline__ void cx(float& v, int& i, int lane, int j, bool asc) {
+  const float ov = __shfl_xor(v, j, 64);
+  const int oi = __shfl_xor(i, j, 64);
+  const bool keep_min = ((lane & j) == 0) == asc;
+  const bool take = keep_min ? cand_lt(ov, oi, v, i) : cand_lt(v, i, ov, oi);
+  if (take) {
+    v = ov;
+    i = oi;
+  }
+}
+
+// ascending sort of the 64 (v, i) pairs held one per lane
+__device__ __forceinline__ void wave_sort64(float& v, int& i, int lane) {
+#pragma unroll
+  for (int kk = 2; kk <= 64; kk <<= 1)
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1) cx(v, i, lane, j, (lane & kk) == 0);
+}
+
+// (bv, bi) sorted ascending, (nv, ni) sorted ascending -> (bv, bi) = the 64 smallest of both, sorted
+__device__ __forceinline__ void wave_merge64(float& bv, int& bi, float nv, int ni, int lane) {
+  const float rv = __shfl(nv, 63 - lane, 64);
+  const int ri = __shfl(ni, 63 - lane, 64);
+  if (cand_lt(rv, ri, bv, bi)) {
+    bv = rv;
+    bi = ri;
+  }
+#pragma unroll
+  for (int j = 32; j > 0; j >>= 1) cx(bv, bi, lane, j, true);
+}
+
+// feed 64 unsorted candidates (one per lane) into the running top list; k-th best = threshold
+__device__ __forceinline__ void wave_offer(float& bv, int& bi, float v, int id, int k, int lane) {
+  const float tv = __shfl(bv, k - 1, 64);
+  const int ti = __shfl(bi, k - 1, 64);
+  if (!__any(cand_lt(v, id, tv, ti))) return;  // wave-uniform
+  wave_sort64(v, id, lane);
+  wave_merge64(bv, bi, v, id, lane);
+}
+
+// Distances of rows [rbase, rbase + 64) (one per lane; rows clamped into [0, cap)) over dims
+// [t0, t1) of the staged chunk starting at dim dc, for QB queries.
+template <int QB>
+__device__ __forceinline__ void scan_dims(const float* __restrict__ xt, size_t cap, int rc, int dc, int t0, int t1,
+                                          const float* qs, float* acc) {
+  const float* col = xt + (size_t)(dc + t0) * cap + rc;
+  int t = t0;
+  for (; t + UNR <= t1; t += UNR, col += UNR * cap) {
+    float x[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) x[u] = __builtin_nontemporal_load(col + (size_t)u * cap);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+#pragma unroll
+      for (int j = 0; j < QB; ++j) {
+        const float df = x[u] - qs[j * DCH + t + u];
+        acc[j] = fmaf(df, df, acc[j]);
+      }
+  }
+  for (; t < t1; ++t, col += cap) {
+    const float x = *col;
+#pragma unroll
+    for (int j = 0; j < QB; ++j) {
+      const float df = x - qs[j * DCH + t];
+      acc[j] = fmaf(df, df, acc[j]);
+    }
+  }
+}
+
+// Flat scan. Row tile = 64 * (4 / S) rows: wave w scans rows 64 * (w / S) .. +63 of the tile over
+// dim slice w % S of every 256-dim chunk. Block bx handles tiles bx, bx + gridDim.x, ...; its
+// queries are q0 = blockIdx.y * QB .. + QB. Output: per query one sorted list of k at [q][bx].
+template <int QB, int S>
+__global__ __launch_bounds__(ST) void l2_scan_kernel(const float* __restrict__ xt, int cap, int d, int row_begin,
+                                                     int row_end, int ntiles, const float* __restrict__ q, int nq,
+                                                     int k, float* __restrict__ out_d, int* __restrict__ out_i,
+                                                     const int* __restrict__ ids_map) {
+  constexpr int RG = 4 / S;
+  constexpr int RB = 64 * RG;
+  extern __shared__ __attribute__((aligned(16))) float sc_smem[];
+  float* qs = sc_smem;              // [QB][DCH]
+  float* red = sc_smem + QB * DCH;  // [S - 1][RG][QB][64]
+  __shared__ float mv[4][64];
+  __shared__ int mi[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = w / S, s = w % S;
+  const int q0 = blockIdx.y * QB;
+  const int nqb = min(QB, nq - q0);
+  float bv[QB];
+  int bi[QB];
+#pragma unroll
+  for (int j = 0; j < QB; ++j) {
+    bv[j] = FLT_MAX;
+    bi[j] = -1;
+  }
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int row = row_begin + tile * RB + 64 * g + lane;
+    const int rc = min(row, cap - 1);  // rows in [row_end, cap) are valid memory; masked below
+    float acc[QB];
+#pragma unroll
+    for (int j = 0; j < QB; ++j) acc[j] = 0.f;
+    for (int dc = 0; dc < d; dc += DCH) {
+      const int dn = min(DCH, d - dc);
+      __syncthreads();  // previous chunk (and the previous tile's slice reduction) consumed
+      for (int e = threadIdx.x; e < QB * DCH; e += ST) {
+        const int j = e / DCH, t = e % DCH;
+        qs[e] = (j < nqb && t < dn) ? q[(size_t)(q0 + j) * d + dc + t] : 0.f;
       }
       __syncthreads();
+      const int per = (dn + S - 1) / S;
+      const int t0 = min(dn, s * per), t1 = min(dn, t0 + per);
+      scan_dims<QB>(xt, (size_t)cap, rc, dc, t0, t1, qs, acc);
     }
-  }
-}
-
-// xt: [d][cap] fp32 column-major database; rows [row_begin, row_end) are searched.
-// For IVF each blockIdx.z selects a (query, probe) row range via `ranges` (nullptr = flat).
-__global__ __launch_bounds__(ST) void l2_block_topk_kernel(const float* __restrict__ xt, int cap, int d,
-                                                           int row_begin, int row_end, const float* __restrict__ q,
-                                                           int nq, int k, float* out_d, int* out_i,
-                                                           const int* __restrict__ ids_map) {
-  __shared__ float qs[QC][DCH];
-  __shared__ float sd[RPB];
-  __shared__ int sidx[RPB];
-  const int q0 = blockIdx.y * QC;
-  const int r0 = row_begin + blockIdx.x * RPB;
-  float acc[RPT][QC];
+    if (S > 1) {
+      if (s > 0) {
 #pragma unroll
-  for (int r = 0; r < RPT; ++r)
+        for (int j = 0; j < QB; ++j) red[(((s - 1) * RG + g) * QB + j) * 64 + lane] = acc[j];
+      }
+      __syncthreads();
+      if (s == 0) {
 #pragma unroll
-    for (int j = 0; j < QC; ++j) acc[r][j] = 0.f;
-
-  for (int dc = 0; dc < d; dc += DCH) {
-    const int dn = min(DCH, d - dc);
-    __syncthreads();
-    for (int e = threadIdx.x; e < QC * DCH; e += ST) {
-      const int j = e / DCH, t = e % DCH;
-      qs[j][t] = (q0 + j < nq && t < dn) ? q[(size_t)(q0 + j) * d + dc + t] : 0.f;
-    }
-    __syncthreads();
-    for (int t = 0; t < dn; ++t) {
-      const float* col = xt + (size_t)(dc + t) * cap;
+        for (int ss = 1; ss < S; ++ss)
 #pragma unroll
-      for (int r = 0; r < RPT; ++r) {
-        const int row = r0 + r * ST + threadIdx.x;
-        const float x = row < row_end ? col[row] : 0.f;
-#pragma unroll
-        for (int j = 0; j < QC; ++j) {
-          const float df = x - qs[j][t];
-          acc[r][j] = fmaf(df, df, acc[r][j]);
-        }
+          for (int j = 0; j < QB; ++j) acc[j] += red[(((ss - 1) * RG + g) * QB + j) * 64 + lane];
       }
     }
-  }
-  const int nblk_out = gridDim.x;
-  for (int j = 0; j < QC && q0 + j < nq; ++j) {
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      const int slot = r * ST + threadIdx.x;
-      const int row = r0 + slot;
+    if (s == 0) {  // wave-uniform
       const bool ok = row < row_end;
-      sd[slot] = ok ? acc[r][j] : FLT_MAX;
-      sidx[slot] = ok ? (ids_map ? ids_map[row] : row) : -1;
+      const int id = ok ? (ids_map ? ids_map[row] : row) : -1;
+#pragma unroll
+      for (int j = 0; j < QB; ++j)
+        if (j < nqb) wave_offer(bv[j], bi[j], ok ? acc[j] : FLT_MAX, id, k, lane);
     }
-    __syncthreads();
-    bitonic_asc(sd, sidx, RPB);
-    for (int i = threadIdx.x; i < k; i += ST) {
-      const size_t o = ((size_t)(q0 + j) * nblk_out + blockIdx.x) * k + i;
-      out_d[o] = sd[i];
-      out_i[o] = sidx[i];
+  }
+  // block merge: the RG list-holding waves (s == 0) -> wave 0 -> k outputs per query
+#pragma unroll
+  for (int j = 0; j < QB; ++j) {
+    if (j >= nqb) continue;  // block-uniform
+    if (RG > 1) {
+      __syncthreads();
+      if (s == 0 && g > 0) {
+        mv[g][lane] = bv[j];
+        mi[g][lane] = bi[j];
+      }
+      __syncthreads();
+      if (w == 0)
+        for (int gg = 1; gg < RG; ++gg) wave_merge64(bv[j], bi[j], mv[gg][lane], mi[gg][lane], lane);
+    }
+    if (w == 0 && lane < k) {
+      const size_t o = ((size_t)(q0 + j) * gridDim.x + blockIdx.x) * k + lane;
+      out_d[o] = bv[j];
+      out_i[o] = bi[j];
     }
   }
 }
 
-// IVF-Flat scan: block (probe p, chunk c) x query q scans rows [start, end) of list
-// probes[q][p] in the list-ordered column-major store -> partial top-k at [q][p*chunks+c].
+// IVF-Flat scan: block (probe p, query qi) scans the whole inverted list probes[qi][p] (store rows
+// [offsets[list], ends[list]); packed lists when ends == nullptr: end = offsets[list + 1]) in
+// 256-row tiles (one wave per 64 rows) -> one sorted list of k at [qi][p].
 constexpr int IVF_DMAX = 2048;
 __global__ __launch_bounds__(ST) void ivf_scan_kernel(const float* __restrict__ xt, int cap, int d,
                                                       const float* __restrict__ q, const int* __restrict__ probes,
-                                                      int nprobe, int chunks, const int* __restrict__ offsets,
-                                                      const int* __restrict__ ends,
-                                                      const int* __restrict__ ids_map, int k, float* out_d,
-                                                      int* out_i) {
+                                                      int nprobe, const int* __restrict__ offsets,
+                                                      const int* __restrict__ ends, const int* __restrict__ ids_map,
+                                                      int k, float* __restrict__ out_d, int* __restrict__ out_i) {
   __shared__ float qs[IVF_DMAX];
-  __shared__ float sd[RPB];
-  __shared__ int sidx[RPB];
-  const int qi = blockIdx.y;
-  const int p = blockIdx.x / chunks, c = blockIdx.x % chunks;
+  __shared__ float mv[4][64];
+  __shared__ int mi[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qi = blockIdx.y, p = blockIdx.x;
   const int list = probes[(size_t)qi * nprobe + p];
-  // list rows [offsets[list], ends[list]) -- lists may carry spare capacity after their rows
-  // (incremental appends); without `ends` the lists are packed: end = offsets[list + 1]
-  const int lend = ends ? ends[list] : offsets[list + 1];
-  const int r0 = offsets[list] + c * RPB;
-  const int r1 = min(lend, r0 + RPB);
+  const int lbeg = list >= 0 ? offsets[list] : 0;
+  const int lend = list < 0 ? 0 : (ends ? ends[list] : offsets[list + 1]);
   for (int t = threadIdx.x; t < d; t += ST) qs[t] = q[(size_t)qi * d + t];
   __syncthreads();
-  float acc[RPT];
+  float bv = FLT_MAX;
+  int bi = -1;
+  for (int r0 = lbeg; r0 < lend; r0 += 4 * 64) {
+    const int row = r0 + 64 * w + lane;
+    const int rc = min(row, cap - 1);
+    float acc = 0.f;
+    const float* col = xt + rc;
+    int t = 0;
+    for (; t + UNR <= d; t += UNR, col += (size_t)UNR * cap) {
+      float x[UNR];
 #pragma unroll
-  for (int r = 0; r < RPT; ++r) acc[r] = 0.f;
-  if (r0 < r1) {
-    for (int t = 0; t < d; ++t) {
-      const float* col = xt + (size_t)t * cap;
-      const float qv = qs[t];
+      for (int u = 0; u < UNR; ++u) x[u] = col[(size_t)u * cap];
 #pragma unroll
-      for (int r = 0; r < RPT; ++r) {
-        const int row = r0 + r * ST + threadIdx.x;
-        const float x = row < r1 ? col[row] : 0.f;
-        const float df = x - qv;
-        acc[r] = fmaf(df, df, acc[r]);
+      for (int u = 0; u < UNR; ++u) {
+        const float df = x[u] - qs[t + u];
+        acc = fmaf(df, df, acc);
       }
     }
+    for (; t < d; ++t, col += cap) {
+      const float df = *col - qs[t];
+      acc = fmaf(df, df, acc);
+    }
+    const bool ok = row < lend;
+    wave_offer(bv, bi, ok ? acc : FLT_MAX, ok ? ids_map[row] : -1, k, lane);
   }
-#pragma unroll
-  for (int r = 0; r < RPT; ++r) {
-    const int slot = r * ST + threadIdx.x;
-    const int row = r0 + slot;
-    const bool ok = row < r1;
-    sd[slot] = ok ? acc[r] : FLT_MAX;
-    sidx[slot] = ok ? ids_map[row] : -1;
+  if (w > 0) {
+    mv[w][lane] = bv;
+    mi[w][lane] = bi;
   }
   __syncthreads();
-  bitonic_asc(sd, sidx, RPB);
-  const int G = gridDim.x;
-  for (int i = threadIdx.x; i < k; i += ST) {
-    const size_t o = ((size_t)qi * G + blockIdx.x) * k + i;
-    out_d[o] = sd[i];
-    out_i[o] = sidx[i];
+  if (w == 0) {
+    for (int gg = 1; gg < 4; ++gg) wave_merge64(bv, bi, mv[gg][lane], mi[gg][lane], lane);
+    if (lane < k) {
+      const size_t o = ((size_t)qi * gridDim.x + p) * k + lane;
+      out_d[o] = bv;
+      out_i[o] = bi;
+    }
   }
 }
 
-// in: [nq][G][k] -> out: [nq][ceil(G/64)][k]
-constexpr int MG = 64;
-__global__ __launch_bounds__(ST) void topk_merge_kernel(const float* __restrict__ in_d, const int* __restrict__ in_i,
-                                                        int G, int k, int n_pow2, float* out_d, int* out_i) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* sd = reinterpret_cast<float*>(smem);
-  int* si = reinterpret_cast<int*>(smem + n_pow2 * sizeof(float));
-  const int qi = blockIdx.y, g0 = blockIdx.x * MG;
-  const int ng = min(MG, G - g0);
-  const int n = ng * k;
-  for (int e = threadIdx.x; e < n_pow2; e += ST) {
-    if (e < n) {
-      const size_t o = ((size_t)qi * G + g0) * k + e;
-      sd[e] = in_d[o];
-      si[e] = in_i[o];
-    } else {
-      sd[e] = FLT_MAX;
-      si[e] = -1;
-    }
+// in: [nq][G][k] sorted lists -> out: [nq][k]. One block per query; each wave takes 64 candidates
+// at a time (64 / k whole lists per step), offers them to its running top list; waves merged last.
+__global__ __launch_bounds__(ST) void topk_lists_merge_kernel(const float* __restrict__ in_d,
+                                                              const int* __restrict__ in_i, int G, int k,
+                                                              float* __restrict__ out_d, int* __restrict__ out_i) {
+  __shared__ float mv[4][64];
+  __shared__ int mi[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qi = blockIdx.x;
+  const int lpw = 64 / k;  // whole lists per 64-lane step
+  const int li = lane / k, e = lane % k;
+  const size_t base = (size_t)qi * G * k;
+  float bv = FLT_MAX;
+  int bi = -1;
+  for (int l0 = w * lpw; l0 < G; l0 += 4 * lpw) {
+    const int l = l0 + li;
+    const bool ok = li < lpw && l < G;
+    const float v = ok ? in_d[base + (size_t)l * k + e] : FLT_MAX;
+    const int id = ok ? in_i[base + (size_t)l * k + e] : -1;
+    wave_offer(bv, bi, v, id, k, lane);
+  }
+  if (w > 0) {
+    mv[w][lane] = bv;
+    mi[w][lane] = bi;
   }
   __syncthreads();
-  bitonic_asc(sd, si, n_pow2);
-  const int Gout = gridDim.x;
-  for (int i = threadIdx.x; i < k; i += ST) {
-    const size_t o = ((size_t)qi * Gout + blockIdx.x) * k + i;
-    out_d[o] = sd[i];
-    out_i[o] = si[i];
+  if (w == 0) {
+    for (int gg = 1; gg < 4; ++gg) wave_merge64(bv, bi, mv[gg][lane], mi[gg][lane], lane);
+    if (lane < k) {
+      out_d[(size_t)qi * k + lane] = bv;
+      out_i[(size_t)qi * k + lane] = bi;
+    }
   }
 }
 
@@ -230,10 +325,16 @@ __device__ __forceinline__ void ka_better(float v, int i, float& bv, int& bi) {
   }
 }
 
+// DUMP: also write every (row, centroid) score -(||c||^2 - 2 x.c) to scores[row][k] -- the IVF
+// coarse search takes its top-nprobe from these (topk_lds, ties -> lower id), so probing and list
+// assignment rank centroids by the SAME numbers (a vector is always found by a query at its own
+// position with nprobe = 1).
+template <bool DUMP>
 __global__ __launch_bounds__(256) void kmeans_assign_kernel(const float* __restrict__ X, int n, int d,
                                                             const float* __restrict__ C,
                                                             const float* __restrict__ cnorm, int k,
-                                                            int* __restrict__ assign, float* __restrict__ dist) {
+                                                            int* __restrict__ assign, float* __restrict__ dist,
+                                                            float* __restrict__ scores) {
   extern __shared__ __attribute__((aligned(16))) float ka_smem[];
   const int xp = d + 4;
   float* xs = ka_smem;                          // [KA_ROWS][xp]
@@ -292,8 +393,16 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(const float* __restr
     const float na = ca < k ? cnorm[ca] : 0.f, nb = cb < k ? cnorm[cb] : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      if (ca < k) ka_better(na - 2.f * acc0[r], ca, bv[r], bi[r]);
-      if (cb < k) ka_better(nb - 2.f * acc1[r], cb, bv[r], bi[r]);
+      const float va = na - 2.f * acc0[r], vb = nb - 2.f * acc1[r];
+      if (ca < k) ka_better(va, ca, bv[r], bi[r]);
+      if (cb < k) ka_better(vb, cb, bv[r], bi[r]);
+      if (DUMP) {
+        const int row = row0 + 16 * rg + 4 * fg + r;
+        if (row < n) {
+          if (ca < k) scores[(size_t)row * k + ca] = -va;
+          if (cb < k) scores[(size_t)row * k + cb] = -vb;
+        }
+      }
     }
   }
   // argmin across the 16 lanes of a row group (same fg), then across the two centroid halves
@@ -318,67 +427,108 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(const float* __restr
     float v = s_bv[0][tid];
     int i = s_bi[0][tid];
     ka_better(s_bv[1][tid], s_bi[1][tid], v, i);
-    assign[row0 + tid] = i;
+    if (assign) assign[row0 + tid] = i;
     if (dist) dist[row0 + tid] = fmaxf(s_xn[tid] + v, 0.f);
   }
 }
 
 }  // namespace
 
-// Partial pass. out buffers must hold nq * ceil((row_end-row_begin)/1024) * k entries.
-// Returns the number of row blocks G through *out_groups.
-RAGK_API int ragk_l2_partial(const float* xt, int cap, int d, int row_begin, int row_end, const float* q, int nq,
-                             int k, float* out_d, int* out_i, const int* ids_map, int* out_groups, hipStream_t st) {
-  const int n = row_end - row_begin;
-  if (nq <= 0 || k <= 0) return 0;
-  if (k > RPB) return (int)hipErrorInvalidValue;
-  const int G = n > 0 ? (n + RPB - 1) / RPB : 1;
-  if (out_groups) *out_groups = G;
-  dim3 grid(G, (nq + QC - 1) / QC);
-  hipLaunchKernelGGL(l2_block_topk_kernel, grid, dim3(ST), 0, st, xt, cap, d, row_begin, n > 0 ? row_end : row_begin,
-                     q, nq, k, out_d, out_i, ids_map);
+// dims split over S waves per row tile: more blocks for small indexes (the summation order,
+// and so the last bits of a distance, depend on S -- i.e. on the index size only)
+static int scan_slices(int n) { return n < 65536 ? 4 : (n < 262144 ? 2 : 1); }
+
+template <int QB, int S>
+static void launch_scan(dim3 grid, size_t lds, hipStream_t st, const float* xt, int cap, int d, int rb, int re,
+                        int ntiles, const float* q, int nq, int k, float* od, int* oi, const int* ids) {
+  hipLaunchKernelGGL((l2_scan_kernel<QB, S>), grid, dim3(ST), lds, st, xt, cap, d, rb, re, ntiles, q, nq, k, od, oi,
+                     ids);
+}
+
+template <int QB>
+static void launch_scan_s(int S, dim3 grid, hipStream_t st, const float* xt, int cap, int d, int rb, int re,
+                          int ntiles, const float* q, int nq, int k, float* od, int* oi, const int* ids) {
+  const size_t lds = (size_t)QB * DCH * 4 + (size_t)(S - 1) * (4 / S) * QB * 64 * 4;
+  if (S == 4) launch_scan<QB, 4>(grid, lds, st, xt, cap, d, rb, re, ntiles, q, nq, k, od, oi, ids);
+  else if (S == 2) launch_scan<QB, 2>(grid, lds, st, xt, cap, d, rb, re, ntiles, q, nq, k, od, oi, ids);
+  else launch_scan<QB, 1>(grid, lds, st, xt, cap, d, rb, re, ntiles, q, nq, k, od, oi, ids);
+}
+
+// Number of partial lists per query the scan of rows [row_begin, row_end) emits (size the
+// partial buffers [nq][G][k] with it).
+RAGK_API int ragk_l2_scan_groups(int row_begin, int row_end, int nq) {
+  const int n = max(0, row_end - row_begin);
+  const int S = scan_slices(n);
+  const int ntiles = (n + 64 * (4 / S) - 1) / (64 * (4 / S));
+  const int qgroups = (max(nq, 1) + 15) / 16;
+  const int target = max(1, 2048 / qgroups);  // bounded list count: the merge stays short
+  return max(1, min(ntiles, target));
+}
+
+// Exact top-k (k <= 64) over rows [row_begin, row_end) of xt[d][cap]; part_d / part_i hold
+// nq * ragk_l2_scan_groups(...) * k entries; results -> out_d / out_i [nq][k].
+RAGK_API int ragk_l2_search(const float* xt, int cap, int d, int row_begin, int row_end, const float* q, int nq,
+                            int k, const int* ids_map, float* part_d, int* part_i, float* out_d, int* out_i,
+                            hipStream_t st) {
+  if (nq <= 0) return 0;
+  if (k < 1 || k > 64 || d < 1 || cap < 1 || row_end > cap) return (int)hipErrorInvalidValue;
+  const int n = max(0, row_end - row_begin);
+  const int S = scan_slices(n);
+  const int ntiles = (n + 64 * (4 / S) - 1) / (64 * (4 / S));
+  const int G = ragk_l2_scan_groups(row_begin, row_end, nq);
+  // queries per block: up to 16 (32 accumulators + the x[] ring would leave one wave per SIMD);
+  // the last group of the y-dimension may be partial (handled in-kernel)
+  const int QB = nq >= 16 ? 16 : (nq >= 8 ? 8 : (nq >= 4 ? 4 : (nq >= 2 ? 2 : 1)));
+  const dim3 grid(G, (nq + QB - 1) / QB);
+  if (QB == 16) launch_scan_s<16>(S, grid, st, xt, cap, d, row_begin, row_end, ntiles, q, nq, k, part_d, part_i, ids_map);
+  else if (QB == 8) launch_scan_s<8>(S, grid, st, xt, cap, d, row_begin, row_end, ntiles, q, nq, k, part_d, part_i, ids_map);
+  else if (QB == 4) launch_scan_s<4>(S, grid, st, xt, cap, d, row_begin, row_end, ntiles, q, nq, k, part_d, part_i, ids_map);
+  else if (QB == 2) launch_scan_s<2>(S, grid, st, xt, cap, d, row_begin, row_end, ntiles, q, nq, k, part_d, part_i, ids_map);
+  else launch_scan_s<1>(S, grid, st, xt, cap, d, row_begin, row_end, ntiles, q, nq, k, part_d, part_i, ids_map);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(topk_lists_merge_kernel, dim3(nq), dim3(ST), 0, st, part_d, part_i, G, k, out_d, out_i);
   return (int)hipGetLastError();
 }
 
-// out buffers: nq * nprobe * chunks * k entries; chunks = ceil(max_list_len / 1024)
-RAGK_API int ragk_ivf_scan(const float* xt, int cap, int d, const float* q, int nq, const int* probes, int nprobe,
-                           int chunks, const int* offsets, const int* ends, const int* ids_map, int k, float* out_d,
-                           int* out_i, hipStream_t st) {
+// IVF: part buffers hold nq * nprobe * k entries; results -> out [nq][k]
+RAGK_API int ragk_ivf_search(const float* xt, int cap, int d, const float* q, int nq, const int* probes, int nprobe,
+                             const int* offsets, const int* ends, const int* ids_map, int k, float* part_d,
+                             int* part_i, float* out_d, int* out_i, hipStream_t st) {
   if (nq <= 0) return 0;
-  if (d > IVF_DMAX || k > RPB || chunks < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(ivf_scan_kernel, dim3(nprobe * chunks, nq), dim3(ST), 0, st, xt, cap, d, q, probes, nprobe,
-                     chunks, offsets, ends, ids_map, k, out_d, out_i);
+  if (d > IVF_DMAX || k < 1 || k > 64 || nprobe < 1 || cap < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ivf_scan_kernel, dim3(nprobe, nq), dim3(ST), 0, st, xt, cap, d, q, probes, nprobe, offsets, ends,
+                     ids_map, k, part_d, part_i);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(topk_lists_merge_kernel, dim3(nq), dim3(ST), 0, st, part_d, part_i, nprobe, k, out_d, out_i);
   return (int)hipGetLastError();
 }
 
 // k-means / IVF assignment: a[i] = argmin_c ||x_i - c||^2 over the k centroids (ties -> lower c),
 // dist[i] = that squared distance. X [n][d], C [k][d] fp32 row-major, cnorm[c] = ||c||^2.
+// scores (optional, nullptr = none): [n][k] floats, see kmeans_assign_kernel<true>
 RAGK_API int ragk_kmeans_assign(const float* X, int n, int d, const float* C, const float* cnorm, int k, int* assign,
-                                float* dist, hipStream_t st) {
+                                float* dist, float* scores, hipStream_t st) {
   if (n <= 0) return 0;
   if (d % KA_DC || d > KA_DMAX || k <= 0 || ((uintptr_t)X & 15) || ((uintptr_t)C & 15)) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)KA_ROWS * (d + 4) * 4 + (size_t)KA_CT * (KA_DC + 4) * 4;
   static bool attr_set = false;  // > 64 KiB of dynamic LDS needs the opt-in (d up to 1024: ~149 KiB)
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kmeans_assign_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       KA_ROWS * (KA_DMAX + 4) * 4 + KA_CT * (KA_DC + 4) * 4);
+    const int mx = KA_ROWS * (KA_DMAX + 4) * 4 + KA_CT * (KA_DC + 4) * 4;
+    hipError_t e = hipFuncSetAttribute((const void*)kmeans_assign_kernel<false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)kmeans_assign_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(kmeans_assign_kernel, dim3((n + KA_ROWS - 1) / KA_ROWS), dim3(256), lds, st, X, n, d, C, cnorm, k,
-                     assign, dist);
-  return (int)hipGetLastError();
-}
-
-RAGK_API int ragk_topk_merge(const float* in_d, const int* in_i, int nq, int G, int k, float* out_d, int* out_i,
-                             hipStream_t st) {
-  if (nq <= 0) return 0;
-  if (k > 64) return (int)hipErrorInvalidValue;
-  int n_pow2 = 1;
-  while (n_pow2 < MG * k) n_pow2 <<= 1;
-  const int gout = (G + MG - 1) / MG;
-  hipLaunchKernelGGL(topk_merge_kernel, dim3(gout, nq), dim3(ST), n_pow2 * 8, st, in_d, in_i, G, k, n_pow2, out_d,
-                     out_i);
+  if (scores)
+    hipLaunchKernelGGL(kmeans_assign_kernel<true>, dim3((n + KA_ROWS - 1) / KA_ROWS), dim3(256), lds, st, X, n, d, C,
+                       cnorm, k, assign, dist, scores);
+  else
+    hipLaunchKernelGGL(kmeans_assign_kernel<false>, dim3((n + KA_ROWS - 1) / KA_ROWS), dim3(256), lds, st, X, n, d, C,
+                       cnorm, k, assign, dist, scores);
   return (int)hipGetLastError();
 }
 

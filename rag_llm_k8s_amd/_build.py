@@ -9,12 +9,16 @@ repository snapshot to the GPU box:
 * ``_ragk_rt*.so``    -- the C++ host runtime in ``csrc/runtime/*.cpp`` (pybind11):
   safetensors mmap reader, faiss-format index I/O, tokenizers, KV block manager.
 
-Incremental: an object is rebuilt only when its source or a header is newer.
+Incremental: an object is rebuilt only when its source or a header is newer -- and everything is
+rebuilt when the content hash of the kernel sources (+ flags) differs from the one recorded at the
+last build. That hash is compiled into the library (``ragk_build_stamp()``); ``ops/_lib.py`` checks
+it against the sources at load, so a library that does not match the tree is never used silently.
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -30,6 +34,30 @@ HIP_LIB = os.path.join(LIB_DIR, "libragk_hip.so")
 
 # per-file flags: gemm_w4.hip is written in its final instruction order (see its header)
 EXTRA_FLAGS = {"gemm_w4.hip": ["-mllvm", "-disable-post-ra"]}
+
+
+HIP_FLAGS = ["-O3", "--offload-arch=" + ARCH, "-fPIC", "-std=c++17", "-Wno-unused-result", "-munsafe-fp-atomics"]
+
+
+def hip_sources():
+    kdir = os.path.join(ROOT, "csrc", "kernels")
+    cdir = os.path.join(ROOT, "csrc", "comm")
+    srcs = sorted(glob.glob(os.path.join(kdir, "*.hip")) + glob.glob(os.path.join(cdir, "*.hip")))
+    headers = sorted(glob.glob(os.path.join(kdir, "*.h")) + glob.glob(os.path.join(cdir, "*.h")))
+    return srcs, headers
+
+
+def source_hash():
+    """Content hash of every kernel source and header plus the compile flags (no mtimes)."""
+    srcs, headers = hip_sources()
+    h = hashlib.sha256()
+    h.update(repr((HIP_FLAGS, sorted(EXTRA_FLAGS.items()))).encode())
+    for f in srcs + headers:
+        h.update(os.path.relpath(f, ROOT).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()[:32]
 
 
 def _newer(src_files, target):
@@ -50,17 +78,25 @@ def build_hip(verbose=False, jobs=None):
     os.makedirs(OBJ_DIR, exist_ok=True)
     os.makedirs(LIB_DIR, exist_ok=True)
     kdir = os.path.join(ROOT, "csrc", "kernels")
-    cdir = os.path.join(ROOT, "csrc", "comm")
-    srcs = sorted(glob.glob(os.path.join(kdir, "*.hip")) + glob.glob(os.path.join(cdir, "*.hip")))
-    headers = glob.glob(os.path.join(kdir, "*.h")) + glob.glob(os.path.join(cdir, "*.h"))
-    flags = ["-O3", "--offload-arch=" + ARCH, "-fPIC", "-std=c++17", "-I" + kdir,
-             "-Wno-unused-result", "-munsafe-fp-atomics"]
+    srcs, headers = hip_sources()
+    flags = HIP_FLAGS + ["-I" + kdir]
+    stamp = source_hash()
+    stamp_txt = os.path.join(OBJ_DIR, "ragk_stamp.txt")
+    prev = open(stamp_txt).read().strip() if os.path.exists(stamp_txt) else None
     objs, todo = [], []
     for s in srcs:
         o = os.path.join(OBJ_DIR, os.path.basename(s) + ".o")
         objs.append(o)
-        if _newer([s] + headers + [os.path.abspath(__file__)], o):
+        if prev != stamp or _newer([s] + headers + [os.path.abspath(__file__)], o):
             todo.append((s, o))
+    stamp_src = os.path.join(OBJ_DIR, "ragk_stamp.cpp")
+    stamp_obj = stamp_src + ".o"
+    if prev != stamp or not os.path.exists(stamp_obj):
+        with open(stamp_src, "w") as f:
+            f.write('extern "C" __attribute__((visibility("default"))) const char* ragk_build_stamp() '
+                    '{ return "%s"; }\n' % stamp)
+        _run(["g++", "-O2", "-fPIC", "-c", stamp_src, "-o", stamp_obj])
+    objs.append(stamp_obj)
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(jobs) as ex:
         futs = [ex.submit(_run, [HIPCC] + flags + EXTRA_FLAGS.get(os.path.basename(s), []) + ["-c", s, "-o", o])
@@ -69,8 +105,10 @@ def build_hip(verbose=False, jobs=None):
             out = f.result()
             if verbose and out.strip():
                 print(out)
-    if todo or _newer(objs, HIP_LIB):
+    if todo or prev != stamp or _newer(objs, HIP_LIB):
         _run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", HIP_LIB])
+        with open(stamp_txt, "w") as f:
+            f.write(stamp + "\n")
     return HIP_LIB
 
 

@@ -11,10 +11,16 @@ extension of SURVEY §2.4 V3.
   (start, size, capacity). An append writes the new rows straight into their lists' free slots (one
   scatter kernel); only when some list runs out of room is the store regrown (capacities x1.5, so
   amortised O(1) per vector) -- an append never rebuilds the store from the host lists.
-* Search: coarse top-nprobe over the centroids (HBM flat kernel), then the ``ivf_scan`` kernel scans
-  every (query, probe) row range [start, start + size) with a per-range top-k, merged by
-  ``topk_merge``. Exact within the probed lists (nprobe = nlist == brute force).
-* Host copies of the lists are kept for faiss-format persistence (faiss_io.write_ivf_flat).
+* Search: coarse top-nprobe over the centroids, then the ``ivf_scan`` kernel scans every (query,
+  probe) list with a wave-resident running top-k, merged by ``topk_lists_merge``. Exact within the
+  probed lists (nprobe = nlist == brute force).
+* Probing and list assignment rank the centroids by the SAME numbers (as faiss, which uses its
+  quantizer for both): on the GPU the MFMA kernel's scores -(||c||^2 - 2 x.c) (argmin for the
+  assignment, topk_lds for the probes, ties -> lower id); elsewhere a row-independent elementwise
+  form. So a query at a stored vector's own position finds it with nprobe = 1.
+* Host copies of the lists are kept for faiss-format persistence (faiss_io.write_ivf_flat) as
+  per-list chunk lists: an append adds one chunk per touched list (O(batch), no re-concatenation);
+  a snapshot concatenates outside the index lock and compacts the chunks it wrote.
 """
 from __future__ import annotations
 
@@ -23,13 +29,24 @@ import threading
 import numpy as np
 import torch
 
-from .flat import FLT_MAX, FlatL2Index
+from .flat import FLT_MAX
 
 MAX_POINTS_PER_CENTROID = 256  # faiss ClusteringParameters default
 
 
 def _native_assign_ok(x):
     return x.is_cuda and x.dtype == torch.float32 and x.shape[1] % 64 == 0 and x.shape[1] <= 1024
+
+
+def _scores_torch(x: torch.Tensor, c: torch.Tensor):
+    """||x - c||^2 of every (row, centroid), elementwise (each row's numbers do not depend on the
+    other rows of the batch, unlike a GEMM whose kernel choice depends on the shape)."""
+    x, c = x.float(), c.float()
+    out = torch.empty((x.shape[0], c.shape[0]), dtype=torch.float32, device=x.device)
+    step = max(1, (1 << 24) // max(1, c.shape[0] * c.shape[1]))
+    for i in range(0, x.shape[0], step):
+        out[i:i + step] = ((x[i:i + step, None, :] - c[None]) ** 2).sum(-1)
+    return out
 
 
 def assign(x: torch.Tensor, c: torch.Tensor, cnorm=None):
@@ -39,8 +56,18 @@ def assign(x: torch.Tensor, c: torch.Tensor, cnorm=None):
 
         a, _ = native.kmeans_assign(x.contiguous(), c.float().contiguous(), cnorm)
         return a.long()
-    d = (x * x).sum(1, keepdim=True) - 2 * x @ c.t() + (c * c).sum(1)[None]
-    return d.argmin(1)
+    return _scores_torch(x, c).argmin(1)
+
+
+def probes(x: torch.Tensor, c: torch.Tensor, cnorm, nprobe):
+    """The nprobe nearest centroids of every row, ranked by the numbers assign() ranks (top-1 ==
+    assign), ties -> lower id. int64 [n, nprobe] on x's device."""
+    nprobe = min(nprobe, c.shape[0])
+    if _native_assign_ok(x) and c.shape[0] <= 24576 and nprobe <= 256:
+        from ..ops import native
+
+        return native.coarse_probes(x.contiguous(), c.float().contiguous(), cnorm, nprobe).long()
+    return torch.sort(_scores_torch(x, c), dim=1, stable=True)[1][:, :nprobe]
 
 
 def kmeans(x: torch.Tensor, k: int, iters: int = 20, seed: int = 0,
@@ -74,9 +101,8 @@ class IVFFlatIndex:
         self.is_trained = False
         self.centroids = None
         self._cnorm = None
-        self.quant = None
-        self.lists = []  # host: per-list float32 [n_i, d] (persistence, CPU search)
-        self.ids = []  # host: per-list int64 [n_i]
+        self._xchunks = []  # host: per list, float32 [m, d] chunks (persistence, CPU search)
+        self._ichunks = []  # host: per list, int64 [m] id chunks
         self.ntotal = 0
         self.metric = 1
         self.regrows = 0
@@ -143,10 +169,8 @@ class IVFFlatIndex:
     def _set_centroids(self, c):
         self.centroids = c.float().contiguous()
         self._cnorm = (self.centroids * self.centroids).sum(1)
-        self.quant = FlatL2Index(self.d, device=self.device, capacity=self.nlist)
-        self.quant.add(self.centroids.cpu())
-        self.lists = [np.zeros((0, self.d), np.float32) for _ in range(self.nlist)]
-        self.ids = [np.zeros(0, np.int64) for _ in range(self.nlist)]
+        self._xchunks = [[] for _ in range(self.nlist)]  # per list: float32 [m, d] arrays, in order
+        self._ichunks = [[] for _ in range(self.nlist)]  # per list: int64 [m] ids
         self.ntotal = 0
         self._reset_store()
         self.is_trained = True
@@ -159,14 +183,14 @@ class IVFFlatIndex:
             if not self.is_trained:
                 self.train(x)
             xd = torch.from_numpy(x).to(self.device)
-            a = assign(xd, self.centroids, self._cnorm).cpu().numpy().astype(np.int64)
+            a = assign(xd, self.centroids, self._cnorm).cpu().numpy().astype(np.int64)  # == probes(..)[:, 0]
             ids = np.arange(self.ntotal, self.ntotal + len(x), dtype=np.int64)
             order = np.argsort(a, kind="stable")
             bounds = np.searchsorted(a[order], np.arange(self.nlist + 1))
             for li in np.nonzero(np.diff(bounds))[0]:
                 sel = order[bounds[li]:bounds[li + 1]]
-                self.lists[li] = np.concatenate([self.lists[li], x[sel]])
-                self.ids[li] = np.concatenate([self.ids[li], ids[sel]])
+                self._xchunks[li].append(x[sel])
+                self._ichunks[li].append(ids[sel])
             if self.device.type == "cuda":
                 self._append_device(xd, a, ids)
             self.ntotal += len(x)
@@ -183,37 +207,28 @@ class IVFFlatIndex:
                 from ..ops import native
 
                 qd = q.to(self.device, non_blocking=True)
-                probes = self._coarse_device(qd, nprobe)  # stays on the device: one host sync per search
-                D, I = native.ivf_search(self._xt, self._cap, qd, probes, self._start_dev, self._ids_dev, k,
+                pr = self._coarse_device(qd, nprobe)  # stays on the device: one host sync per search
+                D, I = native.ivf_search(self._xt, self._cap, qd, pr, self._start_dev, self._ids_dev, k,
                                          max_list=int(self._size.max()), ends=self._end_dev)
                 return D.cpu(), I.cpu()
-            _, probes = self.quant.search(q, nprobe) if nprobe <= 64 else self._coarse_torch(q, nprobe)
-            return self._search_host(q, probes, k)
+            pr = probes(q.to(self.centroids.device), self.centroids, self._cnorm, nprobe).cpu()
+            return self._search_host(q, pr, k)
 
     def _coarse_device(self, qd, nprobe):
-        """Top-nprobe centroids per query as int32 [nq, nprobe] on the device (HBM flat kernel up to
-        64 probes, a torch distance GEMM + topk beyond)."""
-        if nprobe <= 64:
-            _, I = self.quant.search_device(qd, nprobe)
-            return I.int()
-        return self._coarse_torch(qd, nprobe)[1].int()
-
-    def _coarse_torch(self, q, nprobe):
-        c = self.centroids.to(q.device)
-        d = (c * c).sum(1)[None] - 2 * q @ c.t()
-        D, I = d.topk(nprobe, dim=1, largest=False)
-        return D, I
+        """Top-nprobe centroids per query as int32 [nq, nprobe] on the device."""
+        return probes(qd, self.centroids, self._cnorm, nprobe).int().contiguous()
 
     def _search_host(self, q, probes, k):
         nq = q.shape[0]
         D = torch.full((nq, k), FLT_MAX)
         I = torch.full((nq, k), -1, dtype=torch.int64)
+        lists, idl = self.lists, self.ids
         for qi in range(nq):
-            ls = [p for p in probes[qi].tolist() if p >= 0 and len(self.ids[p])]
+            ls = [p for p in probes[qi].tolist() if p >= 0 and len(idl[p])]
             if not ls:
                 continue
-            x = torch.from_numpy(np.concatenate([self.lists[p] for p in ls]))
-            ids = torch.from_numpy(np.concatenate([self.ids[p] for p in ls]))
+            x = torch.from_numpy(np.concatenate([lists[p] for p in ls]))
+            ids = torch.from_numpy(np.concatenate([idl[p] for p in ls]))
             d = ((x - q[qi][None]) ** 2).sum(1)
             order = torch.argsort(d, stable=True)
             kk = min(k, len(order))
@@ -221,17 +236,55 @@ class IVFFlatIndex:
             I[qi, :kk] = ids[order[:kk]]
         return D, I
 
+    # ------------------------------------------------------------------ host lists
+    def _compact(self, li):
+        xs, ids = self._xchunks[li], self._ichunks[li]
+        if len(xs) > 1:
+            self._xchunks[li] = [np.concatenate(xs)]
+            self._ichunks[li] = [np.concatenate(ids)]
+
+    @property
+    def lists(self):
+        """Per-list float32 [n_i, d] host arrays (compacts the chunk lists)."""
+        with self._lock:
+            out = []
+            for li in range(len(self._xchunks)):
+                self._compact(li)
+                out.append(self._xchunks[li][0] if self._xchunks[li] else np.zeros((0, self.d), np.float32))
+            return out
+
+    @property
+    def ids(self):
+        with self._lock:
+            out = []
+            for li in range(len(self._ichunks)):
+                self._compact(li)
+                out.append(self._ichunks[li][0] if self._ichunks[li] else np.zeros(0, np.int64))
+            return out
+
     # ------------------------------------------------------------------ persistence
     def snapshot_writer(self):
-        """Consistent copy of centroids + inverted lists now; the callable writes it atomically."""
+        """Consistent copy of centroids + inverted lists now (the chunk lists are shallow-copied under
+        the lock: O(nlist)); the callable concatenates and writes them atomically, then compacts the
+        chunks it wrote (only if nothing replaced them meanwhile)."""
         with self._lock:
             cents = self.centroids.cpu().numpy() if self.centroids is not None else np.zeros((0, self.d), np.float32)
-            lists, ids, nprobe, d = list(self.lists), list(self.ids), self.nprobe, self.d
+            xch = [list(c) for c in self._xchunks]
+            ich = [list(c) for c in self._ichunks]
+            nprobe, d = self.nprobe, self.d
 
         def write(path):
             from .faiss_io import atomic_write, write_ivf_flat
 
+            lists = [np.concatenate(c) if c else np.zeros((0, d), np.float32) for c in xch]
+            ids = [np.concatenate(c) if c else np.zeros(0, np.int64) for c in ich]
             atomic_write(path, lambda f: write_ivf_flat(f, d, cents, lists, ids, nprobe))
+            with self._lock:
+                for li, (c, x, i) in enumerate(zip(xch, lists, ids)):
+                    cur = self._xchunks[li] if li < len(self._xchunks) else None
+                    if cur is not None and len(c) > 1 and len(cur) >= len(c) and all(a is b for a, b in zip(cur, c)):
+                        self._xchunks[li] = [x] + cur[len(c):]
+                        self._ichunks[li] = [i] + self._ichunks[li][len(c):]
         return write
 
     def write(self, path):
@@ -241,11 +294,13 @@ class IVFFlatIndex:
     def from_lists(cls, r, device="cpu"):
         idx = cls(r["d"], device=device, nlist=r["nlist"], nprobe=max(1, r["nprobe"]))
         idx._set_centroids(torch.from_numpy(np.asarray(r["centroids"], np.float32)).to(idx.device))
-        idx.lists = [np.asarray(x, np.float32).reshape(-1, idx.d) for x in r["lists"]]
-        idx.ids = [np.asarray(x, np.int64) for x in r["ids"]]
-        idx.ntotal = int(sum(len(x) for x in idx.ids))
+        lists = [np.asarray(x, np.float32).reshape(-1, idx.d) for x in r["lists"]]
+        ids = [np.asarray(x, np.int64) for x in r["ids"]]
+        idx._xchunks = [[x] if len(x) else [] for x in lists]
+        idx._ichunks = [[i] if len(i) else [] for i in ids]
+        idx.ntotal = int(sum(len(x) for x in ids))
         if idx.device.type == "cuda" and idx.ntotal:
-            a = np.concatenate([np.full(len(i), li, np.int64) for li, i in enumerate(idx.ids)])
-            x = torch.from_numpy(np.concatenate(idx.lists)).to(idx.device)
-            idx._append_device(x, a, np.concatenate(idx.ids))
+            a = np.concatenate([np.full(len(i), li, np.int64) for li, i in enumerate(ids)])
+            x = torch.from_numpy(np.concatenate(lists)).to(idx.device)
+            idx._append_device(x, a, np.concatenate(ids))
         return idx

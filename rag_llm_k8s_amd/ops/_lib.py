@@ -65,10 +65,10 @@ _SIGS = {
     "ragk_topk_candidates": [P, I, I, I, I, I, I, P, P, S],
     "ragk_sample_candidates": [P, P, I, I, P, P, P, P, P, P, P, S],
     "ragk_sample_candidates_lists": [P, P, I, I, I, P, P, P, P, P, P, P, S],
-    "ragk_l2_partial": [P, I, I, I, I, P, I, I, P, P, P, P, S],
-    "ragk_topk_merge": [P, P, I, I, I, P, P, S],
-    "ragk_ivf_scan": [P, I, I, P, I, P, I, I, P, P, P, I, P, P, S],
-    "ragk_kmeans_assign": [P, I, I, P, P, I, P, P, S],
+    "ragk_l2_scan_groups": [I, I, I],
+    "ragk_l2_search": [P, I, I, I, I, P, I, I, P, P, P, P, P, S],
+    "ragk_ivf_search": [P, I, I, P, I, P, I, P, P, P, I, P, P, P, P, S],
+    "ragk_kmeans_assign": [P, I, I, P, P, I, P, P, P, S],
     "ragk_l2_scatter": [P, I, I, P, P, I, S],
     "ragk_prefetch": [P, ctypes.c_longlong, I, P, S],
     "ragk_spin_us": [I, S],
@@ -120,12 +120,41 @@ def lib():
                 "gfx950 kernel library not built (%s). Run `python -m rag_llm_k8s_amd._build` "
                 "or __graft_entry__.build()." % LIB_PATH)
         h = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        _check_stamp(h)
         for name, args in _SIGS.items():
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = _RESTYPES.get(name, ctypes.c_int)
         _lib = h
         return h
+
+
+def _check_stamp(h):
+    """The library must have been built from the kernel sources in this tree (content hash compiled in
+    by _build.build_hip). RAGK_ALLOW_STALE_LIB=1 skips the check (kernel A/B work only)."""
+    if os.environ.get("RAGK_ALLOW_STALE_LIB") == "1":
+        return
+    from .. import _build
+
+    srcs, _ = _build.hip_sources()
+    if not srcs:  # installed without sources: nothing to compare against
+        return
+    if not hasattr(h, "ragk_build_stamp"):
+        raise NativeLibraryError("%s has no build stamp: rebuild it (python -m rag_llm_k8s_amd._build)" % LIB_PATH)
+    f = h.ragk_build_stamp
+    f.restype = ctypes.c_char_p
+    f.argtypes = []
+    got, want = f().decode(), _build.source_hash()
+    if got != want:
+        raise NativeLibraryError("%s was built from other kernel sources (stamp %s, tree %s): rebuild it "
+                                 "(python -m rag_llm_k8s_amd._build)" % (LIB_PATH, got, want))
+
+
+def build_stamp():
+    h = lib()
+    f = h.ragk_build_stamp
+    f.restype = ctypes.c_char_p
+    return f().decode()
 
 
 def has_symbol(name: str) -> bool:

@@ -749,77 +749,82 @@ def sample_candidates(cand_v, cand_i, temps, top_ks, top_ps, seeds, steps, out_t
 
 # ----------------------------------------------------------------------------- search
 def l2_search(xt, cap, n, q, k, row_begin=0, ids_map=None):
-    """Exact squared-L2 top-k over rows [row_begin, n) of a column-major store xt[d][cap].
-    Returns (D fp32 [nq,k], I int64 [nq,k]) with faiss padding semantics."""
-    _req(xt.dtype == torch.float32 and q.dtype == torch.float32 and q.is_contiguous(), "fp32")
+    """Exact squared-L2 top-k over rows [row_begin, n) of a column-major store xt[d][cap]
+    (csrc/kernels/search.hip: l2_scan with wave-resident running top lists + one list merge).
+    Returns (D fp32 [nq,k], I int64 [nq,k]) with faiss padding semantics (-1, FLT_MAX)."""
+    _req(xt.is_cuda and xt.dtype == torch.float32 and xt.is_contiguous() and xt.dim() == 2, "xt fp32 [d, cap]")
+    _req(q.is_cuda and q.dtype == torch.float32 and q.is_contiguous() and q.dim() == 2, "q fp32 [nq, d]")
     d = xt.shape[0]
     nq = q.shape[0]
     _req(q.shape[1] == d, "dim mismatch")
     _req(1 <= k <= 64, "1 <= k <= 64")
+    _req(xt.shape[1] == cap and 0 <= row_begin <= max(row_begin, n) <= cap, "rows within the store")
+    _req(ids_map is None or (ids_map.dtype == torch.int32 and ids_map.is_cuda and ids_map.numel() >= n), "ids_map")
     L = _lib.lib()
-    G = max(1, -(-(n - row_begin) // 1024))
+    od = torch.empty((nq, k), dtype=torch.float32, device=q.device)
+    oi = torch.empty((nq, k), dtype=torch.int32, device=q.device)
+    if nq == 0:
+        return od, oi.long()
+    G = L.ragk_l2_scan_groups(row_begin, max(n, row_begin), nq)
     pd = torch.empty((nq, G, k), dtype=torch.float32, device=q.device)
     pi = torch.empty((nq, G, k), dtype=torch.int32, device=q.device)
-    check(L.ragk_l2_partial(xt.data_ptr(), cap, d, row_begin, n, q.data_ptr(), nq, k, pd.data_ptr(), pi.data_ptr(),
-                            ptr(ids_map), None, stream_ptr()), "ragk_l2_partial")
-    while G > 1:
-        Go = -(-G // 64)
-        od = torch.empty((nq, Go, k), dtype=torch.float32, device=q.device)
-        oi = torch.empty((nq, Go, k), dtype=torch.int32, device=q.device)
-        check(L.ragk_topk_merge(pd.data_ptr(), pi.data_ptr(), nq, G, k, od.data_ptr(), oi.data_ptr(), stream_ptr()),
-              "ragk_topk_merge")
-        pd, pi, G = od, oi, Go
-    return pd.reshape(nq, k), pi.reshape(nq, k).long()
-
-
-def _merge_all(pd, pi, nq, G, k):
-    L = _lib.lib()
-    while G > 1:
-        Go = -(-G // 64)
-        od = torch.empty((nq, Go, k), dtype=torch.float32, device=pd.device)
-        oi = torch.empty((nq, Go, k), dtype=torch.int32, device=pd.device)
-        check(L.ragk_topk_merge(pd.data_ptr(), pi.data_ptr(), nq, G, k, od.data_ptr(), oi.data_ptr(), stream_ptr()),
-              "ragk_topk_merge")
-        pd, pi, G = od, oi, Go
-    return pd.reshape(nq, k), pi.reshape(nq, k).long()
+    check(L.ragk_l2_search(xt.data_ptr(), cap, d, row_begin, max(n, row_begin), q.data_ptr(), nq, k, ptr(ids_map),
+                           pd.data_ptr(), pi.data_ptr(), od.data_ptr(), oi.data_ptr(), stream_ptr()), "ragk_l2_search")
+    return od, oi.long()
 
 
 def ivf_search(xt, cap, q, probes, offsets, ids_map, k, max_list=None, ends=None):
-    """IVF-Flat scan of the probed lists. probes int32 [nq, nprobe] (device); list i occupies store
-    rows [offsets[i], ends[i]) (ends None: packed lists, offsets has nlist+1 entries); ids_map int32
-    [cap] original id of every store row."""
+    """IVF-Flat scan of the probed lists (one block per (query, probe), wave-resident top lists,
+    then one list merge). probes int32 [nq, nprobe] (device; -1 = no list); list i occupies store rows
+    [offsets[i], ends[i]) (ends None: packed lists, offsets has nlist+1 entries); ids_map int32 [cap]
+    original id of every store row. max_list is accepted for API compatibility (unused)."""
     _req(xt.dtype == torch.float32 and q.dtype == torch.float32 and q.is_contiguous(), "fp32")
     _req(probes.dtype == torch.int32 and offsets.dtype == torch.int32 and ids_map.dtype == torch.int32, "int32")
+    _req(probes.is_contiguous() and probes.is_cuda and offsets.is_cuda and ids_map.is_cuda, "device int32")
     _req(ends is None or (ends.dtype == torch.int32 and ends.is_cuda), "ends int32")
     d = xt.shape[0]
     nq, nprobe = probes.shape
-    _req(1 <= k <= 64 and d <= 2048, "k <= 64, d <= 2048")
-    if max_list is None:
-        max_list = int(((ends - offsets[:ends.numel()]) if ends is not None else (offsets[1:] - offsets[:-1])).max())
-    chunks = max(1, -(-max_list // 1024))
-    G = nprobe * chunks
-    pd = torch.empty((nq, G, k), dtype=torch.float32, device=q.device)
-    pi = torch.empty((nq, G, k), dtype=torch.int32, device=q.device)
-    check(_lib.lib().ragk_ivf_scan(xt.data_ptr(), cap, d, q.data_ptr(), nq, probes.data_ptr(), nprobe, chunks,
-                                   offsets.data_ptr(), ptr(ends), ids_map.data_ptr(), k, pd.data_ptr(),
-                                   pi.data_ptr(), stream_ptr()), "ragk_ivf_scan")
-    return _merge_all(pd, pi, nq, G, k)
+    _req(1 <= k <= 64 and d <= 2048 and nprobe >= 1, "k <= 64, d <= 2048")
+    od = torch.empty((nq, k), dtype=torch.float32, device=q.device)
+    oi = torch.empty((nq, k), dtype=torch.int32, device=q.device)
+    if nq == 0:
+        return od, oi.long()
+    pd = torch.empty((nq, nprobe, k), dtype=torch.float32, device=q.device)
+    pi = torch.empty((nq, nprobe, k), dtype=torch.int32, device=q.device)
+    check(_lib.lib().ragk_ivf_search(xt.data_ptr(), cap, d, q.data_ptr(), nq, probes.data_ptr(), nprobe,
+                                     offsets.data_ptr(), ptr(ends), ids_map.data_ptr(), k, pd.data_ptr(), pi.data_ptr(),
+                                     od.data_ptr(), oi.data_ptr(), stream_ptr()), "ragk_ivf_search")
+    return od, oi.long()
 
 
-def kmeans_assign(x, c, cnorm=None):
+def kmeans_assign(x, c, cnorm=None, scores=None):
     """argmin_j ||x_i - c_j||^2 (ties -> lower j) and that squared distance, on the MFMA distance-GEMM
-    kernel (exact fp32 products). x [n, d], c [k, d] fp32 contiguous on the GPU; d % 64 == 0, <= 1024."""
+    kernel (exact fp32 products). x [n, d], c [k, d] fp32 contiguous on the GPU; d % 64 == 0, <= 1024.
+    scores (optional fp32 [n, k]): receives -(||c_j||^2 - 2 x_i.c_j), the numbers the argmin ranks."""
     _req(x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 2, "x fp32 [n, d]")
     _req(c.is_cuda and c.dtype == torch.float32 and c.is_contiguous() and c.shape[1] == x.shape[1], "c fp32 [k, d]")
     n, d = x.shape
     _req(d % 64 == 0 and d <= 1024, "d % 64 == 0 and d <= 1024")
+    _req(scores is None or (scores.is_cuda and scores.dtype == torch.float32 and scores.is_contiguous()
+                            and tuple(scores.shape) == (n, c.shape[0])), "scores fp32 [n, k]")
     if cnorm is None:
         cnorm = (c * c).sum(1)
     a = torch.empty(n, dtype=torch.int32, device=x.device)
     dist = torch.empty(n, dtype=torch.float32, device=x.device)
     check(_lib.lib().ragk_kmeans_assign(x.data_ptr(), n, d, c.data_ptr(), cnorm.contiguous().data_ptr(), c.shape[0],
-                                        a.data_ptr(), dist.data_ptr(), stream_ptr()), "ragk_kmeans_assign")
+                                        a.data_ptr(), dist.data_ptr(), ptr(scores), stream_ptr()), "ragk_kmeans_assign")
     return a, dist
+
+
+def coarse_probes(x, c, cnorm, nprobe):
+    """IVF coarse search: the nprobe nearest centroids of every row of x (int32 [n, nprobe], ties ->
+    lower id), ranked by the SAME scores kmeans_assign's argmin uses, so top-1 == the list assignment."""
+    n, nl = x.shape[0], c.shape[0]
+    _req(1 <= nprobe <= min(256, nl) and nl <= 24576, "1 <= nprobe <= min(256, nlist), nlist <= 24576")
+    sc = torch.empty((n, nl), dtype=torch.float32, device=x.device)
+    kmeans_assign(x, c, cnorm, scores=sc)
+    _, idx = topk_candidates(sc, nprobe, chunks=1)
+    return idx
 
 
 def l2_scatter(xt, cap, pos, x):

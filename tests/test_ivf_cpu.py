@@ -67,3 +67,32 @@ def test_ivf_low_nprobe_recall_and_roundtrip():
     idx2 = IVFFlatIndex.from_lists(r)
     D2, I2 = idx2.search(torch.from_numpy(q), k)
     assert torch.equal(I, I2) and torch.allclose(D, D2)
+
+
+def test_ivf_cpu_every_vector_found_at_nprobe_1_and_chunked_lists():
+    from rag_llm_k8s_amd.index.ivf import probes
+
+    d = 16
+    xb = _data(1500, d, seed=7)
+    idx = IVFFlatIndex(d, nlist=12, nprobe=1)
+    idx.train(xb)
+    for lo in range(0, 1500, 50):  # many small appends: one chunk per touched list, no re-concatenation
+        idx.add(xb[lo:lo + 50])
+    assert max(len(c) for c in idx._xchunks) > 1
+    x = torch.from_numpy(xb)
+    assert torch.equal(probes(x, idx.centroids, idx._cnorm, 3)[:, 0], assign(x, idx.centroids))
+    D, I = idx.search(x, 1)
+    assert (I[:, 0].numpy() == np.arange(1500)).all()
+    w = idx.snapshot_writer()  # concatenates outside the lock, then compacts what it wrote
+    buf = io.BytesIO()
+    from rag_llm_k8s_amd.index.faiss_io import atomic_write  # noqa: F401  (writer uses it)
+    import tempfile, os
+    p = os.path.join(tempfile.mkdtemp(), "ivf.index")
+    w(p)
+    assert max(len(c) for c in idx._xchunks) == 1
+    r = faiss_io.read_index(p)
+    idx2 = IVFFlatIndex.from_lists(r)
+    D2, I2 = idx2.search(x[:50], 3)
+    D1, I1 = idx.search(x[:50], 3)
+    assert torch.equal(I1, I2)
+    del buf

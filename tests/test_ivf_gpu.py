@@ -55,7 +55,7 @@ def test_ivf_gpu_exact_and_appends():
     # low nprobe: the kernel equals an exact scan of the same probed lists
     idx.nprobe = 6
     D6, I6 = idx.search(q, k)
-    _, probes = idx.quant.search(q, 6)
+    probes = idx._coarse_device(q.to(DEV), 6).cpu()
     Dh, Ih = idx._search_host(q, probes, k)
     assert (I6 == Ih).float().mean() > 0.99
     assert torch.allclose(D6, Dh, rtol=1e-4, atol=1e-2)
@@ -77,3 +77,30 @@ def test_ivf_gpu_reload_from_faiss_lists(tmp_path):
     D2, I2 = idx2.search(q, k)
     assert torch.equal(I, I2) and torch.allclose(D, D2)
     assert (I[:, 0] == torch.arange(0, 6000, 301)).all()
+
+
+def test_ivf_every_stored_vector_found_at_nprobe_1():
+    """Probing and list assignment rank centroids by the same numbers (MFMA scores, ties -> lower
+    id): a query at a stored vector's own position finds it with nprobe = 1 -- including vectors
+    placed exactly half-way between two centroids (ties) and exact duplicates of centroids."""
+    from rag_llm_k8s_amd.index.ivf import IVFFlatIndex, assign, probes
+
+    d = 128
+    xb = _data(3000, d, seed=21, centers=16)
+    idx = IVFFlatIndex(d, device=DEV, nlist=16, nprobe=1)
+    idx.train(xb)
+    c = idx.centroids.cpu().numpy()
+    mids = np.stack([(c[i] + c[(i + 1) % 16]) / 2 for i in range(16)]).astype(np.float32)
+    allx = np.concatenate([xb, mids, c]).astype(np.float32)
+    idx.add(allx)
+    xd = torch.from_numpy(allx).to(DEV)
+    a = assign(xd, idx.centroids, idx._cnorm)
+    p = probes(xd, idx.centroids, idx._cnorm, 4)
+    assert torch.equal(p[:, 0], a)  # top-1 probe == assignment, row by row
+    p1 = probes(xd[:1], idx.centroids, idx._cnorm, 1)  # batch size does not change the ranking
+    assert int(p1[0, 0]) == int(a[0])
+    D, I = idx.search(torch.from_numpy(allx), 1)
+    assert (D[:, 0] <= 1e-3).all()
+    found = I[:, 0].numpy()
+    ok = (found == np.arange(len(allx))) | (D[:, 0].numpy() == 0)
+    assert ok.all()

@@ -1,0 +1,30 @@
+#!/bin/bash
+# Round-3 GPU steps on one MI355X (run via gpurun). STEP selects: search | kernels | suite | bench |
+# prof. Every GPU step has its own time limit; a step that dies of anything but test failures ends the call.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/prof
+STEP=${STEP:-search}
+ok() { rc=$1; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "step failed rc=$rc"; exit $rc; fi; }
+case ",$STEP," in *,search,*)
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_ivf_gpu.py -k "l2_search or ivf or kmeans" -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_search.log 2>&1
+rc=$?; echo "search tests rc=$rc"; tail -15 gpurun_out/pytest_search.log; ok $rc
+timeout -k 10 300 python -u tools/search_bench.py > gpurun_out/search_bench.log 2>&1
+rc=$?; echo "search bench rc=$rc"; cat gpurun_out/search_bench.log; ok $rc
+;; esac
+case ",$STEP," in *,suite,*)
+timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "suite rc=$rc"; tail -15 gpurun_out/pytest_gpu.log; ok $rc
+;; esac
+case ",$STEP," in *,bench,*)
+timeout -k 10 600 python -u bench.py --steps ${BSTEPS:-3} --warmup 1 --json-out gpurun_out/bench.json > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -2 gpurun_out/bench.log; ok $rc
+;; esac
+case ",$STEP," in *,prof,*)
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 1 --warmup 0 --c1 ${PROF_C1:-0} > gpurun_out/prof.log 2>&1
+rc=$?; echo "prof rc=$rc"
+rm -f gpurun_out/prof/*kernel_trace.csv
+python tools/rocprof_summary.py gpurun_out/prof/run_kernel_stats.csv 40 > gpurun_out/rocprof_summary.txt 2>&1
+head -30 gpurun_out/rocprof_summary.txt; ok $rc
+;; esac
+exit 0

@@ -1,0 +1,48 @@
+"""Flat L2 top-k (csrc/kernels/search.hip) on one MI355X: wall time per search call (CUDA events,
+median of 20, index warm in HBM/MALL as in serving) and the effective read rate of the index.
+Shapes of the SURVEY V2 targets: 10k x 384 (MiniLM, bench corpus) at nq = 1 / 32, 1M x 1024 (bge
+scale) at nq = 1 / 32. Prints one JSON line per shape."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from rag_llm_k8s_amd.ops import native as N  # noqa: E402
+
+
+def timed(fn, iters=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(True), torch.cuda.Event(True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    return sorted(ts)[len(ts) // 2]
+
+
+def main():
+    shapes = [(10000, 384, 1, 4), (10000, 384, 32, 4), (10000, 1024, 1, 5), (1000000, 1024, 1, 5),
+              (1000000, 1024, 32, 5), (1000000, 384, 1, 4)]
+    for n, d, nq, k in shapes:
+        torch.manual_seed(0)
+        xt = torch.randn(d, n, device="cuda")
+        q = torch.randn(nq, d, device="cuda")
+        us = timed(lambda: N.l2_search(xt, n, n, q, k))
+        # correctness spot check vs torch (fp32 direct form) on a sample of queries
+        ref = torch.cdist(q[:1].double(), xt.t().double()).pow(2)
+        ri = ref.topk(k, largest=False).indices.cpu()
+        D, I = N.l2_search(xt, n, n, q, k)
+        print(json.dumps(dict(N=n, d=d, nq=nq, k=k, us=round(us, 1), TBps=round(n * d * 4 / us / 1e6, 2),
+                              top1_ok=bool(int(I[0, 0]) == int(ri[0, 0])))), flush=True)
+        del xt
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
