@@ -23,6 +23,15 @@
 // finished call e-1 (stream order), so no peer still reads the half of call e-2 that the
 // next call overwrites, whatever element range any block owns.
 //
+// Fused row-parallel reduction for tensor-parallel decode (ar_add_rmsnorm): the consumer of the
+// split-K o_proj / down GEMMs does the cross-rank reduction itself. Block `row` of every rank sums
+// its fp32 partial slabs of that row, publishes the row in its staging area, waits for block `row`
+// of every peer, then (one-shot) sums all ranks' rows in rank order, or (two-shot) reduces its
+// 1/world column slice in rank order, publishes it as bf16, waits again and gathers the row -- and
+// finishes with the residual add + RMSNorm. Same value on every rank, bit for bit; no standalone
+// all-reduce launch per layer. The row barriers have their own flags / epochs (one per row slot),
+// so a call with M rows advances exactly the epochs of rows 0..M-1, identically on every rank.
+//
 // The whole region is allocated uncached (hipDeviceMallocUncached): payload stores and
 // peer loads bypass the per-XCD L2s; flag stores/polls are system-scope atomics and the
 // reader issues a system-scope acquire after its poll. Every spin is bounded (wall-clock, via
@@ -54,8 +63,19 @@ struct ArFlags {
 
 constexpr size_t FLAG_BYTES = (sizeof(ArFlags) + 4095) & ~size_t(4095);
 
+constexpr int AR_MAX_ROWS = 256;
+struct ArRowFlags {
+  unsigned start[AR_MAX_ROWS][AR_MAX_RANKS];
+  unsigned mid[AR_MAX_ROWS][AR_MAX_RANKS];
+  unsigned epoch[AR_MAX_ROWS];
+};
+constexpr size_t ROW_FLAG_BYTES = (sizeof(ArRowFlags) + 4095) & ~size_t(4095);
+
 struct ArPeers {
   char* base[AR_MAX_RANKS];  // every rank's region (own one included), mapped in this process
+  size_t rows_off;           // fused row area: [ArRowFlags | fp32 stage x2 | bf16 result x2] (0 = none)
+  size_t row_stage_bytes;    // one fp32 staging half: max_rows * max_h * 4
+  size_t row_result_bytes;   // one bf16 result half: max_rows * max_h * 2
   unsigned* host_err;        // host-mapped pinned word: the engine polls it after every step, no sync
   unsigned spin_limit;       // bound of one peer wait, in s_memrealtime ticks (100 MHz)
 };
@@ -163,6 +183,155 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPeers P, int ra
   if (threadIdx.x == 0) mine->epoch[b] = ep;
 }
 
+// Barrier of block `row` with block `row` of every peer over the fused-row flags.
+__device__ bool row_barrier(const ArPeers& P, int rank, int world, int which, int row, unsigned ep) {
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) s_ok = 1;
+  __syncthreads();
+  if (threadIdx.x < world) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: payload visible before the flag
+    ArRowFlags* pf = reinterpret_cast<ArRowFlags*>(P.base[threadIdx.x] + P.rows_off);
+    st_sys(which ? &pf->mid[row][rank] : &pf->start[row][rank], ep);
+    ArRowFlags* mf = reinterpret_cast<ArRowFlags*>(P.base[rank] + P.rows_off);
+    const unsigned* slot = which ? &mf->mid[row][threadIdx.x] : &mf->start[row][threadIdx.x];
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (ld_sys(slot) < ep) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > P.spin_limit) {
+        ArFlags* ef = reinterpret_cast<ArFlags*>(P.base[rank]);
+        st_sys(&ef->error, 1u);
+        if (P.host_err) st_sys(P.host_err, 1u);
+        s_ok = 0;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+__device__ __forceinline__ void ld8f(const char* p, float* f) {
+  const u32x4 a = ld16(p), b = ld16(p + 16);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[i] = __uint_as_float(a[i]);
+    f[4 + i] = __uint_as_float(b[i]);
+  }
+}
+
+constexpr int FR_THREADS = 512;
+constexpr int FR_MAXV = 2;  // 2 x 8 x 512 = 8192 columns in registers
+
+// h[row] = bf16(h[row] + bf16(sum over ranks of sum_s P[s][row])); out[row] = rmsnorm(h[row]) * w
+// (add_partials_rmsnorm_kernel's math with the cross-rank sum inside). grid = M rows.
+template <bool TWO_SHOT>
+__global__ __launch_bounds__(FR_THREADS) void ar_add_rmsnorm_kernel(ArPeers P, int rank, int world,
+                                                                    const float* __restrict__ Pp, int S, int M,
+                                                                    bf16_t* h, int ldh, const bf16_t* __restrict__ w,
+                                                                    bf16_t* out, int ldo, int H, float eps) {
+  __shared__ float red[FR_THREADS / 64];
+  __shared__ unsigned s_ep;
+  const int row = blockIdx.x;
+  ArRowFlags* mine = reinterpret_cast<ArRowFlags*>(P.base[rank] + P.rows_off);
+  if (threadIdx.x == 0) s_ep = mine->epoch[row] + 1;
+  __syncthreads();
+  const unsigned ep = s_ep;
+  const size_t stage_off = P.rows_off + ROW_FLAG_BYTES + (size_t)(ep & 1) * P.row_stage_bytes + (size_t)row * H * 4;
+  const size_t res_off = P.rows_off + ROW_FLAG_BYTES + 2 * P.row_stage_bytes + (size_t)(ep & 1) * P.row_result_bytes +
+                         (size_t)row * H * 2;
+  const int nvec = H >> 3;
+  // 1. this rank's partial row (its split-K slabs summed) -> staging
+#pragma unroll
+  for (int i = 0; i < FR_MAXV; ++i) {
+    const int vi = threadIdx.x + i * FR_THREADS;
+    if (vi < nvec) {
+      float a[8];
+      sum_slabs8(Pp + (size_t)row * H + vi * 8, S, (size_t)M * H, a);
+      f32x4* dst = reinterpret_cast<f32x4*>(P.base[rank] + stage_off + (size_t)vi * 32);
+      dst[0] = f32x4{a[0], a[1], a[2], a[3]};
+      dst[1] = f32x4{a[4], a[5], a[6], a[7]};
+    }
+  }
+  bool ok = row_barrier(P, rank, world, 0, row, ep);
+  float v[FR_MAXV][8];
+  float ss = 0.f;
+  if (!TWO_SHOT) {
+#pragma unroll
+    for (int i = 0; i < FR_MAXV; ++i) {
+      const int vi = threadIdx.x + i * FR_THREADS;
+      if (vi < nvec) {
+        float t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (ok) {
+          for (int p = 0; p < world; ++p) {  // rank order: identical on every rank
+            float f[8];
+            ld8f(P.base[p] + stage_off + (size_t)vi * 32, f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) t[e] += f[e];
+          }
+        }
+        unpack8(*reinterpret_cast<const u32x4*>(h + (size_t)row * ldh + vi * 8), v[i]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[i][e] = bf2f(f2bf(v[i][e] + bf2f(f2bf(t[e]))));
+      }
+    }
+  } else {
+    // 2a. reduce my column slice of the row over all ranks (rank order), publish it as bf16
+    const int per = (nvec + world - 1) / world;
+    const int s0 = min(rank * per, nvec), s1 = min(s0 + per, nvec);
+    for (int vi = s0 + threadIdx.x; vi < s1; vi += FR_THREADS) {
+      float t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (ok) {
+        for (int p = 0; p < world; ++p) {
+          float f[8];
+          ld8f(P.base[p] + stage_off + (size_t)vi * 32, f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t[e] += f[e];
+        }
+      }
+      *reinterpret_cast<u32x4*>(P.base[rank] + res_off + (size_t)vi * 16) = pack8(t);
+    }
+    ok = row_barrier(P, rank, world, 1, row, ep) && ok;
+    // 2b. gather the reduced row (slice owner = vi / per)
+#pragma unroll
+    for (int i = 0; i < FR_MAXV; ++i) {
+      const int vi = threadIdx.x + i * FR_THREADS;
+      if (vi < nvec) {
+        float t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (ok) unpack8(ld16(P.base[vi / per] + res_off + (size_t)vi * 16), t);
+        unpack8(*reinterpret_cast<const u32x4*>(h + (size_t)row * ldh + vi * 8), v[i]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[i][e] = bf2f(f2bf(v[i][e] + t[e]));  // t already bf16-rounded
+      }
+    }
+  }
+  // 3. residual written back, RMSNorm (rmsnorm_kernel's exact order)
+#pragma unroll
+  for (int i = 0; i < FR_MAXV; ++i) {
+    const int vi = threadIdx.x + i * FR_THREADS;
+    if (vi < nvec) {
+      *reinterpret_cast<u32x4*>(h + (size_t)row * ldh + vi * 8) = pack8(v[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += v[i][e] * v[i][e];
+    }
+  }
+  ss = block_sum(ss, red);
+  const float inv = rsqrtf(ss / (float)H + eps);
+#pragma unroll
+  for (int i = 0; i < FR_MAXV; ++i) {
+    const int vi = threadIdx.x + i * FR_THREADS;
+    if (vi < nvec) {
+      float wv[8], o[8];
+      unpack8(*reinterpret_cast<const u32x4*>(w + vi * 8), wv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = wv[e] * bf2f(f2bf(v[i][e] * inv));
+      *reinterpret_cast<u32x4*>(out + (size_t)row * ldo + vi * 8) = pack8(o);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) mine->epoch[row] = ep;
+}
+
 // All-gather: out[p * n16 + v] = rank p's in[v] (16-byte vectors). Used for the vocab-parallel
 // sampler's candidate exchange (a few KB per decode step), so tensor-parallel decode runs with no
 // RCCL call at all and stays inside the captured hipGraph. Same epochs / halves as the all-reduce.
@@ -188,6 +357,7 @@ __global__ __launch_bounds__(AR_THREADS) void allgather_kernel(ArPeers P, int ra
 
 struct ArHandle {
   int rank, world, blocks;
+  int max_rows, max_h;  // fused row area geometry (0 = none)
   size_t data_bytes;  // capacity of one staging half (= max message bytes)
   char* local;
   unsigned* host_err;  // pinned, mapped: host view
@@ -197,18 +367,28 @@ struct ArHandle {
 
 }  // namespace
 
-// Region layout: [flags | stage0 | stage1 | result0 | result1], each stage/result = max_bytes.
+// Region layout: [flags | stage0 | stage1 | result0 | result1], each stage/result = max_bytes, then
+// (max_rows > 0) the fused row area [row flags | fp32 stage x2 | bf16 result x2] of max_rows x max_h.
 // `blocks` (1..80) is the fixed grid of every call on this communicator (same on all ranks).
-RAGK_API void* ragk_ar_create(int rank, int world, long max_bytes, int blocks) {
+RAGK_API void* ragk_ar_create(int rank, int world, long max_bytes, int blocks, int max_rows, int max_h) {
   if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || max_bytes <= 0) return nullptr;
   if (blocks < 1 || blocks > AR_MAX_BLOCKS) return nullptr;
+  if (max_rows < 0 || max_rows > AR_MAX_ROWS || max_h < 0 || max_h > 8 * FR_THREADS * FR_MAXV || max_h % 8) return nullptr;
   ArHandle* h = new ArHandle();
   memset(h, 0, sizeof(*h));
   h->rank = rank;
   h->world = world;
   h->blocks = blocks;
+  h->max_rows = max_h > 0 ? max_rows : 0;
+  h->max_h = max_rows > 0 ? max_h : 0;
   h->data_bytes = ((size_t)max_bytes + 4095) & ~size_t(4095);
-  const size_t total = FLAG_BYTES + 4 * h->data_bytes;
+  size_t total = FLAG_BYTES + 4 * h->data_bytes;
+  if (h->max_rows) {
+    h->peers.rows_off = total;
+    h->peers.row_stage_bytes = ((size_t)h->max_rows * h->max_h * 4 + 4095) & ~size_t(4095);
+    h->peers.row_result_bytes = ((size_t)h->max_rows * h->max_h * 2 + 4095) & ~size_t(4095);
+    total += ROW_FLAG_BYTES + 2 * h->peers.row_stage_bytes + 2 * h->peers.row_result_bytes;
+  }
   void* p = nullptr;
   if (hipExtMallocWithFlags(&p, total, hipDeviceMallocUncached) != hipSuccess) {
     delete h;
@@ -306,6 +486,28 @@ RAGK_API int ragk_ar_allreduce(void* hp, const void* in, void* out, long n, int 
                        (const bf16_t*)in, (bf16_t*)out, n8, h->data_bytes);
   return (int)hipGetLastError();
 }
+
+// Fused decode reduction: P = this rank's fp32 partial slabs [S][M][H]; h [M][ldh] bf16 residual
+// (updated in place), w [H] bf16 norm weight, out [M][ldo] bf16. mode 0 = one-shot, 1 = two-shot.
+RAGK_API int ragk_ar_add_rmsnorm(void* hp, const float* P, int S, int M, void* hres, int ldh, const void* w, void* out,
+                                 int ldo, int H, float eps, int mode, hipStream_t st) {
+  ArHandle* h = (ArHandle*)hp;
+  if (!h || M <= 0) return M == 0 ? 0 : (int)hipErrorInvalidValue;
+  if (!h->max_rows || M > h->max_rows || H > h->max_h || H % 8 || S < 1 || ldh % 8 || ldo % 8 ||
+      ((uintptr_t)P & 15) || ((uintptr_t)hres & 15) || ((uintptr_t)out & 15) || ((uintptr_t)w & 15))
+    return (int)hipErrorInvalidValue;
+  for (int p = 0; p < h->world; ++p)
+    if (!h->peers.base[p]) return (int)hipErrorInvalidValue;
+  if (mode == 1)
+    hipLaunchKernelGGL(ar_add_rmsnorm_kernel<true>, dim3(M), dim3(FR_THREADS), 0, st, h->peers, h->rank, h->world, P, S,
+                       M, (bf16_t*)hres, ldh, (const bf16_t*)w, (bf16_t*)out, ldo, H, eps);
+  else
+    hipLaunchKernelGGL(ar_add_rmsnorm_kernel<false>, dim3(M), dim3(FR_THREADS), 0, st, h->peers, h->rank, h->world, P,
+                       S, M, (bf16_t*)hres, ldh, (const bf16_t*)w, (bf16_t*)out, ldo, H, eps);
+  return (int)hipGetLastError();
+}
+
+RAGK_API int ragk_ar_fused_rows(void* hp) { return hp ? ((ArHandle*)hp)->max_rows : 0; }
 
 // 1 if any bounded spin gave up since creation (a peer never arrived), else 0; < 0 on error.
 RAGK_API int ragk_ar_error(void* hp) {

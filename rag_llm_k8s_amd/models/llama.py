@@ -306,10 +306,15 @@ class LlamaModel:
             h = self.be.gather_rows(h, inp.logits_idx)
         return self.be.rmsnorm(h, self.w.norm, self.cfg.rms_norm_eps)
 
+    def _tp(self):
+        return self.comm is not None and self.comm.size > 1
+
     def _decode_part_ok(self, inp: StepInput, h):
-        if self.comm is not None or inp.meta is None or inp.meta.kind != "decode" or inp.slots is None:
+        if inp.meta is None or inp.meta.kind != "decode" or inp.slots is None:
             return False
         L, M = self.w.layers[0], h.shape[0]
+        if self._tp() and not self.comm.fused_decode_ok(M, h.shape[1]):
+            return False
         return self.be.part_ok(M, L["wqkv"]) and self.be.part_ok(M, L["wo"]) and self.be.part_ok(M, L["wdown"])
 
     def _pf_plan(self, M):
@@ -332,16 +337,32 @@ class LlamaModel:
         norm, down -> next layer's input norm / the final norm), so the reduction adds no launch and
         the GEMMs stream their weights with every load in flight (qkv 26.7 -> 15 us, o_proj 15 -> 11.6,
         down 43 -> 30 at batch 32; tools/bench_decode_gemm.py). Same math and bf16 rounding points as
-        hidden_states (bf16 linear outputs, bf16 residual adds)."""
+        hidden_states (bf16 linear outputs, bf16 residual adds).
+
+        Tensor parallel: the same path on this rank's shard (its heads, its slices of the FFN). The
+        row-parallel o_proj / down reductions happen INSIDE their consumer: comm.add_partials_rmsnorm
+        sums every rank's fp32 slabs over the xGMI peer mappings, adds the residual and normalises in
+        one kernel (csrc/comm/allreduce.hip ar_add_rmsnorm) -- no standalone all-reduce launch, and
+        the row-parallel sum is rounded to bf16 once, as at TP=1. Per layer: qkv GEMM, attention (+RoPE
+        + KV append), o_proj (+ partition merge at batch <= 2), reduce+norm, gate/up, down,
+        reduce+norm. (The batch <= 4 TP=1 fusions that put the input norm into the qkv GEMM and the
+        residual into the down GEMM need the full-rank sum first, so they stay TP=1-only.)"""
         be, w, c = self.be, self.w, self.cfg
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
         M = h.shape[0]
+        tp = self._tp()
+
+        def reduce_norm(P, gamma):
+            if tp:
+                return self.comm.add_partials_rmsnorm(P, h, gamma, c.rms_norm_eps, be)
+            return be.add_partials_rmsnorm(P, h, gamma, c.rms_norm_eps)
+
         attn = torch.empty((M, Hq * D), dtype=h.dtype, device=h.device)
         q = torch.empty((M, Hq * D), dtype=h.dtype, device=h.device)
         layers = w.layers
-        pf = self._pf_plan(M)
+        pf = None if tp else self._pf_plan(M)
         # batch <= 4: the input norm runs inside the qkv GEMM (gemm_part_norm) -- one launch fewer per layer
-        fuse_norm = (DECODE_NORM_FUSED and M <= DECODE_DOWN_SKINNY_MAX_M and not pf
+        fuse_norm = (DECODE_NORM_FUSED and M <= DECODE_DOWN_SKINNY_MAX_M and not pf and not tp
                      and be.part_norm_ok(M, layers[0]["wqkv"]))
         xn = None if fuse_norm else be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
         merge = (DECODE_OPROJ_MERGE and DECODE_ROPE_FUSED and not pf and M <= DECODE_OPROJ_MERGE_MAX_M
@@ -371,10 +392,10 @@ class LlamaModel:
             P = be.gemm_part_merge(attn, inp.meta, L["wo"], Hq) if merge else be.gemm_part(attn, L["wo"])
             if pf:
                 be.pf_arm([(L["wgu"], pf["attn"] // 2, pf["post"])], pf["blocks"])
-            xn = be.add_partials_rmsnorm(P, h, L["ln_post"], c.rms_norm_eps)
+            xn = reduce_norm(P, L["ln_post"])
             a = be.gemm(xn, L["wgu"], epi="silu_mul")
             nxt = layers[li + 1]["ln_in"] if li + 1 < len(layers) else w.norm
-            if M <= DECODE_DOWN_SKINNY_MAX_M:
+            if M <= DECODE_DOWN_SKINNY_MAX_M and not tp:
                 # tiny batch: the register-streaming GEMM with the fused residual + a plain norm beats
                 # the split-K partials + consumer by ~2 us (profiles/decode_gemm_graph_ab_M_r2.log)
                 be.gemm(a, L["wdown"], resid=h, epi="resid", out=h)
@@ -385,7 +406,7 @@ class LlamaModel:
             if pf:
                 be.pf_arm([(layers[li + 1]["wqkv"] if li + 1 < len(layers) else w.lm_head, 0, pf["post"])],
                           pf["blocks"])
-            xn = be.add_partials_rmsnorm(P, h, nxt, c.rms_norm_eps)
+            xn = reduce_norm(P, nxt)
         if inp.logits_idx is not None:
             xn = be.gather_rows(xn, inp.logits_idx)
         return xn

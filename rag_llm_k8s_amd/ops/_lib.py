@@ -81,7 +81,9 @@ _SIGS = {
     "ragk_quant_fp8_rows": [P, I, P, I, P, I, I, S],
     "ragk_gemm_fp8": [P, I, P, I, P, P, I, P, P, I, P, P, I, I, I, I, I, I, S],
     # csrc/comm/allreduce.hip (xGMI peer-mapped all-reduce)
-    "ragk_ar_create": [I, I, ctypes.c_long, I],
+    "ragk_ar_create": [I, I, ctypes.c_long, I, I, I],
+    "ragk_ar_add_rmsnorm": [P, P, I, I, P, I, P, P, I, I, F, I, S],
+    "ragk_ar_fused_rows": [P],
     "ragk_ar_ipc_handle": [P, P],
     "ragk_ar_handle_size": [],
     "ragk_ar_open_peers": [P, P],

@@ -92,6 +92,27 @@ class TPComm:
         dist.all_reduce(x, group=self.group)
         return x
 
+    def add_partials_rmsnorm(self, P: torch.Tensor, h: torch.Tensor, w: torch.Tensor, eps: float, be):
+        """Consumer of a row-parallel split-K decode GEMM (o_proj / down): h <- bf16(h + bf16(sum over
+        ranks and slabs of P)), returns rmsnorm(h) * w. On GPUs one kernel does the cross-rank sum over
+        the peer mappings (no standalone all-reduce launch); elsewhere an fp32 all-reduce of the summed
+        slabs with the same rounding points."""
+        if self.size == 1:
+            return be.add_partials_rmsnorm(P, h, w, eps)
+        self._guard()
+        M, H = h.shape
+        if self.ipc is not None and P.is_cuda and self.ipc.fused_ok(M, H):
+            return self.ipc.add_rmsnorm(P, h, w, eps, torch.empty_like(h))
+        part = P.float().sum(0)
+        dist.all_reduce(part, group=self.group)  # fp32, identical on every rank
+        h.copy_((h.float() + part.to(h.dtype).float()).to(h.dtype))
+        return be.rmsnorm(h, w, eps)
+
+    def fused_decode_ok(self, M: int, H: int) -> bool:
+        """The decode step may use the fused row-parallel reduction at batch M (always true off the
+        peer-mapped path: the fallback is an ordinary all-reduce)."""
+        return self.ipc is None or self.ipc.fused_ok(M, H)
+
     def all_reduce_async(self, x: torch.Tensor):
         """Start an in-place all-reduce of x; returns a handle whose wait() makes the CURRENT stream
         (GPU) or the host (gloo) wait for it. x must not be touched until then."""
@@ -179,6 +200,46 @@ class TPComm:
             dist.all_reduce(y, group=self.group)
             out.copy_(y[self.rank * S:(self.rank + 1) * S])
         return out
+
+
+class SingleRankTPComm:
+    """One-GPU stand-in for rank `rank` of a `size`-way TP group (probes of a TP shard's step time):
+    the model and engine take their TP code paths, and every collective is replaced by a same-sized
+    call of the peer-mapped kernels on a ONE-rank communicator (the barrier and the loads hit local
+    HBM instead of xGMI) -- so launches, kernels and bytes moved per rank are those of the real TP
+    step, minus the xGMI latency."""
+
+    def __init__(self, size, rank, device, max_bytes=None, fused_rows=256, fused_h=8192):
+        from .ipc_allreduce import MAX_BYTES, IPCAllReduce
+
+        self.size, self.rank, self.device = size, rank, device
+        self.group = self.cpu_group = None
+        self.broken = None
+        self.ipc = IPCAllReduce(None, None, 1, 0, device, max_bytes=max_bytes or MAX_BYTES, fused_rows=fused_rows,
+                                fused_h=fused_h)
+
+    def check(self):
+        if self.ipc.error():
+            raise CommError("single-rank peer-mapped kernel timed out")
+
+    def all_reduce(self, x):
+        if self.ipc.fits(x):
+            self.ipc.all_reduce(x)
+        return x
+
+    def add_partials_rmsnorm(self, P, h, w, eps, be):
+        return self.ipc.add_rmsnorm(P, h, w, eps, torch.empty_like(h))
+
+    def fused_decode_ok(self, M, H):
+        return self.ipc.fused_ok(M, H)
+
+    def gather_candidates(self, cv, ci):
+        B, K = cv.shape
+        packed = torch.cat([cv.contiguous().view(torch.int32).reshape(-1), ci.contiguous().reshape(-1)])
+        g = self.ipc.all_gather(packed.repeat(self.size)).view(self.size, 2, B, K)  # size x the bytes
+        gv, gi = g[:, 0].view(torch.float32), g[:, 1]
+        return (gv.permute(1, 0, 2).reshape(B, self.size * K).contiguous(),
+                gi.permute(1, 0, 2).reshape(B, self.size * K).contiguous())
 
 
 class _Done:

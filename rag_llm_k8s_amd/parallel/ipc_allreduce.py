@@ -26,22 +26,32 @@ ONE_SHOT_MAX = int(os.environ.get("RAGK_AR_ONESHOT_MAX", str(512 << 10)))
 SPIN_LIMIT = int(os.environ.get("RAGK_AR_TIMEOUT_US", "0"))  # 0 = kernel default (5 s per peer wait)
 MAX_BYTES = int(os.environ.get("RAGK_AR_MAX_BYTES", str(8 << 20)))
 BLOCKS = int(os.environ.get("RAGK_AR_BLOCKS", "64"))
+# fused decode reduction (ar_add_rmsnorm): row slots and max hidden size of the row area
+FUSED_ROWS = int(os.environ.get("RAGK_AR_FUSED_ROWS", "256"))
+FUSED_H = int(os.environ.get("RAGK_AR_FUSED_H", "8192"))
+# one-shot (every rank reads every peer's fp32 row) while the total read stays below this; two-shot
+# (reduce-scatter of column slices + gather of the bf16 slices, 2 barriers) above it
+FUSED_ONESHOT_BYTES = int(os.environ.get("RAGK_AR_FUSED_ONESHOT_BYTES", str(512 << 10)))
 
 
 class IPCAllReduce:
-    def __init__(self, group, cpu_group, size, rank, device, max_bytes=MAX_BYTES, blocks=BLOCKS, spin_limit=None):
-        """spin_limit: bound of one peer wait inside the kernels, in microseconds (None: env / 5 s)."""
+    def __init__(self, group, cpu_group, size, rank, device, max_bytes=MAX_BYTES, blocks=BLOCKS, spin_limit=None,
+                 fused_rows=FUSED_ROWS, fused_h=FUSED_H):
+        """spin_limit: bound of one peer wait inside the kernels, in microseconds (None: env / 5 s).
+        fused_rows / fused_h: geometry of the fused decode-reduction area (0 rows = none)."""
         if size > 8:
             raise ValueError("peer-mapped all-reduce supports <= 8 ranks (one xGMI node)")
         self.size, self.rank, self.device = size, rank, torch.device(device)
         L = _lib.lib()
         self.L = L
+        self.fused_h = int(fused_h) if fused_rows else 0
         with torch.cuda.device(self.device):
-            h = L.ragk_ar_create(rank, size, int(max_bytes), int(blocks))
+            h = L.ragk_ar_create(rank, size, int(max_bytes), int(blocks), int(fused_rows), self.fused_h)
         if not h:
             raise _lib.NativeLibraryError("ragk_ar_create failed (uncached HBM allocation)")
         self.h = ctypes.c_void_p(h)
         self.max_bytes = int(L.ragk_ar_max_bytes(self.h))
+        self.fused_rows = int(L.ragk_ar_fused_rows(self.h))
         spin = SPIN_LIMIT if spin_limit is None else int(spin_limit)
         if spin > 0:
             self.set_timeout_us(spin)
@@ -106,6 +116,29 @@ class IPCAllReduce:
         if not (out.is_contiguous() and out.numel() == self.size * x.numel() and out.dtype == x.dtype):
             raise ValueError("IPC all-gather: out must hold world * x")
         check(self.L.ragk_ar_allgather(self.h, x.data_ptr(), out.data_ptr(), nb, stream_ptr()), "ragk_ar_allgather")
+        return out
+
+    def fused_ok(self, M: int, H: int) -> bool:
+        return 0 < M <= self.fused_rows and H <= self.fused_h and H % 8 == 0
+
+    def add_rmsnorm(self, P: torch.Tensor, h: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor,
+                    mode: int | None = None):
+        """Fused row-parallel reduction of a split-K decode GEMM's fp32 slabs P [S, M, H] across the TP
+        ranks + residual add into h [M, H] (bf16, in place) + RMSNorm -> out (csrc/comm/allreduce.hip
+        ar_add_rmsnorm). Every rank computes the same bits."""
+        S, M, H = P.shape
+        ok = (P.is_cuda and P.dtype == torch.float32 and P.is_contiguous() and h.dtype == torch.bfloat16
+              and h.shape == (M, H) and h.stride(1) == 1 and out.shape == (M, H) and out.stride(1) == 1
+              and w.dtype == torch.bfloat16 and w.is_contiguous() and w.numel() == H and self.fused_ok(M, H)
+              and h.stride(0) % 8 == 0 and out.stride(0) % 8 == 0)
+        if not ok:
+            raise ValueError("fused all-reduce+rmsnorm: P fp32 [S, M, H], h / out bf16 [M, H], M <= %d, H <= %d"
+                             % (self.fused_rows, self.fused_h))
+        if mode is None:
+            mode = 0 if M * H * 4 * self.size <= FUSED_ONESHOT_BYTES else 1
+        check(self.L.ragk_ar_add_rmsnorm(self.h, P.data_ptr(), S, M, h.data_ptr(), h.stride(0), w.data_ptr(),
+                                         out.data_ptr(), out.stride(0), H, float(eps), int(mode), stream_ptr()),
+              "ragk_ar_add_rmsnorm")
         return out
 
     def gather_fits(self, x: torch.Tensor) -> bool:

@@ -154,7 +154,9 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     t0 = time.time()
     wm = WordModel(n_words=word_vocab, seed=seed)
     lcfg = {"8b": L.llama31_8b, "70b": L.llama31_70b,
-            "tiny": lambda: L.llama_tiny(vocab=1024, layers=2, hidden=512, heads=4, kv_heads=2, inter=512)}[model]()
+            "tiny": lambda: L.llama_tiny(vocab=1024, layers=2, hidden=512, heads=4, kv_heads=2, inter=512),
+            # TP=4/8 layouts: 8 KV heads (1 per rank at TP=8, as Llama-3.1 8B/70B), vocab % 8 != 0
+            "tiny8": lambda: L.llama_tiny(vocab=1001, layers=2, hidden=512, heads=16, kv_heads=8, inter=1024)}[model]()
     ecfg = {"minilm": E.minilm_l6, "bge-large": E.bge_large_en, "bge-m3": E.bge_m3,
             "tiny": lambda: E.EncoderConfig(vocab_size=2048, hidden_size=128, num_hidden_layers=2,
                                             num_attention_heads=4, intermediate_size=256, max_seq_length=128)}[embedder]()

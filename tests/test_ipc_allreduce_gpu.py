@@ -1,9 +1,10 @@
-"""T3 comm tier on one GPU: the peer-mapped all-reduce (csrc/comm/allreduce.hip) with two ranks.
+"""T3 comm tier on one GPU: the peer-mapped all-reduce / all-gather and the fused decode reduction
+(csrc/comm/allreduce.hip) with 2, 4 and 8 ranks.
 
-Both ranks live on the same MI355X (the gpurun box has one GPU); the mechanism is the one the
-8-GPU node uses -- each rank maps the other's uncached staging region through a hipIpc handle
-exchanged over gloo -- only the xGMI hop is replaced by local HBM. Oracle: fp32 sum of both
-ranks' bf16 inputs, rounded once (what the kernel computes, in rank order).
+All ranks live on the same MI355X (the gpurun box has one GPU); the mechanism is the one the
+8-GPU node uses -- each rank maps every other rank's uncached staging region through a hipIpc
+handle exchanged over gloo -- only the xGMI hop is replaced by local HBM. Oracle: fp32 sum of the
+ranks' inputs in rank order, rounded once (what the kernels compute).
 """
 import os
 import socket
@@ -32,15 +33,17 @@ def _inputs(rank, n, it):
     return torch.randn(n, generator=g).bfloat16()
 
 
-def _worker(rank, port, d):
+def _worker(rank, port, d, WORLD=WORLD):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     torch.cuda.set_device(0)
     from rag_llm_k8s_amd.parallel.ipc_allreduce import IPCAllReduce
 
-    ar = IPCAllReduce(None, None, WORLD, rank, "cuda:0", max_bytes=4 << 20, blocks=32)
+    ar = IPCAllReduce(None, None, WORLD, rank, "cuda:0", max_bytes=4 << 20, blocks=32, fused_rows=64, fused_h=4096)
     res = {}
     try:
+        mine = torch.arange(40, dtype=torch.int32, device="cuda") + 1000 * rank  # all-gather
+        res["gather"] = ar.all_gather(mine).cpu()
         for n in SIZES:
             for mode in (0, 1):
                 outs = []
@@ -79,11 +82,27 @@ def _worker(rank, port, d):
         dist.destroy_process_group()
 
 
-def test_ipc_allreduce_two_ranks(native):
+def _spawn(target, world, d, port):
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=target, args=(r, port, d, world)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+            p.join()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return [torch.load(os.path.join(d, "r%d.pt" % r), weights_only=False) for r in range(world)]
+
+
+@pytest.mark.parametrize("WORLD", [2, 4, 8])
+def test_ipc_allreduce_ranks(native, WORLD):
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.get_context("spawn")
-        procs = [ctx.Process(target=_worker, args=(r, port, d)) for r in range(WORLD)]
+        procs = [ctx.Process(target=_worker, args=(r, port, d, WORLD)) for r in range(WORLD)]
         for p in procs:
             p.start()
         for p in procs:
@@ -96,7 +115,10 @@ def test_ipc_allreduce_two_ranks(native):
         out = [torch.load(os.path.join(d, "r%d.pt" % r), weights_only=False) for r in range(WORLD)]
 
     def ref(n, it):
-        return sum(_inputs(r, n, it).float() for r in range(WORLD)).bfloat16()
+        acc = torch.zeros(n)
+        for r in range(WORLD):  # rank order, fp32
+            acc = acc + _inputs(r, n, it).float()
+        return acc.bfloat16()
 
     for n in SIZES:
         for mode in (0, 1):
@@ -106,7 +128,108 @@ def test_ipc_allreduce_two_ranks(native):
                     got = out[r][(n, mode)][it]
                     assert torch.equal(got, want), (n, mode, it, r, (got.float() - want.float()).abs().max())
     for r in range(WORLD):
+        assert torch.equal(out[r]["gather"], torch.cat([torch.arange(40, dtype=torch.int32) + 1000 * p
+                                                        for p in range(WORLD)]))
         assert torch.equal(out[r]["inplace"], ref(8 * 4096, 99))
         for it in range(3):
             assert torch.equal(out[r]["graph"][it], ref(8 * 4096, 200 + it))
         assert out[r]["error"] is False
+
+
+# ---------------------------------------------------------------- fused decode reduction
+H_F = 4096
+FUSED_CASES = [(1, 1), (3, 2), (32, 1), (5, 4), (1, 3), (17, 1)]  # (M rows, S slabs): varying grids
+
+
+def _partials(rank, M, S, it):
+    g = torch.Generator().manual_seed(7919 * rank + 131 * M + 17 * S + it)
+    return torch.randn(S, M, H_F, generator=g) * 0.05
+
+
+def _fused_worker(rank, port, d, WORLD):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    torch.cuda.set_device(0)
+    from rag_llm_k8s_amd.parallel.ipc_allreduce import IPCAllReduce
+
+    ar = IPCAllReduce(None, None, WORLD, rank, "cuda:0", max_bytes=1 << 20, blocks=16, fused_rows=64, fused_h=H_F)
+    res = {}
+    g = torch.Generator().manual_seed(5)
+    w = (1 + 0.1 * torch.randn(H_F, generator=g)).bfloat16().cuda()
+    try:
+        for mode in (0, 1):
+            for it, (M, S) in enumerate(FUSED_CASES):
+                h = (torch.randn(M, H_F, generator=torch.Generator().manual_seed(M + it))).bfloat16().cuda()
+                P = _partials(rank, M, S, it).cuda()
+                out = torch.empty_like(h)
+                ar.add_rmsnorm(P, h, w, 1e-5, out, mode=mode)
+                res[(mode, it)] = (h.cpu(), out.cpu())
+        # captured in a graph, replayed with new partials (row epochs advance inside the graph)
+        M, S = 4, 2
+        P = torch.zeros(S, M, H_F, device="cuda")
+        h = torch.zeros(M, H_F, dtype=torch.bfloat16, device="cuda")
+        out = torch.empty_like(h)
+        gr = torch.cuda.CUDAGraph()
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            with torch.cuda.graph(gr, stream=st):
+                ar.add_rmsnorm(P, h, w, 1e-5, out)
+        torch.cuda.current_stream().wait_stream(st)
+        gl = []
+        for it in range(3):
+            P.copy_(_partials(rank, M, S, 100 + it).cuda())
+            h.copy_(torch.ones(M, H_F).bfloat16())
+            dist.barrier()
+            gr.replay()
+            torch.cuda.synchronize()
+            gl.append((h.cpu().clone(), out.cpu().clone()))
+        res["graph"] = gl
+        res["error"] = ar.error()
+    finally:
+        torch.cuda.synchronize()
+        dist.barrier()
+        ar.close()
+        torch.save(res, os.path.join(d, "r%d.pt" % rank))
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("WORLD", [2, 4, 8])
+def test_fused_allreduce_add_rmsnorm(native, WORLD):
+    """h <- bf16(h + bf16(sum over ranks (rank order) of sum over slabs (slab order) of P)), out = rmsnorm(h):
+    the residual stream is exact vs an fp32 oracle, identical on every rank (bit for bit) in both the
+    one-shot and the two-shot mode, for varying row counts, and inside a replayed graph."""
+    from rag_llm_k8s_amd.ops import reference as R
+
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        out = _spawn(_fused_worker, WORLD, d, port)
+    w = (1 + 0.1 * torch.randn(H_F, generator=torch.Generator().manual_seed(5))).bfloat16()
+
+    def ref(M, S, it, h0):
+        tot = torch.zeros(M, H_F)
+        for r in range(WORLD):
+            P = _partials(r, M, S, it)
+            a = torch.zeros(M, H_F)
+            for s in range(S):
+                a = a + P[s]
+            tot = tot + a
+        return (h0.float() + tot.bfloat16().float()).bfloat16()
+
+    for mode in (0, 1):
+        for it, (M, S) in enumerate(FUSED_CASES):
+            h0 = torch.randn(M, H_F, generator=torch.Generator().manual_seed(M + it)).bfloat16()
+            want = ref(M, S, it, h0)
+            for r in range(WORLD):
+                h, o = out[r][(mode, it)]
+                assert torch.equal(h, want), (mode, it, r)
+                assert torch.equal(o, out[0][(mode, it)][1])
+                ro = R.rmsnorm(want, w, 1e-5)
+                assert ((o.float() - ro.float()).abs().max() <= 0.02 * ro.float().abs().max()), (mode, it)
+    for mode_it in [(0, i) for i in range(len(FUSED_CASES))]:  # one-shot == two-shot, bit for bit
+        assert torch.equal(out[0][mode_it][1], out[0][(1, mode_it[1])][1])
+    for it in range(3):
+        want = ref(4, 2, 100 + it, torch.ones(4, H_F).bfloat16())
+        for r in range(WORLD):
+            assert torch.equal(out[r]["graph"][it][0], want)
+    assert all(out[r]["error"] is False for r in range(WORLD))

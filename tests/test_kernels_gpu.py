@@ -354,7 +354,10 @@ def test_attn_encoder_contig(native, D, H):
 
 
 @pytest.mark.parametrize("kv_lens,Hq,Hkv,target", [([1], 32, 8, 1024), ([65, 300, 4100], 32, 8, 1024),
-                                                   ([777, 5], 32, 8, 8), ([200], 8, 8, 64)])
+                                                   ([777, 5], 32, 8, 8), ([200], 8, 8, 64),
+                                                   # per-rank head layouts at TP=8: 8B (4, 1), 70B (8, 1); TP=4: (8, 2)
+                                                   ([5200, 1, 64], 4, 1, 1024), ([65, 3000], 8, 1, 1024),
+                                                   ([4100, 700], 8, 2, 256), ([1], 4, 1, 8)])
 def test_attn_decode(native, kv_lens, Hq, Hkv, target):
     D = 128
     torch.manual_seed(11)
@@ -403,12 +406,14 @@ def test_attn_decode_fused_merge_matches_separate_and_resets(native):
     assert int(native._attn_counters(DEV)[:B * Hkv].abs().sum()) == 0
 
 
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (4, 1), (8, 1)])
 @pytest.mark.parametrize("kv_lens,target", [([1], 1024), ([5200, 1, 64, 65, 3000, 700], 1024), ([777, 129], 8)])
-def test_attn_decode_rope_matches_unfused(native, kv_lens, target):
+def test_attn_decode_rope_matches_unfused(native, kv_lens, target, Hq, Hkv):
     """attn_decode_rope (q/k RoPE + KV append from the qkv partial slabs inside the attention kernel)
     == rope_kv_partials + attn_decode: same attention output and same cache contents, bit for bit
-    (new token at the end of a block, at a block start, and as the only token)."""
-    D, Hq, Hkv, S = 128, 32, 8, 8
+    (new token at the end of a block, at a block start, and as the only token), at the TP=1 heads and
+    the per-rank heads of TP=8 (8B: 4 q / 1 kv, 70B: 8 / 1)."""
+    D, S = 128, 8
     torch.manual_seed(14)
     kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=5)
     B = len(kv_lens)
@@ -490,17 +495,20 @@ def test_prefill_splitk_model_matches_resid_path(native):
     assert rel_err(outs[1], outs[0]) < 2e-2, rel_err(outs[1], outs[0])
 
 
-@pytest.mark.parametrize("kv_lens,target,fp8", [([5200], 512, False), ([70, 3000], 256, False), ([5200, 64], 256, False),
-                                                ([777, 5300, 65, 2000], 512, False), ([4100], 1024, True),
-                                                ([8100], 512, False)])
-def test_gemm_part_merge_matches_reduce_then_part(native, kv_lens, target, fp8):
+@pytest.mark.parametrize("kv_lens,target,fp8,Hq,Hkv", [([5200], 512, False, 32, 8), ([70, 3000], 256, False, 32, 8),
+                                                        ([5200, 64], 256, False, 32, 8),
+                                                        ([777, 5300, 65, 2000], 512, False, 32, 8),
+                                                        ([4100], 1024, True, 32, 8), ([8100], 512, False, 32, 8),
+                                                        ([5200], 1024, False, 4, 1), ([5200, 70], 1024, False, 8, 1),
+                                                        ([3000], 512, True, 4, 1)])
+def test_gemm_part_merge_matches_reduce_then_part(native, kv_lens, target, fp8, Hq, Hkv):
     """o_proj fed by the UNMERGED split-K decode attention (attn_decode_rope with defer_merge, the
     partitions merged per K-slice inside gemm_part_merge) == attn_decode_rope (reduce launch) followed
     by gemm_part: same slabs up to fp32 summation order (bf16 activation may differ by 1 ulp), and vs an
     fp32 oracle of the attention output. Covers single-partition rows, mixed lengths, M = 1..4, fp8."""
     from rag_llm_k8s_amd.ops.fp8 import quantize_weight
 
-    D, Hq, Hkv, S = 128, 32, 8, 8
+    D, S = 128, 8
     torch.manual_seed(21)
     kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=7)
     B = len(kv_lens)

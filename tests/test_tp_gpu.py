@@ -89,6 +89,34 @@ def _prefill_logits(model, ids):
     return model.forward(inp)
 
 
+def _prefill_decode_logits(model, ids, nxt):
+    """Prefill `ids`, then one decode step of token `nxt` through the model's decode path (the split-K
+    GEMMs with the row-parallel reduction fused into the RMSNorm under TP): its logits (vocab shard)."""
+    from rag_llm_k8s_amd.models.llama import StepInput
+    from rag_llm_k8s_amd.ops.backend import AttnMeta
+    from rag_llm_k8s_amd.ops.native import build_prefill_tiles, decode_partitions
+
+    n = len(ids)
+    nb = -(-(n + 1) // 64)
+    model.allocate_kv_cache(nb + 2)
+    dev = model.device
+    i32 = dict(dtype=torch.int32, device=dev)
+    bt = torch.zeros((1, nb + 1), **i32)
+    bt[0, :nb] = torch.arange(1, nb + 1, **i32)
+    meta = AttnMeta("prefill", torch.tensor([n], **i32), bt, cu_q=torch.tensor([0, n], **i32),
+                    tiles=build_prefill_tiles([n], model.Hq, model.Hkv).to(dev), host_kv_lens=[n], host_q_lens=[n])
+    model.forward(StepInput(torch.tensor(ids, **i32), torch.arange(n, **i32), torch.arange(64, 64 + n, **i32), meta,
+                            torch.tensor([n - 1], **i32)))
+    pt, mp = decode_partitions(8192, 1, model.Hkv)
+    ws_o = torch.empty((1, model.Hq, mp, model.D), dtype=torch.float32, device=dev) if mp > 1 else None
+    ws_ml = torch.empty((1, model.Hq, mp, 2), dtype=torch.float32, device=dev) if mp > 1 else None
+    dm = AttnMeta("decode", torch.tensor([n + 1], **i32), bt, part_tiles=pt, max_parts=mp, ws_o=ws_o, ws_ml=ws_ml)
+    h = torch.empty((1, model.cfg.hidden_size), dtype=torch.bfloat16, device=dev)
+    inp = StepInput(torch.tensor([nxt], **i32), torch.tensor([n], **i32), torch.tensor([64 + n], **i32), dm, None)
+    assert model._decode_part_ok(inp, h)
+    return model.forward(inp)
+
+
 def _init(rank, port):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
                       LOCAL_RANK="0", RAGK_TP_CONTROL="gloo")
@@ -117,20 +145,27 @@ def _tp_worker(rank, port, d):
         local = _prefill_logits(m, ids)  # [1, V/2] this rank's vocab shard
         full = comm.ipc.all_gather(local.contiguous()).view(WORLD, 1, -1)
         res["tp_logits"] = torch.cat([full[r] for r in range(WORLD)], 1)[:, :cfg.vocab_size].cpu()
+        local = _prefill_decode_logits(m, ids, 77)  # decode: fused row-parallel reduction
+        full = comm.ipc.all_gather(local.contiguous()).view(WORLD, 1, -1)
+        res["tp_dec_logits"] = torch.cat([full[r] for r in range(WORLD)], 1)[:, :cfg.vocab_size].cpu()
         if rank == 0:
             ref = LlamaModel(cfg, LlamaWeights.from_state_dict(cfg, sd, ctx.device), ctx.device, max_positions=4096)
             res["ref_logits"] = _prefill_logits(ref, ids).cpu()
+            res["ref_dec_logits"] = _prefill_decode_logits(ref, ids, 77).cpu()
             del ref
         del sd
         torch.cuda.empty_cache()
 
         # engine: graph-captured + asynchronous decode vs eager synchronous, sampled and greedy
-        prompts = [torch.randint(3, cfg.vocab_size, (n,), generator=gen).tolist() for n in (100, 260, 37)]
+        # the 1100-token prompt makes the first prefill step >= RAGK_TP_OVERLAP_MIN (1024): two
+        # micro-batches with the peer-mapped all-reduce on the side stream overlapping the next one
+        prompts = [torch.randint(3, cfg.vocab_size, (n,), generator=gen).tolist() for n in (100, 1100, 37)]
         sampled = SamplingParams(max_new_tokens=12, temperature=0.7, top_p=0.9, top_k=50, ignore_eos=True)
         greedy = SamplingParams(max_new_tokens=12, do_sample=False, ignore_eos=True)
         for graphs in (True, False):
-            eng = LLMEngine(m, num_blocks=64, max_batch=4, max_model_len=1024, use_graphs=graphs,
+            eng = LLMEngine(m, num_blocks=64, max_batch=4, max_model_len=2048, use_graphs=graphs,
                             tp_group=ctx.tp_group, graph_buckets=[1, 2, 4])
+            assert eng.tp_overlap_min_tokens <= 1237
             if graphs:
                 eng.warmup_graphs()
             res[("sampled", graphs)] = eng.generate(prompts, sampled, seeds=[11, 12, 13])
@@ -175,6 +210,11 @@ def test_tp2_llama8b_widths_on_one_gpu(native):
         assert rel < 2e-2, (r, rel)
         assert out[r]["error"] is False
     assert torch.equal(out[0]["tp_logits"], out[1]["tp_logits"])
+    dref = out[0]["ref_dec_logits"]
+    for r in range(WORLD):
+        rel = ((out[r]["tp_dec_logits"] - dref).norm() / dref.norm()).item()
+        assert rel < 2e-2, ("decode", r, rel)
+    assert torch.equal(out[0]["tp_dec_logits"], out[1]["tp_dec_logits"])
     for r in range(WORLD):
         assert out[r][("async", True)] is True
         for kind in ("sampled", "greedy"):
