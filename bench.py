@@ -9,12 +9,15 @@ tokenize -> continuous-batching prefill + hipGraph decode (temperature 0.7, top-
 150 tokens, EOS ignored so every request produces exactly 150 tokens) -> detokenize ->
 "Chatbot:" post-processing.
 
-Multi-GPU: one process per GPU (torchrun). With N > 1 GPUs the default layout is BASELINE config 3:
-ONE tensor-parallel engine over all N GPUs (Megatron TP over xGMI: peer-mapped all-reduce /
-all-gather kernels for decode-sized messages, RCCL for bulk prefill all-reduces, overlapped with
-the next micro-batch's GEMMs), with the concurrency scaled to 32 x N queries per step (weak
-scaling: per-GPU work fixed). `--dp` runs N independent data-parallel replicas instead (k8s
-replicas behind the Service); `--tp T` picks any TP degree dividing N (tp x dp layouts).
+Multi-GPU: one process per GPU (torchrun), weak scaling (32 concurrent queries per GPU per step).
+The default layout is N data-parallel replicas (TP=1 engines, the k8s replicas behind the Service):
+an 8B model plus its KV cache fits one 288 GB GPU many times over, and on this workload tensor
+parallelism only adds xGMI traffic -- a TP=8 step all-reduces ~11 GB per layer-half of prefill
+activations (docs/PERF_NOTES.md, "TP=8 budget"), so a TP=8 engine is comm-bound in prefill while
+its per-rank decode gains do not make up for it. `--tp T` runs T-way tensor-parallel engines
+(Megatron TP over xGMI: the fused peer-mapped reduction in decode, RCCL / peer-mapped all-reduces
+overlapped with the next micro-batch in prefill; BASELINE config 3 is `--tp 8`), tp x dp layouts
+for T < N.
 
 value = total generated tokens of all ranks / max-over-ranks wall time of the K timed steps.
 p50_latency_ms is the wave latency of a step; p50_latency_c1_ms the single-query latency (C=1,
@@ -39,8 +42,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--concurrency", type=int, default=None,
                     help="concurrent queries per engine (TP group) per step; default 32 x TP degree")
-    ap.add_argument("--tp", type=int, default=None, help="TP degree (default: all N GPUs, or 1 with --dp)")
-    ap.add_argument("--dp", action="store_true", help="N data-parallel replicas (TP=1) instead of one TP=N engine")
+    ap.add_argument("--tp", type=int, default=None, help="TP degree per engine (default 1: N data-parallel replicas)")
+    ap.add_argument("--dp", action="store_true", help="N data-parallel replicas (the default; kept for compatibility)")
     ap.add_argument("--model", default="8b", choices=["8b", "70b", "tiny"])
     ap.add_argument("--embedder", default="minilm", choices=["minilm", "bge-large", "bge-m3", "tiny"])
     ap.add_argument("--chunks", type=int, default=10000)
@@ -86,8 +89,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
-    if a.tp is None:
-        a.tp = 1 if a.dp else world
+    if a.tp is None or a.dp:
+        a.tp = 1
     if a.concurrency is None:
         a.concurrency = 32 * a.tp
     if int(os.environ.get("LOCAL_RANK", "0")) == 0:
@@ -113,10 +116,14 @@ def main():
         seeds = [1000 * (step_id + 1000) + i for i in range(len(qs))]
         return svc.generate_batch(qs, params=params, seeds=seeds)
 
+    def sync():  # the CPU plumbing rehearsal (gloo) has no device to synchronise
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
     for w in range(a.warmup):
         run_step(-1 - w)
     D.barrier(ctx)
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     lat, ttft, ptoks, gtoks, step_ms = [], [], [], [], []
     for s in range(a.steps):
@@ -129,7 +136,7 @@ def main():
                 ttft.append(o["_ttft_s"] * 1e3)
                 ptoks.append(o["_prompt_tokens"])
                 gtoks.append(o["_gen_tokens"])
-    torch.cuda.synchronize()
+    sync()
     D.barrier(ctx)
     elapsed = time.perf_counter() - t0
     # single-request latency (the reference serves one query per /generate call): outside the timed

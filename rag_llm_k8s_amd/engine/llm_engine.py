@@ -655,6 +655,8 @@ class LLMEngine:
         return entry
 
     def warmup_graphs(self, sizes=None):
+        if not self.is_cuda:  # CPU plumbing: eager decode, nothing to capture
+            return
         for b in sizes or self.buckets:
             self._decode_graph(b)
 

@@ -12,6 +12,19 @@ rc=$?; echo "search tests rc=$rc"; tail -15 gpurun_out/pytest_search.log; ok $rc
 timeout -k 10 300 python -u tools/search_bench.py > gpurun_out/search_bench.log 2>&1
 rc=$?; echo "search bench rc=$rc"; cat gpurun_out/search_bench.log; ok $rc
 ;; esac
+case ",$STEP," in *,tp,*)
+timeout -k 10 900 python -u -m pytest tests/test_ipc_allreduce_gpu.py tests/test_tp_gpu.py -v --timeout 400 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_tp.log 2>&1
+rc=$?; echo "tp tests rc=$rc"; tail -15 gpurun_out/pytest_tp.log; ok $rc
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "attn_decode or gemm_part_merge" -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_attn_tp.log 2>&1
+rc=$?; echo "attn tp-layout tests rc=$rc"; tail -6 gpurun_out/pytest_attn_tp.log; ok $rc
+;; esac
+case ",$STEP," in *,probe,*)
+timeout -k 10 400 python -u tools/tp_decode_probe.py 1 32 > gpurun_out/tp_probe.log 2>&1
+rc=$?; echo "probe rc=$rc"; cat gpurun_out/tp_probe.log | grep -v amdgpu.ids; ok $rc
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_tp -o tp -- python3 tools/tp_decode_probe.py 1 > gpurun_out/tp_probe_prof.log 2>&1
+rc=$?; echo "probe prof rc=$rc"; rm -f gpurun_out/prof_tp/*kernel_trace.csv
+python tools/rocprof_summary.py gpurun_out/prof_tp/tp_kernel_stats.csv 40 > gpurun_out/tp_probe_summary.txt 2>&1; head -45 gpurun_out/tp_probe_summary.txt; ok $rc
+;; esac
 case ",$STEP," in *,suite,*)
 timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "suite rc=$rc"; tail -15 gpurun_out/pytest_gpu.log; ok $rc
