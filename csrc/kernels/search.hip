@@ -74,6 +74,48 @@ __device__ __forceinline__ void wave_offer(float& bv, int& bi, float v, int id, 
   wave_merge64(bv, bi, v, id, lane);
 }
 
+// wave_offer for QB queries at once (the same 64 rows, one candidate per lane and query): the QB
+// bitonic networks run interleaved step by step, so the cross-lane permutes of one query's
+// dependent chain hide behind the others' (one query at a time left a 16-query block
+// latency-bound on ~28 dependent permute round trips per query). Skipped outright when no query's
+// candidates beat its current k-th best.
+template <int QB>
+__device__ __forceinline__ void wave_offer_q(float (&bv)[QB], int (&bi)[QB], float (&v)[QB], int id, int nqb, int k,
+                                             int lane) {
+  bool any = false;
+#pragma unroll
+  for (int q = 0; q < QB; ++q) {
+    if (q < nqb) {
+      const float tv = __shfl(bv[q], k - 1, 64);
+      const int ti = __shfl(bi[q], k - 1, 64);
+      any |= __any(cand_lt(v[q], id, tv, ti));
+    }
+  }
+  if (!any) return;  // wave-uniform
+  int ix[QB];
+#pragma unroll
+  for (int q = 0; q < QB; ++q) ix[q] = id;
+#pragma unroll
+  for (int kk = 2; kk <= 64; kk <<= 1)
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int q = 0; q < QB; ++q) cx(v[q], ix[q], lane, j, (lane & kk) == 0);
+#pragma unroll
+  for (int q = 0; q < QB; ++q) {
+    const float rv = __shfl(v[q], 63 - lane, 64);
+    const int ri = __shfl(ix[q], 63 - lane, 64);
+    if (cand_lt(rv, ri, bv[q], bi[q])) {
+      bv[q] = rv;
+      bi[q] = ri;
+    }
+  }
+#pragma unroll
+  for (int j = 32; j > 0; j >>= 1)
+#pragma unroll
+    for (int q = 0; q < QB; ++q) cx(bv[q], bi[q], lane, j, true);
+}
+
 // Distances of rows [rbase, rbase + 64) (one per lane; rows clamped into [0, cap)) over dims
 // [t0, t1) of the staged chunk starting at dim dc, for QB queries.
 template <int QB>
@@ -163,8 +205,8 @@ __global__ __launch_bounds__(ST) void l2_scan_kernel(const float* __restrict__ x
       const bool ok = row < row_end;
       const int id = ok ? (ids_map ? ids_map[row] : row) : -1;
 #pragma unroll
-      for (int j = 0; j < QB; ++j)
-        if (j < nqb) wave_offer(bv[j], bi[j], ok ? acc[j] : FLT_MAX, id, k, lane);
+      for (int j = 0; j < QB; ++j) acc[j] = (ok && j < nqb) ? acc[j] : FLT_MAX;
+      wave_offer_q<QB>(bv, bi, acc, ok ? id : -1, nqb, k, lane);
     }
   }
   // block merge: the RG list-holding waves (s == 0) -> wave 0 -> k outputs per query

@@ -61,13 +61,15 @@ class IPCAllReduce:
         hs = L.ragk_ar_handle_size()
         buf = ctypes.create_string_buffer(hs)
         check(L.ragk_ar_ipc_handle(self.h, buf), "hipIpcGetMemHandle")
-        handles = [None] * size
-        dist.all_gather_object(handles, bytes(buf.raw), group=cpu_group)
+        handles = [bytes(buf.raw)]
+        if size > 1:  # a one-rank communicator (single-GPU probes) has no peers to map
+            handles = [None] * size
+            dist.all_gather_object(handles, bytes(buf.raw), group=cpu_group)
         joined = ctypes.create_string_buffer(b"".join(handles), hs * size)
         with torch.cuda.device(self.device):
             check(L.ragk_ar_open_peers(self.h, joined), "hipIpcOpenMemHandle")
-        # every rank must have mapped its peers before anyone signals into them
-        dist.barrier(group=cpu_group)
+        if size > 1:  # every rank must have mapped its peers before anyone signals into them
+            dist.barrier(group=cpu_group)
 
     def self_test(self, group=None) -> bool:
         """Cross-check one call of each mode against a host (gloo) sum; False disables the path."""

@@ -25,6 +25,11 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 rc=$?; echo "probe prof rc=$rc"; rm -f gpurun_out/prof_tp/*kernel_trace.csv
 python tools/rocprof_summary.py gpurun_out/prof_tp/tp_kernel_stats.csv 40 > gpurun_out/tp_probe_summary.txt 2>&1; head -45 gpurun_out/tp_probe_summary.txt; ok $rc
 ;; esac
+case ",$STEP," in *,searchprof,*)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_search -o s -- python3 tools/search_bench.py > gpurun_out/search_prof.log 2>&1
+rc=$?; echo "search prof rc=$rc"; rm -f gpurun_out/prof_search/*kernel_trace.csv
+python tools/rocprof_summary.py gpurun_out/prof_search/s_kernel_stats.csv 20 > gpurun_out/search_prof_summary.txt 2>&1; head -20 gpurun_out/search_prof_summary.txt; grep '^{' gpurun_out/search_prof.log; ok $rc
+;; esac
 case ",$STEP," in *,suite,*)
 timeout -k 10 1100 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "suite rc=$rc"; tail -15 gpurun_out/pytest_gpu.log; ok $rc
