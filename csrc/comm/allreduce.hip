@@ -39,6 +39,7 @@
 // in pinned host memory (polled by the engine after each step) -- and the block reads no peer data.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../kernels/common.h"
@@ -73,6 +74,7 @@ constexpr size_t ROW_FLAG_BYTES = (sizeof(ArRowFlags) + 4095) & ~size_t(4095);
 
 struct ArPeers {
   char* base[AR_MAX_RANKS];  // every rank's region (own one included), mapped in this process
+  int fences;                // 1: system-scope release/acquire fences around every flag (A/B, RAGK_AR_FENCES=1)
   size_t rows_off;           // fused row area: [ArRowFlags | fp32 stage x2 | bf16 result x2] (0 = none)
   size_t row_stage_bytes;    // one fp32 staging half: max_rows * max_h * 4
   size_t row_result_bytes;   // one bf16 result half: max_rows * max_h * 2
@@ -187,9 +189,15 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPeers P, int ra
 __device__ bool row_barrier(const ArPeers& P, int rank, int world, int which, int row, unsigned ep) {
   __shared__ int s_ok;
   if (threadIdx.x == 0) s_ok = 1;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its payload stores are complete
   __syncthreads();
+  // The whole region is uncached (hipDeviceMallocUncached): payload stores are write-through to HBM
+  // and no cache level holds a copy of a peer's bytes, so ordering needs no L2 write-back / invalidate:
+  // every storing wave drains its stores (vmcnt(0)) before the barrier above, then one lane per peer
+  // stores the flag (system-scope atomic). A system-scope release fence here would also write back
+  // every other dirty L2 line (the GEMM slabs just produced) -- microseconds per row barrier.
   if (threadIdx.x < world) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: payload visible before the flag
+    if (P.fences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     ArRowFlags* pf = reinterpret_cast<ArRowFlags*>(P.base[threadIdx.x] + P.rows_off);
     st_sys(which ? &pf->mid[row][rank] : &pf->start[row][rank], ep);
     ArRowFlags* mf = reinterpret_cast<ArRowFlags*>(P.base[rank] + P.rows_off);
@@ -205,7 +213,8 @@ __device__ bool row_barrier(const ArPeers& P, int rank, int world, int which, in
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (P.fences) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: no load moves above the poll
   }
   __syncthreads();
   return s_ok != 0;
@@ -402,6 +411,10 @@ RAGK_API void* ragk_ar_create(int rank, int world, long max_bytes, int blocks, i
   h->local = (char*)p;
   h->peers.base[rank] = h->local;
   h->peers.spin_limit = AR_TIMEOUT_TICKS;
+  {
+    const char* f = getenv("RAGK_AR_FENCES");
+    h->peers.fences = (f && f[0] == '1') ? 1 : 0;
+  }
   void* he = nullptr;
   if (hipHostMalloc(&he, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
     h->host_err = (unsigned*)he;

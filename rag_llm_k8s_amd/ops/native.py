@@ -82,6 +82,7 @@ def use_dec(M, N, K, epi):
 
 
 STREAM_DEFAULT = os.environ.get("RAGK_STREAM_GEMM", "1") == "1"
+STREAM_MIN_ROWS = int(os.environ.get("RAGK_STREAM_MIN_ROWS", "16384"))
 
 
 def use_stream(M, N, K, epi, fp8=False):
@@ -90,7 +91,7 @@ def use_stream(M, N, K, epi, fp8=False):
     fp8 2.6 vs 1.5 at M=32) and other 16k-32k-row weights. Below that, the fixed pipeline-fill +
     split-K reduction latencies lose to the register-streaming kernels (profiles/tune_stream_r1.json)."""
     rows = 2 * N if epi == "silu_mul" else N
-    if M > 64 or not (16384 <= rows < 32768) or K % 128:
+    if M > 64 or not (STREAM_MIN_ROWS <= rows < 32768) or K % 128:
         return False
     return M > 16 if fp8 else True
 
@@ -598,15 +599,17 @@ def attn_prefill(q, k, v, cu_q, kv_lens, tiles, out, Hq, Hkv, D, causal=True, pa
 
 
 DECODE_TARGET_BLOCKS = int(os.environ.get("RAGK_DECODE_BLOCKS", "512"))
+DECODE_MIN_TILES = int(os.environ.get("RAGK_DECODE_MIN_TILES", "4"))
 
 
-def decode_partitions(max_kv_len, batch, Hkv, target_blocks=None, min_tiles=4):
+def decode_partitions(max_kv_len, batch, Hkv, target_blocks=None, min_tiles=None):
     """(part_tiles, max_parts) for split-K decode: grid = max_parts x Hkv x batch >= target_blocks.
 
     The kernel spreads each sequence's actual KV tiles evenly over the max_parts partitions
     (at least ``part_tiles`` = min_tiles tiles each, attention.hip:decode_part_tiles), so the grid can
     be sized once for the longest allowed context (hipGraph capture) without idle partitions."""
     target_blocks = DECODE_TARGET_BLOCKS if target_blocks is None else target_blocks
+    min_tiles = DECODE_MIN_TILES if min_tiles is None else min_tiles
     max_kt = max(1, (max_kv_len + 63) // 64)
     mp = max(1, min(-(-target_blocks // (batch * Hkv)), -(-max_kt // min_tiles)))
     return min_tiles, mp
