@@ -33,10 +33,33 @@ __device__ __forceinline__ bool cand_lt(float av, int ai, float bv, int bi) {
   return av < bv || (av == bv && (unsigned)ai < (unsigned)bi);
 }
 
+// value of lane (lane ^ j), j a power of two that is a compile-time constant after unrolling: lane
+// swaps within a quad are DPP moves (VALU latency), 4..16 ds_swizzle (no address VGPR), 32
+// v_permlane32_swap -- none is the generic ds_bpermute whose round trip bounded every step of the
+// networks below.
+__device__ __forceinline__ int xor_lane(int v, int j, int lane) {
+  if (j == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  if (j == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  if (j == 4) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (4 << 10));
+  if (j == 8) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (8 << 10));
+  if (j == 16) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (16 << 10));
+  if (j == 32) {
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return lane < 32 ? (int)p[1] : (int)p[0];
+  }
+  return __shfl_xor(v, j, 64);
+}
+
+// value of lane 63 - lane (= lane ^ 63): DPP row mirror (lane ^ 15), then xor 16 and xor 32
+__device__ __forceinline__ int rev_lane(int v, int lane) {
+  return xor_lane(xor_lane(__builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false), 16, lane), 32, lane);
+}
+__device__ __forceinline__ float rev_lane(float v, int lane) { return __int_as_float(rev_lane(__float_as_int(v), lane)); }
+
 // one compare-exchange step of a lane-level bitonic network (partner = lane ^ j)
 __device__ __forceinline__ void cx(float& v, int& i, int lane, int j, bool asc) {
-  const float ov = __shfl_xor(v, j, 64);
-  const int oi = __shfl_xor(i, j, 64);
+  const float ov = __int_as_float(xor_lane(__float_as_int(v), j, lane));
+  const int oi = xor_lane(i, j, lane);
   const bool keep_min = ((lane & j) == 0) == asc;
   const bool take = keep_min ? cand_lt(ov, oi, v, i) : cand_lt(v, i, ov, oi);
   if (take) {
@@ -55,8 +78,8 @@ __device__ __forceinline__ void wave_sort64(float& v, int& i, int lane) {
 
 // (bv, bi) sorted ascending, (nv, ni) sorted ascending -> (bv, bi) = the 64 smallest of both, sorted
 __device__ __forceinline__ void wave_merge64(float& bv, int& bi, float nv, int ni, int lane) {
-  const float rv = __shfl(nv, 63 - lane, 64);
-  const int ri = __shfl(ni, 63 - lane, 64);
+  const float rv = rev_lane(nv, lane);
+  const int ri = rev_lane(ni, lane);
   if (cand_lt(rv, ri, bv, bi)) {
     bv = rv;
     bi = ri;
@@ -67,8 +90,8 @@ __device__ __forceinline__ void wave_merge64(float& bv, int& bi, float nv, int n
 
 // feed 64 unsorted candidates (one per lane) into the running top list; k-th best = threshold
 __device__ __forceinline__ void wave_offer(float& bv, int& bi, float v, int id, int k, int lane) {
-  const float tv = __shfl(bv, k - 1, 64);
-  const int ti = __shfl(bi, k - 1, 64);
+  const float tv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bv), k - 1));  // k uniform
+  const int ti = __builtin_amdgcn_readlane(bi, k - 1);
   if (!__any(cand_lt(v, id, tv, ti))) return;  // wave-uniform
   wave_sort64(v, id, lane);
   wave_merge64(bv, bi, v, id, lane);
@@ -86,8 +109,8 @@ __device__ __forceinline__ void wave_offer_q(float (&bv)[QB], int (&bi)[QB], flo
 #pragma unroll
   for (int q = 0; q < QB; ++q) {
     if (q < nqb) {
-      const float tv = __shfl(bv[q], k - 1, 64);
-      const int ti = __shfl(bi[q], k - 1, 64);
+      const float tv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bv[q]), k - 1));
+      const int ti = __builtin_amdgcn_readlane(bi[q], k - 1);
       any |= __any(cand_lt(v[q], id, tv, ti));
     }
   }
@@ -103,8 +126,8 @@ __device__ __forceinline__ void wave_offer_q(float (&bv)[QB], int (&bi)[QB], flo
       for (int q = 0; q < QB; ++q) cx(v[q], ix[q], lane, j, (lane & kk) == 0);
 #pragma unroll
   for (int q = 0; q < QB; ++q) {
-    const float rv = __shfl(v[q], 63 - lane, 64);
-    const int ri = __shfl(ix[q], 63 - lane, 64);
+    const float rv = rev_lane(v[q], lane);
+    const int ri = rev_lane(ix[q], lane);
     if (cand_lt(rv, ri, bv[q], bi[q])) {
       bv[q] = rv;
       bi[q] = ri;
@@ -231,6 +254,163 @@ __global__ __launch_bounds__(ST) void l2_scan_kernel(const float* __restrict__ x
   }
 }
 
+// Batched queries (nq >= 16: the BLAS path of faiss' IndexFlatL2): ||x||^2 + ||q||^2 - 2 x.q with the
+// dot products on the exact fp32-input MFMA (v_mfma_f32_16x16x4_f32: a k-ordered fmaf chain), 16 rows x
+// 16 queries per instruction. Block = 4 waves x 64 rows per iteration, QT query tiles of 16 (all of a
+// <= 32-query batch in one block: the index is streamed from HBM once). Lane l of a wave loads
+// x[row0 + 16 rt + (l & 15)][k0 + (l >> 4)] (A fragment) and reads q^T[k0 + (l >> 4)][16 qt + (l & 15)]
+// from LDS (B fragment); its accumulators hold rows 16 rt + 4 (l >> 4) + r of query 16 qt + (l & 15).
+// Selection: every lane keeps a sorted list of the MK best (distance, id) of its query among the rows
+// it sees (MK >= k; a quarter of the rows of its query per wave), and the block merges the 16 lists of
+// each query (4 lanes x 4 waves) -> one sorted list of k per query. Distances clamp at 0 like faiss.
+constexpr int MQ_MK = 8;   // k <= 8 on this path
+constexpr int MQ_KU = 8;   // k-steps (of 4 dims) per unrolled group
+constexpr int MQ_DMAX = 1024;
+
+// LDS floats of region 0: q^T during the scan, the candidate lists at the merge (aliased)
+__host__ __device__ inline int mq_region0(int d, int QT) { return max(d * 16 * QT, 2 * 16 * QT * 128); }
+
+template <int QT, int RT>
+__global__ __launch_bounds__(ST) void l2_mfma_kernel(const float* __restrict__ xt, int cap, int d, int row_begin,
+                                                     int row_end, int ntiles, const float* __restrict__ q, int nq,
+                                                     int k, float* __restrict__ out_d, int* __restrict__ out_i,
+                                                     const int* __restrict__ ids_map) {
+  extern __shared__ __attribute__((aligned(16))) float mq_smem[];
+  float* qsT = mq_smem;                              // [d][16 * QT]: q transposed (scan)
+  float* cd = mq_smem;                               // [16 * QT][128] candidates (merge, aliases qsT)
+  int* ci = reinterpret_cast<int*>(mq_smem + 16 * QT * 128);
+  float* qn = mq_smem + mq_region0(d, QT);           // [16 * QT] ||q||^2
+  float* xnl = qn + 16 * QT;                         // [4 waves][16 * RT] ||x||^2 of the wave's rows
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q0 = blockIdx.y * 16 * QT;
+  const int nqb = min(16 * QT, nq - q0);
+  for (int e = threadIdx.x; e < d * 16 * QT; e += ST) {
+    const int t = e / (16 * QT), j = e % (16 * QT);
+    qsT[e] = j < nqb ? q[(size_t)(q0 + j) * d + t] : 0.f;
+  }
+  __syncthreads();
+  if (threadIdx.x < 16 * QT) {
+    float sq = 0.f;
+    for (int t = 0; t < d; ++t) sq = fmaf(qsT[t * 16 * QT + threadIdx.x], qsT[t * 16 * QT + threadIdx.x], sq);
+    qn[threadIdx.x] = sq;
+  }
+  __syncthreads();
+  const int fr = lane & 15, fg = lane >> 4;
+  // per-lane sorted lists, one per query tile
+  float lv[QT][MQ_MK];
+  int lix[QT][MQ_MK];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int m = 0; m < MQ_MK; ++m) {
+      lv[qt][m] = FLT_MAX;
+      lix[qt][m] = -1;
+    }
+  float qnv[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) qnv[qt] = qn[16 * qt + fr];
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int rbase = row_begin + tile * (64 * RT) + 16 * RT * w;
+    int rc[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) rc[rt] = min(rbase + 16 * rt + fr, cap - 1);
+    f32x4 acc[RT][QT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) acc[rt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float xs[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) xs[rt] = 0.f;
+    const int nk = d / 4;  // host guarantees d % (4 * MQ_KU) == 0
+    for (int k0 = 0; k0 < nk; k0 += MQ_KU) {
+      float a[MQ_KU][RT];
+#pragma unroll
+      for (int u = 0; u < MQ_KU; ++u) {
+        const float* col = xt + (size_t)(4 * (k0 + u) + fg) * cap;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) a[u][rt] = col[rc[rt]];
+      }
+#pragma unroll
+      for (int u = 0; u < MQ_KU; ++u) {
+        float b[QT];
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) b[qt] = qsT[(4 * (k0 + u) + fg) * 16 * QT + 16 * qt + fr];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          xs[rt] = fmaf(a[u][rt], a[u][rt], xs[rt]);
+#pragma unroll
+          for (int qt = 0; qt < QT; ++qt)
+            acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][rt], b[qt], acc[rt][qt], 0, 0, 0);
+        }
+      }
+    }
+    // ||x||^2 of row 16 rt + fr: the 4 dim phases (lanes fr, fr+16, fr+32, fr+48) summed in order
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      float t = xs[rt];
+      t += __int_as_float(xor_lane(__float_as_int(t), 16, lane));
+      t += __int_as_float(xor_lane(__float_as_int(t), 32, lane));
+      if (fg == 0) xnl[w * 16 * RT + 16 * rt + fr] = t;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's xnl writes landed (wave-local rows)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = 16 * rt + 4 * fg + r;
+        const int row = rbase + rl;
+        const bool ok = row < row_end;
+        const int id = ok ? (ids_map ? ids_map[row] : row) : -1;
+        const float xn = xnl[w * 16 * RT + rl];
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+          const float dv = ok ? fmaxf(xn + qnv[qt] - 2.f * acc[rt][qt][r], 0.f) : FLT_MAX;
+          if (cand_lt(dv, id, lv[qt][MQ_MK - 1], lix[qt][MQ_MK - 1])) {  // insert (rare once warm)
+            float cv = dv;
+            int cidx = id;
+#pragma unroll
+            for (int m = 0; m < MQ_MK; ++m) {
+              if (cand_lt(cv, cidx, lv[qt][m], lix[qt][m])) {
+                const float tv = lv[qt][m];
+                const int ti = lix[qt][m];
+                lv[qt][m] = cv;
+                lix[qt][m] = cidx;
+                cv = tv;
+                cidx = ti;
+              }
+            }
+          }
+        }
+      }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // merge: query j's lists live in lanes with fr == j % 16 of every wave: 4 waves x 4 lane groups x MQ_MK
+  __syncthreads();  // every wave is done reading q^T: the candidate lists reuse its LDS
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int m = 0; m < MQ_MK; ++m) {
+      const int j = 16 * qt + fr;
+      const int slot = (w * 4 + fg) * MQ_MK + m;  // 0 .. 127
+      cd[(size_t)j * 128 + slot] = lv[qt][m];
+      ci[(size_t)j * 128 + slot] = lix[qt][m];
+    }
+  __syncthreads();
+  for (int j = w; j < nqb; j += 4) {  // one wave per query: 128 candidates -> two 64-lane offers
+    float bv = FLT_MAX;
+    int bi = -1;
+    wave_offer(bv, bi, cd[(size_t)j * 128 + lane], ci[(size_t)j * 128 + lane], k, lane);
+    wave_offer(bv, bi, cd[(size_t)j * 128 + 64 + lane], ci[(size_t)j * 128 + 64 + lane], k, lane);
+    if (lane < k) {
+      const size_t o = ((size_t)(q0 + j) * gridDim.x + blockIdx.x) * k + lane;
+      out_d[o] = bv;
+      out_i[o] = bi;
+    }
+  }
+}
+
 // IVF-Flat scan: block (probe p, query qi) scans the whole inverted list probes[qi][p] (store rows
 // [offsets[list], ends[list]); packed lists when ends == nullptr: end = offsets[list + 1]) in
 // 256-row tiles (one wave per 64 rows) -> one sorted list of k at [qi][p].
@@ -290,13 +470,15 @@ __global__ __launch_bounds__(ST) void ivf_scan_kernel(const float* __restrict__ 
   }
 }
 
-// in: [nq][G][k] sorted lists -> out: [nq][k]. One block per query; each wave takes 64 candidates
-// at a time (64 / k whole lists per step), offers them to its running top list; waves merged last.
-__global__ __launch_bounds__(ST) void topk_lists_merge_kernel(const float* __restrict__ in_d,
-                                                              const int* __restrict__ in_i, int G, int k,
-                                                              float* __restrict__ out_d, int* __restrict__ out_i) {
-  __shared__ float mv[4][64];
-  __shared__ int mi[4][64];
+// in: [nq][G][k] sorted lists -> out: [nq][k]. One block of MW waves per query; each wave takes 64
+// candidates at a time (64 / k whole lists per step) and offers them to its running top list; the
+// waves' lists are merged last.
+constexpr int MW = 16;
+__global__ __launch_bounds__(MW * 64) void topk_lists_merge_kernel(const float* __restrict__ in_d,
+                                                                   const int* __restrict__ in_i, int G, int k,
+                                                                   float* __restrict__ out_d, int* __restrict__ out_i) {
+  __shared__ float mv[MW][64];
+  __shared__ int mi[MW][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int qi = blockIdx.x;
   const int lpw = 64 / k;  // whole lists per 64-lane step
@@ -304,20 +486,18 @@ __global__ __launch_bounds__(ST) void topk_lists_merge_kernel(const float* __res
   const size_t base = (size_t)qi * G * k;
   float bv = FLT_MAX;
   int bi = -1;
-  for (int l0 = w * lpw; l0 < G; l0 += 4 * lpw) {
+  for (int l0 = w * lpw; l0 < G; l0 += MW * lpw) {
     const int l = l0 + li;
     const bool ok = li < lpw && l < G;
     const float v = ok ? in_d[base + (size_t)l * k + e] : FLT_MAX;
     const int id = ok ? in_i[base + (size_t)l * k + e] : -1;
     wave_offer(bv, bi, v, id, k, lane);
   }
-  if (w > 0) {
-    mv[w][lane] = bv;
-    mi[w][lane] = bi;
-  }
+  mv[w][lane] = bv;
+  mi[w][lane] = bi;
   __syncthreads();
   if (w == 0) {
-    for (int gg = 1; gg < 4; ++gg) wave_merge64(bv, bi, mv[gg][lane], mi[gg][lane], lane);
+    for (int gg = 1; gg < MW; ++gg) wave_merge64(bv, bi, mv[gg][lane], mi[gg][lane], lane);
     if (lane < k) {
       out_d[(size_t)qi * k + lane] = bv;
       out_i[(size_t)qi * k + lane] = bi;
@@ -496,15 +676,36 @@ static void launch_scan_s(int S, dim3 grid, hipStream_t st, const float* xt, int
   else launch_scan<QB, 1>(grid, lds, st, xt, cap, d, rb, re, ntiles, q, nq, k, od, oi, ids);
 }
 
+// the MFMA path (batched queries, k <= 8, d % 32 == 0) for nq >= this
+static int g_mfma_min_nq = 16;
+RAGK_API int ragk_l2_search_set_mfma_min_nq(int n) {
+  g_mfma_min_nq = n > 0 ? n : 16;
+  return 0;
+}
+static bool use_mfma(int nq, int k, int d) {
+  return nq >= g_mfma_min_nq && k <= MQ_MK && d % (4 * MQ_KU) == 0 && d <= MQ_DMAX;
+}
+static size_t mfma_lds(int d, int QT) { return ((size_t)mq_region0(d, QT) + 16 * QT + 4 * 64) * 4; }
+static int mfma_rt(int n) { return n < 262144 ? 1 : 4; }  // 16 or 64 rows per wave and tile
+
 // Number of partial lists per query the scan of rows [row_begin, row_end) emits (size the
 // partial buffers [nq][G][k] with it).
 RAGK_API int ragk_l2_scan_groups(int row_begin, int row_end, int nq) {
   const int n = max(0, row_end - row_begin);
   const int S = scan_slices(n);
-  const int ntiles = (n + 64 * (4 / S) - 1) / (64 * (4 / S));
+  const int ntiles = (n + 64 * (4 / S) - 1) / (64 * (4 / S));  // (the MFMA path's 256-row tiles: <= this)
   const int qgroups = (max(nq, 1) + 15) / 16;
   const int target = max(1, 2048 / qgroups);  // bounded list count: the merge stays short
   return max(1, min(ntiles, target));
+}
+
+// As ragk_l2_scan_groups, for the kernel ragk_l2_search actually launches for (nq, k, d).
+RAGK_API int ragk_l2_search_groups(int row_begin, int row_end, int nq, int k, int d) {
+  if (!use_mfma(nq, k, d)) return ragk_l2_scan_groups(row_begin, row_end, nq);
+  const int n = max(0, row_end - row_begin);
+  const int ntiles = (n + 64 * mfma_rt(n) - 1) / (64 * mfma_rt(n));
+  const int qgroups = (nq + 31) / 32;
+  return max(1, min(ntiles, max(1, 2048 / qgroups)));
 }
 
 // Exact top-k (k <= 64) over rows [row_begin, row_end) of xt[d][cap]; part_d / part_i hold
@@ -514,10 +715,41 @@ RAGK_API int ragk_l2_search(const float* xt, int cap, int d, int row_begin, int 
                             hipStream_t st) {
   if (nq <= 0) return 0;
   if (k < 1 || k > 64 || d < 1 || cap < 1 || row_end > cap) return (int)hipErrorInvalidValue;
+  if (use_mfma(nq, k, d)) {
+    static bool attr = false;
+    if (!attr) {
+      hipError_t e = hipSuccess;
+      const void* fns[4] = {(const void*)l2_mfma_kernel<1, 1>, (const void*)l2_mfma_kernel<1, 4>,
+                            (const void*)l2_mfma_kernel<2, 1>, (const void*)l2_mfma_kernel<2, 4>};
+      for (int i = 0; i < 4 && e == hipSuccess; ++i)
+        e = hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)mfma_lds(MQ_DMAX, 1 + i / 2));
+      if (e != hipSuccess) return (int)e;
+      attr = true;
+    }
+    const int n = max(0, row_end - row_begin);
+    const int RT = mfma_rt(n);
+    const int ntiles = (n + 64 * RT - 1) / (64 * RT);
+    const int G = ragk_l2_search_groups(row_begin, row_end, nq, k, d);
+    const int QT = nq >= 32 ? 2 : 1;
+    const dim3 grid(G, (nq + 16 * QT - 1) / (16 * QT));
+    const size_t lds = mfma_lds(d, QT);
+#define RAGK_MQ(Q, R) hipLaunchKernelGGL((l2_mfma_kernel<Q, R>), grid, dim3(ST), lds, st, xt, cap, d, row_begin, row_end, \
+                                         ntiles, q, nq, k, part_d, part_i, ids_map)
+    if (QT == 2) {
+      if (RT == 4) RAGK_MQ(2, 4); else RAGK_MQ(2, 1);
+    } else {
+      if (RT == 4) RAGK_MQ(1, 4); else RAGK_MQ(1, 1);
+    }
+#undef RAGK_MQ
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(topk_lists_merge_kernel, dim3(nq), dim3(MW * 64), 0, st, part_d, part_i, G, k, out_d, out_i);
+    return (int)hipGetLastError();
+  }
   const int n = max(0, row_end - row_begin);
   const int S = scan_slices(n);
   const int ntiles = (n + 64 * (4 / S) - 1) / (64 * (4 / S));
-  const int G = ragk_l2_scan_groups(row_begin, row_end, nq);
+  const int G = ragk_l2_search_groups(row_begin, row_end, nq, k, d);
   // queries per block: up to 16 (32 accumulators + the x[] ring would leave one wave per SIMD);
   // the last group of the y-dimension may be partial (handled in-kernel)
   const int QB = nq >= 16 ? 16 : (nq >= 8 ? 8 : (nq >= 4 ? 4 : (nq >= 2 ? 2 : 1)));
@@ -529,7 +761,7 @@ RAGK_API int ragk_l2_search(const float* xt, int cap, int d, int row_begin, int 
   else launch_scan_s<1>(S, grid, st, xt, cap, d, row_begin, row_end, ntiles, q, nq, k, part_d, part_i, ids_map);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(topk_lists_merge_kernel, dim3(nq), dim3(ST), 0, st, part_d, part_i, G, k, out_d, out_i);
+  hipLaunchKernelGGL(topk_lists_merge_kernel, dim3(nq), dim3(MW * 64), 0, st, part_d, part_i, G, k, out_d, out_i);
   return (int)hipGetLastError();
 }
 
@@ -543,7 +775,8 @@ RAGK_API int ragk_ivf_search(const float* xt, int cap, int d, const float* q, in
                      ids_map, k, part_d, part_i);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(topk_lists_merge_kernel, dim3(nq), dim3(ST), 0, st, part_d, part_i, nprobe, k, out_d, out_i);
+  hipLaunchKernelGGL(topk_lists_merge_kernel, dim3(nq), dim3(MW * 64), 0, st, part_d, part_i, nprobe, k, out_d,
+                     out_i);
   return (int)hipGetLastError();
 }
 

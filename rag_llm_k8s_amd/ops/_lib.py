@@ -66,6 +66,8 @@ _SIGS = {
     "ragk_sample_candidates": [P, P, I, I, P, P, P, P, P, P, P, S],
     "ragk_sample_candidates_lists": [P, P, I, I, I, P, P, P, P, P, P, P, S],
     "ragk_l2_scan_groups": [I, I, I],
+    "ragk_l2_search_groups": [I, I, I, I, I],
+    "ragk_l2_search_set_mfma_min_nq": [I],
     "ragk_l2_search": [P, I, I, I, I, P, I, I, P, P, P, P, P, S],
     "ragk_ivf_search": [P, I, I, P, I, P, I, P, P, P, I, P, P, P, P, S],
     "ragk_kmeans_assign": [P, I, I, P, P, I, P, P, P, S],

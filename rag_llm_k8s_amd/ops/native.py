@@ -751,9 +751,15 @@ def sample_candidates(cand_v, cand_i, temps, top_ks, top_ps, seeds, steps, out_t
 
 
 # ----------------------------------------------------------------------------- search
+def l2_search_set_mfma_min_nq(n):
+    """Batches of at least n queries (k <= 8, d % 32 == 0) take the MFMA ||x||^2+||q||^2-2x.q path."""
+    check(_lib.lib().ragk_l2_search_set_mfma_min_nq(int(n)), "ragk_l2_search_set_mfma_min_nq")
+
+
 def l2_search(xt, cap, n, q, k, row_begin=0, ids_map=None):
     """Exact squared-L2 top-k over rows [row_begin, n) of a column-major store xt[d][cap]
-    (csrc/kernels/search.hip: l2_scan with wave-resident running top lists + one list merge).
+    (csrc/kernels/search.hip: l2_scan with wave-resident running top lists + one list merge; batches
+    of >= 16 queries with k <= 8 on the fp32-MFMA distance GEMM, faiss' BLAS form).
     Returns (D fp32 [nq,k], I int64 [nq,k]) with faiss padding semantics (-1, FLT_MAX)."""
     _req(xt.is_cuda and xt.dtype == torch.float32 and xt.is_contiguous() and xt.dim() == 2, "xt fp32 [d, cap]")
     _req(q.is_cuda and q.dtype == torch.float32 and q.is_contiguous() and q.dim() == 2, "q fp32 [nq, d]")
@@ -768,7 +774,7 @@ def l2_search(xt, cap, n, q, k, row_begin=0, ids_map=None):
     oi = torch.empty((nq, k), dtype=torch.int32, device=q.device)
     if nq == 0:
         return od, oi.long()
-    G = L.ragk_l2_scan_groups(row_begin, max(n, row_begin), nq)
+    G = L.ragk_l2_search_groups(row_begin, max(n, row_begin), nq, k, d)
     pd = torch.empty((nq, G, k), dtype=torch.float32, device=q.device)
     pi = torch.empty((nq, G, k), dtype=torch.int32, device=q.device)
     check(L.ragk_l2_search(xt.data_ptr(), cap, d, row_begin, max(n, row_begin), q.data_ptr(), nq, k, ptr(ids_map),

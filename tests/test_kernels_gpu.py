@@ -657,7 +657,9 @@ def test_sampling_support_matches_hf_rules(native):
 
 @pytest.mark.parametrize("N,d,nq,k", [(0, 64, 2, 5), (3, 64, 1, 5), (10000, 384, 32, 4), (5000, 1024, 3, 10),
                                       (70000, 128, 9, 8), (300000, 32, 3, 64), (1000, 100, 40, 1),
-                                      (129, 384, 16, 64), (20000, 1024, 1, 5)])
+                                      (129, 384, 16, 64), (20000, 1024, 1, 5),
+                                      # MFMA path (nq >= 16, k <= 8): 16 and 64 rows per wave, 1 / 2 query tiles
+                                      (300000, 64, 33, 5), (5000, 1024, 16, 8), (777, 96, 70, 3)])
 def test_l2_search(native, N, d, nq, k):
     torch.manual_seed(15)
     xb = torch.randn(N, d)
@@ -699,6 +701,30 @@ def test_l2_search_ties_ids_map_and_row_range(native, N):
     assert I3[:, 3:].eq(-1).all() and torch.all(D3[:, 3:] == torch.finfo(torch.float32).max)
 
 
+def test_l2_search_mfma_path_matches_scan_path(native):
+    """The batched-query MFMA path (||x||^2 + ||q||^2 - 2 x.q) and the direct-form scan agree: same ids
+    up to swaps of near-equal distances, distances within fp32 rounding; exact duplicates come out in
+    ascending id order on both."""
+    torch.manual_seed(7)
+    N, d, nq, k = 40000, 384, 32, 5
+    base = torch.randn(N // 2, d)
+    xb = torch.cat([base, base])  # row i and i + N/2 identical
+    cap = N + 1
+    xt = torch.zeros(d, cap, device=DEV)
+    native.l2_append(xt, cap, 0, xb.to(DEV))
+    q = (base[:nq] + 0.05 * torch.randn(nq, d)).to(DEV)
+    Dm, Im = native.l2_search(xt, cap, N, q, k)
+    native.l2_search_set_mfma_min_nq(10 ** 6)
+    try:
+        Ds, Is = native.l2_search(xt, cap, N, q, k)
+    finally:
+        native.l2_search_set_mfma_min_nq(16)
+    assert torch.allclose(Dm.cpu(), Ds.cpu(), rtol=1e-4, atol=1e-2)
+    for j in range(nq):  # nearest: the perturbed source row and its duplicate, lower id first
+        assert Im[j, :2].tolist() == [j, j + N // 2] and Is[j, :2].tolist() == [j, j + N // 2]
+    assert (Im == Is).float().mean() > 0.95
+
+
 def test_l2_search_guard_canaries(native):
     """Outputs and partial-list buffers of the search are sized exactly: kernels write nothing past
     them (sentinel-padded allocations; SURVEY §5 OOB checks)."""
@@ -708,7 +734,7 @@ def test_l2_search_guard_canaries(native):
     xt = torch.zeros(d, cap, device=DEV)
     native.l2_append(xt, cap, 0, torch.randn(N, d, device=DEV))
     L = native._lib.lib()
-    G = L.ragk_l2_scan_groups(0, N, nq)
+    G = L.ragk_l2_search_groups(0, N, nq, k, d)
     pad = 4096
     q = torch.randn(nq, d, device=DEV)
     bufs = [torch.full((2 * pad + n,), -7.0, device=DEV) for n in (nq * G * k, nq * k)]
