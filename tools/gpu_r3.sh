@@ -7,7 +7,7 @@ mkdir -p gpurun_out/prof
 STEP=${STEP:-search}
 ok() { rc=$1; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "step failed rc=$rc"; exit $rc; fi; }
 case ",$STEP," in *,search,*)
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_ivf_gpu.py -k "l2_search or ivf or kmeans" -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_search.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_ivf_gpu.py tests/test_canary_gpu.py -k "l2_search or ivf or kmeans or bounds" -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_search.log 2>&1
 rc=$?; echo "search tests rc=$rc"; tail -15 gpurun_out/pytest_search.log; ok $rc
 timeout -k 10 300 python -u tools/search_bench.py > gpurun_out/search_bench.log 2>&1
 rc=$?; echo "search bench rc=$rc"; cat gpurun_out/search_bench.log; ok $rc
