@@ -139,19 +139,52 @@ __device__ __forceinline__ void wave_offer_q(float (&bv)[QB], int (&bi)[QB], flo
     for (int q = 0; q < QB; ++q) cx(bv[q], bi[q], lane, j, true);
 }
 
+// As wave_offer_q with a separate candidate id per query (lists of different queries).
+template <int NQ>
+__device__ __forceinline__ void wave_offer_multi(float (&bv)[NQ], int (&bi)[NQ], float (&v)[NQ], int (&ix)[NQ], int k,
+                                                 int lane) {
+  bool any = false;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const float tv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bv[q]), k - 1));
+    const int ti = __builtin_amdgcn_readlane(bi[q], k - 1);
+    any |= __any(cand_lt(v[q], ix[q], tv, ti));
+  }
+  if (!any) return;
+#pragma unroll
+  for (int kk = 2; kk <= 64; kk <<= 1)
+#pragma unroll
+    for (int j = kk >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) cx(v[q], ix[q], lane, j, (lane & kk) == 0);
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const float rv = rev_lane(v[q], lane);
+    const int ri = rev_lane(ix[q], lane);
+    if (cand_lt(rv, ri, bv[q], bi[q])) {
+      bv[q] = rv;
+      bi[q] = ri;
+    }
+  }
+#pragma unroll
+  for (int j = 32; j > 0; j >>= 1)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) cx(bv[q], bi[q], lane, j, true);
+}
+
 // Distances of rows [rbase, rbase + 64) (one per lane; rows clamped into [0, cap)) over dims
 // [t0, t1) of the staged chunk starting at dim dc, for QB queries.
-template <int QB>
+template <int QB, int U = (QB <= 2 ? 32 : UNR)>
 __device__ __forceinline__ void scan_dims(const float* __restrict__ xt, size_t cap, int rc, int dc, int t0, int t1,
                                           const float* qs, float* acc) {
   const float* col = xt + (size_t)(dc + t0) * cap + rc;
   int t = t0;
-  for (; t + UNR <= t1; t += UNR, col += UNR * cap) {
-    float x[UNR];
+  for (; t + U <= t1; t += U, col += U * cap) {
+    float x[U];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) x[u] = __builtin_nontemporal_load(col + (size_t)u * cap);
+    for (int u = 0; u < U; ++u) x[u] = col[(size_t)u * cap];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < QB; ++j) {
         const float df = x[u] - qs[j * DCH + t + u];
@@ -267,8 +300,11 @@ constexpr int MQ_MK = 8;   // k <= 8 on this path
 constexpr int MQ_KU = 8;   // k-steps (of 4 dims) per unrolled group
 constexpr int MQ_DMAX = 1024;
 
-// LDS floats of region 0: q^T during the scan, the candidate lists at the merge (aliased)
-__host__ __device__ inline int mq_region0(int d, int QT) { return max(d * 16 * QT, 2 * 16 * QT * 128); }
+constexpr int MQ_DCH = 256;  // query dims staged per LDS chunk (4 blocks per CU fit)
+// LDS floats of region 0: a q^T chunk during the scan, the candidate lists at the merge (aliased)
+__host__ __device__ inline int mq_region0(int d, int QT) {
+  return max(min(d, MQ_DCH) * 16 * QT, 2 * 16 * QT * 128);
+}
 
 template <int QT, int RT>
 __global__ __launch_bounds__(ST) void l2_mfma_kernel(const float* __restrict__ xt, int cap, int d, int row_begin,
@@ -276,7 +312,7 @@ __global__ __launch_bounds__(ST) void l2_mfma_kernel(const float* __restrict__ x
                                                      int k, float* __restrict__ out_d, int* __restrict__ out_i,
                                                      const int* __restrict__ ids_map) {
   extern __shared__ __attribute__((aligned(16))) float mq_smem[];
-  float* qsT = mq_smem;                              // [d][16 * QT]: q transposed (scan)
+  float* qsT = mq_smem;                              // [MQ_DCH][16 * QT]: q transposed, one dim chunk
   float* cd = mq_smem;                               // [16 * QT][128] candidates (merge, aliases qsT)
   int* ci = reinterpret_cast<int*>(mq_smem + 16 * QT * 128);
   float* qn = mq_smem + mq_region0(d, QT);           // [16 * QT] ||q||^2
@@ -284,14 +320,12 @@ __global__ __launch_bounds__(ST) void l2_mfma_kernel(const float* __restrict__ x
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q0 = blockIdx.y * 16 * QT;
   const int nqb = min(16 * QT, nq - q0);
-  for (int e = threadIdx.x; e < d * 16 * QT; e += ST) {
-    const int t = e / (16 * QT), j = e % (16 * QT);
-    qsT[e] = j < nqb ? q[(size_t)(q0 + j) * d + t] : 0.f;
-  }
-  __syncthreads();
-  if (threadIdx.x < 16 * QT) {
+  if (threadIdx.x < 16 * QT) {  // ||q||^2 (a k-ordered fma chain, as the dot products)
     float sq = 0.f;
-    for (int t = 0; t < d; ++t) sq = fmaf(qsT[t * 16 * QT + threadIdx.x], qsT[t * 16 * QT + threadIdx.x], sq);
+    if ((int)threadIdx.x < nqb) {
+      const float* qr = q + (size_t)(q0 + threadIdx.x) * d;
+      for (int t = 0; t < d; ++t) sq = fmaf(qr[t], qr[t], sq);
+    }
     qn[threadIdx.x] = sq;
   }
   __syncthreads();
@@ -322,12 +356,19 @@ __global__ __launch_bounds__(ST) void l2_mfma_kernel(const float* __restrict__ x
     float xs[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) xs[rt] = 0.f;
-    const int nk = d / 4;  // host guarantees d % (4 * MQ_KU) == 0
-    for (int k0 = 0; k0 < nk; k0 += MQ_KU) {
+    for (int dc = 0; dc < d; dc += MQ_DCH) {
+    const int dn = min(MQ_DCH, d - dc);  // host guarantees d % (4 * MQ_KU) == 0
+    __syncthreads();  // every wave is done with the previous chunk
+    for (int e = threadIdx.x; e < dn * 16 * QT; e += ST) {
+      const int t = e / (16 * QT), j = e % (16 * QT);
+      qsT[e] = j < nqb ? q[(size_t)(q0 + j) * d + dc + t] : 0.f;
+    }
+    __syncthreads();
+    for (int k0 = 0; k0 < dn / 4; k0 += MQ_KU) {
       float a[MQ_KU][RT];
 #pragma unroll
       for (int u = 0; u < MQ_KU; ++u) {
-        const float* col = xt + (size_t)(4 * (k0 + u) + fg) * cap;
+        const float* col = xt + (size_t)(dc + 4 * (k0 + u) + fg) * cap;
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) a[u][rt] = col[rc[rt]];
       }
@@ -345,6 +386,7 @@ __global__ __launch_bounds__(ST) void l2_mfma_kernel(const float* __restrict__ x
         }
       }
     }
+    }  // dim chunk
     // ||x||^2 of row 16 rt + fr: the 4 dim phases (lanes fr, fr+16, fr+32, fr+48) summed in order
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
@@ -398,15 +440,32 @@ __global__ __launch_bounds__(ST) void l2_mfma_kernel(const float* __restrict__ x
       ci[(size_t)j * 128 + slot] = lix[qt][m];
     }
   __syncthreads();
-  for (int j = w; j < nqb; j += 4) {  // one wave per query: 128 candidates -> two 64-lane offers
-    float bv = FLT_MAX;
-    int bi = -1;
-    wave_offer(bv, bi, cd[(size_t)j * 128 + lane], ci[(size_t)j * 128 + lane], k, lane);
-    wave_offer(bv, bi, cd[(size_t)j * 128 + 64 + lane], ci[(size_t)j * 128 + 64 + lane], k, lane);
-    if (lane < k) {
-      const size_t o = ((size_t)(q0 + j) * gridDim.x + blockIdx.x) * k + lane;
-      out_d[o] = bv;
-      out_i[o] = bi;
+  // wave w merges queries w, w + 4, ... (4 * QT of them) with interleaved networks: each query's 128
+  // candidates are two 64-lane offers
+  {
+    constexpr int NQW = 4 * QT;
+    float bv[NQW], v0[NQW], v1[NQW];
+    int bi[NQW], i0[NQW], i1[NQW];
+#pragma unroll
+    for (int t = 0; t < NQW; ++t) {
+      const int j = w + 4 * t;
+      bv[t] = FLT_MAX;
+      bi[t] = -1;
+      v0[t] = cd[(size_t)j * 128 + lane];
+      i0[t] = ci[(size_t)j * 128 + lane];
+      v1[t] = cd[(size_t)j * 128 + 64 + lane];
+      i1[t] = ci[(size_t)j * 128 + 64 + lane];
+    }
+    wave_offer_multi<NQW>(bv, bi, v0, i0, k, lane);
+    wave_offer_multi<NQW>(bv, bi, v1, i1, k, lane);
+#pragma unroll
+    for (int t = 0; t < NQW; ++t) {
+      const int j = w + 4 * t;
+      if (j < nqb && lane < k) {
+        const size_t o = ((size_t)(q0 + j) * gridDim.x + blockIdx.x) * k + lane;
+        out_d[o] = bv[t];
+        out_i[o] = bi[t];
+      }
     }
   }
 }
@@ -486,12 +545,20 @@ __global__ __launch_bounds__(MW * 64) void topk_lists_merge_kernel(const float* 
   const size_t base = (size_t)qi * G * k;
   float bv = FLT_MAX;
   int bi = -1;
-  for (int l0 = w * lpw; l0 < G; l0 += MW * lpw) {
-    const int l = l0 + li;
-    const bool ok = li < lpw && l < G;
-    const float v = ok ? in_d[base + (size_t)l * k + e] : FLT_MAX;
-    const int id = ok ? in_i[base + (size_t)l * k + e] : -1;
+  // software-pipelined: the next step's candidates are loaded before this step's network runs (its
+  // data-dependent branch otherwise keeps hipcc from hoisting them: one memory latency per step)
+  int l0 = w * lpw;
+  bool ok = li < lpw && l0 + li < G;
+  float v = ok ? in_d[base + (size_t)(l0 + li) * k + e] : FLT_MAX;
+  int id = ok ? in_i[base + (size_t)(l0 + li) * k + e] : -1;
+  for (; l0 < G; l0 += MW * lpw) {
+    const int ln = l0 + MW * lpw + li;
+    const bool okn = li < lpw && ln < G;
+    const float vn = okn ? in_d[base + (size_t)ln * k + e] : FLT_MAX;
+    const int idn = okn ? in_i[base + (size_t)ln * k + e] : -1;
     wave_offer(bv, bi, v, id, k, lane);
+    v = vn;
+    id = idn;
   }
   mv[w][lane] = bv;
   mi[w][lane] = bi;
