@@ -33,16 +33,21 @@ __device__ __forceinline__ bool cand_lt(float av, int ai, float bv, int bi) {
   return av < bv || (av == bv && (unsigned)ai < (unsigned)bi);
 }
 
-// value of lane (lane ^ j), j a power of two that is a compile-time constant after unrolling: lane
-// swaps within a quad are DPP moves (VALU latency), 4..16 ds_swizzle (no address VGPR), 32
-// v_permlane32_swap -- none is the generic ds_bpermute whose round trip bounded every step of the
-// networks below.
+// value of lane (lane ^ j), j a power of two that is a compile-time constant after unrolling: every
+// exchange stays on the VALU -- DPP quad permutes / mirrors (one or two moves) for j <= 8,
+// v_permlane16_swap / v_permlane32_swap for 16 / 32 -- instead of the LDS-pipe ds_bpermute (or
+// ds_swizzle) whose round trip bounded every step of the networks below.
 __device__ __forceinline__ int xor_lane(int v, int j, int lane) {
   if (j == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
   if (j == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  if (j == 4) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (4 << 10));
-  if (j == 8) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (8 << 10));
-  if (j == 16) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (16 << 10));
+  if (j == 4)  // (i ^ 3) then the 8-lane mirror (i ^ 7): i ^ 4
+    return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x1B, 0xF, 0xF, false), 0x141, 0xF, 0xF, false);
+  if (j == 8)  // 8-lane mirror (i ^ 7) then the row mirror (i ^ 15): i ^ 8
+    return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false), 0x140, 0xF, 0xF, false);
+  if (j == 16) {  // odd rows of vdst <-> even rows of vsrc
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return ((lane >> 4) & 1) ? (int)p[0] : (int)p[1];
+  }
   if (j == 32) {
     const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
     return lane < 32 ? (int)p[1] : (int)p[0];
