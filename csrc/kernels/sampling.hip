@@ -10,6 +10,7 @@
 //      keep the global top-K, apply temperature, top-p, and draw with a
 //      counter-based RNG (seed, step) -- deterministic across TP ranks.
 #include "common.h"
+#include <float.h>
 using namespace ragk;
 
 namespace {
@@ -238,6 +239,51 @@ __global__ __launch_bounds__(TK_THREADS) void topk_lds_kernel(const float* __res
   }
 }
 
+// Small-batch top-K (decode batch <= 4): many short chunks (~4k logits) so one row's selection spreads
+// over ~32 CUs, each chunk selected without radix passes: every wave keeps a running sorted top-64 of
+// its share of the chunk in its lanes (keys = -logit, the network sorts ascending, ties -> lower vocab
+// id; a 64-logit tile that cannot enter the list is skipped), the block merges its 4 lists. Output as
+// topk_lds: K candidates per chunk, value descending, ids ascending within equal values.
+constexpr int TW_THREADS = 256;
+constexpr int TW_VMAX = 6144;  // chunk sizes this kernel takes (larger chunks: topk_lds)
+
+__global__ __launch_bounds__(TW_THREADS) void topk_wave_kernel(const float* __restrict__ logits, int ld, int Vtot,
+                                                               int K, int vocab_offset, int chunks, float* cand_v,
+                                                               int* cand_i) {
+  __shared__ float mv[4][64];
+  __shared__ int mi[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x / chunks, chunk = blockIdx.x % chunks;
+  const int Vc = ((Vtot + chunks - 1) / chunks + 7) & ~7;
+  const int c0 = min(chunk * Vc, Vtot);
+  const int V = min(Vtot - c0, Vc);
+  const float* row = logits + (size_t)b * ld + c0;
+  const int id0 = vocab_offset + c0;
+  float bv = INFINITY;  // padding sorts after real -inf logits (id 0xffffffff unsigned)
+  int bi = -1;
+  int i = w * 64 + lane;
+  float x = i < V ? row[i] : 0.f;
+  for (int base = w * 64; base < V; base += 4 * 64) {
+    const bool ok = i < V;
+    const int in = i + 4 * 64;
+    const float xn = in < V ? row[in] : 0.f;  // next tile in flight while this one is offered
+    wave_offer(bv, bi, ok ? -x : INFINITY, ok ? id0 + i : -1, K, lane);
+    x = xn;
+    i = in;
+  }
+  mv[w][lane] = bv;
+  mi[w][lane] = bi;
+  __syncthreads();
+  if (w == 0) {
+    for (int g = 1; g < 4; ++g) wave_merge64(bv, bi, mv[g][lane], mi[g][lane], lane);
+    if (lane < K) {
+      const size_t o = ((size_t)b * chunks + chunk) * K + lane;
+      cand_v[o] = bi >= 0 ? -bv : -INFINITY;
+      cand_i[o] = bi;
+    }
+  }
+}
+
 __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -260,7 +306,34 @@ __global__ __launch_bounds__(SC_THREADS) void sample_candidates_kernel(
   const int b = blockIdx.x;
   int K = top_ks[b];
   if (K <= 0 || K > n_cand) K = n_cand;
-  if (K <= 64 && list_len > 0) {
+  if (K <= 64 && list_len > 0 && list_len <= 64 && n_cand / list_len > 8) {
+    // Many lists (small-batch chunked top-k, x TP ranks): merged by the lane network -- wave w folds
+    // lists w, w + 4, ... into its running sorted top-64 (keys = -value), then wave 0 folds the four.
+    const int R = n_cand / list_len;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float bv = INFINITY;
+    int bi = -1;
+    for (int r = w; r < R; r += SC_THREADS / 64) {
+      const size_t o = (size_t)b * n_cand + (size_t)r * list_len + lane;
+      const int id = lane < list_len ? cand_i[o] : -1;
+      const float v = lane < list_len ? cand_v[o] : -INFINITY;
+      wave_merge64(bv, bi, id >= 0 ? -v : INFINITY, id, lane);
+    }
+    sv[w * 64 + lane] = bv;
+    si[w * 64 + lane] = bi;
+    __syncthreads();
+    if (w == 0) {
+      for (int g = 1; g < SC_THREADS / 64; ++g) wave_merge64(bv, bi, sv[g * 64 + lane], si[g * 64 + lane], lane);
+      mv[lane] = bi >= 0 ? -bv : -INFINITY;
+      mi[lane] = bi;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      sv[threadIdx.x] = mv[threadIdx.x];
+      si[threadIdx.x] = mi[threadIdx.x];
+    }
+    __syncthreads();
+  } else if (K <= 64 && list_len > 0) {
     // The candidate lists (R = n_cand / list_len of them) are each sorted in the total order
     // (value desc, vocabulary id asc as unsigned, position asc): the global top-64 is found by
     // ranking every candidate -- its position in its own list plus a binary search per other list --
@@ -407,6 +480,11 @@ RAGK_API int ragk_topk_candidates(const float* logits, int ld, int B, int V, int
   if (B <= 0) return 0;
   if (K < 1 || K > MAXK || chunks < 1 || chunks > 64) return (int)hipErrorInvalidValue;
   const int Vc = ((V + chunks - 1) / chunks + 7) & ~7;
+  if (K <= 64 && Vc <= TW_VMAX && chunks >= 8) {  // small batch, many short chunks
+    hipLaunchKernelGGL(topk_wave_kernel, dim3(B * chunks), dim3(TW_THREADS), 0, st, logits, ld, V, K, vocab_offset,
+                       chunks, cand_v, cand_i);
+    return (int)hipGetLastError();
+  }
   if (Vc <= TK_VMAX) {
     static bool attr = false;  // > 64 KiB of dynamic LDS needs the opt-in
     if (!attr) {

@@ -29,79 +29,6 @@ constexpr int ST = 256;   // threads per block (4 waves)
 constexpr int DCH = 256;  // query dims staged per LDS chunk
 constexpr int UNR = 16;   // dims (independent loads) in flight per lane
 
-__device__ __forceinline__ bool cand_lt(float av, int ai, float bv, int bi) {
-  return av < bv || (av == bv && (unsigned)ai < (unsigned)bi);
-}
-
-// value of lane (lane ^ j), j a power of two that is a compile-time constant after unrolling: every
-// exchange stays on the VALU -- DPP quad permutes / mirrors (one or two moves) for j <= 8,
-// v_permlane16_swap / v_permlane32_swap for 16 / 32 -- instead of the LDS-pipe ds_bpermute (or
-// ds_swizzle) whose round trip bounded every step of the networks below.
-__device__ __forceinline__ int xor_lane(int v, int j, int lane) {
-  if (j == 1) return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-  if (j == 2) return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  if (j == 4)  // (i ^ 3) then the 8-lane mirror (i ^ 7): i ^ 4
-    return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x1B, 0xF, 0xF, false), 0x141, 0xF, 0xF, false);
-  if (j == 8)  // 8-lane mirror (i ^ 7) then the row mirror (i ^ 15): i ^ 8
-    return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false), 0x140, 0xF, 0xF, false);
-  if (j == 16) {  // odd rows of vdst <-> even rows of vsrc
-    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return ((lane >> 4) & 1) ? (int)p[0] : (int)p[1];
-  }
-  if (j == 32) {
-    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return lane < 32 ? (int)p[1] : (int)p[0];
-  }
-  return __shfl_xor(v, j, 64);
-}
-
-// value of lane 63 - lane (= lane ^ 63): DPP row mirror (lane ^ 15), then xor 16 and xor 32
-__device__ __forceinline__ int rev_lane(int v, int lane) {
-  return xor_lane(xor_lane(__builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false), 16, lane), 32, lane);
-}
-__device__ __forceinline__ float rev_lane(float v, int lane) { return __int_as_float(rev_lane(__float_as_int(v), lane)); }
-
-// one compare-exchange step of a lane-level bitonic network (partner = lane ^ j)
-__device__ __forceinline__ void cx(float& v, int& i, int lane, int j, bool asc) {
-  const float ov = __int_as_float(xor_lane(__float_as_int(v), j, lane));
-  const int oi = xor_lane(i, j, lane);
-  const bool keep_min = ((lane & j) == 0) == asc;
-  const bool take = keep_min ? cand_lt(ov, oi, v, i) : cand_lt(v, i, ov, oi);
-  if (take) {
-    v = ov;
-    i = oi;
-  }
-}
-
-// ascending sort of the 64 (v, i) pairs held one per lane
-__device__ __forceinline__ void wave_sort64(float& v, int& i, int lane) {
-#pragma unroll
-  for (int kk = 2; kk <= 64; kk <<= 1)
-#pragma unroll
-    for (int j = kk >> 1; j > 0; j >>= 1) cx(v, i, lane, j, (lane & kk) == 0);
-}
-
-// (bv, bi) sorted ascending, (nv, ni) sorted ascending -> (bv, bi) = the 64 smallest of both, sorted
-__device__ __forceinline__ void wave_merge64(float& bv, int& bi, float nv, int ni, int lane) {
-  const float rv = rev_lane(nv, lane);
-  const int ri = rev_lane(ni, lane);
-  if (cand_lt(rv, ri, bv, bi)) {
-    bv = rv;
-    bi = ri;
-  }
-#pragma unroll
-  for (int j = 32; j > 0; j >>= 1) cx(bv, bi, lane, j, true);
-}
-
-// feed 64 unsorted candidates (one per lane) into the running top list; k-th best = threshold
-__device__ __forceinline__ void wave_offer(float& bv, int& bi, float v, int id, int k, int lane) {
-  const float tv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bv), k - 1));  // k uniform
-  const int ti = __builtin_amdgcn_readlane(bi, k - 1);
-  if (!__any(cand_lt(v, id, tv, ti))) return;  // wave-uniform
-  wave_sort64(v, id, lane);
-  wave_merge64(bv, bi, v, id, lane);
-}
-
 // wave_offer for QB queries at once (the same 64 rows, one candidate per lane and query): the QB
 // bitonic networks run interleaved step by step, so the cross-lane permutes of one query's
 // dependent chain hide behind the others' (one query at a time left a 16-query block

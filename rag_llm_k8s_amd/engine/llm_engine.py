@@ -36,7 +36,9 @@ from ..ops.backend import AttnMeta
 from ..utils import faults
 from .kv_manager import BLOCK, make_block_manager
 
-SMALL_BATCH_TOPK_MAX_B = int(os.environ.get("RAGK_TOPK_SMALL_B", "0"))  # off: see docs/PERF_NOTES.md
+# decode batches up to this size split each row's top-k over ~31 chunks of ~4k logits (topk_wave_kernel,
+# merged by the sampler's lane network); larger batches use 7 radix-select chunks (topk_lds)
+SMALL_BATCH_TOPK_MAX_B = int(os.environ.get("RAGK_TOPK_SMALL_B", "4"))
 SMALL_BATCH_TOPK_CHUNK = int(os.environ.get("RAGK_TOPK_SMALL_CHUNK", "4096"))
 
 log = logging.getLogger(__name__)

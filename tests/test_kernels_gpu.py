@@ -1,6 +1,7 @@
 """T1 kernel tier: every gfx950 HIP kernel vs a plain PyTorch fp32 reference of the same op."""
 import math
 
+import numpy as np
 import pytest
 import torch
 
@@ -613,7 +614,8 @@ def test_topk_and_greedy(native):
 
 
 @pytest.mark.parametrize("V,K,chunks,topk", [(128256, 64, 7, 50), (4000, 50, 3, 50), (30000, 64, 16, 64),
-                                              (37, 50, 3, 40)])
+                                              (37, 50, 3, 40), (128256, 64, 31, 50), (16032, 64, 4, 50),
+                                              (20000, 50, 12, 50)])
 def test_sample_list_merge_matches_sort(native, V, K, chunks, topk):
     """Rank-merging the sorted per-chunk candidate lists (top_k <= 64) samples exactly the same tokens
     as the full bitonic sort of all candidates: sampled (many seeds), greedy, and with -inf padding
@@ -626,6 +628,40 @@ def test_sample_list_merge_matches_sort(native, V, K, chunks, topk):
     for temp in (0.7, 0.0):
         args = (torch.full((B,), temp, device=DEV), torch.full((B,), topk, dtype=torch.int32, device=DEV),
                 torch.full((B,), 0.9, device=DEV), torch.arange(B, dtype=torch.int64, device=DEV) * 31 + 7,
+                torch.arange(B, dtype=torch.int32, device=DEV))
+        a = native.sample_candidates(cv, ci, *args)
+        b = native.sample_candidates(cv, ci, *args, list_len=K)
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,V,chunks", [(1, 128256, 31), (4, 128256, 31), (3, 16032, 9), (2, 5000, 8), (2, 200, 9)])
+def test_small_batch_topk_chunks_exact(native, B, V, chunks):
+    """Small decode batches: many short chunks selected by the wave-network kernel -- each chunk's list is
+    the exact sorted top-K of its slice (ties: lower id first), and the sampler's network merge of the
+    lists equals the full sort."""
+    torch.manual_seed(B * V)
+    K = 64
+    logits = (torch.randn(B, V, device=DEV) * 3).contiguous()
+    logits[:, 7] = logits[:, 3]  # exact ties
+    logits[:, 100:164] = logits[:, 100:101]  # a run of 64 equal values
+    cv, ci = native.topk_candidates(logits, K, chunks=chunks)
+    Vc = ((V + chunks - 1) // chunks + 7) & ~7
+    n_valid = 0
+    for c in range(chunks):
+        sl = logits[:, c * Vc: min((c + 1) * Vc, V)].cpu()
+        kk = min(K, sl.shape[1])
+        if kk <= 0:
+            continue
+        n_valid += kk
+        for b in range(B):  # reference order: value descending, index ascending
+            idx = torch.from_numpy(np.lexsort((np.arange(sl.shape[1]), -sl[b].numpy())))
+            assert torch.equal(ci[b, c * K:c * K + kk].cpu().long(), idx[:kk] + c * Vc), (b, c)
+            assert torch.equal(cv[b, c * K:c * K + kk].cpu(), sl[b, idx[:kk]])
+    valid = ci >= 0
+    assert int(valid.sum()) == B * n_valid and bool(torch.isinf(cv[~valid]).all())
+    for temp in (0.7, 0.0):
+        args = (torch.full((B,), temp, device=DEV), torch.full((B,), 50, dtype=torch.int32, device=DEV),
+                torch.full((B,), 0.9, device=DEV), torch.arange(B, dtype=torch.int64, device=DEV) * 3 + 1,
                 torch.arange(B, dtype=torch.int32, device=DEV))
         a = native.sample_candidates(cv, ci, *args)
         b = native.sample_candidates(cv, ci, *args, list_len=K)
