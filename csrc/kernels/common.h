@@ -264,8 +264,11 @@ __device__ __forceinline__ void pf_rider(const PfArgs& a, int r, int nr) {
 // ---- lane-level bitonic networks over (value, id) pairs held one per lane of a wave (ascending by
 // value, ties -> lower id as unsigned): the wave-resident top-64 lists of the L2 search and the
 // small-batch sampler top-k. Every lane exchange stays on the VALU.
+// Branch-free (bitwise | and &, selects): the short-circuit forms compiled to exec-mask branches around
+// every compare-exchange, ~15 scalar / branch instructions per network step on a one-wave-per-SIMD
+// dependent chain.
 __device__ __forceinline__ bool cand_lt(float av, int ai, float bv, int bi) {
-  return av < bv || (av == bv && (unsigned)ai < (unsigned)bi);
+  return (av < bv) | ((av == bv) & ((unsigned)ai < (unsigned)bi));
 }
 
 // value of lane (lane ^ j), j a power of two that is a compile-time constant after unrolling: every
@@ -301,11 +304,10 @@ __device__ __forceinline__ void cx(float& v, int& i, int lane, int j, bool asc) 
   const float ov = __int_as_float(xor_lane(__float_as_int(v), j, lane));
   const int oi = xor_lane(i, j, lane);
   const bool keep_min = ((lane & j) == 0) == asc;
-  const bool take = keep_min ? cand_lt(ov, oi, v, i) : cand_lt(v, i, ov, oi);
-  if (take) {
-    v = ov;
-    i = oi;
-  }
+  // keep_min: take the partner iff it precedes; keep_max: iff it does not (equal pairs: either)
+  const bool take = keep_min == cand_lt(ov, oi, v, i);
+  v = take ? ov : v;
+  i = take ? oi : i;
 }
 
 // ascending sort of the 64 (v, i) pairs held one per lane
@@ -320,10 +322,9 @@ __device__ __forceinline__ void wave_sort64(float& v, int& i, int lane) {
 __device__ __forceinline__ void wave_merge64(float& bv, int& bi, float nv, int ni, int lane) {
   const float rv = rev_lane(nv, lane);
   const int ri = rev_lane(ni, lane);
-  if (cand_lt(rv, ri, bv, bi)) {
-    bv = rv;
-    bi = ri;
-  }
+  const bool take = cand_lt(rv, ri, bv, bi);
+  bv = take ? rv : bv;
+  bi = take ? ri : bi;
 #pragma unroll
   for (int j = 32; j > 0; j >>= 1) cx(bv, bi, lane, j, true);
 }

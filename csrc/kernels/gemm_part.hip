@@ -88,13 +88,28 @@ __host__ __device__ inline int mg_groups(int M, int KS) {
   return pg;
 }
 
-template <int MT, int NKS, bool FP8 = false, int NR = 0, int NV = 1, bool MG = false>
+// SG (down projection at decode batch <= 4 under tensor parallelism): the activation is silu(gate) * up
+// of the packed gate/up projection's UNREDUCED split-K partials Pgu[S1][M][2K] (gemm_part of the
+// packed weight, 128-row tiles of [64 gate | 64 up], ops/reference.py pack_gate_up): each block sums
+// the S1 slabs of the gate and up columns of its own K-slice, applies silu(g) * u (fp32, rounded to
+// bf16 once -- the silu_mul epilogue's math) and stages the slice in LDS. The gate/up GEMM then
+// streams its shard with every load in flight instead of the register-streaming skinny kernel
+// (12.8 us for a 29 MB TP=8 shard, profiles/tp_decode_probe_kernels_r3.txt). One item per thread:
+// row tid / CPR, 8 columns (tid % CPR) * 8; all S1 slabs' loads issued before the weight stream.
+constexpr int SG_MAXS = 4;
+struct SiluArgs {
+  const float* pgu;  // [S1][M][2K]
+  int S1;
+};
+
+template <int MT, int NKS, bool FP8 = false, int NR = 0, int NV = 1, bool MG = false, bool SG = false>
 __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), MG ? 2 : 1) void gemm_part_kernel(const bf16_t* __restrict__ X, int ldx,
                                                                   const bf16_t* __restrict__ W, int ldw,
                                                                   float* __restrict__ P, int M, int N, int K,
                                                                   const float* __restrict__ wscale = nullptr,
                                                                   const bf16_t* __restrict__ gamma = nullptr,
-                                                                  float eps = 0.f, MergeArgs mg = {}) {
+                                                                  float eps = 0.f, MergeArgs mg = {},
+                                                                  SiluArgs sg = {}) {
   constexpr int KS = NKS * 64;          // K-slice of the block (two halves of NKS k-steps of 32)
   constexpr int XROWS = 16 * MT;
   constexpr int ROWB = KS * 2;          // bytes per LDS row
@@ -116,7 +131,7 @@ __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), MG ? 2 : 1) voi
   constexpr int CPR = ROWB / 16;                 // chunks per row
   constexpr int PIECES = XBYTES / 1024;          // 1-KiB pieces (64 lanes x 16 B)
   constexpr int PPW = PIECES / (PT_THREADS / 64);
-  static_assert(PIECES % (PT_THREADS / 64) == 0 && CPR >= 64, "activation slice shape");
+  static_assert(PIECES % (PT_THREADS / 64) == 0 && CPR >= 16, "activation slice shape");
   u32x4 hv[NORM ? NR : 1][NV];  // NORM: raw row vectors (tid & 255) + 256 i
   u32x4 gv[NV];
   if constexpr (NORM) {
@@ -214,7 +229,22 @@ __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), MG ? 2 : 1) voi
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-  } else {
+  }
+  f32x4 sgv[SG ? SG_MAXS : 1][4];  // SG: gate lo/hi, up lo/hi of each slab
+  if constexpr (SG) {
+    // (loads unconditional: row / slab clamped, masked at use, so one counted vmcnt retires them)
+    const int r = min(tid / CPR, M - 1), c = tid % CPR;
+    const int j = kbase + 8 * c;
+    const float* pg = sg.pgu + (size_t)r * 2 * K + (j >> 6) * 128 + (j & 63);
+#pragma unroll
+    for (int s2 = 0; s2 < SG_MAXS; ++s2) {
+      const float* ps = pg + (size_t)min(s2, sg.S1 - 1) * M * 2 * K;
+      sgv[s2][0] = *reinterpret_cast<const f32x4*>(ps);
+      sgv[s2][1] = *reinterpret_cast<const f32x4*>(ps + 4);
+      sgv[s2][2] = *reinterpret_cast<const f32x4*>(ps + 64);
+      sgv[s2][3] = *reinterpret_cast<const f32x4*>(ps + 68);
+    }
+  } else if constexpr (!NORM && !MG) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int p = wid * PPW + i;
@@ -248,6 +278,29 @@ __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), MG ? 2 : 1) voi
   // vmcnt(NLD): the DMA / row loads (older than the NLD weight loads) have landed
   __builtin_amdgcn_s_waitcnt((NLD & 15) | (((NLD >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (SG) {
+    const int r = tid / CPR, c = tid % CPR;
+    if (r < M) {
+      f32x4 g0 = sgv[0][0], g1 = sgv[0][1], u0 = sgv[0][2], u1 = sgv[0][3];
+#pragma unroll
+      for (int s2 = 1; s2 < SG_MAXS; ++s2) {
+        if (s2 < sg.S1) {
+          g0 += sgv[s2][0];
+          g1 += sgv[s2][1];
+          u0 += sgv[s2][2];
+          u1 += sgv[s2][3];
+        }
+      }
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = silu(g0[e]) * u0[e];
+        o[4 + e] = silu(g1[e]) * u1[e];
+      }
+      *reinterpret_cast<u32x4*>(smem + r * ROWB + 16 * ((c & ~15) | ((c & 15) ^ (r & 15)))) = pack8(o);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
   if constexpr (NORM) {
     // RMSNorm statistics (rmsnorm_kernel order), then the normalised slice -> LDS (rows >= M are
     // left as they are: their accumulator rows are never stored)
@@ -349,25 +402,26 @@ __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), MG ? 2 : 1) voi
   }
 }
 
-template <int MT, bool FP8 = false, int NR = 0, int NV = 1, bool MG = false>
+template <int MT, bool FP8 = false, int NR = 0, int NV = 1, bool MG = false, bool SG = false>
 int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K, int ks_steps,
                    hipStream_t st, const float* wscale = nullptr, const void* gamma = nullptr, float eps = 0.f,
-                   MergeArgs mg = {}) {
+                   MergeArgs mg = {}, SiluArgs sg = {}) {
   const int KS = ks_steps * 64;
   const dim3 grid((N + PT_NB - 1) / PT_NB, K / KS);
 #define RAGK_PART(NK)                                                                                       \
   case NK:                                                                                                  \
     if constexpr (16 * MT * NK * 64 * 2 <= 128 * 1024 && (16 * MT * NK * 64 * 2) % 8192 == 0 &&           \
-                  (NR == 0 || NK == 8 || NK == 16) && (!MG || NK == 8)) {                                   \
-      hipLaunchKernelGGL((gemm_part_kernel<MT, NK, FP8, NR, NV, MG>), grid, dim3(PT_THREADS + (MG ? MG_THREADS : 0)), \
+                  (NR == 0 || NK == 8 || NK == 16) && (!MG || NK == 4 || NK == 8) && (!SG || NK <= 16)) {   \
+      hipLaunchKernelGGL((gemm_part_kernel<MT, NK, FP8, NR, NV, MG, SG>), grid, dim3(PT_THREADS + (MG ? MG_THREADS : 0)), \
                          0, st,                                                                             \
                          (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, P, M, N, K, wscale, (const bf16_t*)gamma, \
-                         eps, mg);                                                                          \
+                         eps, mg, sg);                                                                      \
       break;                                                                                                \
     } else {                                                                                                \
       return (int)hipErrorInvalidValue;                                                                     \
     }
   switch (ks_steps) {
+    RAGK_PART(4)
     RAGK_PART(8)
     RAGK_PART(14)
     RAGK_PART(16)
@@ -382,9 +436,11 @@ int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int
 
 }  // namespace
 
-// Slice choice: K-slice KS = 64 * ks_steps (ks_steps in {8, 14, 16, 28, 32}; 14 / 28 divide the
-// K = 14336 of Llama's down projection into 16 / 8 slabs); S = K / KS slabs.
-// Picks the largest slice that still gives >= 256 blocks and fits the activation slice in LDS.
+// Slice choice: K-slice KS = 64 * ks_steps (ks_steps in {4, 8, 14, 16, 28, 32}; 14 / 28 divide the
+// K = 14336 of Llama's down projection into 16 / 8 slabs; 4 = 256-wide slices for the narrow K of
+// tensor-parallel shards: down at TP=8 has K = 1792 = 7 x 256, o_proj K = 512); S = K / KS slabs.
+// Picks the largest slice that still gives >= g_part_min_blocks blocks and fits the activation slice
+// in LDS, else the smallest legal slice (most blocks).
 static int g_part_min_blocks = 256;
 RAGK_API int ragk_gemm_part_set_min_blocks(int n) {
   g_part_min_blocks = n > 0 ? n : 256;
@@ -395,7 +451,7 @@ RAGK_API int ragk_gemm_part_ksteps(int M, int N, int K) {
   const int mt = (M + 15) / 16;
   const int nb = (N + PT_NB - 1) / PT_NB;
   int best = 0;
-  for (int ks : {32, 28, 16, 14, 8}) {
+  for (int ks : {32, 28, 16, 14, 8, 4}) {
     const int KS = ks * 64;
     if (K % KS) continue;
     if (16 * mt * KS * 2 > 128 * 1024 || (16 * mt * KS * 2) % 8192) continue;  // LDS; 8 waves x 1-KiB DMA pieces
@@ -438,6 +494,24 @@ RAGK_API int ragk_gemm_part_norm(const void* X, int ldx, const void* gamma, floa
 #undef RAGK_PN
 }
 
+// Down projection fed by the packed gate/up projection's split-K partials (SG above): P = partials of
+// (silu(gate) * up) . W^T, gate / up = sum of the S1 slabs of pgu [S1][M][2K] (gemm_part of the packed
+// [2K, H] weight). M <= 4, S1 <= 4, K % 64 == 0, one staging item per thread (M * 8 * ks_steps <= 512).
+RAGK_API int ragk_gemm_part_silu(const float* pgu, int S1, const void* W, int ldw, float* P, int M, int N, int K,
+                                 int ks_steps, hipStream_t st) {
+  if (M <= 0) return 0;
+  if (!pgu || M > 4 || S1 < 1 || S1 > SG_MAXS || K % 64 || ks_steps <= 0 || ks_steps > 16 ||
+      K % (64 * ks_steps) || M * 8 * ks_steps > PT_THREADS)
+    return (int)hipErrorInvalidValue;
+  return launch_part_mt<1, false, 0, 1, false, true>(nullptr, 0, W, ldw, P, M, N, K, ks_steps, st, nullptr, nullptr,
+                                                      0.f, {}, SiluArgs{pgu, S1});
+}
+
+RAGK_API int ragk_gemm_part_silu_ok(int M, int S1, int K, int ks_steps) {
+  return M >= 1 && M <= 4 && S1 >= 1 && S1 <= SG_MAXS && K % 64 == 0 && ks_steps > 0 && ks_steps <= 16 &&
+         K % (64 * ks_steps) == 0 && M * 8 * ks_steps <= PT_THREADS;
+}
+
 // W8A16 variant: W = e4m3fn [N][K] bytes (ldw in bytes), wscale = fp32 [N]; same slabs / slices.
 RAGK_API int ragk_gemm_part_fp8(const void* X, int ldx, const void* W8, int ldw, const float* wscale, float* P, int M,
                                 int N, int K, int ks_steps, hipStream_t st) {
@@ -457,13 +531,13 @@ RAGK_API int ragk_gemm_part_fp8(const void* X, int ldx, const void* W8, int ldw,
 
 // o_proj fed by the decode attention's unmerged partitions (MG above; the attention launched with its
 // merge deferred, ragk_attn_decode_set_defer). X (bf16 rows, out_stride) is the attention output buffer:
-// rows whose sequence used one partition are read from it. M <= 4, head dim 128, K = Hq * 128, 8-step
-// K-slices (a 16-step slice spills), at most MG_MAXPP partitions per thread. w8 / wscale: fp8 weights (ldw in bytes).
+// rows whose sequence used one partition are read from it. M <= 4, head dim 128, K = Hq * 128, 8- or
+// 4-step K-slices (a 16-step slice spills), at most MG_MAXPP partitions per thread. w8 / wscale: fp8 weights (ldw in bytes).
 RAGK_API int ragk_gemm_part_merge(const float* part_o, const float* part_ml, const void* out, int out_stride,
                                   const int* kv_lens, int Hq, int part_tiles, int max_parts, const void* W, int ldw,
                                   const float* wscale, float* P, int M, int N, int K, int ks_steps, hipStream_t st) {
   if (M <= 0) return 0;
-  if (M > MG_MAXR || K != Hq * MG_D || ks_steps != 8 || K % (64 * ks_steps) || max_parts < 2 ||
+  if (M > MG_MAXR || K != Hq * MG_D || (ks_steps != 8 && ks_steps != 4) || K % (64 * ks_steps) || max_parts < 2 ||
       !part_o || !part_ml || !out || !kv_lens || part_tiles < 1)
     return (int)hipErrorInvalidValue;
   const int npg = mg_groups(M, ks_steps * 64);
@@ -476,7 +550,7 @@ RAGK_API int ragk_gemm_part_merge(const float* part_o, const float* part_ml, con
 }
 
 RAGK_API int ragk_gemm_part_merge_ok(int M, int K, int Hq, int max_parts, int ks_steps) {
-  if (M <= 0 || M > MG_MAXR || K != Hq * MG_D || ks_steps != 8 || max_parts < 2) return 0;
+  if (M <= 0 || M > MG_MAXR || K != Hq * MG_D || (ks_steps != 8 && ks_steps != 4) || max_parts < 2) return 0;
   const int npg = mg_groups(M, ks_steps * 64);
   return (max_parts + npg - 1) / npg <= MG_MAXPP;
 }

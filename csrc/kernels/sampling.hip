@@ -262,11 +262,13 @@ __global__ __launch_bounds__(TW_THREADS) void topk_wave_kernel(const float* __re
   float bv = INFINITY;  // padding sorts after real -inf logits (id 0xffffffff unsigned)
   int bi = -1;
   int i = w * 64 + lane;
-  float x = i < V ? row[i] : 0.f;
+  // loads unconditional (index clamped, masked at use): a load behind a branch gets its own vmcnt(0),
+  // which would wait for the prefetched next tile as well
+  float x = row[min(i, V - 1)];
   for (int base = w * 64; base < V; base += 4 * 64) {
     const bool ok = i < V;
     const int in = i + 4 * 64;
-    const float xn = in < V ? row[in] : 0.f;  // next tile in flight while this one is offered
+    const float xn = row[min(in, V - 1)];  // next tile in flight while this one is offered
     wave_offer(bv, bi, ok ? -x : INFINITY, ok ? id0 + i : -1, K, lane);
     x = xn;
     i = in;

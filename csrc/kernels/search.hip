@@ -461,13 +461,14 @@ __global__ __launch_bounds__(ST) void ivf_scan_kernel(const float* __restrict__ 
   }
 }
 
-// in: [nq][G][k] sorted lists -> out: [nq][k]. One block of MW waves per query; each wave takes 64
+// in: [nq][G][k] sorted lists -> out: [nq][k] (distances fp32, ids int64). One block of MW waves per query; each wave takes 64
 // candidates at a time (64 / k whole lists per step) and offers them to its running top list; the
 // waves' lists are merged last.
 constexpr int MW = 16;
 __global__ __launch_bounds__(MW * 64) void topk_lists_merge_kernel(const float* __restrict__ in_d,
                                                                    const int* __restrict__ in_i, int G, int k,
-                                                                   float* __restrict__ out_d, int* __restrict__ out_i) {
+                                                                   float* __restrict__ out_d,
+                                                                   long long* __restrict__ out_i) {
   __shared__ float mv[MW][64];
   __shared__ int mi[MW][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -499,7 +500,7 @@ __global__ __launch_bounds__(MW * 64) void topk_lists_merge_kernel(const float* 
     for (int gg = 1; gg < MW; ++gg) wave_merge64(bv, bi, mv[gg][lane], mi[gg][lane], lane);
     if (lane < k) {
       out_d[(size_t)qi * k + lane] = bv;
-      out_i[(size_t)qi * k + lane] = bi;
+      out_i[(size_t)qi * k + lane] = bi;  // int64 ids: the caller's final type, no widening launch
     }
   }
 }
@@ -710,8 +711,8 @@ RAGK_API int ragk_l2_search_groups(int row_begin, int row_end, int nq, int k, in
 // Exact top-k (k <= 64) over rows [row_begin, row_end) of xt[d][cap]; part_d / part_i hold
 // nq * ragk_l2_scan_groups(...) * k entries; results -> out_d / out_i [nq][k].
 RAGK_API int ragk_l2_search(const float* xt, int cap, int d, int row_begin, int row_end, const float* q, int nq,
-                            int k, const int* ids_map, float* part_d, int* part_i, float* out_d, int* out_i,
-                            hipStream_t st) {
+                            int k, const int* ids_map, float* part_d, int* part_i, float* out_d,
+                            long long* out_i, hipStream_t st) {
   if (nq <= 0) return 0;
   if (k < 1 || k > 64 || d < 1 || cap < 1 || row_end > cap) return (int)hipErrorInvalidValue;
   if (use_mfma(nq, k, d)) {
@@ -767,7 +768,7 @@ RAGK_API int ragk_l2_search(const float* xt, int cap, int d, int row_begin, int 
 // IVF: part buffers hold nq * nprobe * k entries; results -> out [nq][k]
 RAGK_API int ragk_ivf_search(const float* xt, int cap, int d, const float* q, int nq, const int* probes, int nprobe,
                              const int* offsets, const int* ends, const int* ids_map, int k, float* part_d,
-                             int* part_i, float* out_d, int* out_i, hipStream_t st) {
+                             int* part_i, float* out_d, long long* out_i, hipStream_t st) {
   if (nq <= 0) return 0;
   if (d > IVF_DMAX || k < 1 || k > 64 || nprobe < 1 || cap < 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(ivf_scan_kernel, dim3(nprobe, nq), dim3(ST), 0, st, xt, cap, d, q, probes, nprobe, offsets, ends,

@@ -40,7 +40,11 @@ DECODE_NORM_FUSED = os.environ.get("RAGK_DECODE_NORM_FUSED", "1") == "1"
 # decode batch <= 4: the o_proj split-K GEMM merges the attention's split-K partitions itself
 # (gemm_part_merge), so the attention's separate merge launch disappears
 DECODE_OPROJ_MERGE = os.environ.get("RAGK_DECODE_OPROJ_MERGE", "1") == "1"
-DECODE_OPROJ_MERGE_MAX_M = int(os.environ.get("RAGK_DECODE_OPROJ_MERGE_MAX_M", "2"))  # batch 4: 2 merge rounds, slower
+DECODE_OPROJ_MERGE_MAX_M = int(os.environ.get("RAGK_DECODE_OPROJ_MERGE_MAX_M", "2"))
+# decode batch <= 4: gate/up as split-K partials, silu(gate) * up formed inside the down GEMM's staging
+# (gemm_part.hip SG): "tp" = under tensor parallelism only (the TP=1 batch <= 4 path keeps the skinny
+# down GEMM with its fused residual), "1" = always, "0" = never
+DECODE_SILU_FUSED = os.environ.get("RAGK_DECODE_SILU_FUSED", "tp")  # batch 4: 2 merge rounds, slower
 
 
 @dataclass
@@ -364,6 +368,11 @@ class LlamaModel:
         # batch <= 4: the input norm runs inside the qkv GEMM (gemm_part_norm) -- one launch fewer per layer
         fuse_norm = (DECODE_NORM_FUSED and M <= DECODE_DOWN_SKINNY_MAX_M and not pf and not tp
                      and be.part_norm_ok(M, layers[0]["wqkv"]))
+        # batch <= 4 (TP): silu(gate) * up inside the down GEMM; the down partials then go through the
+        # reduce + norm consumer, so the next layer's input norm is not fused into its qkv GEMM
+        silu_fused = (not pf and (DECODE_SILU_FUSED == "1" or (DECODE_SILU_FUSED == "tp" and tp))
+                      and be.part_silu_ok(M, layers[0]["wgu"], layers[0]["wdown"]))
+        fuse_norm = fuse_norm and not silu_fused
         xn = None if fuse_norm else be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
         merge = (DECODE_OPROJ_MERGE and DECODE_ROPE_FUSED and not pf and M <= DECODE_OPROJ_MERGE_MAX_M
                  and be.part_merge_ok(M, inp.meta, layers[0]["wo"], Hq, D))
@@ -393,8 +402,12 @@ class LlamaModel:
             if pf:
                 be.pf_arm([(L["wgu"], pf["attn"] // 2, pf["post"])], pf["blocks"])
             xn = reduce_norm(P, L["ln_post"])
-            a = be.gemm(xn, L["wgu"], epi="silu_mul")
             nxt = layers[li + 1]["ln_in"] if li + 1 < len(layers) else w.norm
+            if silu_fused:
+                P = be.gemm_part_silu(be.gemm_part_gu(xn, L["wgu"]), L["wdown"])
+                xn = reduce_norm(P, nxt)
+                continue
+            a = be.gemm(xn, L["wgu"], epi="silu_mul")
             if M <= DECODE_DOWN_SKINNY_MAX_M and not tp:
                 # tiny batch: the register-streaming GEMM with the fused residual + a plain norm beats
                 # the split-K partials + consumer by ~2 us (profiles/decode_gemm_graph_ab_M_r2.log)

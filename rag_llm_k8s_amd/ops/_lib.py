@@ -40,6 +40,8 @@ _SIGS = {
     "ragk_attn_decode_set_defer": [I],
     "ragk_gemm_part_merge": [P, P, P, I, P, I, I, I, P, I, P, P, I, I, I, I, S],
     "ragk_gemm_part_merge_ok": [I, I, I, I, I],
+    "ragk_gemm_part_silu": [P, I, P, I, P, I, I, I, I, S],
+    "ragk_gemm_part_silu_ok": [I, I, I, I],
     "ragk_attn_prefill_set_waves": [I],
     "ragk_attn_prefill_stamp": [P, I, P, P, P, I, P, P, P, I, P, I, I, I, F, P, S],
     "ragk_gemm_w4_diag": [I, I, P, I, P, I, P, I, I, I, I, P, S],

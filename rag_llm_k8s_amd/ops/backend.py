@@ -127,6 +127,20 @@ class TorchBackend:
     def part_norm_ok(self, M, w):
         return self.enable_part and M <= 4 and not isinstance(w, Fp8Weight) and w.shape[1] <= 8192
 
+    def part_silu_ok(self, M, w_gu, w_down):
+        return (self.enable_part and M <= 4 and not isinstance(w_gu, Fp8Weight) and not isinstance(w_down, Fp8Weight)
+                and w_down.shape[1] % 64 == 0)
+
+    def gemm_part_gu(self, x, w):
+        return self.gemm_part(x, w)
+
+    def gemm_part_silu(self, pgu, w):
+        gu = pgu.float().sum(0)
+        M, K2 = gu.shape
+        t = gu.view(M, K2 // 128, 2, 64)
+        a = (torch.nn.functional.silu(t[:, :, 0, :]) * t[:, :, 1, :]).reshape(M, K2 // 2).to(torch.bfloat16)
+        return self.gemm_part(a, w)
+
     def gemm_part_norm(self, h, gamma, eps, w):
         return self.gemm_part(R.rmsnorm(h, gamma, eps), w)
 
@@ -258,6 +272,15 @@ class NativeBackend(TorchBackend):
 
     def gemm_part_norm(self, h, gamma, eps, w):
         return self.n.gemm_part_norm(h, gamma, eps, w)
+
+    def part_silu_ok(self, M, w_gu, w_down):
+        return self.enable_part and self.n.gemm_part_silu_ok(M, w_gu, w_down)
+
+    def gemm_part_gu(self, x, w):
+        return self.n.gemm_part_gu(x, w)
+
+    def gemm_part_silu(self, pgu, w):
+        return self.n.gemm_part_silu(pgu, w)
 
     def pf_arm(self, ranges, blocks):
         self.n.pf_arm(ranges, blocks)

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import math
 import os
+import threading
 
 import torch
 
@@ -327,6 +328,67 @@ def gemm_part_merge(attn_out, kv_lens, part_tiles, max_parts, ws_o, ws_ml, Hq, w
         ws_o.data_ptr(), ws_ml.data_ptr(), attn_out.data_ptr(), attn_out.stride(0), kv_lens.data_ptr(), Hq,
         part_tiles, max_parts, wt.data_ptr(), wt.stride(0), w.scale.data_ptr() if fp8 else None, out.data_ptr(), M, N,
         K, ks, stream_ptr()), "ragk_gemm_part_merge")
+    return out
+
+
+SILU_MAX_SLABS = 4  # gemm_part.hip SG_MAXS
+
+
+def gemm_part_gu_ks(K):
+    """K-slice steps of the packed gate/up partial GEMM feeding gemm_part_silu: at most 4 slabs."""
+    for ks in (4, 8, 16, 32):
+        if K % (64 * ks) == 0 and K // (64 * ks) <= SILU_MAX_SLABS:
+            return ks
+    return 0
+
+
+def _silu_ks(M, N, K):
+    """K-slice steps of gemm_part_silu: the SG variant is built for 4/8/16-step slices with one staging
+    item per thread (M * 8 * ks <= 512); as gemm_part_slabs, the widest slice reaching PART_MIN_BLOCKS."""
+    legal = [ks for ks in (16, 8, 4) if K % (64 * ks) == 0 and M * 8 * ks <= 512]
+    nb = -(-N // 64)
+    for ks in legal:
+        if nb * (K // (64 * ks)) >= PART_MIN_BLOCKS:
+            return ks
+    return legal[-1] if legal else 0
+
+
+def gemm_part_silu_ok(M, w_gu, w_down):
+    """Whether the down projection can take silu(gate) * up straight from the gate/up partial slabs."""
+    if not (isinstance(w_gu, torch.Tensor) and isinstance(w_down, torch.Tensor)):
+        return False
+    N, K = w_down.shape
+    ks_gu = gemm_part_gu_ks(w_gu.shape[1])
+    if w_gu.shape[0] != 2 * K or K % 64 or ks_gu == 0 or M > 4:
+        return False
+    S1 = w_gu.shape[1] // (64 * ks_gu)
+    ks = _silu_ks(M, N, K)
+    return ks > 0 and bool(_lib.lib().ragk_gemm_part_silu_ok(M, S1, K, ks))
+
+
+def gemm_part_gu(x, w_gu):
+    """Split-K partials of the packed gate/up projection with at most 4 slabs (gemm_part_silu's input)."""
+    return gemm_part(x, w_gu, ks=gemm_part_gu_ks(x.shape[1]))
+
+
+def gemm_part_silu(pgu, w, out=None):
+    """Down-projection partials P[S, M, N] of silu(gate) * up, where gate / up are the sums of the slabs
+    of pgu [S1, M, 2K] (gemm_part_gu output, packed [64 gate | 64 up] column tiles): the reduction and
+    the activation happen in the down GEMM's LDS staging (gemm_part.hip SG) -- no silu_mul launch and
+    the gate/up GEMM streams its weights split-K."""
+    _bf16_2d(w, "w")
+    _req(pgu.dtype == torch.float32 and pgu.is_cuda and pgu.is_contiguous() and pgu.dim() == 3, "pgu fp32 [S1, M, 2K]")
+    S1, M, K2 = pgu.shape
+    N, K = w.shape
+    _req(K2 == 2 * K, "pgu holds packed gate/up columns of width 2K")
+    ks = _silu_ks(M, N, K)
+    _req(ks > 0 and _lib.lib().ragk_gemm_part_silu_ok(M, S1, K, ks), "gemm_part_silu shape")
+    S = K // (64 * ks)
+    if out is None:
+        out = torch.empty((S, M, N), dtype=torch.float32, device=pgu.device)
+    _req(out.shape == (S, M, N) and out.dtype == torch.float32, "out [S, M, N] fp32")
+    check(_lib.lib().ragk_gemm_part_silu(pgu.data_ptr(), S1, w.data_ptr(), w.stride(0), out.data_ptr(), M, N, K, ks,
+                                         stream_ptr()), "ragk_gemm_part_silu")
     return out
 
 
@@ -756,11 +818,35 @@ def l2_search_set_mfma_min_nq(n):
     check(_lib.lib().ragk_l2_search_set_mfma_min_nq(int(n)), "ragk_l2_search_set_mfma_min_nq")
 
 
+_search_ws = {}
+_search_lock = threading.Lock()
+
+
+def _search_out(nq, k, device):
+    """(D fp32 [nq, k], I int64 [nq, k]) as views of ONE allocation (the merge kernel writes int64 ids)."""
+    buf = torch.empty(nq * k * 3, dtype=torch.int32, device=device)
+    return buf[2 * nq * k:].view(torch.float32).view(nq, k), buf[:2 * nq * k].view(torch.int64).view(nq, k)
+
+
+def _search_partials(n_entries, device):
+    """Per-(device, stream) grow-only partial-list workspace (fp32 distances + int32 ids). Callers hold
+    _search_lock from here until both kernels of the search are enqueued, so two searches on one stream
+    never interleave their scan / merge pair over the same buffer."""
+    key = (str(device), stream_ptr())
+    ws = _search_ws.get(key)
+    if ws is None or ws.numel() < 2 * n_entries:
+        ws = torch.empty(max(2 * n_entries, 1 << 16), dtype=torch.int32, device=device)
+        _search_ws[key] = ws
+    return ws[:n_entries].view(torch.float32), ws[n_entries:2 * n_entries]
+
+
 def l2_search(xt, cap, n, q, k, row_begin=0, ids_map=None):
     """Exact squared-L2 top-k over rows [row_begin, n) of a column-major store xt[d][cap]
     (csrc/kernels/search.hip: l2_scan with wave-resident running top lists + one list merge; batches
     of >= 16 queries with k <= 8 on the fp32-MFMA distance GEMM, faiss' BLAS form).
-    Returns (D fp32 [nq,k], I int64 [nq,k]) with faiss padding semantics (-1, FLT_MAX)."""
+    Returns (D fp32 [nq,k], I int64 [nq,k]) with faiss padding semantics (-1, FLT_MAX).
+    Host cost per call: one output allocation and two ctypes calls (the partial lists live in a
+    cached workspace), so a single-query search is not dominated by launch overhead."""
     _req(xt.is_cuda and xt.dtype == torch.float32 and xt.is_contiguous() and xt.dim() == 2, "xt fp32 [d, cap]")
     _req(q.is_cuda and q.dtype == torch.float32 and q.is_contiguous() and q.dim() == 2, "q fp32 [nq, d]")
     d = xt.shape[0]
@@ -770,16 +856,16 @@ def l2_search(xt, cap, n, q, k, row_begin=0, ids_map=None):
     _req(xt.shape[1] == cap and 0 <= row_begin <= max(row_begin, n) <= cap, "rows within the store")
     _req(ids_map is None or (ids_map.dtype == torch.int32 and ids_map.is_cuda and ids_map.numel() >= n), "ids_map")
     L = _lib.lib()
-    od = torch.empty((nq, k), dtype=torch.float32, device=q.device)
-    oi = torch.empty((nq, k), dtype=torch.int32, device=q.device)
+    od, oi = _search_out(nq, k, q.device)
     if nq == 0:
-        return od, oi.long()
+        return od, oi
     G = L.ragk_l2_search_groups(row_begin, max(n, row_begin), nq, k, d)
-    pd = torch.empty((nq, G, k), dtype=torch.float32, device=q.device)
-    pi = torch.empty((nq, G, k), dtype=torch.int32, device=q.device)
-    check(L.ragk_l2_search(xt.data_ptr(), cap, d, row_begin, max(n, row_begin), q.data_ptr(), nq, k, ptr(ids_map),
-                           pd.data_ptr(), pi.data_ptr(), od.data_ptr(), oi.data_ptr(), stream_ptr()), "ragk_l2_search")
-    return od, oi.long()
+    with _search_lock:
+        pd, pi = _search_partials(nq * G * k, q.device)
+        check(L.ragk_l2_search(xt.data_ptr(), cap, d, row_begin, max(n, row_begin), q.data_ptr(), nq, k,
+                               ptr(ids_map), pd.data_ptr(), pi.data_ptr(), od.data_ptr(), oi.data_ptr(), stream_ptr()),
+              "ragk_l2_search")
+    return od, oi
 
 
 def ivf_search(xt, cap, q, probes, offsets, ids_map, k, max_list=None, ends=None):
@@ -794,16 +880,15 @@ def ivf_search(xt, cap, q, probes, offsets, ids_map, k, max_list=None, ends=None
     d = xt.shape[0]
     nq, nprobe = probes.shape
     _req(1 <= k <= 64 and d <= 2048 and nprobe >= 1, "k <= 64, d <= 2048")
-    od = torch.empty((nq, k), dtype=torch.float32, device=q.device)
-    oi = torch.empty((nq, k), dtype=torch.int32, device=q.device)
+    od, oi = _search_out(nq, k, q.device)
     if nq == 0:
-        return od, oi.long()
-    pd = torch.empty((nq, nprobe, k), dtype=torch.float32, device=q.device)
-    pi = torch.empty((nq, nprobe, k), dtype=torch.int32, device=q.device)
-    check(_lib.lib().ragk_ivf_search(xt.data_ptr(), cap, d, q.data_ptr(), nq, probes.data_ptr(), nprobe,
-                                     offsets.data_ptr(), ptr(ends), ids_map.data_ptr(), k, pd.data_ptr(), pi.data_ptr(),
-                                     od.data_ptr(), oi.data_ptr(), stream_ptr()), "ragk_ivf_search")
-    return od, oi.long()
+        return od, oi
+    with _search_lock:
+        pd, pi = _search_partials(nq * nprobe * k, q.device)
+        check(_lib.lib().ragk_ivf_search(xt.data_ptr(), cap, d, q.data_ptr(), nq, probes.data_ptr(), nprobe,
+                                         offsets.data_ptr(), ptr(ends), ids_map.data_ptr(), k, pd.data_ptr(),
+                                         pi.data_ptr(), od.data_ptr(), oi.data_ptr(), stream_ptr()), "ragk_ivf_search")
+    return od, oi
 
 
 def kmeans_assign(x, c, cnorm=None, scores=None):

@@ -75,6 +75,20 @@ def test_gemm_part_slabs_in_bounds(native, M, N, K):
     assert rel_err(P.sum(0), x.float() @ w.float().t()) < 1e-4
 
 
+@pytest.mark.parametrize("M,I,H", [(1, 1792, 4096), (3, 3584, 4096), (4, 7168, 4096)])
+def test_gemm_part_silu_slabs_in_bounds(native, M, I, H):
+    torch.manual_seed(I)
+    x = torch.randn(M, H, device=DEV).bfloat16()
+    wgu = (torch.randn(2 * I, H, device=DEV) / math.sqrt(H)).bfloat16()
+    wd = (torch.randn(H, I, device=DEV) / math.sqrt(I)).bfloat16()
+    pgu = native.gemm_part_gu(x, wgu)
+    P0 = native.gemm_part_silu(pgu, wd)
+    buf, P = guarded(tuple(P0.shape), torch.float32)
+    native.gemm_part_silu(pgu, wd, out=P)
+    assert intact(buf)
+    assert torch.equal(P, P0)
+
+
 def test_prefill_splitk_slabs_in_bounds(native):
     torch.manual_seed(3)
     M, N, K, ns = 1300, 1032, 1024, 2

@@ -774,7 +774,8 @@ def test_l2_search_guard_canaries(native):
     pad = 4096
     q = torch.randn(nq, d, device=DEV)
     bufs = [torch.full((2 * pad + n,), -7.0, device=DEV) for n in (nq * G * k, nq * k)]
-    ibufs = [torch.full((2 * pad + n,), -7, dtype=torch.int32, device=DEV) for n in (nq * G * k, nq * k)]
+    ibufs = [torch.full((2 * pad + n,), -7, dtype=dt, device=DEV)
+             for n, dt in zip((nq * G * k, nq * k), (torch.int32, torch.int64))]
     views = [b[pad:pad + n] for b, n in zip(bufs, (nq * G * k, nq * k))]
     iviews = [b[pad:pad + n] for b, n in zip(ibufs, (nq * G * k, nq * k))]
     native.check(L.ragk_l2_search(xt.data_ptr(), cap, d, 0, N, q.data_ptr(), nq, k, None, views[0].data_ptr(),
@@ -785,7 +786,7 @@ def test_l2_search_guard_canaries(native):
         assert b[:pad].eq(-7.0).all() and b[-pad:].eq(-7.0).all()
         assert ib[:pad].eq(-7).all() and ib[-pad:].eq(-7).all()
     Dr, Ir = R.l2_knn(xt[:, :N].t().cpu(), q.cpu(), k)
-    assert torch.equal(iviews[1].view(nq, k).long().cpu(), Ir)
+    assert torch.equal(iviews[1].view(nq, k).cpu(), Ir)  # int64 ids straight from the merge kernel
 
 
 @pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
@@ -819,7 +820,8 @@ def test_gemm_stream_bf16(native, M, N, K):
 
 
 @pytest.mark.parametrize("M", [1, 7, 16, 32, 33, 64])
-@pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (384, 512), (1000, 1024)])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (384, 512), (1000, 1024),
+                                 (4096, 1792), (768, 4096), (4096, 512)])  # TP=8 shard down / qkv / o_proj
 def test_gemm_part(native, M, N, K):
     """Decode GEMM v5: fp32 split-K partial slabs sum to x @ w^T."""
     torch.manual_seed(3)
@@ -831,6 +833,27 @@ def test_gemm_part(native, M, N, K):
     P = native.gemm_part(x, w)
     assert P.shape == (S, M, N)
     assert rel_err(P.sum(0), x.float() @ w.float().t()) < 2e-3
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("I,H", [(1792, 4096), (3584, 4096), (7168, 4096), (3584, 8192), (14336, 4096)])
+def test_gemm_part_silu(native, M, I, H):
+    """Down partials fed by the packed gate/up partial slabs: P.sum(0) = bf16(silu(g) * u) @ w_down^T,
+    g / u = the slab sums (TP shard shapes: I = 14336 / TP, 70B H = 8192)."""
+    torch.manual_seed(M + I)
+    x = torch.randn(M, H, device=DEV).bfloat16()
+    wgu = (torch.randn(2 * I, H, device=DEV) / math.sqrt(H)).bfloat16()
+    wd = (torch.randn(H, I, device=DEV) / math.sqrt(I)).bfloat16()
+    assert native.gemm_part_silu_ok(M, wgu, wd)
+    pgu = native.gemm_part_gu(x, wgu)
+    assert pgu.shape[0] <= native.SILU_MAX_SLABS and pgu.shape[1:] == (M, 2 * I)
+    assert rel_err(pgu.sum(0), x.float() @ wgu.float().t()) < 2e-3
+    P = native.gemm_part_silu(pgu, wd)
+    gu = pgu.sum(0).view(M, I // 64, 2, 64)
+    a = (torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(M, I).bfloat16()
+    assert rel_err(P.sum(0), a.float() @ wd.float().t()) < 2e-3
+    ref = R.linear(x.float().cpu(), wgu.float().cpu(), None, None, epi="silu_mul").bfloat16().float() @ wd.float().cpu().t()
+    assert rel_err(P.sum(0), ref) < 1e-2
 
 
 @pytest.mark.parametrize("S,M,H", [(1, 3, 384), (4, 32, 4096), (7, 17, 4096), (9, 32, 4096), (16, 5, 4096)])

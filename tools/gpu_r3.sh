@@ -7,10 +7,24 @@ mkdir -p gpurun_out/prof
 STEP=${STEP:-search}
 ok() { rc=$1; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "step failed rc=$rc"; exit $rc; fi; }
 case ",$STEP," in *,search,*)
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_ivf_gpu.py tests/test_canary_gpu.py -k "l2_search or ivf or kmeans or bounds" -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_search.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_ivf_gpu.py tests/test_canary_gpu.py -k "l2_search or ivf or kmeans or bounds or topk or sampl" -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_search.log 2>&1
 rc=$?; echo "search tests rc=$rc"; tail -15 gpurun_out/pytest_search.log; ok $rc
 timeout -k 10 300 python -u tools/search_bench.py > gpurun_out/search_bench.log 2>&1
 rc=$?; echo "search bench rc=$rc"; cat gpurun_out/search_bench.log; ok $rc
+timeout -k 10 200 python -u tools/sampler_bench.py > gpurun_out/sampler_bench.log 2>&1
+rc=$?; echo "sampler bench rc=$rc"; grep '^{' gpurun_out/sampler_bench.log; ok $rc
+;; esac
+case ",$STEP," in *,part,*)
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_canary_gpu.py -k "gemm_part or silu" -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_part.log 2>&1
+rc=$?; echo "part tests rc=$rc"; tail -8 gpurun_out/pytest_part.log; ok $rc
+DG_TP=8 timeout -k 10 300 python -u tools/bench_decode_gemm.py 1 4 32 > gpurun_out/decode_gemm_tp8.log 2>&1
+rc=$?; echo "tp8 gemm bench rc=$rc"; grep "^M=" gpurun_out/decode_gemm_tp8.log; ok $rc
+;; esac
+case ",$STEP," in *,siluab,*)
+for v in tp 1; do
+RAGK_DECODE_SILU_FUSED=$v RAGK_DECODE_TIMING=1 DA_STEPS=48 timeout -k 10 400 python -u tools/decode_anatomy.py 1 4 > gpurun_out/siluab_$v.log 2>&1
+rc=$?; echo "silu fused=$v rc=$rc"; grep "^B=" gpurun_out/siluab_$v.log; ok $rc
+done
 ;; esac
 case ",$STEP," in *,tp,*)
 timeout -k 10 900 python -u -m pytest tests/test_ipc_allreduce_gpu.py tests/test_tp_gpu.py -v --timeout 400 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_tp.log 2>&1

@@ -1,5 +1,7 @@
 """Flat L2 top-k (csrc/kernels/search.hip) on one MI355X: wall time per search call (CUDA events,
-median of 20, index warm in HBM/MALL as in serving) and the effective read rate of the index.
+median of 20, index warm in HBM/MALL as in serving; includes the host-side call), the device time
+(the call captured in a hipGraph, 20 replays back to back: the two kernels and their launch gap) and
+the effective read rate of the index at the device time.
 Shapes of the SURVEY V2 targets: 10k x 384 (MiniLM, bench corpus) at nq = 1 / 32, 1M x 1024 (bge
 scale) at nq = 1 / 32. Prints one JSON line per shape."""
 import json
@@ -34,11 +36,22 @@ def main():
         xt = torch.randn(d, n, device="cuda")
         q = torch.randn(nq, d, device="cuda")
         us = timed(lambda: N.l2_search(xt, n, n, q, k))
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            N.l2_search(xt, n, n, q, k)  # workspace for this stream
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(20):
+                    N.l2_search(xt, n, n, q, k)
+        torch.cuda.current_stream().wait_stream(s)
+        dev = timed(g.replay, iters=10, warmup=2) / 20
         # correctness spot check vs torch (fp32 direct form) on a sample of queries
         ref = torch.cdist(q[:1].double(), xt.t().double()).pow(2)
         ri = ref.topk(k, largest=False).indices.cpu()
         D, I = N.l2_search(xt, n, n, q, k)
-        print(json.dumps(dict(N=n, d=d, nq=nq, k=k, us=round(us, 1), TBps=round(n * d * 4 / us / 1e6, 2),
+        print(json.dumps(dict(N=n, d=d, nq=nq, k=k, us=round(us, 1), dev_us=round(dev, 1),
+                              TBps=round(n * d * 4 / dev / 1e6, 2),
                               top1_ok=bool(int(I[0, 0]) == int(ri[0, 0])))), flush=True)
         del xt
         torch.cuda.empty_cache()
