@@ -853,7 +853,7 @@ def test_gemm_part_silu(native, M, I, H):
     a = (torch.nn.functional.silu(gu[:, :, 0]) * gu[:, :, 1]).reshape(M, I).bfloat16()
     assert rel_err(P.sum(0), a.float() @ wd.float().t()) < 2e-3
     ref = R.linear(x.float().cpu(), wgu.float().cpu(), None, None, epi="silu_mul").bfloat16().float() @ wd.float().cpu().t()
-    assert rel_err(P.sum(0), ref) < 1e-2
+    assert rel_err(P.sum(0).cpu(), ref) < 1e-2
 
 
 @pytest.mark.parametrize("S,M,H", [(1, 3, 384), (4, 32, 4096), (7, 17, 4096), (9, 32, 4096), (16, 5, 4096)])
