@@ -409,6 +409,751 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_prefill_kernel(Prefill
 }
 
 // ------------------------------------------------------------------------------------
+// Ping-pong prefill attention (Llama config: D 128, 4 query heads per KV head, causal, paged
+// cache < 4 GiB). One 8-wave block per CU: waves 0-3 (group A) and 4-7 (group B) each own 32 query
+// rows of the same 4 heads, so wave w and its SIMD partner w + 4 run the same program one segment
+// apart. A segment is the interval between two block barriers; in every segment one group is in
+// its MFMA phase (PV of tile u-1 + QK^T of tile u: 64 MFMAs, LDS fragment reads) while the other
+// is in its VALU phase (online softmax of its tile, the next K or V tile's LDS-DMA). The stamp
+// build of attn_prefill_kernel put a wave at ~4.3k cycles per tile for 1024 cycles of its own
+// MFMAs: the two co-resident waves of a SIMD (independent 4-wave blocks) reached their softmax
+// at the same time and left the matrix pipe idle; here the barrier schedule makes the softmax of
+// one wave and the MFMAs of its partner coincide (MI355X_MICROARCH.md "Two waves per SIMD").
+//
+// K/V ring of 3 slots (tile t in slot t % 3), segment s (A: MFMA phase when s is even, B when odd):
+//   A (MFMA): seg 2u   PV(u-1) + QK(u)       A (VALU): seg 2u+1  softmax(u), DMA K(u+2)
+//   B (MFMA): seg 2u+1 PV(u-1) + QK(u)       B (VALU): seg 2u+2  softmax(u), DMA V(u+2)
+// K(t) is read in segments 2t / 2t+1 and rewritten (as K(t+3)) in 2t+3; V(t) read in 2t+2 / 2t+3,
+// rewritten in 2t+4. The VALU phase ends with vmcnt(4) (only the DMAs it just issued may stay in
+// flight), so every tile lands >= 2 segments after its DMA was issued, before the barrier that
+// precedes its first reader. Prologue: K(0), V(0), K(1). 2n + 2 segments for n KV tiles.
+// Same arithmetic as attn_prefill_kernel (bit-identical outputs).
+constexpr int PP_NS = 3;
+
+template <typename F, int... Is>
+__device__ __forceinline__ void pp_static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void pp_static_for(F&& f) {
+  pp_static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// One MFMA phase: 16 PV steps (d-tile dt = i / 2, key step ks = i % 2; two tr-read pairs per
+// fragment) or 16 QK^T steps (key sub-tile t = j / 4, d-step ks = j % 4; one b128 read). The LDS
+// fragment of step i + PF is requested before the MFMAs of step i and a scheduling fence follows
+// every step, so at most PF + 1 fragments are live. Fragment addresses are the load_vt / load_k
+// images (D = 128: kswz(R) = R & 15, vswz(r) = 2 (r & 7)) rebuilt per phase from an opaque copy of
+// the lane id: loop-invariant per-lane offsets hoisted out of the segment loop spilled (12 VGPRs).
+template <bool PV, int PF>
+__device__ __forceinline__ void pp_mfma_phase(const char* sV, const char* sK, int lane, const bf16x8 (&pb)[2][2],
+                                              const bf16x8 (&qf)[2][Cfg<128>::KS], f32x4 (&o)[Cfg<128>::DT][2],
+                                              f32x4 (&s)[4][2]) {
+  constexpr int N = 16;
+  int ln = lane;
+  asm volatile("" : "+v"(ln));
+  // V^T: rows r0 = 32 ks + 4 h + (i >> 2) and r0 + 16, chunk (2 dt + b) ^ 2 (r0 & 7), half i & 1
+  const int vi = ln & 15, vr = 4 * (ln >> 4) + (vi >> 2);
+  const int vx = vr & 7;
+  const char* vb = sV + vr * 256 + 16 * ((vi >> 1) & 1) + 8 * (vi & 1);
+  // K: row 16 t + fr, chunk (4 s + fh) ^ fr
+  const int fr = ln & 15;
+  const char* kb = sK + fr * 256 + 16 * ((ln >> 4) ^ (fr & 3));
+  const int kx = fr >> 2;
+  auto frag = [&](auto ic) -> bf16x8 {
+    constexpr int i = decltype(ic)::value;
+    if constexpr (PV) {
+      constexpr int dt = i >> 1, ks = i & 1;
+      const char* p = vb + ks * 32 * 256 + 32 * (dt ^ vx);
+      const bf16x4 x0 = tr_read(p), x1 = tr_read(p + 16 * 256);
+      return (bf16x8){x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    } else {
+      constexpr int t = i >> 2, ks = i & 3;
+      return *reinterpret_cast<const bf16x8*>(kb + t * 16 * 256 + 64 * (ks ^ kx));
+    }
+  };
+  bf16x8 ring[PF + 1];
+  pp_static_for<PF>([&](auto ic) { ring[decltype(ic)::value] = frag(ic); });
+  pp_static_for<N>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    if constexpr (i + PF < N) ring[(i + PF) % (PF + 1)] = frag(std::integral_constant<int, i + PF>{});
+    const bf16x8 f = ring[i % (PF + 1)];
+    if constexpr (PV) {
+      constexpr int dt = i >> 1, ks = i & 1;
+      o[dt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f, pb[ks][0], o[dt][0], 0, 0, 0);
+      o[dt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f, pb[ks][1], o[dt][1], 0, 0, 0);
+    } else {
+      constexpr int t = i >> 2, ks = i & 3;
+      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      s[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f, qf[0][ks], ks == 0 ? z : s[t][0], 0, 0, 0);
+      s[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f, qf[1][ks], ks == 0 ? z : s[t][1], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
+template <int PRIO_B, int PF = 2, bool STAMP = false>
+__global__ __launch_bounds__(512, 2) void attn_prefill_pp_kernel(PrefillArgs a) {
+  constexpr int D = 128;
+  using C = Cfg<D>;
+  constexpr bool CAUSAL = true;
+  __shared__ __attribute__((aligned(16))) char smem[2 * PP_NS * C::TILEB];  // [K slots][V slots]
+  __shared__ int s_bt[MAX_BT];
+
+  const int lane = threadIdx.x & 63;
+  const int wid_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int grp = wid_u >> 2, hs = wid_u & 3;
+  const int seq = a.tiles[2 * blockIdx.x], q_start = a.tiles[2 * blockIdx.x + 1];
+  const int G = a.Hq / a.Hkv;
+  const int groups_per_kv = G / 4;
+  const int kvh = blockIdx.y / groups_per_kv;
+  const int hq = kvh * G + (blockIdx.y % groups_per_kv) * 4 + hs;
+  const int pbase = q_start + grp * 32;
+
+  const int q_off = a.cu_q[seq];
+  const int q_len = a.cu_q[seq + 1] - q_off;
+  const int kv_len = a.kv_lens[seq];
+  const int ctx0 = kv_len - q_len;
+  const int blk_qmax = min(q_start + 64, q_len) - 1;
+  const int n_keys = min(kv_len, ctx0 + blk_qmax + 1);
+  const int n_kt = (n_keys + KT - 1) / KT;
+  const int wave_pmax = ctx0 + min(pbase + 31, q_len - 1);
+  const int fr = lane & 15, fh = lane >> 4;
+
+  bf16x8 qf[2][C::KS];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    int qi = pbase + 16 * qt + fr;
+    qi = qi < q_len ? qi : q_len - 1;
+    const bf16_t* qp = a.q + (size_t)(q_off + qi) * a.q_stride + hq * D + 8 * fh;
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) qf[qt][s] = *reinterpret_cast<const bf16x8*>(qp + 32 * s);
+  }
+  f32x4 o[C::DT][2];
+#pragma unroll
+  for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) o[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m_i[2] = {-INFINITY, -INFINITY}, l_i[2] = {0.f, 0.f};
+  f32x4 s[4][2];
+  bf16x8 pb[2][2];
+
+  const int* bt = a.block_tables + (size_t)seq * a.bt_stride;
+  for (int i = threadIdx.x; i < n_kt; i += 512) s_bt[i] = bt[i];
+
+  // pieces hs, hs + 4, hs + 8, hs + 12 of a 16-piece K / V tile (the wave's share in its group)
+  int koff[4], voff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = hs + 4 * i;
+    const int row = p * C::RPP + lane / C::NC, ph = lane % C::NC;
+    koff[i] = row * C::ROWB + 16 * (ph ^ kswz<D>(row));
+    voff[i] = row * C::ROWB + 16 * (ph ^ vswz<D>(row));
+  }
+  const i32x4 srd_k = make_srd(a.k, a.kv_bytes);
+  const i32x4 srd_v = make_srd(a.v, a.kv_bytes);
+  auto stage = [&](int kt, bool is_v) {
+    const int soff = __builtin_amdgcn_readfirstlane(
+        (int)((unsigned)(s_bt[kt] * a.Hkv + kvh) * (unsigned)(KT * D * 2)));
+    char* base = smem + ((is_v ? PP_NS : 0) + kt % PP_NS) * C::TILEB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) blds16(is_v ? srd_v : srd_k, is_v ? voff[i] : koff[i], soff, base + (hs + 4 * i) * 1024);
+  };
+  __syncthreads();  // s_bt
+  if (grp == 0) {
+    stage(0, false);
+    stage(0, true);
+  } else if (n_kt > 1) {
+    stage(1, false);
+  }
+  wait_vmcnt0();
+  __syncthreads();
+  if constexpr (PRIO_B) {
+    if (grp == 1) __builtin_amdgcn_s_setprio(1);
+  }
+
+  const float c = a.scale_log2;
+  // MFMA phase of tile u: PV(u-1) (V slot (u-1) % 3) and QK^T(u) (K slot u % 3)
+  auto mfma_phase = [&](int u) {
+    if (u >= 1 && u - 1 < n_kt && (u - 1) * KT <= wave_pmax)
+      pp_mfma_phase<true, PF>(smem + (PP_NS + (u + PP_NS - 1) % PP_NS) * C::TILEB, nullptr, lane, pb, qf, o, s);
+    if (u < n_kt && u * KT <= wave_pmax)
+      pp_mfma_phase<false, PF>(nullptr, smem + (u % PP_NS) * C::TILEB, lane, pb, qf, o, s);
+  };
+  // VALU phase of tile u in segment seg: softmax(u) -> pb (O rescaled), then this segment's DMA
+  // (odd seg: group A stages K((seg + 3) / 2); even: group B stages V(seg / 2 + 1))
+  auto valu_phase = [&](int u, int seg) {
+    const int k0 = u * KT;
+    if (u >= 0 && u < n_kt && k0 <= wave_pmax) {
+      const bool need_mask = (k0 + KT - 1 > ctx0 + pbase) || (k0 + KT > kv_len);
+      float alpha[2];
+      auto softmax = [&](auto mask_tag, const int qt) {
+        constexpr bool MASK = decltype(mask_tag)::value;
+        const int qpos = ctx0 + pbase + 16 * qt + fr;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = s[t][qt][r];
+            if constexpr (MASK) {
+              const int kj = k0 + 16 * t + 4 * fh + r;
+              const bool ok = kj < kv_len && kj <= qpos;
+              x = ok ? x : -INFINITY;
+              s[t][qt][r] = x;
+            }
+            mx = fmaxf(mx, x);
+          }
+        mx = max_xor16(mx);
+        mx = max_xor32(mx);
+        const float mxs = mx * c;
+        alpha[qt] = 1.f;
+        if (mxs > m_i[qt] + RESCALE_LOG2) {
+          alpha[qt] = m_i[qt] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_i[qt] - mxs);
+          m_i[qt] = mxs;
+        }
+        const float mref = m_i[qt] == -INFINITY ? 0.f : m_i[qt];
+        float ls = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[t][qt][r], c, -mref));
+            s[t][qt][r] = pv;
+            ls += pv;
+          }
+        l_i[qt] = l_i[qt] * alpha[qt] + ls;
+      };
+      if (need_mask) {
+        softmax(std::true_type{}, 0);
+        softmax(std::true_type{}, 1);
+      } else {
+        softmax(std::false_type{}, 0);
+        softmax(std::false_type{}, 1);
+      }
+      if (__builtin_amdgcn_ballot_w64(alpha[0] != 1.f || alpha[1] != 1.f)) {
+#pragma unroll
+        for (int dt = 0; dt < C::DT; ++dt)
+#pragma unroll
+          for (int qt = 0; qt < 2; ++qt) o[dt][qt] *= alpha[qt];
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) pb[ks][qt] = pack_p(s[2 * ks][qt], s[2 * ks + 1][qt]);
+    }
+    const int item = (seg & 1) ? (seg + 3) >> 1 : (seg >> 1) + 1;
+    if (item < n_kt) {
+      stage(item, (seg & 1) == 0);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      wait_vmcnt0();
+    }
+  };
+  // stamp build: per wave [MFMA phase, barrier after it, VALU phase, barrier after it, segments]
+  unsigned long long stp[5] = {0, 0, 0, 0, 0};
+  unsigned long long t0 = 0;
+  auto stamp = [&](int i) {
+    if constexpr (STAMP) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      stp[i] += t - t0;
+      t0 = t;
+    }
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
+  // 2 n_kt + 2 segments, two per iteration; group A: [MFMA(u) | VALU(u)], group B one segment
+  // behind: [VALU(u-1) | MFMA(u)]
+  if (grp == 0) {
+    for (int u = 0; u <= n_kt; ++u) {
+      mfma_phase(u);
+      stamp(0);
+      barrier();
+      stamp(1);
+      valu_phase(u, 2 * u + 1);
+      stamp(2);
+      barrier();
+      stamp(3);
+    }
+  } else {
+    for (int u = 0; u <= n_kt; ++u) {
+      valu_phase(u - 1, 2 * u);
+      stamp(2);
+      barrier();
+      stamp(3);
+      mfma_phase(u);
+      stamp(0);
+      barrier();
+      stamp(1);
+    }
+  }
+  if constexpr (STAMP) {
+    stp[4] = n_kt + 1;
+    if (lane == 0 && g_attn_dbg) {
+      unsigned long long* d = g_attn_dbg + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 8 + wid_u) * 6;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) d[i] = stp[i];
+    }
+  }
+  if constexpr (PRIO_B) {
+    if (grp == 1) __builtin_amdgcn_s_setprio(0);
+  }
+
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    float l = l_i[qt];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int qi = pbase + 16 * qt + fr;
+    if (qi < q_len) {
+      bf16_t* op = a.out + (size_t)(q_off + qi) * a.out_stride + hq * D + 4 * fh;
+#pragma unroll
+      for (int dt = 0; dt < C::DT; ++dt) {
+        const f32x4 v = o[dt][qt] * inv;
+        *reinterpret_cast<uint2*>(op + 16 * dt) = make_uint2(pk2bf(v[0], v[1]), pk2bf(v[2], v[3]));
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Software-pipelined prefill attention, one wave per SIMD (Llama config: D 128, 4 query heads per
+// KV head, causal, paged cache < 4 GiB). attn_prefill_kernel runs two waves per SIMD, each in
+// lockstep phases QK^T -> softmax -> PV: the stamps put a wave at ~4.3k cycles per 64-key tile for
+// 1024 cycles of its own 16x16x32 MFMAs (~48 % matrix-pipe use), and a barrier-alternated 8-wave
+// variant (attn_prefill_pp_kernel) was slower still -- the two waves of a SIMD share one vector
+// issue port, and a 16x16x32 MFMA holds it 8 of its 16 cycles. Here:
+//   * 32x32x16 MFMAs (the issue port is held 8 of 32 cycles per MFMA, MI355X_MICROARCH.md cycle
+//     constants), 32 per tile per wave, and ONE wave per SIMD (4-wave block, one block per CU);
+//   * iteration t issues PV(t-1) then QK^T(t+1) on the matrix pipe while the same wave's VALU runs the
+//     online softmax of tile t between them: 32 slots, one MFMA each, the LDS fragment of slot i + 2
+//     and a softmax chunk (max in slots 0..3, row statistics in 4, one element's fma / exp / add per
+//     slot from 5 on: at most one transcendental per MFMA gap). Every MFMA is an ordered volatile asm
+//     and each chunk's inputs / results are pinned, so neither the IR passes nor the scheduler can
+//     regroup the stream; S is double-buffered (tile loop unrolled by two), P is single-buffered
+//     (P(t-1)[ks] is dead before P(t)[ks] is packed);
+//   * K / V ring of 4 slots, K staged 3 and V 2 tiles ahead, so iteration t's last two slots can read
+//     the first PV fragments of iteration t + 1; LDS-DMA as inline asm (the intrinsic made the
+//     waitcnt pass drain vmcnt(0) before every later ds_read); one vmcnt + barrier per tile.
+// Diagonal / ragged tiles (masked softmax), the first tile (no PV) and the last (no QK) run the same
+// MFMA stream with its halves guarded and the whole softmax after it.
+// Layouts (v_mfma_f32_32x32x16_bf16, lane l, h = l >> 5): A[i = l & 31][k = 8h + j], B[k = 8h + j][n = l & 31],
+// C[8b + 4h + r][l & 31] in acc[4b + r]. S^T = K Q^T: lane holds query pbase + (l & 31), keys
+// 32 kb + 8b + 4h + r. P^T fragment of key step ks (16 keys) = acc S[ks / 2][8 (ks % 2) + j] (keys
+// 16 ks + 8 (j / 4) + 4h + j % 4), so V^T is read with the same key order: ds_read_b64_tr_b16 of rows
+// 16 ks + 4h + (i >> 2) and + 8 (i = l & 15) gives lane l the d column 32 db + 16 ((l >> 4) & 1) + i.
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+constexpr int V3_NS = 4;
+constexpr int V3_PF = 4, V3_RING = 8;  // ring size divides the 32 slots (continuity across iterations)
+
+// MFMA through the builtin (the compiler's hazard recognizer then covers every MFMA-result read: as
+// inline asm the compiler treated the results as ready and could copy an accumulator before the MFMA
+// retired). The slot order is kept by a scheduling barrier after every slot. Callers never chain two
+// on the same accumulator back to back (PV db-minor, QK^T alternating key blocks).
+__device__ __forceinline__ void mfma32_v(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+}
+__device__ __forceinline__ void mfma32_v0(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  const f32x16 z = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, z, 0, 0, 0);
+}
+// Empty volatile asm on a value: the computation of x cannot move across the pin (inputs pinned at
+// the start of a slot's VALU chunk, results at its end: the chunk stays between its two MFMAs).
+template <typename T>
+__device__ __forceinline__ void pin(T& x) {
+  asm volatile("" : "+v"(x));
+}
+__device__ __forceinline__ void pin_s(int& x) { asm volatile("" : "+s"(x)); }
+// The asm MFMAs are opaque to the compiler's hazard recognizer: a VALU read of an MFMA result needs
+// the XDL-write -> VALU-read wait states (18 for a 16-pass op), and a VALU write read by an MFMA a few.
+__device__ __forceinline__ void mfma_result_wait() {}
+// LDS-DMA piece as inline asm: the compiler's waitcnt pass cannot tell which LDS bytes a
+// buffer_load ... lds intrinsic writes, so it drained vmcnt(0) before the next ds_read of ANY slot
+// (an HBM round trip per fragment read). The kernel orders its slots itself (vmcnt + barrier per
+// iteration) and issues every LDS-DMA of the kernel through this, so M0 is never live for the compiler.
+__device__ __forceinline__ void blds16_asm(i32x4 srd, int voff, int soff, unsigned lds_addr) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(lds_addr), "v"(voff), "s"(srd),
+               "s"(soff));
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(unsigned long long)(const __attribute__((address_space(3))) char*)p;
+}
+
+// NW = 8: two groups of 4 waves (query rows q_start + [0, 32) and + [32, 64)) share every K / V tile,
+// so each SIMD runs two of these streams and one wave's dependency stalls are the other's issue slots.
+// DIAG (stamp builds only, wrong results): 1 = no softmax chunks in the fast slots, 2 = no fragment reads
+template <int NW = 4, bool STAMP = false, int DIAG = 0>
+__global__ __launch_bounds__(NW * 64, NW / 4) void attn_prefill_v3_kernel(PrefillArgs a) {
+  constexpr int D = 128;
+  using C = Cfg<D>;
+  __shared__ __attribute__((aligned(16))) char smem[2 * V3_NS * C::TILEB];  // [K slots][V slots] 128 KB
+  __shared__ int s_bt[MAX_BT];
+
+  constexpr int PPW = 16 / NW;  // DMA pieces per wave per K or V tile
+  const int lane = threadIdx.x & 63;
+  const int wid_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int seq = a.tiles[2 * blockIdx.x], q_start = a.tiles[2 * blockIdx.x + 1];
+  const int G = a.Hq / a.Hkv;
+  const int groups_per_kv = G / 4;
+  const int kvh = blockIdx.y / groups_per_kv;
+  const int hq = kvh * G + (blockIdx.y % groups_per_kv) * 4 + (wid_u & 3);
+  const int pbase = q_start + 32 * (wid_u >> 2);
+
+  const int q_off = a.cu_q[seq];
+  const int q_len = a.cu_q[seq + 1] - q_off;
+  const int kv_len = a.kv_lens[seq];
+  const int ctx0 = kv_len - q_len;
+  // block-uniform tile counts (every wave runs the same iterations and barriers)
+  const int blk_qmax = min(q_start + 8 * NW, q_len) - 1;
+  const int n_keys = min(kv_len, ctx0 + blk_qmax + 1);
+  const int n_kt = (n_keys + KT - 1) / KT;
+  const int h = lane >> 5, l32 = lane & 31;
+  // tiles [0, n_fast) need no mask for any wave: every key <= the block's first query position and < kv_len
+  const int n_fast = min((ctx0 + q_start + 1) / KT, kv_len / KT);
+
+  // Q^T fragments (B operand): query pbase + l32, d = 16 s + 8 h + [0, 8)
+  bf16x8 qf[8];
+  {
+    int qi = pbase + l32;
+    qi = qi < q_len ? qi : q_len - 1;
+    const bf16_t* qp = a.q + (size_t)(q_off + qi) * a.q_stride + hq * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qp + 16 * s);
+  }
+  const int* bt = a.block_tables + (size_t)seq * a.bt_stride;
+  for (int i = threadIdx.x; i < n_kt; i += NW * 64) s_bt[i] = bt[i];
+
+  // DMA: pieces PPW wid + i (i < PPW) of a 16-piece tile (rows 4 p .. 4 p + 3, one 16-B chunk per lane)
+  int koff[PPW], voff[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int p = PPW * wid_u + i;
+    const int row = p * C::RPP + lane / C::NC, ph = lane % C::NC;
+    koff[i] = row * C::ROWB + 16 * (ph ^ kswz<D>(row));
+    voff[i] = row * C::ROWB + 16 * (ph ^ vswz<D>(row));
+  }
+  const i32x4 srd_k = make_srd(a.k, a.kv_bytes);
+  const i32x4 srd_v = make_srd(a.v, a.kv_bytes);
+  const unsigned lds0 = lds_addr(smem);
+  auto tile_soff = [&](int kt) {
+    return __builtin_amdgcn_readfirstlane((int)((unsigned)(s_bt[kt] * a.Hkv + kvh) * (unsigned)(KT * D * 2)));
+  };
+  auto kslot_off = [&](int kt) { return (kt & (V3_NS - 1)) * C::TILEB; };
+  auto vslot_off = [&](int kt) { return (V3_NS + (kt & (V3_NS - 1))) * C::TILEB; };
+  auto stage_piece = [&](int kt, int soff, bool is_v, int i) {
+    blds16_asm(is_v ? srd_v : srd_k, is_v ? voff[i] : koff[i], soff,
+               lds0 + (is_v ? vslot_off(kt) : kslot_off(kt)) + (PPW * wid_u + i) * 1024);
+  };
+  auto stage = [&](int kt, bool is_v) {
+    const int soff = tile_soff(kt);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) stage_piece(kt, soff, is_v, i);
+  };
+
+  // per-lane fragment offsets (bytes within a tile)
+  // K (A of QK^T): row 32 kb + l32, chunk (2 s + h) ^ (l & 15) = 16 (h ^ (l & 1)) + 32 (s ^ ((l & 15) >> 1))
+  const int kx = (lane & 15) >> 1;
+  const int kbase = l32 * 256 + 16 * (h ^ (lane & 1));
+  // V^T (A of PV): rows 16 ks + 4h + (i >> 2) [+ 8], chunk (2 (2 db + c16) + ((i >> 1) & 1)) ^ 2 (row & 7)
+  const int vi = lane & 15, c16 = (lane >> 4) & 1;
+  const int vrow = 4 * h + (vi >> 2);
+  const int vbase = vrow * 256 + 16 * ((vi >> 1) & 1) + 8 * (vi & 1);
+  const int vx = vrow & 7;
+  auto kfrag = [&](int tile_off, int kb, int s) -> bf16x8 {
+    return *reinterpret_cast<const bf16x8*>(smem + tile_off + kbase + kb * 32 * 256 + 32 * (s ^ kx));
+  };
+  auto vfrag = [&](int tile_off, int db, int ks) -> bf16x8 {
+    const char* p = smem + tile_off + vbase + ks * 16 * 256 + 32 * ((2 * db + c16) ^ vx);
+    const bf16x4 x0 = tr_read(p), x1 = tr_read(p + 8 * 256);
+    return (bf16x8){x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  };
+
+  f32x16 o[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[db][e] = 0.f;
+  float m_i = -INFINITY, l_i = 0.f;
+  f32x16 S0[2], S1[2];
+  bf16x8 P[4];
+  // fragment of MFMA slot i in ring[i % V3_RING], read V3_PF slots ahead (LDS latency ~100+ cycles: at
+  // 2 slots ahead every MFMA waited on its own ds_read)
+  bf16x8 ring[V3_RING];
+  const float c = a.scale_log2;
+
+  __syncthreads();  // s_bt
+#pragma unroll
+  for (int kt = 0; kt < 3; ++kt)
+    if (kt < n_kt) stage(kt, false);
+  stage(0, true);
+  if (n_kt > 1) stage(1, true);
+  wait_vmcnt0();
+  __syncthreads();
+
+  auto pack_p32 = [&](const f32x16& A, int e0) -> bf16x8 {
+    return (bf16x8){f2bf_s(A[e0]), f2bf_s(A[e0 + 1]), f2bf_s(A[e0 + 2]), f2bf_s(A[e0 + 3]),
+                    f2bf_s(A[e0 + 4]), f2bf_s(A[e0 + 5]), f2bf_s(A[e0 + 6]), f2bf_s(A[e0 + 7])};
+  };
+  // simple (non-interleaved) pieces for the warm-up tile and the epilogue
+  auto qk_simple = [&](int kt, f32x16 (&S)[2]) {
+#pragma unroll
+    for (int sd = 0; sd < 8; ++sd)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        const bf16x8 f = kfrag(kslot_off(kt), kb, sd);
+        if (sd == 0) mfma32_v0(S[kb], f, qf[sd]);
+        else mfma32_v(S[kb], f, qf[sd]);
+      }
+  };
+  auto pv_simple = [&](int kt) {
+    const int vo = vslot_off(kt);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int db = 0; db < 4; ++db) mfma32_v(o[db], vfrag(vo, db, ks), P[ks]);
+  };
+  // whole-tile online softmax: this lane's query, 32 of the tile's 64 keys -> P; returns alpha
+  auto softmax = [&](auto mask_tag, int k0, f32x16 (&S)[2]) -> float {
+    constexpr bool MASK = decltype(mask_tag)::value;
+    if constexpr (MASK) {
+      const int qpos = ctx0 + pbase + l32;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int kj = k0 + 32 * kb + 8 * (e >> 2) + 4 * h + (e & 3);
+          S[kb][e] = (kj < kv_len && kj <= qpos) ? S[kb][e] : -INFINITY;
+        }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) mx = fmaxf(mx, S[kb][e]);
+    mx = max_xor32(mx);
+    const float mxs = mx * c;
+    const bool up = mxs > m_i + RESCALE_LOG2;
+    const float alpha = up ? (m_i == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_i - mxs)) : 1.f;
+    m_i = up ? mxs : m_i;
+    const float mref = m_i == -INFINITY ? 0.f : m_i;
+    float ls = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float pe = __builtin_amdgcn_exp2f(__builtin_fmaf(S[kb][e], c, -mref));
+        S[kb][e] = pe;
+        ls += pe;
+      }
+    l_i = l_i * alpha + ls;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) P[ks] = pack_p32(S[ks >> 1], 8 * (ks & 1));
+    return alpha;
+  };
+  auto rescale = [&](float alpha) {
+    if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db] *= alpha;
+    }
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  unsigned long long stp[4] = {0, 0, 0, 0};
+  // Fast iteration t (1 <= t < t_end: tile t unmasked, PV(t-1) and QK^T(t+1) exist). MFMA slots
+  // 0..15: PV(t-1) (V slot t-1; ks = i / 4, db = i % 4), 16..31: QK^T(t+1) (K slot t+1; kb = i % 2,
+  // d-step (i-16) / 2). Slot i reads the fragment of slot i + V3_PF; the last V3_PF slots read the
+  // first PV(t) fragments of the next iteration. Softmax(t) of S_cur -> P in chunks. DMA: K(t+3) (slots 6..18),
+  // V(t+2) (22..28). Then O *= alpha(t) (rare), vmcnt (this iteration's DMAs stay in flight), barrier.
+  auto fast = [&](int t, f32x16 (&S_cur)[2], f32x16 (&S_next)[2]) {
+    unsigned long long t0 = 0;
+    if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
+    const int vo = vslot_off(t - 1), ko = kslot_off(t + 1), vno = vslot_off(t);
+    const bool st_k = t + 3 < n_kt, st_v = t + 2 < n_kt;
+    const int soff_k = tile_soff(st_k ? t + 3 : 0);
+    const int soff_v = tile_soff(st_v ? t + 2 : 0);
+    float alpha = 1.f, mx = -INFINITY, mref = 0.f, ls = 0.f, pend = 0.f;
+    pp_static_for<32>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      // MFMA slot i
+      if constexpr (i < 16) {
+        mfma32_v(o[i % 4], ring[i % V3_RING], P[i / 4]);
+      } else {
+        constexpr int kb = i % 2, sd = (i - 16) / 2;
+        if constexpr (sd == 0) mfma32_v0(S_next[kb], ring[i % V3_RING], qf[sd]);
+        else mfma32_v(S_next[kb], ring[i % V3_RING], qf[sd]);
+      }
+      // fragment for slot i + V3_PF (the per-lane bases x tile offsets are CSE'd: 12 address adds per
+      // iteration; the scheduling barrier at the end of the slot keeps each read in its slot)
+      constexpr int j = i + V3_PF;
+      if constexpr (DIAG != 2) {
+        const int ao = j < 16 ? vo : (j < 32 ? ko : vno);
+        if constexpr (j < 16) ring[j % V3_RING] = vfrag(ao, j % 4, j / 4);
+        else if constexpr (j < 32) ring[j % V3_RING] = kfrag(ao, j % 2, (j - 16) / 2);
+        else ring[j % V3_RING] = vfrag(ao, (j - 32) % 4, (j - 32) / 4);
+      }
+      // softmax chunk: max in slots 0..3, row statistics in 4, one element per slot from 5 on
+      if constexpr (DIAG == 1) {
+      } else if constexpr (i < 4) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = S_cur[i / 2][8 * (i % 2) + e];
+          pin(v[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mx = fmaxf(mx, v[e]);
+        pin(mx);
+      } else if constexpr (i == 4) {
+        mx = max_xor32(mx);
+        const float mxs = mx * c;
+        const bool up = mxs > m_i + RESCALE_LOG2;
+        alpha = up ? (m_i == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_i - mxs)) : 1.f;
+        m_i = up ? mxs : m_i;
+        mref = m_i == -INFINITY ? 0.f : m_i;
+        pin(alpha);
+        pin(m_i);
+        pin(mref);
+      } else {
+        // elements x with 5 + (27 x) / 32 == i; each exp result is added to the row sum one element
+        // later (no exp -> add dependency inside a slot: that was a wait state per element)
+        pp_static_for<32>([&](auto xc) {
+          constexpr int x = decltype(xc)::value;
+          if constexpr (5 + (27 * x) / 32 == i) {
+            float sv = S_cur[x >> 4][x & 15];
+            pin(sv);
+            ls += pend;
+            const float pe = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -mref));
+            S_cur[x >> 4][x & 15] = pe;
+            pend = pe;
+            if constexpr (x % 8 == 7) {
+              P[x / 8] = pack_p32(S_cur[x / 16], 8 * ((x / 8) & 1));
+              pin(P[x / 8]);
+            }
+            pin(ls);
+            pin(pend);
+          }
+        });
+      }
+      // DMA pieces: K(t+3) in slots 6, 10, 14, 18; V(t+2) in slots 22, 24, 26, 28 (the first PPW of each)
+      if constexpr (i >= 6 && i <= 18 && (i - 6) % 4 == 0 && (i - 6) / 4 < PPW) {
+        if (st_k) stage_piece(t + 3, soff_k, false, (i - 6) / 4);
+      }
+      if constexpr (i >= 22 && i <= 28 && (i - 22) % 2 == 0 && (i - 22) / 2 < PPW) {
+        if (st_v) stage_piece(t + 2, soff_v, true, (i - 22) / 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    l_i = l_i * alpha + (ls + pend);
+    if constexpr (STAMP) {
+      const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+      stp[0] += t1 - t0;
+      t0 = t1;
+    }
+    rescale(alpha);
+    // this iteration's DMAs (PPW per issued tile) stay in flight, the previous iteration's have landed
+    if constexpr (PPW == 4) {
+      if (st_k && st_v) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (st_k || st_v) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else wait_vmcnt0();
+    } else {
+      if (st_k && st_v) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (st_k || st_v) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else wait_vmcnt0();
+    }
+    barrier();
+    if constexpr (STAMP) stp[1] += __builtin_amdgcn_s_memtime() - t0;
+  };
+
+  unsigned long long te = 0;
+  if constexpr (STAMP) te = __builtin_amdgcn_s_memtime();
+  qk_simple(0, S0);  // S(0)
+  mfma_result_wait();
+  // fast iterations: [1, t_end); warm-up tile 0 when there is at least one
+  const int t_end = min(n_fast, n_kt - 1);
+  int t = 0;
+  if (t_end >= 1) {
+    // tile 0 (unmasked, QK^T(1) exists): softmax(0), S(1), DMA K(3) / V(2), the first PV(0) fragments
+    softmax(std::false_type{}, 0, S0);
+    qk_simple(1, S1);
+    mfma_result_wait();
+    if (3 < n_kt) stage(3, false);
+    if (2 < n_kt) stage(2, true);
+#pragma unroll
+    for (int j = 0; j < V3_PF; ++j) ring[j] = vfrag(vslot_off(0), j % 4, j / 4);
+    barrier();  // (O is zero: no rescale; the prologue DMAs were drained)
+    t = 1;
+    for (; t + 1 < t_end; t += 2) {
+      fast(t, S1, S0);
+      fast(t + 1, S0, S1);
+    }
+    if (t < t_end) {
+      fast(t, S1, S0);
+      ++t;
+    }
+    if (t & 1) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) S0[kb] = S1[kb];
+    }
+  }
+  if constexpr (STAMP) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    stp[2] += t1 - te - stp[0] - stp[1];
+    te = t1;
+  }
+  // epilogue: tiles [t, n_kt) (masked diagonal / ragged ones and the last; at most 3), S(t) in S0, P(t-1)
+  // pending. Every tile they touch is staged after V(t + 2) here (the ring holds it), then drained.
+  if (t + 2 < n_kt) stage(t + 2, true);
+  wait_vmcnt0();
+  barrier();
+  if (t >= 1) pv_simple(t - 1);
+  for (; t < n_kt; ++t) {
+    const int k0 = t * KT;
+    const bool need_mask = (k0 + KT - 1 > ctx0 + pbase) || (k0 + KT > kv_len);
+    mfma_result_wait();  // S(t) and O from the MFMAs just issued
+    const float alpha = need_mask ? softmax(std::true_type{}, k0, S0) : softmax(std::false_type{}, k0, S0);
+    rescale(alpha);
+    pv_simple(t);
+    if (t + 1 < n_kt) qk_simple(t + 1, S0);
+  }
+  if constexpr (STAMP) stp[3] += __builtin_amdgcn_s_memtime() - te;
+  if constexpr (STAMP) {
+    if (lane == 0 && g_attn_dbg) {
+      unsigned long long* d = g_attn_dbg + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * NW + wid_u) * 6;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) d[i] = stp[i];
+      d[4] = n_kt;
+      d[5] = max(0, min(n_fast, n_kt - 1) - 1);  // fast iterations
+    }
+  }
+
+  // finalize: O^T[32 db + 8 b + 4 h + r][query] = o[db][4 b + r] / l; {r0, r1} = {l_i, partner's l_i}
+  const auto lr = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_i), __float_as_uint(l_i), false, false);
+  const float l = __uint_as_float(lr[0]) + __uint_as_float(lr[1]);
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  const int qi = pbase + l32;
+  if (qi < q_len) {
+    bf16_t* op = a.out + (size_t)(q_off + qi) * a.out_stride + hq * D + 4 * h;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int e = 4 * b;
+        *reinterpret_cast<uint2*>(op + 32 * db + 8 * b) =
+            make_uint2(pk2bf(o[db][e] * inv, o[db][e + 1] * inv), pk2bf(o[db][e + 2] * inv, o[db][e + 3] * inv));
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Decode attention (one query token per sequence), split-K over context partitions.
 // ------------------------------------------------------------------------------------
 struct DecodeArgs {
@@ -797,18 +1542,40 @@ __global__ void attn_decode_reduce_kernel(DecodeArgs a, int D) {
 int g_prefill_waves = 4;
 int g_prefill_prio = 1;  // PRIO variant of the Llama config (D 128, 4 heads per block, causal, paged)
 int g_prefill_buf = 1;   // BUF staging for that config when the cache is < 4 GiB
+// Ping-pong 8-wave kernel for the Llama config (0 off, 1 on, 2 on + static priority for waves 4-7);
+// when on, every 4-heads-per-block config uses 64-query tiles (the 8-wave kernel where the cache
+// is too large for buffer staging).
+int g_prefill_pp = 0;
 
 template <int D, int GB, bool CAUSAL, bool PAGED>
 hipError_t launch_prefill(const PrefillArgs& a, int n_tiles, hipStream_t st) {
   const int G = a.Hq / a.Hkv;
   dim3 grid(n_tiles, a.Hkv * (G / GB));
   if constexpr (D == 128 && GB == 4 && CAUSAL && PAGED) {
-    if (g_prefill_waves == 4 && g_prefill_prio == 1 && g_prefill_buf && a.kv_bytes) {
+    if (g_prefill_pp && a.kv_bytes) {
+      switch (g_prefill_pp) {
+        case 1: hipLaunchKernelGGL((attn_prefill_pp_kernel<0, 2>), grid, dim3(512), 0, st, a); break;
+        case 2: hipLaunchKernelGGL((attn_prefill_pp_kernel<1, 2>), grid, dim3(512), 0, st, a); break;
+        case 3: hipLaunchKernelGGL((attn_prefill_pp_kernel<1, 4>), grid, dim3(512), 0, st, a); break;
+        case 4: hipLaunchKernelGGL((attn_prefill_pp_kernel<1, 8>), grid, dim3(512), 0, st, a); break;
+        case 5: hipLaunchKernelGGL((attn_prefill_pp_kernel<1, 8, true>), grid, dim3(512), 0, st, a); break;
+        case 6: hipLaunchKernelGGL((attn_prefill_v3_kernel<4>), grid, dim3(256), 0, st, a); break;
+        case 7: hipLaunchKernelGGL((attn_prefill_v3_kernel<4, true>), grid, dim3(256), 0, st, a); break;
+        case 8: hipLaunchKernelGGL((attn_prefill_v3_kernel<4, true, 1>), grid, dim3(256), 0, st, a); break;
+        case 9: hipLaunchKernelGGL((attn_prefill_v3_kernel<4, true, 2>), grid, dim3(256), 0, st, a); break;
+        case 10: hipLaunchKernelGGL((attn_prefill_v3_kernel<8>), grid, dim3(512), 0, st, a); break;
+        case 11: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true>), grid, dim3(512), 0, st, a); break;
+        case 12: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true, 1>), grid, dim3(512), 0, st, a); break;
+        default: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true, 2>), grid, dim3(512), 0, st, a); break;
+      }
+      return hipGetLastError();
+    }
+    if (!g_prefill_pp && g_prefill_waves == 4 && g_prefill_prio == 1 && g_prefill_buf && a.kv_bytes) {
       hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 4, 1, true>), grid, dim3(256), 0, st, a);
       return hipGetLastError();
     }
   }
-  if (GB == 4 && g_prefill_waves == 8)
+  if (GB == 4 && (g_prefill_waves == 8 || (g_prefill_pp >= 1 && g_prefill_pp <= 5) || g_prefill_pp >= 10))
     hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 8>), grid, dim3(512), 0, st, a);
   else if (D == 128 && GB == 4 && CAUSAL && PAGED && g_prefill_prio == 1)
     hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 4, 1>), grid, dim3(256), 0, st, a);
@@ -837,6 +1604,10 @@ RAGK_API int ragk_attn_prefill_stamp(const void* q, int q_stride, const void* k,
   return (int)hipGetLastError();
 }
 
+RAGK_API int ragk_attn_set_dbg(unsigned long long* dbg) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_dbg), &dbg, sizeof(dbg), 0, hipMemcpyHostToDevice);
+}
+
 RAGK_API int ragk_attn_prefill_set_prio(int v) {
   if (v < 0 || v > 2) return (int)hipErrorInvalidValue;
   g_prefill_prio = v;
@@ -859,7 +1630,17 @@ RAGK_API int ragk_attn_prefill_set_waves(int w) {
 RAGK_API int ragk_attn_prefill_qtile(int Hq, int Hkv) {
   const int G = Hq / Hkv;
   const int GB = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
-  return 32 * ((GB == 4 ? g_prefill_waves : 4) / GB);
+  const bool pp64 = (g_prefill_pp >= 1 && g_prefill_pp <= 5) || g_prefill_pp >= 10;
+  return 32 * ((GB == 4 ? (pp64 ? 8 : g_prefill_waves) : 4) / GB);
+}
+
+// 0 off; 1..4 variants (1: fragment prefetch 2 steps; 2: + priority for waves 4-7; 3 / 4: + prefetch
+// 4 / 8 steps); 5: the stamp build of variant 4 (g_attn_dbg set by ragk_attn_set_dbg); 6: the
+// software-pipelined one-wave-per-SIMD kernel (attn_prefill_v3_kernel, 32-query tiles); 7: its stamps
+RAGK_API int ragk_attn_prefill_set_pp(int v) {
+  if (v < 0 || v > 13) return (int)hipErrorInvalidValue;
+  g_prefill_pp = v;
+  return 0;
 }
 
 RAGK_API int ragk_attn_prefill(const void* q, int q_stride, const void* k, const void* v, int kv_stride,

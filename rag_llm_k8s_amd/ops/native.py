@@ -602,12 +602,21 @@ def gather_rows(x, idx, out=None):
 
 # ----------------------------------------------------------------------------- attention
 PREFILL_WAVES = int(os.environ.get("RAGK_PREFILL_WAVES", "4"))
+# prefill attention kernel for the Llama config (D 128, 4 query heads per KV head, causal, paged):
+# 0 = the 4-wave kernel; 10 = the software-pipelined 8-wave kernel (attention.hip
+# attn_prefill_v3_kernel: 32x32x16 MFMAs with the online softmax interleaved into the MFMA stream,
+# two 32-query groups sharing each K/V tile; 6-10 % faster, tools/attn_pp_ab.py); 1 / 2 = the
+# barrier-alternated ping-pong kernel and 6 = the one-wave-per-SIMD v3 (A/B only, both slower)
+PREFILL_PP = int(os.environ.get("RAGK_PREFILL_PP", "10"))
 _prefill_waves_set = [None]
 
 
-def set_prefill_waves(w):
-    """Waves per prefill-attention block when 4 query heads share a KV head (4 or 8)."""
+def set_prefill_waves(w, pp=None):
+    """Waves per prefill-attention block when 4 query heads share a KV head (4 or 8), and the
+    ping-pong kernel mode (64-query tiles when on). Tile lists built before a change are invalid."""
     check(_lib.lib().ragk_attn_prefill_set_waves(int(w)), "ragk_attn_prefill_set_waves")
+    pp = PREFILL_PP if pp is None else int(pp)
+    check(_lib.lib().ragk_attn_prefill_set_pp(pp), "ragk_attn_prefill_set_pp")
     _prefill_waves_set[0] = int(w)
 
 
@@ -616,7 +625,7 @@ def prefill_qtile(Hq, Hkv):
     if not torch.cuda.is_available():  # CPU engine: tiles are unused by the torch backend
         G = Hq // Hkv
         GB = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
-        return 32 * (4 // GB)
+        return 32 * ((8 if GB == 4 and PREFILL_PP in (1, 2, 10) else 4) // GB)
     if _prefill_waves_set[0] is None:
         set_prefill_waves(PREFILL_WAVES)
     return _lib.lib().ragk_attn_prefill_qtile(Hq, Hkv)

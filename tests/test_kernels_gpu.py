@@ -334,6 +334,47 @@ def test_attn_prefill_paged(native, q_lens, kv_lens, Hq, Hkv):
     assert rel_err(out.cpu().reshape(T, Hq, D), ref) < 2e-2
 
 
+@pytest.mark.parametrize("q_lens,kv_lens,Hq,Hkv", [([37], [37], 8, 2), ([100, 64, 1], [100, 300, 129], 32, 8),
+                                                   ([5, 70], [513, 70], 8, 1), ([1], [1], 4, 1),
+                                                   ([64, 65], [64, 200], 4, 1),
+                                                   ([2048, 1104], [4096, 5200], 32, 8)])
+@pytest.mark.parametrize("pp", [1, 2, 6, 10])
+def test_attn_prefill_pingpong(native, q_lens, kv_lens, Hq, Hkv, pp):
+    """Alternative prefill kernels for the Llama config vs the 4-wave kernel and the fp32 oracle, on
+    ragged query tails, chunked prefill (q_len < kv_len), single-tile sequences and 8 query heads per
+    KV head. pp 1 / 2: 8-wave ping-pong (64-query tiles, 3-slot K/V ring), bit-identical (same MFMA
+    and softmax order). pp 6: software-pipelined one-wave-per-SIMD kernel (32x32x16 MFMAs: another
+    fp32 summation order, so within bf16 rounding of the 4-wave kernel)."""
+    D = 128
+    torch.manual_seed(19)
+    kc, vc, bt = _paged_setup(kv_lens, Hkv, D)
+    T = sum(q_lens)
+    q = torch.randn(T, Hq * D).bfloat16()
+    cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(q_lens), 0)), dtype=torch.int32)
+    kvl = torch.tensor(kv_lens, dtype=torch.int32)
+    args = (q.to(DEV), kc.to(DEV), vc.to(DEV), cu.to(DEV), kvl.to(DEV))
+    outs = []
+    try:
+        for mode in (0, pp):
+            native.set_prefill_waves(4, pp=mode)
+            tiles = native.build_prefill_tiles(q_lens, Hq, Hkv)
+            assert (tiles[:, 1] % (64 if mode in (1, 2, 10) else 32) == 0).all()
+            out = torch.full((T, Hq * D), float("nan"), device=DEV).bfloat16()
+            native.attn_prefill(*args, tiles.to(DEV), out, Hq, Hkv, D, causal=True, paged=True,
+                                block_tables=bt.to(DEV))
+            outs.append(out.cpu())
+    finally:
+        native.set_prefill_waves(native.PREFILL_WAVES)
+    if pp in (1, 2):
+        assert torch.equal(outs[0], outs[1])
+    else:
+        assert rel_err(outs[1], outs[0]) < 1e-2
+    ref = R.attention_varlen(q.reshape(T, Hq, D), None, None, cu, kvl, True, 1 / math.sqrt(D),
+                             k_full=lambda s: R.paged_kv_view(kc, bt[s], kv_lens[s], 64),
+                             v_full=lambda s: R.paged_kv_view(vc, bt[s], kv_lens[s], 64))
+    assert rel_err(outs[1].reshape(T, Hq, D), ref) < 2e-2
+
+
 @pytest.mark.parametrize("D,H", [(32, 12), (64, 16)])
 def test_attn_encoder_contig(native, D, H):
     torch.manual_seed(10)
