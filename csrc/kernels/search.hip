@@ -252,13 +252,29 @@ __global__ __launch_bounds__(ST) void l2_mfma_kernel(const float* __restrict__ x
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int q0 = blockIdx.y * 16 * QT;
   const int nqb = min(16 * QT, nq - q0);
-  if (threadIdx.x < 16 * QT) {  // ||q||^2 (a k-ordered fma chain, as the dot products)
+  {
+    // ||q||^2 by the whole block: query j = tid / QP, part p = tid % QP sums dims p, p + QP, ...
+    // (consecutive threads read consecutive floats, 8 loads in flight), parts summed in order by
+    // shuffles. One thread per query walking all d dims with a dependent load each was ~60 us of a
+    // 10k-row search.
+    constexpr int QP = ST / (16 * QT);  // parts per query: 8 (QT 2) or 16 (QT 1)
+    const int j = threadIdx.x / QP, p = threadIdx.x % QP;
     float sq = 0.f;
-    if ((int)threadIdx.x < nqb) {
-      const float* qr = q + (size_t)(q0 + threadIdx.x) * d;
-      for (int t = 0; t < d; ++t) sq = fmaf(qr[t], qr[t], sq);
+    if (j < nqb) {
+      const float* qr = q + (size_t)(q0 + j) * d;
+      int t = p;
+      for (; t + 7 * QP < d; t += 8 * QP) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = qr[t + u * QP];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sq = fmaf(v[u], v[u], sq);
+      }
+      for (; t < d; t += QP) sq = fmaf(qr[t], qr[t], sq);
     }
-    qn[threadIdx.x] = sq;
+#pragma unroll
+    for (int o = 1; o < QP; o <<= 1) sq += __shfl_xor(sq, o, 64);
+    if (p == 0) qn[j] = sq;
   }
   __syncthreads();
   const int fr = lane & 15, fg = lane >> 4;
@@ -291,19 +307,41 @@ __global__ __launch_bounds__(ST) void l2_mfma_kernel(const float* __restrict__ x
     for (int dc = 0; dc < d; dc += MQ_DCH) {
     const int dn = min(MQ_DCH, d - dc);  // host guarantees d % (4 * MQ_KU) == 0
     __syncthreads();  // every wave is done with the previous chunk
-    for (int e = threadIdx.x; e < dn * 16 * QT; e += ST) {
-      const int t = e / (16 * QT), j = e % (16 * QT);
-      qsT[e] = j < nqb ? q[(size_t)(q0 + j) * d + dc + t] : 0.f;
+    // q^T chunk: consecutive threads read consecutive dims of one query (coalesced; the transposed LDS
+    // writes are the cheap side)
+    // (8 loads per thread in flight: a one-at-a-time loop paid a full L2 latency per element)
+    const int tot = dn * 16 * QT;
+    for (int e0 = threadIdx.x; e0 < tot; e0 += 16 * ST) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int e = min(e0 + u * ST, tot - 1);
+        const int j = e / dn, t = e % dn;
+        v[u] = q[(size_t)(q0 + min(j, nqb - 1)) * d + dc + t];
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int e = e0 + u * ST;
+        if (e < tot) {
+          const int j = e / dn, t = e % dn;
+          qsT[t * 16 * QT + j] = j < nqb ? v[u] : 0.f;
+        }
+      }
     }
     __syncthreads();
-    for (int k0 = 0; k0 < dn / 4; k0 += MQ_KU) {
-      float a[MQ_KU][RT];
+    // index columns of the next group of MQ_KU k-steps are requested before the current group's
+    // MFMAs (two register buffers, loop unrolled by two): one group at a time left every group
+    // waiting a full memory latency (12 round trips per 384-dim tile)
+    const int nk = dn / 4;  // multiple of MQ_KU
+    auto load_grp = [&](int k0, float (&a)[MQ_KU][RT]) {
 #pragma unroll
       for (int u = 0; u < MQ_KU; ++u) {
         const float* col = xt + (size_t)(dc + 4 * (k0 + u) + fg) * cap;
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) a[u][rt] = col[rc[rt]];
       }
+    };
+    auto mma_grp = [&](int k0, const float (&a)[MQ_KU][RT]) {
 #pragma unroll
       for (int u = 0; u < MQ_KU; ++u) {
         float b[QT];
@@ -317,6 +355,21 @@ __global__ __launch_bounds__(ST) void l2_mfma_kernel(const float* __restrict__ x
             acc[rt][qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][rt], b[qt], acc[rt][qt], 0, 0, 0);
         }
       }
+    };
+    // three register buffers, two groups in flight ahead of the MFMAs (a group's 8 k-steps of MFMA
+    // are far shorter than one memory latency)
+    float a0[MQ_KU][RT], a1[MQ_KU][RT], a2[MQ_KU][RT];
+    load_grp(0, a0);
+    if (MQ_KU < nk) load_grp(MQ_KU, a1);
+    for (int k0 = 0; k0 < nk; k0 += 3 * MQ_KU) {
+      if (k0 + 2 * MQ_KU < nk) load_grp(k0 + 2 * MQ_KU, a2);
+      mma_grp(k0, a0);
+      if (k0 + MQ_KU >= nk) break;
+      if (k0 + 3 * MQ_KU < nk) load_grp(k0 + 3 * MQ_KU, a0);
+      mma_grp(k0 + MQ_KU, a1);
+      if (k0 + 2 * MQ_KU >= nk) break;
+      if (k0 + 4 * MQ_KU < nk) load_grp(k0 + 4 * MQ_KU, a1);
+      mma_grp(k0 + 2 * MQ_KU, a2);
     }
     }  // dim chunk
     // ||x||^2 of row 16 rt + fr: the 4 dim phases (lanes fr, fr+16, fr+32, fr+48) summed in order
@@ -372,31 +425,54 @@ __global__ __launch_bounds__(ST) void l2_mfma_kernel(const float* __restrict__ x
       ci[(size_t)j * 128 + slot] = lix[qt][m];
     }
   __syncthreads();
-  // wave w merges queries w, w + 4, ... (4 * QT of them) with interleaved networks: each query's 128
-  // candidates are two 64-lane offers
+  // wave w merges queries w, w + 4, ... (4 * QT of them). A query's 128 candidates are 16 sorted
+  // lists of MQ_MK: lane l holds entries 2 (l >> 4) and 2 (l >> 4) + 1 of list l & 15 (a sorted pair),
+  // and k rounds of a wave-wide argmin over the lanes' first entries emit the top k in order (the
+  // winner shifts its pair). Two full 64-lane bitonic offers per query cost ~3x the steps for k <= 8.
   {
     constexpr int NQW = 4 * QT;
-    float bv[NQW], v0[NQW], v1[NQW];
-    int bi[NQW], i0[NQW], i1[NQW];
+    float v0[NQW], v1[NQW];
+    int i0[NQW], i1[NQW];
+    const int slot = (lane & 15) * MQ_MK + 2 * (lane >> 4);
 #pragma unroll
     for (int t = 0; t < NQW; ++t) {
       const int j = w + 4 * t;
-      bv[t] = FLT_MAX;
-      bi[t] = -1;
-      v0[t] = cd[(size_t)j * 128 + lane];
-      i0[t] = ci[(size_t)j * 128 + lane];
-      v1[t] = cd[(size_t)j * 128 + 64 + lane];
-      i1[t] = ci[(size_t)j * 128 + 64 + lane];
+      v0[t] = cd[(size_t)j * 128 + slot];
+      i0[t] = ci[(size_t)j * 128 + slot];
+      v1[t] = cd[(size_t)j * 128 + slot + 1];
+      i1[t] = ci[(size_t)j * 128 + slot + 1];
     }
-    wave_offer_multi<NQW>(bv, bi, v0, i0, k, lane);
-    wave_offer_multi<NQW>(bv, bi, v1, i1, k, lane);
+    for (int r = 0; r < k; ++r) {
+      float mv[NQW];
+      int mi[NQW];
 #pragma unroll
-    for (int t = 0; t < NQW; ++t) {
-      const int j = w + 4 * t;
-      if (j < nqb && lane < k) {
-        const size_t o = ((size_t)(q0 + j) * gridDim.x + blockIdx.x) * k + lane;
-        out_d[o] = bv[t];
-        out_i[o] = bi[t];
+      for (int t = 0; t < NQW; ++t) {
+        mv[t] = v0[t];
+        mi[t] = i0[t];
+      }
+#pragma unroll
+      for (int jx = 1; jx < 64; jx <<= 1)
+#pragma unroll
+        for (int t = 0; t < NQW; ++t) {
+          const float ov = __int_as_float(xor_lane(__float_as_int(mv[t]), jx, lane));
+          const int oi = xor_lane(mi[t], jx, lane);
+          const bool take = cand_lt(ov, oi, mv[t], mi[t]);
+          mv[t] = take ? ov : mv[t];
+          mi[t] = take ? oi : mi[t];
+        }
+#pragma unroll
+      for (int t = 0; t < NQW; ++t) {
+        const bool won = (v0[t] == mv[t]) & (i0[t] == mi[t]);
+        v0[t] = won ? v1[t] : v0[t];
+        i0[t] = won ? i1[t] : i0[t];
+        v1[t] = won ? FLT_MAX : v1[t];
+        i1[t] = won ? -1 : i1[t];
+        const int j = w + 4 * t;
+        if (j < nqb && lane == 0) {
+          const size_t o = ((size_t)(q0 + j) * gridDim.x + blockIdx.x) * k + r;
+          out_d[o] = mv[t];
+          out_i[o] = mi[t];
+        }
       }
     }
   }

@@ -31,6 +31,8 @@ def timed(fn, iters=20, warmup=3):
 def main():
     shapes = [(10000, 384, 1, 4), (10000, 384, 32, 4), (10000, 1024, 1, 5), (1000000, 1024, 1, 5),
               (1000000, 1024, 32, 5), (1000000, 384, 1, 4)]
+    if os.environ.get("SB_SHAPES"):  # e.g. "10000x384x32x4,..."
+        shapes = [tuple(int(v) for v in sh.split("x")) for sh in os.environ["SB_SHAPES"].split(",")]
     for n, d, nq, k in shapes:
         torch.manual_seed(0)
         xt = torch.randn(d, n, device="cuda")
