@@ -787,7 +787,9 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 // NW = 8: two groups of 4 waves (query rows q_start + [0, 32) and + [32, 64)) share every K / V tile,
 // so each SIMD runs two of these streams and one wave's dependency stalls are the other's issue slots.
 // DIAG (stamp builds only, wrong results): 1 = no softmax chunks in the fast slots, 2 = no fragment reads
-template <int NW = 4, bool STAMP = false, int DIAG = 0>
+// PRIO_B: static s_setprio 1 for waves 4-7 over the tile loop (MI355X_MICROARCH.md "Two waves per SIMD"
+// item 4: the second-dispatched half loses every arbitration otherwise).
+template <int NW = 4, bool STAMP = false, int DIAG = 0, int PRIO_B = 0>
 __global__ __launch_bounds__(NW * 64, NW / 4) void attn_prefill_v3_kernel(PrefillArgs a) {
   constexpr int D = 128;
   using C = Cfg<D>;
@@ -1075,6 +1077,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void attn_prefill_v3_kernel(Prefil
 
   unsigned long long te = 0;
   if constexpr (STAMP) te = __builtin_amdgcn_s_memtime();
+  if constexpr (PRIO_B) {
+    if (wid_u >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   qk_simple(0, S0);  // S(0)
   mfma_result_wait();
   // fast iterations: [1, t_end); warm-up tile 0 when there is at least one
@@ -1566,7 +1571,9 @@ hipError_t launch_prefill(const PrefillArgs& a, int n_tiles, hipStream_t st) {
         case 10: hipLaunchKernelGGL((attn_prefill_v3_kernel<8>), grid, dim3(512), 0, st, a); break;
         case 11: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true>), grid, dim3(512), 0, st, a); break;
         case 12: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true, 1>), grid, dim3(512), 0, st, a); break;
-        default: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true, 2>), grid, dim3(512), 0, st, a); break;
+        case 14: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, false, 0, 1>), grid, dim3(512), 0, st, a); break;
+        case 13: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true, 2>), grid, dim3(512), 0, st, a); break;
+        default: hipLaunchKernelGGL((attn_prefill_v3_kernel<8>), grid, dim3(512), 0, st, a); break;
       }
       return hipGetLastError();
     }
@@ -1638,7 +1645,7 @@ RAGK_API int ragk_attn_prefill_qtile(int Hq, int Hkv) {
 // 4 / 8 steps); 5: the stamp build of variant 4 (g_attn_dbg set by ragk_attn_set_dbg); 6: the
 // software-pipelined one-wave-per-SIMD kernel (attn_prefill_v3_kernel, 32-query tiles); 7: its stamps
 RAGK_API int ragk_attn_prefill_set_pp(int v) {
-  if (v < 0 || v > 13) return (int)hipErrorInvalidValue;
+  if (v < 0 || v > 14) return (int)hipErrorInvalidValue;
   g_prefill_pp = v;
   return 0;
 }

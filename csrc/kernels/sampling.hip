@@ -240,18 +240,27 @@ __global__ __launch_bounds__(TK_THREADS) void topk_lds_kernel(const float* __res
 }
 
 // Small-batch top-K (decode batch <= 4): many short chunks (~4k logits) so one row's selection spreads
-// over ~32 CUs, each chunk selected without radix passes: every wave keeps a running sorted top-64 of
-// its share of the chunk in its lanes (keys = -logit, the network sorts ascending, ties -> lower vocab
-// id; a 64-logit tile that cannot enter the list is skipped), the block merges its 4 lists. Output as
-// topk_lds: K candidates per chunk, value descending, ids ascending within equal values.
+// over ~32 CUs, each chunk selected without radix passes. Keys = -logit (ascending = best first), ties
+// -> lower vocab id. Per wave (its ~1k logits, all in registers):
+//   1. every lane's best element; the 64 lane bests sorted by one network -> a valid top-64 list L;
+//   2. T = L[K-1]: at least K elements precede or equal it, so only elements strictly before T (other
+//      than the lane bests already in L) can still enter the top K -- on logits ~9 % of them;
+//   3. those survivors are compacted through LDS (wave prefix count) and offered 64 at a time.
+// Offering every 64-logit tile instead cost a full 27-step network on nearly every tile (each tile of
+// a not-yet-warm list improves it): ~16 networks per wave, ~20 us per row at batch 1. The block then
+// merges its 4 lists. Output as topk_lds: K candidates per chunk, value descending, ids ascending
+// within equal values.
 constexpr int TW_THREADS = 256;
 constexpr int TW_VMAX = 6144;  // chunk sizes this kernel takes (larger chunks: topk_lds)
+constexpr int TW_NT = TW_VMAX / 256;  // logits per lane
 
 __global__ __launch_bounds__(TW_THREADS) void topk_wave_kernel(const float* __restrict__ logits, int ld, int Vtot,
                                                                int K, int vocab_offset, int chunks, float* cand_v,
                                                                int* cand_i) {
   __shared__ float mv[4][64];
   __shared__ int mi[4][64];
+  __shared__ float sk[4][TW_NT * 64];  // per-wave survivor keys / ids (worst case: every logit)
+  __shared__ int sid[4][TW_NT * 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int b = blockIdx.x / chunks, chunk = blockIdx.x % chunks;
   const int Vc = ((Vtot + chunks - 1) / chunks + 7) & ~7;
@@ -259,19 +268,60 @@ __global__ __launch_bounds__(TW_THREADS) void topk_wave_kernel(const float* __re
   const int V = min(Vtot - c0, Vc);
   const float* row = logits + (size_t)b * ld + c0;
   const int id0 = vocab_offset + c0;
-  float bv = INFINITY;  // padding sorts after real -inf logits (id 0xffffffff unsigned)
-  int bi = -1;
-  int i = w * 64 + lane;
-  // loads unconditional (index clamped, masked at use): a load behind a branch gets its own vmcnt(0),
-  // which would wait for the prefetched next tile as well
-  float x = row[min(i, V - 1)];
-  for (int base = w * 64; base < V; base += 4 * 64) {
-    const bool ok = i < V;
-    const int in = i + 4 * 64;
-    const float xn = row[min(in, V - 1)];  // next tile in flight while this one is offered
-    wave_offer(bv, bi, ok ? -x : INFINITY, ok ? id0 + i : -1, K, lane);
-    x = xn;
-    i = in;
+  // element t of this lane: chunk index w*64 + lane + 256 t (loads unconditional, index clamped)
+  float key[TW_NT];
+#pragma unroll
+  for (int t = 0; t < TW_NT; ++t) key[t] = -row[min(w * 64 + lane + 256 * t, V - 1)];  // (V = 0: row[-1], in the row)
+  auto elem_id = [&](int t) { return w * 64 + lane + 256 * t; };
+  // 1. lane best (padding sorts after real -inf logits: key +inf, id -1 = 0xffffffff unsigned)
+  float bv = INFINITY;
+  int bi = -1, bt = -1;
+#pragma unroll
+  for (int t = 0; t < TW_NT; ++t) {
+    const int e = elem_id(t);
+    const bool ok = e < V;
+    const float kv = ok ? key[t] : INFINITY;
+    const int id = ok ? id0 + e : -1;
+    const bool take = cand_lt(kv, id, bv, bi);
+    bv = take ? kv : bv;
+    bi = take ? id : bi;
+    bt = take ? t : bt;
+  }
+  // 2. sorted list of the lane bests; threshold = its K-th entry
+  wave_sort64(bv, bi, lane);
+  const float tv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bv), K - 1));
+  const int ti = __builtin_amdgcn_readlane(bi, K - 1);
+  // 3. survivors (strictly before the threshold, not this lane's best) -> LDS, compacted
+  int cnt = 0;
+#pragma unroll
+  for (int t = 0; t < TW_NT; ++t) {
+    const int e = elem_id(t);
+    cnt += (e < V && t != bt && cand_lt(key[t], id0 + e, tv, ti)) ? 1 : 0;
+  }
+  int incl = cnt;  // inclusive prefix over lanes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  const int total = __shfl(incl, 63, 64);
+  if (total > 0) {
+    int pos = incl - cnt;
+#pragma unroll
+    for (int t = 0; t < TW_NT; ++t) {
+      const int e = elem_id(t);
+      if (e < V && t != bt && cand_lt(key[t], id0 + e, tv, ti)) {
+        sk[w][pos] = key[t];
+        sid[w][pos] = id0 + e;
+        ++pos;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's survivor writes landed
+    __builtin_amdgcn_wave_barrier();
+    for (int base = 0; base < total; base += 64) {
+      const bool ok = base + lane < total;
+      wave_offer(bv, bi, ok ? sk[w][base + lane] : INFINITY, ok ? sid[w][base + lane] : -1, K, lane);
+    }
   }
   mv[w][lane] = bv;
   mi[w][lane] = bi;

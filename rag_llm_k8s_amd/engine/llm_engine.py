@@ -37,8 +37,10 @@ from ..utils import faults
 from .kv_manager import BLOCK, make_block_manager
 
 # decode batches up to this size split each row's top-k over ~31 chunks of ~4k logits (topk_wave_kernel,
-# merged by the sampler's lane network); larger batches use 7 radix-select chunks (topk_lds)
-SMALL_BATCH_TOPK_MAX_B = int(os.environ.get("RAGK_TOPK_SMALL_B", "4"))
+# threshold-filtered lane networks, merged by the sampler's lane network); larger batches use 7
+# radix-select chunks (topk_lds). tools/sampler_bench.py: top-k + sample 21.0 us at batch 1 (7 chunks:
+# 40.1), 33.6 us at batch 32 (7 chunks: 41.2) -- profiles/sampler_bench_r3.log
+SMALL_BATCH_TOPK_MAX_B = int(os.environ.get("RAGK_TOPK_SMALL_B", "64"))
 SMALL_BATCH_TOPK_CHUNK = int(os.environ.get("RAGK_TOPK_SMALL_CHUNK", "4096"))
 
 log = logging.getLogger(__name__)

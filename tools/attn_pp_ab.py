@@ -20,7 +20,7 @@ def main():
     lens = [int(x) for x in os.environ.get("AP_LENS", "5400,5400,5400,5400,5400,5400").split(",")]
     ctx = [int(x) for x in os.environ.get("AP_CTX", ",".join("0" for _ in lens)).split(",")]
     rounds = int(os.environ.get("AP_ROUNDS", "5"))
-    modes = [int(x) for x in os.environ.get("AP_MODES", "0,6,10").split(",")]
+    modes = [int(x) for x in os.environ.get("AP_MODES", "0,10,14").split(",")]
     dev = "cuda:0"
     torch.manual_seed(0)
     kvl_l = [q + c for q, c in zip(lens, ctx)]
