@@ -240,26 +240,44 @@ __global__ __launch_bounds__(FR_THREADS) void ar_add_rmsnorm_kernel(ArPeers P, i
                                                                     bf16_t* h, int ldh, const bf16_t* __restrict__ w,
                                                                     bf16_t* out, int ldo, int H, float eps) {
   __shared__ float red[FR_THREADS / 64];
-  __shared__ unsigned s_ep;
   const int row = blockIdx.x;
   ArRowFlags* mine = reinterpret_cast<ArRowFlags*>(P.base[rank] + P.rows_off);
-  if (threadIdx.x == 0) s_ep = mine->epoch[row] + 1;
-  __syncthreads();
-  const unsigned ep = s_ep;
+  const int nvec = H >> 3;
+  // 0. every load that does not wait on a peer is issued together, one memory round trip instead of
+  // four serial ones (at batch 1 this kernel is a single block: its latency is the sum of its round
+  // trips): this row's epoch (uncached flag region; every wave reads the same word), this rank's
+  // split-K slabs, the residual row and the norm weights.
+  const unsigned ep_ld = mine->epoch[row];
+  const size_t slab = (size_t)M * H;
+  f32x4 pv[FR_MAXV][PSU][2];
+  u32x4 hv[FR_MAXV], gv[FR_MAXV];
+#pragma unroll
+  for (int i = 0; i < FR_MAXV; ++i) {
+    const int vi = min((int)threadIdx.x + i * FR_THREADS, nvec - 1);
+    if (i * FR_THREADS < nvec) {  // block-uniform
+      load_slabs8(Pp + (size_t)row * H + vi * 8, S, slab, pv[i]);
+      hv[i] = *reinterpret_cast<const u32x4*>(h + (size_t)row * ldh + vi * 8);
+      gv[i] = *reinterpret_cast<const u32x4*>(w + vi * 8);
+    }
+  }
+  float a[FR_MAXV][8];
+#pragma unroll
+  for (int i = 0; i < FR_MAXV; ++i) {
+    const int vi = min((int)threadIdx.x + i * FR_THREADS, nvec - 1);
+    if (i * FR_THREADS < nvec) add_slabs8(pv[i], Pp + (size_t)row * H + vi * 8, S, slab, a[i]);
+  }
+  const unsigned ep = __builtin_amdgcn_readfirstlane(ep_ld) + 1;
   const size_t stage_off = P.rows_off + ROW_FLAG_BYTES + (size_t)(ep & 1) * P.row_stage_bytes + (size_t)row * H * 4;
   const size_t res_off = P.rows_off + ROW_FLAG_BYTES + 2 * P.row_stage_bytes + (size_t)(ep & 1) * P.row_result_bytes +
                          (size_t)row * H * 2;
-  const int nvec = H >> 3;
   // 1. this rank's partial row (its split-K slabs summed) -> staging
 #pragma unroll
   for (int i = 0; i < FR_MAXV; ++i) {
     const int vi = threadIdx.x + i * FR_THREADS;
     if (vi < nvec) {
-      float a[8];
-      sum_slabs8(Pp + (size_t)row * H + vi * 8, S, (size_t)M * H, a);
       f32x4* dst = reinterpret_cast<f32x4*>(P.base[rank] + stage_off + (size_t)vi * 32);
-      dst[0] = f32x4{a[0], a[1], a[2], a[3]};
-      dst[1] = f32x4{a[4], a[5], a[6], a[7]};
+      dst[0] = f32x4{a[i][0], a[i][1], a[i][2], a[i][3]};
+      dst[1] = f32x4{a[i][4], a[i][5], a[i][6], a[i][7]};
     }
   }
   bool ok = row_barrier(P, rank, world, 0, row, ep);
@@ -279,7 +297,7 @@ __global__ __launch_bounds__(FR_THREADS) void ar_add_rmsnorm_kernel(ArPeers P, i
             for (int e = 0; e < 8; ++e) t[e] += f[e];
           }
         }
-        unpack8(*reinterpret_cast<const u32x4*>(h + (size_t)row * ldh + vi * 8), v[i]);
+        unpack8(hv[i], v[i]);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[i][e] = bf2f(f2bf(v[i][e] + bf2f(f2bf(t[e]))));
       }
@@ -308,7 +326,7 @@ __global__ __launch_bounds__(FR_THREADS) void ar_add_rmsnorm_kernel(ArPeers P, i
       if (vi < nvec) {
         float t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (ok) unpack8(ld16(P.base[vi / per] + res_off + (size_t)vi * 16), t);
-        unpack8(*reinterpret_cast<const u32x4*>(h + (size_t)row * ldh + vi * 8), v[i]);
+        unpack8(hv[i], v[i]);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[i][e] = bf2f(f2bf(v[i][e] + t[e]));  // t already bf16-rounded
       }
@@ -331,7 +349,7 @@ __global__ __launch_bounds__(FR_THREADS) void ar_add_rmsnorm_kernel(ArPeers P, i
     const int vi = threadIdx.x + i * FR_THREADS;
     if (vi < nvec) {
       float wv[8], o[8];
-      unpack8(*reinterpret_cast<const u32x4*>(w + vi * 8), wv);
+      unpack8(gv[i], wv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = wv[e] * bf2f(f2bf(v[i][e] * inv));
       *reinterpret_cast<u32x4*>(out + (size_t)row * ldo + vi * 8) = pack8(o);

@@ -134,7 +134,23 @@ struct PrefillArgs {
   int Hq, Hkv;
   float scale_log2;
   unsigned kv_bytes;                       // PAGED: bytes of one cache (K or V) if < 4 GiB, else 0
+  int n_hg;                                // > 0: 1-D grid of n_tiles x n_hg, head group fastest
 };
+
+// Prefill block -> (tile index, head group). 1-D grid, head group fastest (n_hg > 0, the default): the
+// workgroups dispatch in the tile list's order -- heaviest causal tiles first -- across EVERY head (a 2-D
+// grid dispatches head 0's whole list before head 1's, so the last heads' longest tiles start late and
+// set the tail), and the round-robin XCD placement of consecutive workgroups keeps each head group on
+// one XCD when n_hg is a multiple of 8 (its K/V tiles are re-read from that XCD's L2 by every query tile).
+__device__ inline void prefill_block(const PrefillArgs& a, int& tile, int& hg) {
+  if (a.n_hg > 0) {
+    tile = (int)blockIdx.x / a.n_hg;
+    hg = (int)blockIdx.x - tile * a.n_hg;
+  } else {
+    tile = blockIdx.x;
+    hg = blockIdx.y;
+  }
+}
 
 __device__ unsigned long long* g_attn_dbg = nullptr;  // stamp build only
 
@@ -156,11 +172,13 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_prefill_kernel(Prefill
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
-  const int seq = a.tiles[2 * blockIdx.x], q_start = a.tiles[2 * blockIdx.x + 1];
+  int tix, hg;
+  prefill_block(a, tix, hg);
+  const int seq = a.tiles[2 * tix], q_start = a.tiles[2 * tix + 1];
   const int G = a.Hq / a.Hkv;
   const int groups_per_kv = G / GB;
-  const int kvh = blockIdx.y / groups_per_kv;
-  const int gsub = blockIdx.y % groups_per_kv;
+  const int kvh = hg / groups_per_kv;
+  const int gsub = hg % groups_per_kv;
   const int hq = kvh * G + gsub * GB + (wid % GB);
   const int pbase = q_start + (wid / GB) * 32;
 
@@ -503,11 +521,13 @@ __global__ __launch_bounds__(512, 2) void attn_prefill_pp_kernel(PrefillArgs a) 
   const int lane = threadIdx.x & 63;
   const int wid_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int grp = wid_u >> 2, hs = wid_u & 3;
-  const int seq = a.tiles[2 * blockIdx.x], q_start = a.tiles[2 * blockIdx.x + 1];
+  int tix, hg;
+  prefill_block(a, tix, hg);
+  const int seq = a.tiles[2 * tix], q_start = a.tiles[2 * tix + 1];
   const int G = a.Hq / a.Hkv;
   const int groups_per_kv = G / 4;
-  const int kvh = blockIdx.y / groups_per_kv;
-  const int hq = kvh * G + (blockIdx.y % groups_per_kv) * 4 + hs;
+  const int kvh = hg / groups_per_kv;
+  const int hq = kvh * G + (hg % groups_per_kv) * 4 + hs;
   const int pbase = q_start + grp * 32;
 
   const int q_off = a.cu_q[seq];
@@ -799,11 +819,13 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void attn_prefill_v3_kernel(Prefil
   constexpr int PPW = 16 / NW;  // DMA pieces per wave per K or V tile
   const int lane = threadIdx.x & 63;
   const int wid_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int seq = a.tiles[2 * blockIdx.x], q_start = a.tiles[2 * blockIdx.x + 1];
+  int tix, hg;
+  prefill_block(a, tix, hg);
+  const int seq = a.tiles[2 * tix], q_start = a.tiles[2 * tix + 1];
   const int G = a.Hq / a.Hkv;
   const int groups_per_kv = G / 4;
-  const int kvh = blockIdx.y / groups_per_kv;
-  const int hq = kvh * G + (blockIdx.y % groups_per_kv) * 4 + (wid_u & 3);
+  const int kvh = hg / groups_per_kv;
+  const int hq = kvh * G + (hg % groups_per_kv) * 4 + (wid_u & 3);
   const int pbase = q_start + 32 * (wid_u >> 2);
 
   const int q_off = a.cu_q[seq];
@@ -1552,10 +1574,15 @@ int g_prefill_buf = 1;   // BUF staging for that config when the cache is < 4 Gi
 // is too large for buffer staging).
 int g_prefill_pp = 0;
 
+// Block order (prefill_block): 1 = 1-D grid, head group fastest (default); 0 = 2-D (tile, head group).
+int g_prefill_order = 1;
+
 template <int D, int GB, bool CAUSAL, bool PAGED>
-hipError_t launch_prefill(const PrefillArgs& a, int n_tiles, hipStream_t st) {
+hipError_t launch_prefill(PrefillArgs a, int n_tiles, hipStream_t st) {
   const int G = a.Hq / a.Hkv;
-  dim3 grid(n_tiles, a.Hkv * (G / GB));
+  const int n_hg = a.Hkv * (G / GB);
+  a.n_hg = g_prefill_order ? n_hg : 0;
+  const dim3 grid = a.n_hg ? dim3(n_tiles * n_hg) : dim3(n_tiles, n_hg);
   if constexpr (D == 128 && GB == 4 && CAUSAL && PAGED) {
     if (g_prefill_pp && a.kv_bytes) {
       switch (g_prefill_pp) {
@@ -1660,7 +1687,7 @@ RAGK_API int ragk_attn_prefill(const void* q, int q_stride, const void* k, const
   const unsigned long long cache_bytes = paged ? (unsigned long long)kv_stride * Hkv * KT * D * 2 : 0ull;
   PrefillArgs a{(const bf16_t*)q, q_stride, (const bf16_t*)k, (const bf16_t*)v, kv_stride, block_tables, bt_stride,
                 cu_q, cu_kv, kv_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, scale * 1.4426950408889634f,
-                cache_bytes < (1ull << 32) ? (unsigned)cache_bytes : 0u};
+                cache_bytes < (1ull << 32) ? (unsigned)cache_bytes : 0u, 0};
   const int G = Hq / Hkv;
   const int GB = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
 #define RAGK_PF(DD, GG, CC, PP)                                                          \
@@ -1678,6 +1705,11 @@ RAGK_API int ragk_attn_prefill(const void* q, int q_stride, const void* k, const
   RAGK_PF(64, 1, true, false)
 #undef RAGK_PF
   return (int)hipErrorInvalidValue;
+}
+
+RAGK_API int ragk_attn_prefill_set_order(int order) {
+  g_prefill_order = order ? 1 : 0;
+  return 0;
 }
 
 // K/V cache-policy switch for decode (0 = default, 1 = non-temporal loads; the KV stream is read

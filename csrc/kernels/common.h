@@ -85,6 +85,46 @@ __device__ __forceinline__ void sum_slabs8(const float* P, int S, size_t slab, f
   }
 }
 
+// sum_slabs8 split in two, so a kernel can put other independent loads (residual row, norm weights)
+// in flight with the first PSU slabs' loads: load_slabs8 issues them (index clamped), add_slabs8 sums
+// them in slab order and streams any slabs beyond PSU serially.
+__device__ __forceinline__ void load_slabs8(const float* P, int S, size_t slab, f32x4 (&p)[PSU][2]) {
+#pragma unroll
+  for (int u = 0; u < PSU; ++u) {
+    const f32x4* ps = reinterpret_cast<const f32x4*>(P + (size_t)min(u, S - 1) * slab);
+    p[u][0] = ps[0];
+    p[u][1] = ps[1];
+  }
+}
+__device__ __forceinline__ void add_slabs8(const f32x4 (&p)[PSU][2], const float* P, int S, size_t slab, float* a) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = 0.f;
+#pragma unroll
+  for (int u = 0; u < PSU; ++u) {
+    if (u < S) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a[e] += p[u][0][e];
+        a[4 + e] += p[u][1][e];
+      }
+    }
+  }
+  for (int s0 = PSU; s0 < S; s0 += PSU) {  // same order as sum_slabs8: one accumulator, slab by slab
+    f32x4 q[PSU][2];
+    load_slabs8(P + (size_t)s0 * slab, S - s0, slab, q);
+#pragma unroll
+    for (int u = 0; u < PSU; ++u) {
+      if (s0 + u < S) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] += q[u][0][e];
+          a[4 + e] += q[u][1][e];
+        }
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ void sum_partials8(const float* P, int S, size_t slab, float* a) {
   sum_slabs8(P, S, slab, a);
 #pragma unroll

@@ -366,13 +366,26 @@ __global__ __launch_bounds__(PNT) void add_partials_rmsnorm_kernel(const float* 
   float v[MAXV][8];
   const int nvec = H >> 3;
   float ss = 0.f;
+  // every independent load in flight together (one memory round trip, not three): the first PSU
+  // slabs, the residual row and the norm weights
+  f32x4 pv[MAXV][PSU][2];
+  u32x4 hv[MAXV], gv[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int vi = min((int)threadIdx.x + i * PNT, nvec - 1);
+    if (i * PNT < nvec) {  // block-uniform
+      load_slabs8(P + (size_t)row * H + vi * 8, S, (size_t)M * H, pv[i]);
+      hv[i] = *reinterpret_cast<const u32x4*>(hr + vi * 8);
+      gv[i] = *reinterpret_cast<const u32x4*>(w + vi * 8);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MAXV; ++i) {
     const int vi = threadIdx.x + i * PNT;
     if (vi < nvec) {
       float a[8];
-      sum_slabs8(P + (size_t)row * H + vi * 8, S, (size_t)M * H, a);
-      unpack8(*reinterpret_cast<const u32x4*>(hr + vi * 8), v[i]);
+      add_slabs8(pv[i], P + (size_t)row * H + vi * 8, S, (size_t)M * H, a);
+      unpack8(hv[i], v[i]);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[i][e] = bf2f(f2bf(v[i][e] + bf2f(f2bf(a[e]))));
       *reinterpret_cast<u32x4*>(hr + vi * 8) = pack8(v[i]);
@@ -387,7 +400,7 @@ __global__ __launch_bounds__(PNT) void add_partials_rmsnorm_kernel(const float* 
     const int vi = threadIdx.x + i * PNT;
     if (vi < nvec) {
       float wv[8], o[8];
-      unpack8(*reinterpret_cast<const u32x4*>(w + vi * 8), wv);
+      unpack8(gv[i], wv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = wv[e] * bf2f(f2bf(v[i][e] * inv));
       *reinterpret_cast<u32x4*>(out + (size_t)row * ldo + vi * 8) = pack8(o);

@@ -44,6 +44,7 @@ _SIGS = {
     "ragk_gemm_part_silu_ok": [I, I, I, I],
     "ragk_attn_prefill_set_waves": [I],
     "ragk_attn_prefill_set_pp": [I],
+    "ragk_attn_prefill_set_order": [I],
     "ragk_attn_set_dbg": [P],
     "ragk_attn_prefill_stamp": [P, I, P, P, P, I, P, P, P, I, P, I, I, I, F, P, S],
     "ragk_gemm_w4_diag": [I, I, P, I, P, I, P, I, I, I, I, P, S],

@@ -608,6 +608,9 @@ PREFILL_WAVES = int(os.environ.get("RAGK_PREFILL_WAVES", "4"))
 # two 32-query groups sharing each K/V tile; 6-10 % faster, tools/attn_pp_ab.py); 1 / 2 = the
 # barrier-alternated ping-pong kernel and 6 = the one-wave-per-SIMD v3 (A/B only, both slower)
 PREFILL_PP = int(os.environ.get("RAGK_PREFILL_PP", "10"))
+# prefill block order (attention.hip prefill_block): 1 = one grid dimension, head group fastest, so the
+# heaviest causal tiles of every head start first and each XCD serves one KV head; 0 = (tile, head) grid
+PREFILL_ORDER = int(os.environ.get("RAGK_PREFILL_ORDER", "1"))
 _prefill_waves_set = [None]
 
 
@@ -617,6 +620,7 @@ def set_prefill_waves(w, pp=None):
     check(_lib.lib().ragk_attn_prefill_set_waves(int(w)), "ragk_attn_prefill_set_waves")
     pp = PREFILL_PP if pp is None else int(pp)
     check(_lib.lib().ragk_attn_prefill_set_pp(pp), "ragk_attn_prefill_set_pp")
+    check(_lib.lib().ragk_attn_prefill_set_order(PREFILL_ORDER), "ragk_attn_prefill_set_order")
     _prefill_waves_set[0] = int(w)
 
 

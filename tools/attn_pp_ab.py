@@ -21,6 +21,12 @@ def main():
     ctx = [int(x) for x in os.environ.get("AP_CTX", ",".join("0" for _ in lens)).split(",")]
     rounds = int(os.environ.get("AP_ROUNDS", "5"))
     modes = [int(x) for x in os.environ.get("AP_MODES", "0,10,14").split(",")]
+    # block orders (attention.hip prefill_block): 1 = head group fastest (default), 0 = (tile, head) grid
+    orders = [int(x) for x in os.environ.get("AP_ORDERS", "1").split(",")]
+    from rag_llm_k8s_amd.ops import _lib
+
+    def set_order(o):
+        _lib.check(_lib.lib().ragk_attn_prefill_set_order(o), "order")
     dev = "cuda:0"
     torch.manual_seed(0)
     kvl_l = [q + c for q, c in zip(lens, ctx)]
@@ -39,28 +45,30 @@ def main():
     cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(lens), 0)), dtype=torch.int32, device=dev)
     kvl = torch.tensor(kvl_l, dtype=torch.int32, device=dev)
     flops = sum(4 * Hq * D * (q_ * c_ + q_ * q_ / 2) for q_, c_ in zip(lens, ctx))
-    tiles, outs = {}, {}
+    tiles = {}
     for m in modes:
         N.set_prefill_waves(4, pp=m)
         tiles[m] = N.build_prefill_tiles(lens, Hq, Hkv).to(dev)
-        outs[m] = torch.empty(T, Hq * D, device=dev).bfloat16()
-    times = {m: [] for m in modes}
+    keys = [(m, o) for m in modes for o in orders]
+    outs = {(m, o): torch.empty(T, Hq * D, device=dev).bfloat16() for m, o in keys}
+    times = {k: [] for k in keys}
     for r in range(rounds + 1):
-        for m in modes:
+        for m, o in keys:
             N.set_prefill_waves(4, pp=m)
+            set_order(o)
             a, b = torch.cuda.Event(True), torch.cuda.Event(True)
             a.record()
             for _ in range(5):
-                N.attn_prefill(q, kc, vc, cu, kvl, tiles[m], outs[m], Hq, Hkv, D, causal=True, paged=True,
+                N.attn_prefill(q, kc, vc, cu, kvl, tiles[m], outs[(m, o)], Hq, Hkv, D, causal=True, paged=True,
                                block_tables=bt)
             b.record()
             b.synchronize()
             if r:
-                times[m].append(a.elapsed_time(b) / 5 * 1e3)
+                times[(m, o)].append(a.elapsed_time(b) / 5 * 1e3)
+    set_order(1)
     if os.environ.get("AP_STAMP", "1") == "1":
         # stamp build of the software-pipelined kernel (pp mode 7): per wave [fast slots, fast wait +
         # barrier, prologue + warm-up, epilogue] cycles, fast iterations
-        from rag_llm_k8s_amd.ops import _lib
         for smode, sname, nw in ((7, "4w full", 4), (11, "8w full", 8), (12, "8w no softmax", 8),
                                  (13, "8w no LDS reads", 8)):
             N.set_prefill_waves(4, pp=smode)
@@ -80,7 +88,6 @@ def main():
                      d[:, 0, 5].mean(), d[:, 0, 4].mean()))
     if os.environ.get("AP_STAMP_PP", "0") == "1":
         # stamp build (pp mode 5 = variant 4 + s_memtime per phase): mean cycles per segment pair
-        from rag_llm_k8s_amd.ops import _lib
         N.set_prefill_waves(4, pp=5)
         t5 = N.build_prefill_tiles(lens, Hq, Hkv).to(dev)
         grid = t5.shape[0] * Hkv
@@ -97,15 +104,16 @@ def main():
             m = dd[:, :, :4].sum((0, 1)) / n
             print("stamps %s per tile: MFMA phase %.0f | barrier %.0f | VALU phase %.0f | barrier %.0f = %.0f cycles"
                   " (64 MFMA x 16 = 1024 per wave)" % (name, *m.tolist(), m.sum().item()))
-        print("stamp build bit-identical:", torch.equal(o5, outs[modes[0]]))
+        print("stamp build bit-identical:", torch.equal(o5, outs[keys[0]]))
     def rel(a_, b_):
         return ((a_.float() - b_.float()).norm() / b_.float().norm()).item()
     N.set_prefill_waves(4, pp=0)
-    for m in modes:
-        t = sorted(times[m])[len(times[m]) // 2]
-        same = torch.equal(outs[m], outs[modes[0]])
-        print("lens=%s ctx=%s pp=%d  %.1f us  %.0f TF  bit-identical=%s rel=%.2e" % (lens[0], ctx[0], m, t, flops / t / 1e6, same,
-                                                                                 rel(outs[m], outs[modes[0]])))
+    for m, o in keys:
+        t = sorted(times[(m, o)])[len(times[(m, o)]) // 2]
+        ref = outs[keys[0]]
+        same = torch.equal(outs[(m, o)], ref)
+        print("lens=%s ctx=%s pp=%d order=%d  %.1f us  %.0f TF  bit-identical=%s rel=%.2e" % (
+            lens[0], ctx[0], m, o, t, flops / t / 1e6, same, rel(outs[(m, o)], ref)))
 
 
 if __name__ == "__main__":

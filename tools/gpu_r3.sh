@@ -39,6 +39,24 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 rc=$?; echo "probe prof rc=$rc"; rm -f gpurun_out/prof_tp/*kernel_trace.csv
 python tools/rocprof_summary.py gpurun_out/prof_tp/tp_kernel_stats.csv 40 > gpurun_out/tp_probe_summary.txt 2>&1; head -45 gpurun_out/tp_probe_summary.txt; ok $rc
 ;; esac
+case ",$STEP," in *,probeab,*)
+for mt in ${PAB_TILES:-4 2 1}; do
+RAGK_DECODE_MIN_TILES=$mt timeout -k 10 300 python -u tools/tp_decode_probe.py ${PAB_B:-1 32} > gpurun_out/tp_probe_mt$mt.log 2>&1
+rc=$?; echo "probe min_tiles=$mt rc=$rc"; grep "^B=" gpurun_out/tp_probe_mt$mt.log; ok $rc
+done
+;; esac
+case ",$STEP," in *,normt,*)
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_canary_gpu.py -k "partials or norm" -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_normt.log 2>&1
+rc=$?; echo "norm tests rc=$rc"; tail -4 gpurun_out/pytest_normt.log; ok $rc
+;; esac
+case ",$STEP," in *,order,*)
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_canary_gpu.py -k "prefill" -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_order.log 2>&1
+rc=$?; echo "prefill tests rc=$rc"; tail -4 gpurun_out/pytest_order.log; ok $rc
+for cfg in "5215:0" "5400,5400,5400,5400,5400,5400:0,0,0,0,0,0" "2048:3072"; do
+AP_LENS=${cfg%%:*} AP_CTX=${cfg##*:} AP_MODES=10 AP_ORDERS=1,0 AP_STAMP=0 AP_ROUNDS=7 timeout -k 10 200 python -u tools/attn_pp_ab.py > gpurun_out/order_ab.log 2>&1
+rc=$?; echo "order A/B $cfg rc=$rc"; grep "^lens" gpurun_out/order_ab.log; ok $rc
+done
+;; esac
 case ",$STEP," in *,searchprof,*)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_search -o s -- python3 tools/search_bench.py > gpurun_out/search_prof.log 2>&1
 rc=$?; echo "search prof rc=$rc"; rm -f gpurun_out/prof_search/*kernel_trace.csv
