@@ -96,7 +96,7 @@ __host__ __device__ inline int mg_groups(int M, int KS) {
 // streams its shard with every load in flight instead of the register-streaming skinny kernel
 // (12.8 us for a 29 MB TP=8 shard, profiles/tp_decode_probe_kernels_r3.txt). One item per thread:
 // row tid / CPR, 8 columns (tid % CPR) * 8; all S1 slabs' loads issued before the weight stream.
-constexpr int SG_MAXS = 4;
+constexpr int SG_MAXS = 8;
 struct SiluArgs {
   const float* pgu;  // [S1][M][2K]
   int S1;
@@ -496,7 +496,7 @@ RAGK_API int ragk_gemm_part_norm(const void* X, int ldx, const void* gamma, floa
 
 // Down projection fed by the packed gate/up projection's split-K partials (SG above): P = partials of
 // (silu(gate) * up) . W^T, gate / up = sum of the S1 slabs of pgu [S1][M][2K] (gemm_part of the packed
-// [2K, H] weight). M <= 4, S1 <= 4, K % 64 == 0, one staging item per thread (M * 8 * ks_steps <= 512).
+// [2K, H] weight). M <= 4, S1 <= SG_MAXS, K % 64 == 0, one staging item per thread (M * 8 * ks_steps <= 512).
 RAGK_API int ragk_gemm_part_silu(const float* pgu, int S1, const void* W, int ldw, float* P, int M, int N, int K,
                                  int ks_steps, hipStream_t st) {
   if (M <= 0) return 0;

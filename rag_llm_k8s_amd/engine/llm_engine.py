@@ -730,8 +730,15 @@ class LLMEngine:
         fin = self._collect(prev, in_flight=set(id(s) for s in seqs))
         self._inflight = cur
         self.stats["decode_steps"] += 1
+        self._count_batch(n)
         self.stats["decode_s"] += time.perf_counter() - t0
         return fin
+
+    def _count_batch(self, n):
+        """Decode steps per batch size (stats["decode_batch_hist"]): how well the schedule keeps the
+        weight stream of each decode step amortised over many sequences."""
+        h = self.stats.setdefault("decode_batch_hist", {})
+        h[n] = h.get(n, 0) + 1
 
     def _collect(self, step, in_flight=frozenset()):
         """Wait for an in-flight decode step, accept its tokens, free what it no longer touches."""
@@ -806,6 +813,7 @@ class LLMEngine:
                 self._finish(s, r)
                 finished.append(s)
         self.stats["decode_steps"] += 1
+        self._count_batch(n)
         self.stats["decode_tokens"] += n
         self.stats["decode_s"] += time.perf_counter() - t0
         return finished

@@ -331,11 +331,12 @@ def gemm_part_merge(attn_out, kv_lens, part_tiles, max_parts, ws_o, ws_ml, Hq, w
     return out
 
 
-SILU_MAX_SLABS = 4  # gemm_part.hip SG_MAXS
+SILU_MAX_SLABS = 8  # gemm_part.hip SG_MAXS
 
 
 def gemm_part_gu_ks(K):
-    """K-slice steps of the packed gate/up partial GEMM feeding gemm_part_silu: at most 4 slabs."""
+    """K-slice steps of the packed gate/up partial GEMM feeding gemm_part_silu: at most SILU_MAX_SLABS
+    slabs (8: 448 blocks for the TP=8 shard's 3584-row gate/up at K = 4096, 224 with 4)."""
     for ks in (4, 8, 16, 32):
         if K % (64 * ks) == 0 and K // (64 * ks) <= SILU_MAX_SLABS:
             return ks
@@ -367,7 +368,7 @@ def gemm_part_silu_ok(M, w_gu, w_down):
 
 
 def gemm_part_gu(x, w_gu):
-    """Split-K partials of the packed gate/up projection with at most 4 slabs (gemm_part_silu's input)."""
+    """Split-K partials of the packed gate/up projection with at most SILU_MAX_SLABS slabs (gemm_part_silu's input)."""
     return gemm_part(x, w_gu, ks=gemm_part_gu_ks(x.shape[1]))
 
 
