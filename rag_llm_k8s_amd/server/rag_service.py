@@ -441,7 +441,7 @@ class RagService:
                 seqs[i] = eng.add_request(self._prompt_ids(None, ids=ids), p_use, seed=seed_of[i])
                 queued.append(seqs[i])
 
-        rest, err = None, []
+        rest, err, t_rest = None, [], []
         if tp:
             flat, lens = (self.tok.encode_batch_flat([fulls[i] for i in rows], add_special_tokens=True)
                           if lead else (None, None))
@@ -460,6 +460,7 @@ class RagService:
                     try:
                         tail = rows[head:]
                         submit(tail, self.tok.encode_batch([fulls[i] for i in tail], add_special_tokens=True))
+                        t_rest.append(time.perf_counter())
                     except Exception as e:  # surfaced below, after the engine drains
                         err.append(e)
                 rest = threading.Thread(target=_rest, daemon=True)
@@ -491,6 +492,8 @@ class RagService:
         st = eng.stats
         st["retrieve_s"] = st.get("retrieve_s", 0.0) + (t_ret - t0)
         st["prompt_build_s"] = st.get("prompt_build_s", 0.0) + (t_prep - t_ret)
+        if t_rest:  # when the helper thread had queued the tail prompts (after the head's first step)
+            st["tail_queued_s"] = st.get("tail_queued_s", 0.0) + (t_rest[0] - t_prep)
         outs = []
         for s, ctx in zip(seqs, ctxs):
             if s is None:
