@@ -96,7 +96,7 @@ __host__ __device__ inline int mg_groups(int M, int KS) {
 // streams its shard with every load in flight instead of the register-streaming skinny kernel
 // (12.8 us for a 29 MB TP=8 shard, profiles/tp_decode_probe_kernels_r3.txt). One item per thread:
 // row tid / CPR, 8 columns (tid % CPR) * 8; all S1 slabs' loads issued before the weight stream.
-constexpr int SG_MAXS = 8;
+constexpr int SG_MAXS = 4;
 struct SiluArgs {
   const float* pgu;  // [S1][M][2K]
   int S1;

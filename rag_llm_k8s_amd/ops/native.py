@@ -331,12 +331,13 @@ def gemm_part_merge(attn_out, kv_lens, part_tiles, max_parts, ws_o, ws_ml, Hq, w
     return out
 
 
-SILU_MAX_SLABS = 8  # gemm_part.hip SG_MAXS
+SILU_MAX_SLABS = 4  # gemm_part.hip SG_MAXS
 
 
 def gemm_part_gu_ks(K):
     """K-slice steps of the packed gate/up partial GEMM feeding gemm_part_silu: at most SILU_MAX_SLABS
-    slabs (8: 448 blocks for the TP=8 shard's 3584-row gate/up at K = 4096, 224 with 4)."""
+    slabs. (8 slabs: the TP=8 shard's gate/up 8.2 -> 7.9 us with 448 blocks, but the down GEMM's
+    staging of 8 slabs 7.2 -> 9.4 us; docs/PERF_NOTES.md, TP decode.)"""
     for ks in (4, 8, 16, 32):
         if K % (64 * ks) == 0 and K // (64 * ks) <= SILU_MAX_SLABS:
             return ks
