@@ -107,8 +107,9 @@ class Tokenizer:
             self._split_ok_v = ok
         return ok
 
-    def _encode_split(self, text, add_special_tokens):
-        n = max(2, min(ENCODE_THREADS, len(text) // 2048))
+    @staticmethod
+    def _pieces(text, n):
+        """`text` cut into about n pieces at split-safe boundaries (see SPLIT_MIN_CHARS)."""
         step = len(text) // n
         cuts, pos = [0], 0
         for _ in range(n - 1):
@@ -120,12 +121,32 @@ class Tokenizer:
             cuts.append(i)
             pos = i
         cuts.append(len(text))
-        pieces = [text[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
+        return [text[a:b] for a, b in zip(cuts[:-1], cuts[1:])]
+
+    def _encode_split(self, text, add_special_tokens):
+        pieces = self._pieces(text, max(2, min(ENCODE_THREADS, len(text) // 2048)))
         out = self.impl.encode_batch(pieces, False, ENCODE_THREADS, -1)
         ids = list(self._special_prefix) if add_special_tokens else []
         for x in out:
             ids.extend(x)
         return ids
+
+    def _encode_batch_split(self, texts, add_special_tokens):
+        """encode_batch of fewer texts than worker threads (C=1: one ~20 KB RAG prompt, ~6 ms on a single
+        worker): every long text is cut as in encode() and all pieces go to the workers in one call, then
+        each text is reassembled (special prefix + its pieces' ids in order) -- ~2 ms."""
+        per = max(2, ENCODE_THREADS // len(texts))
+        pieces, owner = [], []
+        for ti, t in enumerate(texts):
+            n = min(per, len(t) // 2048) if len(t) >= self.SPLIT_MIN_CHARS else 1
+            ps = self._pieces(t, n) if n > 1 else [t]
+            pieces.extend(ps)
+            owner.extend([ti] * len(ps))
+        enc = self.impl.encode_batch(pieces, False, ENCODE_THREADS, -1)
+        out = [list(self._special_prefix) if add_special_tokens else [] for _ in texts]
+        for ti, x in zip(owner, enc):
+            out[ti].extend(x)
+        return out
 
     def encode(self, text, add_special_tokens=True, max_length=None):
         if max_length is None and len(text) >= self.SPLIT_MIN_CHARS and self._split_ok():
@@ -149,7 +170,11 @@ class Tokenizer:
             encs = self.impl.encode_batch(list(texts), add_special_tokens=add_special_tokens)
             out = [e.ids for e in encs]
         elif hasattr(self.impl, "encode_batch"):  # C++ worker threads, GIL released
-            out = self.impl.encode_batch(list(texts), add_special_tokens, ENCODE_THREADS,
+            texts = list(texts)
+            if (max_length is None and len(texts) < ENCODE_THREADS and self._split_ok()
+                    and any(len(t) >= self.SPLIT_MIN_CHARS for t in texts)):
+                return self._encode_batch_split(texts, add_special_tokens)
+            out = self.impl.encode_batch(texts, add_special_tokens, ENCODE_THREADS,
                                          -1 if max_length is None else int(max_length))
         else:
             out = [self.impl.encode(t, add_special_tokens) for t in texts]

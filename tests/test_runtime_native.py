@@ -99,6 +99,11 @@ def test_bpe_llama3_split_regex_with_specials(rt, corpus, tmp_path):
         for sp in (True, False):
             assert ft.encode(t, add_special_tokens=sp) == tok.encode(t, add_special_tokens=sp).ids, (t[:40], sp)
     assert ft._split_ok()
+    # encode_batch of fewer texts than workers (C=1) cuts the long ones the same way, short ones mixed in
+    for batch in ([longs[1]], longs[:3], [longs[0], "short text", longs[4]]):
+        for sp in (True, False):
+            want = [e.ids for e in tok.encode_batch(batch, add_special_tokens=sp)]
+            assert [list(x) for x in ft.encode_batch(batch, add_special_tokens=sp)] == want, (len(batch), sp)
 
 
 def test_encode_batch_concurrent_callers(rt, corpus, tmp_path):
