@@ -32,7 +32,7 @@ PP_MIN_M = int(os.environ.get("RAGK_PP_MIN_M", "1024"))
 PP_VARIANT = int(os.environ.get("RAGK_PP_VARIANT", "2"))
 # large-M kernel: "w4" (default) = 4-wave 128x128-per-wave (gemm_w4.hip, path 6), "pp" = 8-wave
 # ping-pong (path 2). Library GEMMs (hipBLASLt) are never dispatched from here: they are the
-# yardstick of tools/gemm_probe.py / tools/blaslt_choice.py only.
+# yardstick of tools/gemm_probe.py (torch.mm) only.
 PREFILL_GEMM = os.environ.get("RAGK_PREFILL_GEMM", "w4")
 _pp_variant_set = [None]
 
