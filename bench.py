@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--model", default="8b", choices=["8b", "70b", "tiny"])
     ap.add_argument("--embedder", default="minilm", choices=["minilm", "bge-large", "bge-m3", "tiny"])
     ap.add_argument("--chunks", type=int, default=10000)
+    ap.add_argument("--chunk-words", type=int, default=1000, help="words per corpus chunk (reference chunker: 1000)")
     ap.add_argument("--retrieve-k", type=int, default=4)
     ap.add_argument("--context-k", type=int, default=4)
     ap.add_argument("--max-new-tokens", type=int, default=150)
@@ -60,6 +61,11 @@ def parse():
                     help="TP prefill with Megatron sequence parallelism (reduce-scatter/all-gather)")
     ap.add_argument("--c1", type=int, default=5,
                     help="after the timed steps: this many single queries one at a time (C=1 latency; untimed)")
+    ap.add_argument("--c1-tp", type=int, default=3,
+                    help="N > 1 data-parallel runs: after the headline, this many C=1 queries on ONE TP=N engine "
+                         "spanning every GPU (untimed; p50_latency_c1_tp_ms, the xGMI latency path); 0 = skip")
+    ap.add_argument("--c1-tp-timeout", type=float, default=float(os.environ.get("RAGK_BENCH_TP_TIMEOUT", "420")),
+                    help="seconds the TP=N C=1 phase may take before the headline line is printed without it")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -72,6 +78,44 @@ def pct(xs, p):
     f = int(k)
     c = min(f + 1, len(xs) - 1)
     return xs[f] + (xs[c] - xs[f]) * (k - f)
+
+
+def tp_c1_phase(a, ctx, params):
+    """C=1 latency of one TP=N engine over all N GPUs of the job (BASELINE config 3's layout), run after
+    the data-parallel headline in the same process group: a TP group of every rank, the peer-mapped
+    collectives over xGMI (fences on across devices), the same synthetic workload shape. Untimed for
+    `value`; returns (p50 ms, ttft p50 ms, samples)."""
+    import dataclasses
+
+    import torch
+    import torch.distributed as dist
+
+    from rag_llm_k8s_amd.parallel.comm import TPComm
+    from rag_llm_k8s_amd.utils.workload import build_workload, make_queries
+
+    ranks = list(range(ctx.world))
+    grp = dist.new_group(ranks)
+    cgrp = dist.new_group(ranks, backend="gloo")
+    tctx = dataclasses.replace(ctx, tp=ctx.world, tp_rank=ctx.rank, dp=1, dp_rank=0, tp_group=grp,
+                               tp_cpu_group=cgrp, dp_group=None)
+    comm = TPComm(grp, tctx.tp, tctx.tp_rank, ctx.device, cgrp)
+    wl = build_workload(model=a.model, embedder=a.embedder, n_chunks=a.chunks, chunk_words=a.chunk_words,
+                        retrieve_k=a.retrieve_k, context_k=a.context_k, max_new_tokens=a.max_new_tokens, max_batch=4,
+                        device=ctx.device,
+                        ctx=tctx, tp_comm=comm, seed=0, use_graphs=not a.no_graphs, index_type=a.index,
+                        dtype=a.dtype)
+    wl.svc.engine.warmup_graphs()
+    lat, ttft = [], []
+    for i in range(a.c1_tp + 1):  # the first query warms the TP path
+        q = make_queries(wl.wm, 1, seed=888000 + i)
+        o = wl.svc.generate_batch(q, params=params, seeds=[5151 + i])[0]
+        if i and "_latency_s" in o:
+            lat.append(o["_latency_s"] * 1e3)
+            ttft.append(o["_ttft_s"] * 1e3)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    return (round(pct(lat, 50), 1) if lat else None, round(pct(ttft, 50), 1) if ttft else None, len(lat),
+            bool(comm.ipc is not None), bool(comm.ipc is not None and comm.ipc.fences))
 
 
 def main():
@@ -89,7 +133,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (a.gpus, world), file=sys.stderr)
-    if a.tp is None or a.dp:
+    if a.dp and a.tp not in (None, 1):
+        raise SystemExit("bench.py: --dp (N data-parallel TP=1 replicas) conflicts with --tp %d" % a.tp)
+    if a.tp is None:
         a.tp = 1
     if a.concurrency is None:
         a.concurrency = 32 * a.tp
@@ -100,8 +146,9 @@ def main():
     dev = ctx.device
     comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, dev, ctx.tp_cpu_group) if ctx.tp > 1 else None
     t_setup = time.time()
-    wl = build_workload(model=a.model, embedder=a.embedder, n_chunks=a.chunks, retrieve_k=a.retrieve_k,
-                        context_k=a.context_k, max_new_tokens=a.max_new_tokens, max_batch=a.concurrency,
+    wl = build_workload(model=a.model, embedder=a.embedder, n_chunks=a.chunks, chunk_words=a.chunk_words,
+                        retrieve_k=a.retrieve_k, context_k=a.context_k, max_new_tokens=a.max_new_tokens,
+                        max_batch=a.concurrency,
                         device=dev, ctx=ctx, tp_comm=comm, seed=0, use_graphs=not a.no_graphs, index_type=a.index,
                         dtype=a.dtype, index_vectors=a.index_vectors)
     svc = wl.svc
@@ -175,8 +222,8 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16" if a.dtype == "bf16" else "fp8-weights (bf16 activations/KV)",
             "data": "synthetic (random-init weights of the named architectures; Zipfian pseudo-English corpus "
-                    "of %d x 1000-word chunks%s; trained 128k BPE + %s tokenizers)" % (
-                        a.chunks, (" + %d embedded 1000-word topical chunks" % (a.index_vectors - a.chunks)
+                    "of %d x %d-word chunks%s; trained 128k BPE + %s tokenizers)" % (
+                        a.chunks, a.chunk_words, (" + %d embedded 1000-word topical chunks" % (a.index_vectors - a.chunks)
                                    if a.index_vectors > a.chunks else ""),
                         "XLM-R SentencePiece Unigram" if a.embedder == "bge-m3" else "WordPiece"),
             "config": {
@@ -202,11 +249,48 @@ def main():
             # ingest throughput of the corpus build (tokenize + batched varlen encoder, one GPU)
             "ingest_embed_chunks_per_s": round(a.chunks / max(1e-9, allstats[0]["setup"].get("embed_s", 0.0)), 1),
         }
-        line = json.dumps(res)
+    else:
+        res = None
+
+    def emit(r):
+        line = json.dumps(r)
         print(line, flush=True)
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
+
+    # TP=N C=1 latency over every GPU of the job (after the headline; never changes `value`). At N = 1
+    # (or when the headline engine already spans the job) the headline's own C=1 is that number.
+    if ctx.tp == ctx.world or a.c1_tp <= 0:
+        if res is not None:
+            res["p50_latency_c1_tp_ms"] = res["p50_latency_c1_ms"] if ctx.tp == ctx.world else None
+            res["c1_tp_degree"] = ctx.tp
+            emit(res)
+        D.shutdown(ctx)
+        return
+    import threading
+
+    done = threading.Event()
+
+    def watchdog():  # a hung cross-device phase must not cost the headline line
+        if not done.wait(a.c1_tp_timeout):
+            if res is not None:
+                res.update(p50_latency_c1_tp_ms=None, c1_tp_degree=ctx.world,
+                           c1_tp_error="timeout after %.0f s" % a.c1_tp_timeout)
+                emit(res)
+            os._exit(0)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        p50, tt, n, ipc, fences = tp_c1_phase(a, ctx, params)
+        tp_res = dict(p50_latency_c1_tp_ms=p50, ttft_c1_tp_p50_ms=tt, c1_tp_degree=ctx.world, c1_tp_queries=n,
+                      c1_tp_peer_mapped=ipc, c1_tp_fences=fences)
+    except Exception as e:  # recorded, not fatal: the headline stands on its own
+        tp_res = dict(p50_latency_c1_tp_ms=None, c1_tp_degree=ctx.world, c1_tp_error="%s: %s" % (type(e).__name__, e))
+    done.set()
+    if res is not None:
+        res.update(tp_res)
+        emit(res)
     D.shutdown(ctx)
 
 

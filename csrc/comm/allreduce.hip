@@ -186,16 +186,21 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPeers P, int ra
 }
 
 // Barrier of block `row` with block `row` of every peer over the fused-row flags.
+// One shared flag per barrier of a kernel (`which`): the two-shot kernel calls this twice, and a wave
+// still reading the first barrier's result must never see the second call's reset.
 __device__ bool row_barrier(const ArPeers& P, int rank, int world, int which, int row, unsigned ep) {
-  __shared__ int s_ok;
+  __shared__ int s_oks[2];
+  int& s_ok = s_oks[which & 1];
   if (threadIdx.x == 0) s_ok = 1;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its payload stores are complete
   __syncthreads();
-  // The whole region is uncached (hipDeviceMallocUncached): payload stores are write-through to HBM
-  // and no cache level holds a copy of a peer's bytes, so ordering needs no L2 write-back / invalidate:
-  // every storing wave drains its stores (vmcnt(0)) before the barrier above, then one lane per peer
-  // stores the flag (system-scope atomic). A system-scope release fence here would also write back
-  // every other dirty L2 line (the GEMM slabs just produced) -- microseconds per row barrier.
+  // The whole region is uncached (hipDeviceMallocUncached): payload stores are write-through and no
+  // cache level holds a copy of a peer's bytes. With every peer on THIS device that is enough: every
+  // storing wave drains its stores (vmcnt(0)) before the barrier above, then one lane per peer stores
+  // the flag (system-scope atomic). Peers on other GPUs read over xGMI, where that ordering is not
+  // established by one memory controller, so the host turns the system-scope release / acquire fences
+  // on whenever any peer region lives on another device (ragk_ar_set_fences; parallel/ipc_allreduce.py
+  // decides from the ranks' device ids). Measured cost on one GPU: +0.6 % of a TP=8-shard decode step.
   if (threadIdx.x < world) {
     if (P.fences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     ArRowFlags* pf = reinterpret_cast<ArRowFlags*>(P.base[threadIdx.x] + P.rows_off);
@@ -482,6 +487,17 @@ RAGK_API int ragk_ar_set_spin_limit(void* hp, unsigned limit_us) {
   h->peers.spin_limit = limit;
   return 0;
 }
+
+// System-scope release/acquire fences around the fused row barriers: 1 on, 0 off. Required when any
+// peer region is on another device (xGMI); optional for same-device probes.
+RAGK_API int ragk_ar_set_fences(void* hp, int on) {
+  ArHandle* h = (ArHandle*)hp;
+  if (!h) return (int)hipErrorInvalidValue;
+  h->peers.fences = on ? 1 : 0;
+  return 0;
+}
+
+RAGK_API int ragk_ar_get_fences(void* hp) { return hp ? ((ArHandle*)hp)->peers.fences : -1; }
 
 // Host address of the pinned error word (0 = healthy): readable at any time without a device sync.
 RAGK_API void* ragk_ar_error_host_ptr(void* hp) { return ((ArHandle*)hp)->host_err; }

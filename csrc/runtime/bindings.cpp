@@ -24,6 +24,11 @@ static py::dtype np_dtype(const std::string& dt) {
 
 PYBIND11_MODULE(_ragk_rt, m) {
   m.doc() = "rag_llm_k8s_amd native host runtime (safetensors mmap, faiss I/O, KV blocks, tokenizers)";
+#ifndef RAGK_RT_STAMP
+#define RAGK_RT_STAMP "unstamped"
+#endif
+  // content hash of csrc/runtime at build time (_build.runtime_source_hash), checked at import
+  m.def("build_stamp", []() { return std::string(RAGK_RT_STAMP); });
 
   py::class_<SafeTensors, std::shared_ptr<SafeTensors>>(m, "SafeTensors")
       .def(py::init<const std::string&>())

@@ -117,32 +117,59 @@ def runtime_ext_path():
     return os.path.join(LIB_DIR, "_ragk_rt" + suffix)
 
 
+RT_FLAGS = ["-O2", "-fPIC", "-std=c++17", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"]
+
+
+def runtime_sources():
+    rdir = os.path.join(ROOT, "csrc", "runtime")
+    return sorted(glob.glob(os.path.join(rdir, "*.cpp"))), sorted(glob.glob(os.path.join(rdir, "*.h")))
+
+
+def runtime_source_hash():
+    """Content hash of the host-runtime sources + flags, compiled into _ragk_rt (build_stamp()) and
+    checked by runtime.native_rt() at import: a stale runtime (tokenizer, block manager) never loads
+    silently -- the same contract as libragk_hip.so's stamp."""
+    srcs, headers = runtime_sources()
+    h = hashlib.sha256()
+    h.update(repr(RT_FLAGS).encode())
+    for f in srcs + headers:
+        h.update(os.path.relpath(f, ROOT).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()[:32]
+
+
 def build_runtime(verbose=False):
     import pybind11
 
     os.makedirs(LIB_DIR, exist_ok=True)
     rdir = os.path.join(ROOT, "csrc", "runtime")
-    srcs = sorted(glob.glob(os.path.join(rdir, "*.cpp")))
+    srcs, headers = runtime_sources()
     if not srcs:
         return None
-    headers = glob.glob(os.path.join(rdir, "*.h"))
     target = runtime_ext_path()
     os.makedirs(OBJ_DIR, exist_ok=True)
     inc = ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"], "-I" + rdir]
-    flags = ["-O2", "-fPIC", "-std=c++17", "-fvisibility=hidden", "-Wall", "-Wno-unused-function"]
+    stamp = runtime_source_hash()
+    stamp_txt = os.path.join(OBJ_DIR, "rt_stamp.txt")
+    prev = open(stamp_txt).read().strip() if os.path.exists(stamp_txt) else None
+    flags = RT_FLAGS + ['-DRAGK_RT_STAMP="%s"' % stamp]
     objs, todo = [], []
     for s in srcs:
         o = os.path.join(OBJ_DIR, "rt_" + os.path.basename(s) + ".o")
         objs.append(o)
-        if _newer([s] + headers, o):
+        if prev != stamp or _newer([s] + headers, o):
             todo.append((s, o))
     with cf.ThreadPoolExecutor(min(8, os.cpu_count() or 4)) as ex:
         for f in [ex.submit(_run, ["g++"] + flags + inc + ["-c", s, "-o", o]) for s, o in todo]:
             out = f.result()
             if verbose and out.strip():
                 print(out)
-    if todo or _newer(objs, target):
+    if todo or prev != stamp or _newer(objs, target):
         _run(["g++", "-shared", "-fPIC"] + objs + ["-o", target])
+        with open(stamp_txt, "w") as f:
+            f.write(stamp + "\n")
     return target
 
 

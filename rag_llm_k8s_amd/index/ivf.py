@@ -63,11 +63,40 @@ def probes(x: torch.Tensor, c: torch.Tensor, cnorm, nprobe):
     """The nprobe nearest centroids of every row, ranked by the numbers assign() ranks (top-1 ==
     assign), ties -> lower id. int64 [n, nprobe] on x's device."""
     nprobe = min(nprobe, c.shape[0])
-    if _native_assign_ok(x) and c.shape[0] <= 24576 and nprobe <= 256:
+    if _native_assign_ok(x):
         from ..ops import native
 
-        return native.coarse_probes(x.contiguous(), c.float().contiguous(), cnorm, nprobe).long()
+        cf = c.float().contiguous()
+        if c.shape[0] <= 24576 and nprobe <= 256:
+            return native.coarse_probes(x.contiguous(), cf, cnorm, nprobe).long()
+        # past the top-k kernel's limits: the assignment kernel's own scores -(||c||^2 - 2 x.c), sorted
+        # (descending = nearest first, stable -> ties to the lower id), in row chunks of <= 64 MB
+        xc = x.contiguous()
+        out = torch.empty((x.shape[0], nprobe), dtype=torch.long, device=x.device)
+        step = max(1, (16 << 20) // c.shape[0])
+        for i in range(0, x.shape[0], step):
+            xs = xc[i:i + step]
+            sc = torch.empty((xs.shape[0], c.shape[0]), dtype=torch.float32, device=x.device)
+            native.kmeans_assign(xs, cf, cnorm, scores=sc)
+            out[i:i + step] = torch.sort(sc, dim=1, descending=True, stable=True)[1][:, :nprobe]
+        return out
     return torch.sort(_scores_torch(x, c), dim=1, stable=True)[1][:, :nprobe]
+
+
+def _assign_train(x: torch.Tensor, c: torch.Tensor):
+    """k-means training assignment: the MFMA kernel on the GPU; elsewhere one GEMM per row chunk
+    (argmin of ||c||^2 - 2 x.c). Training needs no row independence, only speed -- the elementwise
+    form of _scores_torch is for search-time probing, where a row's ranking must not depend on
+    the batch it arrives in."""
+    if _native_assign_ok(x):
+        return assign(x, c)
+    xf, cf = x.float(), c.float()
+    cn = (cf * cf).sum(1)
+    out = torch.empty(xf.shape[0], dtype=torch.long, device=xf.device)
+    step = max(1, (1 << 24) // max(1, cf.shape[0]))
+    for i in range(0, xf.shape[0], step):
+        out[i:i + step] = torch.addmm(cn[None, :], xf[i:i + step], cf.t(), alpha=-2.0).argmin(1)
+    return out
 
 
 def kmeans(x: torch.Tensor, k: int, iters: int = 20, seed: int = 0,
@@ -83,7 +112,7 @@ def kmeans(x: torch.Tensor, k: int, iters: int = 20, seed: int = 0,
         n = x.shape[0]
     c = x[torch.randperm(n, generator=g)[:k].to(x.device)].clone()
     for _ in range(iters):
-        a = assign(x, c)
+        a = _assign_train(x, c)
         s = torch.zeros_like(c).index_add_(0, a, x)
         cnt = torch.bincount(a, minlength=k).float()
         empty = cnt == 0

@@ -195,21 +195,34 @@ class DocumentStore:
                 self._persister.start()
 
     def _persist_loop(self):
-        while True:
-            with self._wlock:
-                if not self._dirty:
-                    # deregister while still holding the lock: an add() after this point sees
-                    # _persister None and starts a new writer (no lost wake-up)
-                    self._persister = None
-                    return
-                self._dirty = False
-                writer, meta = self._snapshot()  # host copy under the lock (consistent vectors + metadata)
-                self._writing += 1
-            try:
-                self._write(writer, meta)  # file I/O outside the lock: searches and appends continue
-            except Exception as e:  # keep serving from HBM; the next append retries the snapshot
-                self._persist_error = e
-                log.error("index snapshot failed: %s", e)
+        clean = False
+        try:
+            while True:
+                with self._wlock:
+                    if not self._dirty:
+                        # deregister while still holding the lock: an add() after this point sees
+                        # _persister None and starts a new writer (no lost wake-up)
+                        self._persister = None
+                        clean = True
+                        return
+                    # host copy under the lock (consistent vectors + metadata); a failure here (e.g. the
+                    # device copy after a GPU fault) leaves _dirty set, so the next append retries
+                    writer, meta = self._snapshot()
+                    self._dirty = False
+                    self._writing += 1
+                try:
+                    self._write(writer, meta)  # file I/O outside the lock: searches and appends continue
+                except Exception as e:  # keep serving from HBM; the next append retries the snapshot
+                    self._persist_error = e
+                    log.error("index snapshot failed: %s", e)
+        except Exception as e:
+            self._persist_error = e
+            log.error("index snapshot thread failed: %s", e)
+        finally:
+            if not clean:  # any abnormal exit deregisters too: the next persist_async starts a new writer
+                with self._wlock:
+                    if self._persister is threading.current_thread():
+                        self._persister = None
 
     def flush(self):
         """Wait until every scheduled snapshot is on disk."""

@@ -101,6 +101,8 @@ _SIGS = {
     "ragk_ar_error_host_ptr": [P],
     "ragk_ar_allgather": [P, P, P, ctypes.c_long, S],
     "ragk_ar_destroy": [P],
+    "ragk_ar_set_fences": [P, I],
+    "ragk_ar_get_fences": [P],
 }
 _RESTYPES = {"ragk_ar_create": ctypes.c_void_p, "ragk_ar_error_host_ptr": ctypes.c_void_p, "ragk_ar_max_bytes": ctypes.c_long, "ragk_ar_destroy": None}
 

@@ -631,7 +631,10 @@ def prefill_qtile(Hq, Hkv):
     if not torch.cuda.is_available():  # CPU engine: tiles are unused by the torch backend
         G = Hq // Hkv
         GB = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
-        return 32 * ((8 if GB == 4 and PREFILL_PP in (1, 2, 10) else 4) // GB)
+        # the library's predicate (attention.hip ragk_attn_prefill_qtile): 64-query tiles for the
+        # ping-pong / v3 modes 1..5 and >= 10, else the configured waves per block
+        pp64 = 1 <= PREFILL_PP <= 5 or PREFILL_PP >= 10
+        return 32 * ((8 if pp64 else PREFILL_WAVES) // GB if GB == 4 else 4 // GB)
     if _prefill_waves_set[0] is None:
         set_prefill_waves(PREFILL_WAVES)
     return _lib.lib().ragk_attn_prefill_qtile(Hq, Hkv)

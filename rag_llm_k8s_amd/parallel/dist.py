@@ -30,6 +30,7 @@ class DistCtx:
     tp_cpu_group: Optional[object] = None
     dp_group: Optional[object] = None
     initialized: bool = False
+    device_ids: Optional[list] = None  # device_identity() of every rank (multi-GPU jobs)
 
     @property
     def is_first(self):
@@ -57,6 +58,11 @@ def init_distributed(tp: int = 1, backend: Optional[str] = None, timeout_s: int 
         ctx.initialized = True
     if world % tp:
         raise ValueError("WORLD_SIZE %d not divisible by tp %d" % (world, tp))
+    if world > 1 and use_cuda:
+        idents = [None] * world
+        dist.all_gather_object(idents, device_identity(ctx.device))
+        ctx.device_ids = idents
+        check_distinct_devices(idents, allow_shared=os.environ.get("RAGK_ALLOW_SHARED_DEVICE", "0") == "1")
     ctx.dp = world // tp
     ctx.tp_rank = rank % tp
     ctx.dp_rank = rank // tp
@@ -73,6 +79,51 @@ def init_distributed(tp: int = 1, backend: Optional[str] = None, timeout_s: int 
             if rank in ranks:
                 ctx.dp_group = grp
     return ctx
+
+
+def device_identity(device) -> str:
+    """A string naming the PHYSICAL GPU behind `device` (stable across processes on one host): PCI
+    domain/bus/device, else the device uuid, else host + ordinal. CPU devices: host + "cpu"."""
+    import socket
+
+    host = socket.gethostname()
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return "%s/cpu" % host
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    try:
+        p = torch.cuda.get_device_properties(idx)
+        pci = (getattr(p, "pci_domain_id", None), getattr(p, "pci_bus_id", None), getattr(p, "pci_device_id", None))
+        if all(v is not None for v in pci) and any(pci):
+            return "%s/pci:%04x:%02x:%02x" % (host, *pci)
+        uuid = str(getattr(p, "uuid", "") or "")
+        if uuid:
+            return "%s/uuid:%s" % (host, uuid)
+    except Exception:
+        pass
+    return "%s/cuda:%d" % (host, idx)
+
+
+def shared_device_ranks(idents):
+    """Groups of ranks whose identities (device_identity) name the same physical GPU: [[r, r', ...], ...]
+    (empty when every rank has its own device)."""
+    by = {}
+    for r, d in enumerate(idents):
+        by.setdefault(d, []).append(r)
+    return [rs for rs in by.values() if len(rs) > 1]
+
+
+def check_distinct_devices(idents, allow_shared=False):
+    """Self-test of a multi-GPU job: every rank must drive its own GPU. N processes on one device run
+    (the single-GPU TP rehearsals do exactly that), but a job that CLAIMS N GPUs while two ranks share
+    one would report single-device numbers as multi-GPU ones, and its peer-mapped collectives would
+    skip the cross-device fences. Raises unless allow_shared (RAGK_ALLOW_SHARED_DEVICE=1)."""
+    shared = [rs for rs in shared_device_ranks(idents) if not str(idents[rs[0]]).endswith("/cpu")]
+    if shared and not allow_shared:
+        raise RuntimeError("ranks %s share a GPU (%s) while the job claims one GPU per rank; set "
+                           "RAGK_ALLOW_SHARED_DEVICE=1 for a deliberate single-device rehearsal"
+                           % (shared, ", ".join(sorted({idents[rs[0]] for rs in shared}))))
+    return shared
 
 
 def barrier(ctx: DistCtx):

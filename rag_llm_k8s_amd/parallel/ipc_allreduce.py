@@ -34,6 +34,20 @@ FUSED_H = int(os.environ.get("RAGK_AR_FUSED_H", "8192"))
 FUSED_ONESHOT_BYTES = int(os.environ.get("RAGK_AR_FUSED_ONESHOT_BYTES", str(512 << 10)))
 
 
+def fences_for(cross_device: bool, env=None) -> bool:
+    """Fence policy of the fused row barriers. Peers on other GPUs (xGMI): always on -- the uncached
+    staging region orders payload before flag only within one device's memory controller. All peers
+    on this device (single-GPU rehearsals / probes): RAGK_AR_FENCES=1 turns them on, default off."""
+    env = os.environ.get("RAGK_AR_FENCES", "") if env is None else env
+    if cross_device:
+        if env == "0":
+            import logging
+
+            logging.getLogger(__name__).warning("RAGK_AR_FENCES=0 ignored: peer regions live on other GPUs")
+        return True
+    return env == "1"
+
+
 class IPCAllReduce:
     def __init__(self, group, cpu_group, size, rank, device, max_bytes=MAX_BYTES, blocks=BLOCKS, spin_limit=None,
                  fused_rows=FUSED_ROWS, fused_h=FUSED_H):
@@ -61,10 +75,17 @@ class IPCAllReduce:
         hs = L.ragk_ar_handle_size()
         buf = ctypes.create_string_buffer(hs)
         check(L.ragk_ar_ipc_handle(self.h, buf), "hipIpcGetMemHandle")
-        handles = [bytes(buf.raw)]
+        from .dist import device_identity
+
+        me = (bytes(buf.raw), device_identity(self.device))
+        recs = [me]
         if size > 1:  # a one-rank communicator (single-GPU probes) has no peers to map
-            handles = [None] * size
-            dist.all_gather_object(handles, bytes(buf.raw), group=cpu_group)
+            recs = [None] * size
+            dist.all_gather_object(recs, me, group=cpu_group)
+        handles = [r[0] for r in recs]
+        self.peer_devices = [r[1] for r in recs]
+        self.cross_device = any(d != me[1] for d in self.peer_devices)
+        self.set_fences(fences_for(self.cross_device))
         joined = ctypes.create_string_buffer(b"".join(handles), hs * size)
         with torch.cuda.device(self.device):
             check(L.ragk_ar_open_peers(self.h, joined), "hipIpcOpenMemHandle")
@@ -86,6 +107,14 @@ class IPCAllReduce:
         ok &= bool(torch.equal(got, torch.cat([torch.arange(64, dtype=torch.int32) + 1000 * r
                                                for r in range(self.size)])))
         return ok
+
+    def set_fences(self, on: bool):
+        """System-scope release/acquire fences around the fused row barriers (allreduce.hip row_barrier)."""
+        check(self.L.ragk_ar_set_fences(self.h, int(bool(on))), "ragk_ar_set_fences")
+
+    @property
+    def fences(self) -> bool:
+        return self.L.ragk_ar_get_fences(self.h) == 1
 
     def set_timeout_us(self, us: int):
         """Bound of one peer wait inside the kernels (a rank's first launch of a kernel can lag its

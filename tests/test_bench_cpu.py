@@ -1,0 +1,47 @@
+"""bench.py contract on the CPU (gloo) rehearsal: one JSON line from rank 0 with the driver's keys, and
+for N > 1 data-parallel runs the TP=N C=1 latency appended after the headline (tiny model)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench(n, *extra):
+    args = ["--gpus", str(n), "--model", "tiny", "--embedder", "tiny", "--chunks", "48", "--chunk-words", "60",
+            "--concurrency", "2", "--max-new-tokens", "3", "--steps", "1", "--warmup", "0", "--c1", "1"] + list(extra)
+    if n == 1:
+        cmd = [sys.executable, "bench.py"] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py"] + args
+    env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_appends_tp_c1():
+    res = _bench(2, "--c1-tp", "1")
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in res
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2" and res["value"] > 0
+    assert res["c1_tp_degree"] == 2 and res["p50_latency_c1_tp_ms"] > 0, res
+    assert "c1_tp_error" not in res
+
+
+def test_bench_one_rank_tp_line_is_the_headline_c1():
+    res = _bench(1)
+    assert res["c1_tp_degree"] == 1 and res["p50_latency_c1_tp_ms"] == res["p50_latency_c1_ms"]

@@ -29,3 +29,24 @@ def test_library_stamp_matches_tree_and_stale_is_refused(monkeypatch):
     monkeypatch.setenv("RAGK_ALLOW_STALE_LIB", "1")
     _lib._check_stamp(h)
     assert os.path.exists(os.path.join(_build.OBJ_DIR, "ragk_stamp.txt"))
+
+
+def test_runtime_hash_is_content_based(monkeypatch):
+    h = _build.runtime_source_hash()
+    assert len(h) == 32 and h == _build.runtime_source_hash()
+    monkeypatch.setattr(_build, "RT_FLAGS", _build.RT_FLAGS + ["-DX"])
+    assert _build.runtime_source_hash() != h
+
+
+@pytest.mark.skipif(not os.path.exists(_build.runtime_ext_path()), reason="runtime not built")
+def test_runtime_stamp_matches_tree_and_stale_is_refused(monkeypatch):
+    from rag_llm_k8s_amd import runtime
+
+    mod = runtime.native_rt()
+    assert mod is not None and mod.build_stamp() == _build.runtime_source_hash()
+    monkeypatch.delenv("RAGK_ALLOW_STALE_LIB", raising=False)
+    monkeypatch.setattr(_build, "runtime_source_hash", lambda: "0" * 32)
+    with pytest.raises(runtime.StaleRuntimeError, match="other runtime sources"):
+        runtime.check_rt_stamp(mod)
+    monkeypatch.setenv("RAGK_ALLOW_STALE_LIB", "1")
+    runtime.check_rt_stamp(mod)
