@@ -1,6 +1,6 @@
-"""Tensor parallelism on the GPU, as far as one MI355X allows: two ranks on cuda:0.
+"""Tensor parallelism on the GPU, as far as one MI355X allows: 2, 4 and 8 ranks on cuda:0.
 
-Both ranks run the real TP code path -- Megatron-sharded Llama weights at Llama-3.1-8B widths
+Every rank runs the real TP code path -- Megatron-sharded Llama weights at Llama-3.1-8B widths
 (hidden 4096, 32/8 heads, FFN 14336, 128,256-token vocabulary; 2 layers), the peer-mapped
 all-reduce / all-gather kernels (csrc/comm/allreduce.hip, hipIpc handles exchanged over gloo),
 the vocab-parallel sampler with its candidate all-gather, graph-captured and asynchronous decode --
@@ -21,7 +21,14 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
-WORLD = 2
+WORLD = 2  # the fault test; the engine test is parametrized over 2 / 4 / 8 ranks
+
+
+def _log(rank, world, msg):
+    """Progress on stderr (inherited from pytest): a long 8-rank run is never silent for minutes."""
+    import sys
+
+    print("[tp%d r%d %.0fs] %s" % (world, rank, time.monotonic() % 100000, msg), file=sys.stderr, flush=True)
 
 
 def _free_port():
@@ -117,16 +124,18 @@ def _prefill_decode_logits(model, ids, nxt):
     return model.forward(inp)
 
 
-def _init(rank, port):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD),
-                      LOCAL_RANK="0", RAGK_TP_CONTROL="gloo")
+def _init(rank, port, world=WORLD):
+    # every rank on cuda:0 on purpose: the distinctness self-test must be told so
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", RAGK_TP_CONTROL="gloo", RAGK_ALLOW_SHARED_DEVICE="1")
     from rag_llm_k8s_amd.parallel.dist import init_distributed
 
-    return init_distributed(tp=WORLD, backend="gloo")
+    return init_distributed(tp=world, backend="gloo")
 
 
-def _tp_worker(rank, port, d):
-    ctx = _init(rank, port)
+def _tp_worker(rank, port, d, world):
+    WORLD = world
+    ctx = _init(rank, port, world)
     from rag_llm_k8s_amd.engine.llm_engine import LLMEngine, SamplingParams
     from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights
     from rag_llm_k8s_amd.parallel.comm import TPComm
@@ -138,6 +147,7 @@ def _tp_worker(rank, port, d):
         sd = _state_dict(cfg)
         comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, ctx.device, ctx.tp_cpu_group, ipc_max_bytes=16 << 20)
         res["ipc"] = comm.ipc is not None
+        _log(rank, world, "comm up (peer-mapped: %s)" % res["ipc"])
         w = LlamaWeights.from_state_dict(cfg, sd, ctx.device, ctx.tp_rank, ctx.tp)
         m = LlamaModel(cfg, w, ctx.device, comm=comm, max_positions=4096)
         gen = torch.Generator().manual_seed(7)
@@ -148,6 +158,7 @@ def _tp_worker(rank, port, d):
         local = _prefill_decode_logits(m, ids, 77)  # decode: fused row-parallel reduction
         full = comm.ipc.all_gather(local.contiguous()).view(WORLD, 1, -1)
         res["tp_dec_logits"] = torch.cat([full[r] for r in range(WORLD)], 1)[:, :cfg.vocab_size].cpu()
+        _log(rank, world, "prefill + decode logits")
         if rank == 0:
             ref = LlamaModel(cfg, LlamaWeights.from_state_dict(cfg, sd, ctx.device), ctx.device, max_positions=4096)
             res["ref_logits"] = _prefill_logits(ref, ids).cpu()
@@ -171,6 +182,7 @@ def _tp_worker(rank, port, d):
             res[("sampled", graphs)] = eng.generate(prompts, sampled, seeds=[11, 12, 13])
             res[("greedy", graphs)] = eng.generate(prompts, greedy)
             res[("async", graphs)] = eng.async_decode
+            _log(rank, world, "engine graphs=%s" % graphs)
             del eng
             torch.cuda.empty_cache()
         res["error"] = comm.ipc.error()
@@ -183,11 +195,12 @@ def _tp_worker(rank, port, d):
         dist.destroy_process_group()
 
 
-def _spawn(target, timeout=600):
+def _spawn(target, timeout=600, world=WORLD):
     port = _free_port()
     d = tempfile.mkdtemp()
     ctx = mp.get_context("spawn")
-    procs = [ctx.Process(target=target, args=(r, port, d)) for r in range(WORLD)]
+    extra = (world,) if target is _tp_worker else ()
+    procs = [ctx.Process(target=target, args=(r, port, d) + extra) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -197,24 +210,32 @@ def _spawn(target, timeout=600):
             p.kill()
             p.join()
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    return [torch.load(os.path.join(d, "r%d.pt" % r), weights_only=False) for r in range(WORLD)]
+    return [torch.load(os.path.join(d, "r%d.pt" % r), weights_only=False) for r in range(world)]
 
 
-def test_tp2_llama8b_widths_on_one_gpu(native):
-    out = _spawn(_tp_worker)
-    assert out[0]["ipc"] and out[1]["ipc"], "peer-mapped collectives must pass their self-test"
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tp_llama8b_widths_on_one_gpu(native, world):
+    """TP=2/4/8 shards of Llama-3.1-8B widths (TP=8: 4 query heads, 1 KV head, 1792 FFN rows, a 16k-row
+    vocab shard per rank), 2 layers, every rank a process on cuda:0: prefill logits and fused-decode
+    logits vs TP=1, graph + async decode == eager, the same samples on every rank, and the micro-batched
+    overlap prefill (the 1100-token prompt)."""
+    WORLD = world
+    out = _spawn(_tp_worker, world=world)
+    assert all(o["ipc"] for o in out), "peer-mapped collectives must pass their self-test"
     ref = out[0]["ref_logits"]
     for r in range(WORLD):
         got = out[r]["tp_logits"]
         rel = ((got - ref).norm() / ref.norm()).item()
         assert rel < 2e-2, (r, rel)
         assert out[r]["error"] is False
-    assert torch.equal(out[0]["tp_logits"], out[1]["tp_logits"])
+    for r in range(1, WORLD):
+        assert torch.equal(out[0]["tp_logits"], out[r]["tp_logits"])
     dref = out[0]["ref_dec_logits"]
     for r in range(WORLD):
         rel = ((out[r]["tp_dec_logits"] - dref).norm() / dref.norm()).item()
         assert rel < 2e-2, ("decode", r, rel)
-    assert torch.equal(out[0]["tp_dec_logits"], out[1]["tp_dec_logits"])
+    for r in range(1, WORLD):
+        assert torch.equal(out[0]["tp_dec_logits"], out[r]["tp_dec_logits"])
     for r in range(WORLD):
         assert out[r][("async", True)] is True
         for kind in ("sampled", "greedy"):
@@ -222,7 +243,8 @@ def test_tp2_llama8b_widths_on_one_gpu(native):
             assert [len(x) for x in g] == [12, 12, 12]
             assert g == e, (r, kind, g, e)  # graph-captured async TP decode == eager synchronous
     for kind in ("sampled", "greedy"):
-        assert out[0][(kind, True)] == out[1][(kind, True)]  # every rank sampled the same tokens
+        for r in range(1, WORLD):
+            assert out[0][(kind, True)] == out[r][(kind, True)]  # every rank sampled the same tokens
 
 
 def _fault_worker(rank, port, d):
