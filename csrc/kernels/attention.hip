@@ -1202,6 +1202,7 @@ struct DecodeArgs {
   const float* qkv_p; long long p_slab; int ldp, S;
   const int* positions; const int* slots;
   const float* cos_t; const float* sin_t;
+  int nb;                                  // batch (0: gridDim.z, the 3-D launch)
 };
 
 // Tiles per partition of one sequence: its KV tiles spread evenly over all max_parts partitions
@@ -1213,24 +1214,41 @@ __device__ __forceinline__ int decode_part_tiles(int n_kt, const DecodeArgs& a) 
   return max(a.part_tiles, (n_kt + a.max_parts - 1) / a.max_parts);
 }
 
-template <int D, int G, bool NT = false>
-__global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArgs pf) {
+// LDS of one decode-attention block: one V tile per wave, then the block's rotated q (G x D bf16).
+template <int D, int G>
+constexpr int decode_lds_bytes() { return 4 * Cfg<D>::TILEB + G * D * 2; }
+
+// Signal of a decode-attention block inside the fused attention + o_proj launch (attn_oproj_kernel):
+// every storing wave has drained its write-through (sc1) stores, then one lane adds to the agent-scope
+// counter the o_proj blocks poll (MI355X_MICROARCH.md "Valid forms": sc1 stores, vmcnt(0), barrier,
+// agent atomic; the consumer polls with sc1 loads and reads the bytes with sc1 loads only).
+__device__ __forceinline__ void decode_signal(int* cnt) {
+  wait_vmcnt0();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One split-K partition block of decode attention: partition `part` of KV head `kvh` of sequence `b`.
+// FUSED (attn_oproj_kernel): the partition record is written write-through even for a single-partition
+// sequence (the o_proj blocks merge records only), there is no merge here, and the block signals
+// `fused_cnt` when its records are out -- also when it has no tiles (the counter counts every block).
+template <int D, int G, bool NT = false, bool FUSED = false>
+__device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part, int kvh, int b, char* smem,
+                                                  int* fused_cnt = nullptr) {
   using C = Cfg<D>;
   static_assert(G <= 16, "at most 16 query heads per KV head");
-  __shared__ __attribute__((aligned(16))) char smem[4 * C::TILEB];  // one V tile per wave
-  if ((int)blockIdx.x >= a.max_parts) {  // MALL prefetch rider (block-uniform): x beyond the partitions
-    const int ex = gridDim.x - a.max_parts;
-    pf_rider(pf, (blockIdx.x - a.max_parts) + ex * (blockIdx.y + gridDim.y * blockIdx.z), ex * gridDim.y * gridDim.z);
-    return;
-  }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
-  const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int kv_len = a.kv_lens[b];
   const int n_kt = (kv_len + KT - 1) / KT;
   const int pt = decode_part_tiles(n_kt, a);
   const int kt0 = part * pt;
-  if (kt0 >= n_kt) return;  // block-uniform early exit (before any barrier)
+  if (kt0 >= n_kt) {  // block-uniform early exit (before any barrier)
+    if constexpr (FUSED) {
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(fused_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   const int kt1 = min(kt0 + pt, n_kt);
   const int nparts = (n_kt + pt - 1) / pt;
   const int fr = lane & 15, fh = lane >> 4;
@@ -1262,7 +1280,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
     // pair of 8-vectors per thread (G * D/16 threads, all slab loads of a thread in flight together),
     // staged through LDS; in the block owning the last KV tile, other threads append the new
     // token's k (rotated) and v meanwhile. One barrier covers both.
-    __shared__ __attribute__((aligned(16))) bf16_t s_q[G * D];
+    bf16_t* s_q = reinterpret_cast<bf16_t*>(smem + 4 * C::TILEB);
     constexpr int NV = D / 16;  // pairs per head
     const int pos = a.positions[b];
     const float* prow = a.qkv_p + (size_t)b * a.ldp;
@@ -1386,7 +1404,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
   }
 
   // partition-statistics buffers as write-through (sc1) buffer resources for the fused merge
-  const unsigned pbytes = (unsigned)((size_t)gridDim.z * a.Hq * a.max_parts * 4);
+  const unsigned pbytes = (unsigned)((size_t)(a.nb ? a.nb : (int)gridDim.z) * a.Hq * a.max_parts * 4);
   const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(a.part_o, (short)0, (int)(pbytes * D), 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_ml = __builtin_amdgcn_make_buffer_rsrc(a.part_ml, (short)0, (int)(pbytes * 2), 0x00020000);
 
@@ -1417,11 +1435,11 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
       O += so[(w * 16 + g) * D + d] * sc;
     }
     const int hq = kvh * G + g;
-    if (nparts == 1) {
+    if (nparts == 1 && !FUSED) {
       a.out[(size_t)b * a.out_stride + hq * D + d] = f2bf(L > 0.f ? O / L : 0.f);
     } else {
       const size_t pi = ((size_t)b * a.Hq + hq) * a.max_parts + part;
-      if (a.counters) {  // fused merge: write-through (sc1) stores, read back by another CU below
+      if (FUSED || a.counters) {  // write-through (sc1) stores, read back by another CU
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(O), rs_o, (int)((pi * D + d) * 4), 0, 16);
         if (d == 0) {
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(M), rs_ml, (int)(pi * 8), 0, 16);
@@ -1435,6 +1453,10 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
         }
       }
     }
+  }
+  if constexpr (FUSED) {
+    decode_signal(fused_cnt);
+    return;
   }
   if (nparts == 1 || a.counters == nullptr) return;
 
@@ -1497,6 +1519,206 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArg
     a.out[(size_t)b * a.out_stride + (kvh * G + g) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
   }
   if (threadIdx.x == 0) __hip_atomic_store(a.counters + b * a.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int D, int G, bool NT = false>
+__global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArgs pf) {
+  __shared__ __attribute__((aligned(16))) char smem[decode_lds_bytes<D, G>()];
+  if ((int)blockIdx.x >= a.max_parts) {  // MALL prefetch rider (block-uniform): x beyond the partitions
+    const int ex = gridDim.x - a.max_parts;
+    pf_rider(pf, (blockIdx.x - a.max_parts) + ex * (blockIdx.y + gridDim.y * blockIdx.z), ex * gridDim.y * gridDim.z);
+    return;
+  }
+  attn_decode_block<D, G, NT>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+}
+
+// ------------------------------------------------------------------------------------
+// Fused decode attention + o_proj (batch <= 4): one launch instead of attention -> o_proj.
+// ------------------------------------------------------------------------------------
+// Blocks [0, na) are attention partition blocks (attn_decode_block<FUSED>); blocks [na, na + nob) are
+// o_proj split-K blocks. An o_proj block issues its whole weight slice (64 output columns x KS, straight
+// to VGPRs, non-temporal) as soon as it is dispatched -- while the attention blocks still stream the KV
+// cache -- then polls the attention-done counter, merges the split-K partitions of the heads of its
+// K-slice into an LDS activation slice and runs the MFMAs; its fp32 partial slab goes to the
+// add_partials_rmsnorm consumer as gemm_part_merge's does. The o_proj weight stream (33.5 MB per layer
+// at 8B) overlaps the attention instead of following it. Deadlock-free by construction: only o_proj
+// blocks wait, and only on attention blocks, which have lower indices (dispatched first) and never
+// wait; the wait is bounded anyway (error word, never a hang). Counters: cnt[0] attention blocks done,
+// cnt[1] o_proj blocks past their wait (the last one re-arms both for the next layer / replay),
+// cnt[2] error.
+struct OprojArgs {
+  const bf16_t* W; int ldw;  // o_proj weight [N][K] bf16
+  float* P;                  // [K / KS][M][N] fp32 partial slabs
+  int M, N, K;
+  int na, nob;               // attention blocks, o_proj blocks
+  int* cnt;
+  unsigned spin_limit;       // s_memrealtime ticks (100 MHz)
+};
+constexpr int OP_MAXP = 64;  // partitions per (row, head) merged in LDS
+
+template <int D, int NLD>
+__device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const OprojArgs& o, int ob, char* smem) {
+  constexpr int KS = 32 * NLD;          // K-slice (NLD 32-k MFMA steps, one 16-B load each per lane)
+  constexpr int ROWB = KS * 2;          // bytes per row of the LDS activation slice
+  constexpr int HPB = KS / D;           // attention heads in the slice
+  static_assert(KS % D == 0, "slice = whole heads");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fh = lane >> 4;
+  const int ncb = (o.N + 63) / 64;
+  const int cb = ob % ncb, s = ob / ncb;
+  const int n0 = cb * 64, kbase = s * KS, h0 = kbase / D;
+  const int M = o.M;
+
+  // 1) the weight slice, all loads in flight before anything else (wave w: columns n0 + 16w + fr)
+  const int wrow = min(n0 + 16 * wid + fr, o.N - 1);
+  const bf16_t* wp = o.W + (size_t)wrow * o.ldw + kbase + 8 * fh;
+  bf16x8 wf[NLD];
+#pragma unroll
+  for (int ks = 0; ks < NLD; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
+
+  // 2) wait for every attention block (one lane polls with sc1 loads; the others wait at the barrier)
+  if (tid == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(o.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < o.na) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > o.spin_limit) {  // never hang: flag it, compute garbage
+        __hip_atomic_store(o.cnt + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+
+  // 3) merge the partitions of (row r, head h0 + j): pass 1 the statistics -> per-partition scales and
+  //    the merged sum in LDS, pass 2 the partial outputs (all loads of a thread in flight: the scales are
+  //    known, so there is no running rescale chain). Records are read write-through (sc1), as written.
+  const unsigned pbytes = (unsigned)((size_t)M * a.Hq * a.max_parts * 4);
+  const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(a.part_o, (short)0, (int)(pbytes * D), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_ml = __builtin_amdgcn_make_buffer_rsrc(a.part_ml, (short)0, (int)(pbytes * 2), 0x00020000);
+  float* s_sc = reinterpret_cast<float*>(smem + 16 * ROWB);  // [M][HPB][OP_MAXP] max, then scale
+  float* s_l = s_sc + 4 * HPB * OP_MAXP;                      // [M][HPB][OP_MAXP] partition sums
+  float* s_il = s_l + 4 * HPB * OP_MAXP;                      // [M][HPB] 1 / merged sum (0 if empty)
+  int* s_np = reinterpret_cast<int*>(s_il + 4 * HPB);         // [M] partitions of row r
+  if (tid < M) {
+    const int n_kt = (a.kv_lens[tid] + KT - 1) / KT;
+    const int pt = decode_part_tiles(n_kt, a);
+    s_np[tid] = (n_kt + pt - 1) / pt;
+  }
+  __syncthreads();
+  const int MP = a.max_parts;
+  for (int e = tid; e < M * HPB * MP; e += 256) {
+    const int p = e % MP, j = (e / MP) % HPB, r = e / (MP * HPB);
+    float m = -INFINITY, l = 0.f;
+    if (p < s_np[r]) {
+      const int pi = ((r * a.Hq + h0 + j) * MP + p) * 8;
+      m = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ml, pi, 0, 16));
+      l = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ml, pi + 4, 0, 16));
+    }
+    s_sc[(r * HPB + j) * OP_MAXP + p] = m;
+    s_l[(r * HPB + j) * OP_MAXP + p] = l;
+  }
+  __syncthreads();
+  if (tid < M * HPB) {
+    float* sc = s_sc + tid * OP_MAXP;
+    const float* sl = s_l + tid * OP_MAXP;
+    float mx = -INFINITY;
+    for (int p = 0; p < MP; ++p) mx = fmaxf(mx, sc[p]);
+    const float mu = mx == -INFINITY ? 0.f : mx;
+    float L = 0.f;
+    for (int p = 0; p < MP; ++p) {
+      const float f = sc[p] == -INFINITY ? 0.f : exp2f(sc[p] - mu);
+      sc[p] = f;
+      L += sl[p] * f;
+    }
+    s_il[tid] = L > 0.f ? 1.f / L : 0.f;
+  }
+  __syncthreads();
+  // pass 2: task = (row r, head j, 4 dims d4); npg adjacent lanes split a task's partitions
+  const int ntask = M * HPB * (D / 4);
+  int npg = 1;
+  while (npg < 8 && ntask * npg * 2 <= 256) npg *= 2;
+  for (int t0 = 0; t0 < ntask * npg; t0 += 256) {
+    const int tt = t0 + tid;
+    const bool act = tt < ntask * npg;
+    const int task = (act ? tt : 0) / npg, pg = tt % npg;
+    const int d4 = task % (D / 4), j = (task / (D / 4)) % HPB, r = task / ((D / 4) * HPB);
+    const int np = s_np[r];
+    const float* sc = s_sc + (r * HPB + j) * OP_MAXP;
+    const int base = ((r * a.Hq + h0 + j) * MP) * D * 4 + d4 * 16;
+    f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
+    for (int p0 = pg; p0 < np; p0 += 8 * npg) {  // 8 records per thread in flight
+      u32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int p = min(p0 + i * npg, np - 1);
+        v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_o, base + p * D * 4, 0, 16));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float f = p0 + i * npg < np ? sc[p0 + i * npg] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc4[e] += __uint_as_float(v[i][e]) * f;
+      }
+    }
+    for (int off = 1; off < npg; off <<= 1)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc4[e] += __shfl_xor(acc4[e], off, 64);
+    if (act && pg == 0) {
+      const float il = s_il[r * HPB + j];
+      uint2 w;
+      w.x = pk2bf(acc4[0] * il, acc4[1] * il);
+      w.y = pk2bf(acc4[2] * il, acc4[3] * il);
+      const int cc = j * (D / 8) + d4 / 2;  // 16-B chunk of the slice row; 8-B half d4 & 1
+      const int c = (cc & ~15) | ((cc & 15) ^ (r & 15));
+      *reinterpret_cast<uint2*>(smem + r * ROWB + 16 * c + 8 * (d4 & 1)) = w;
+    }
+  }
+  __syncthreads();
+
+  // 4) MFMA over the slice: A = activation rows (fr), B = this wave's weight columns
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NLD; ++ks) {
+    const int chunk = 4 * ks + fh;
+    const bf16x8 xf = *reinterpret_cast<const bf16x8*>(smem + fr * ROWB + 16 * ((chunk & ~15) | ((chunk & 15) ^ (fr & 15))));
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[ks], acc, 0, 0, 0);
+  }
+  const int col = n0 + 16 * wid + fr;
+  if (fh == 0 && col < o.N) {
+    float* ps = o.P + (size_t)s * M * o.N;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r < M) ps[(size_t)r * o.N + col] = acc[r];
+  }
+  // 5) re-arm: the last o_proj block past its wait resets both counters (every attention block is done
+  //    and every o_proj block has read cnt[0] by then; the next launch is stream-ordered after this one)
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(o.cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == o.nob - 1) {
+      __hip_atomic_store(o.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o.cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <int D, int G, int NLD>
+constexpr int attn_oproj_lds() {
+  constexpr int a = decode_lds_bytes<D, G>();
+  constexpr int o = 16 * 64 * NLD + (2 * 4 * (32 * NLD / D) * OP_MAXP + 4 * (32 * NLD / D) + 4) * 4;
+  return a > o ? a : o;
+}
+
+template <int D, int G, int NLD>
+__global__ __launch_bounds__(256, 2) void attn_oproj_kernel(DecodeArgs a, OprojArgs o) {
+  __shared__ __attribute__((aligned(16))) char smem[attn_oproj_lds<D, G, NLD>()];
+  const int bid = blockIdx.x;
+  if (bid < o.na) {
+    const int mp = a.max_parts;
+    attn_decode_block<D, G, false, true>(a, bid % mp, (bid / mp) % a.Hkv, bid / (mp * a.Hkv), smem, o.cnt);
+    return;
+  }
+  oproj_merge_block<D, NLD>(a, o, bid - o.na, smem);
 }
 
 // merge split-K partitions: grid (Hq, B), block D threads. The partition statistics are loaded by
@@ -1787,5 +2009,45 @@ static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* co
   RAGK_DC(64, 4)
   RAGK_DC(128, 2)
 #undef RAGK_DC
+  return (int)hipErrorInvalidValue;
+}
+
+// Fused decode attention (RoPE + KV append from the qkv split-K slabs, as ragk_attn_decode_rope) and
+// o_proj split-K partials (as ragk_gemm_part_merge) in ONE launch: attn_oproj_kernel. B <= 4, D = 128,
+// G in {4, 8}; Wo bf16 [N][Hq * D] (ldw elements); Pout fp32 [K / KS][B][N], KS = 64 * ks_steps
+// (ks_steps 4 or 8). cnt: >= 3 zeroed ints owned by the caller (re-armed by the kernel itself).
+// part_o / part_ml: the partition workspace (required, also for one partition).
+RAGK_API int ragk_attn_oproj_fused(const float* P, int S, int ldp, const int* positions, const int* slots,
+                                   const float* cos_t, const float* sin_t, void* kc, void* vc,
+                                   const int* block_tables, int bt_stride, const int* kv_lens, float* part_o,
+                                   float* part_ml, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
+                                   float scale, const void* Wo, int ldw, float* Pout, int N, int ks_steps, int* cnt,
+                                   unsigned spin_us, hipStream_t st) {
+  if (B <= 0) return 0;
+  const int G = Hq / (Hkv > 0 ? Hkv : 1);
+  const int K = Hq * D;
+  const int KS = 64 * ks_steps;
+  if (B > 4 || D != 128 || Hq % Hkv || (G != 4 && G != 8) || (ks_steps != 4 && ks_steps != 8) || K % KS ||
+      part_tiles < 1 || max_parts < 1 || max_parts > OP_MAXP || S < 1 || ldp < (Hq + 2 * Hkv) * D || !P ||
+      !positions || !slots || !cos_t || !sin_t || !part_o || !part_ml || !Wo || !Pout || !cnt || N <= 0 ||
+      ldw < K)
+    return (int)hipErrorInvalidValue;
+  DecodeArgs a{nullptr, 0, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, bt_stride, kv_lens,
+               part_o, part_ml, nullptr, 0, Hq, Hkv, part_tiles, max_parts,
+               scale * 1.4426950408889634f, nullptr, P, (long long)B * ldp, ldp, S, positions, slots, cos_t, sin_t, B};
+  const unsigned long long ticks = (unsigned long long)(spin_us ? spin_us : 1000000u) * 100ull;
+  OprojArgs o{(const bf16_t*)Wo, ldw, Pout, B, N, K, max_parts * Hkv * B, ((N + 63) / 64) * (K / KS), cnt,
+              (unsigned)(ticks > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : ticks)};
+  const dim3 grid(o.na + o.nob);
+#define RAGK_AO(GG, NL)                                                                       \
+  if (G == GG && 2 * ks_steps == NL) {                                                        \
+    hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL>), grid, dim3(256), 0, st, a, o);       \
+    return (int)hipGetLastError();                                                            \
+  }
+  RAGK_AO(4, 8)
+  RAGK_AO(4, 16)
+  RAGK_AO(8, 8)
+  RAGK_AO(8, 16)
+#undef RAGK_AO
   return (int)hipErrorInvalidValue;
 }

@@ -376,13 +376,19 @@ class LlamaModel:
         xn = None if fuse_norm else be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
         merge = (DECODE_OPROJ_MERGE and DECODE_ROPE_FUSED and not pf and M <= DECODE_OPROJ_MERGE_MAX_M
                  and be.part_merge_ok(M, inp.meta, layers[0]["wo"], Hq, D))
+        # batch <= 4: attention and o_proj in ONE launch (attention.hip attn_oproj_kernel) -- the o_proj
+        # weight stream overlaps the KV stream instead of following it
+        fused_ao = (DECODE_ROPE_FUSED and not pf and be.attn_oproj_ok(M, inp.meta, layers[0]["wo"], Hq, Hkv, D))
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
             if fuse_norm:
                 P = be.gemm_part_norm(h, L["ln_in"], c.rms_norm_eps, L["wqkv"])
             else:
                 P = be.gemm_part(xn, L["wqkv"])
-            if merge:
+            if fused_ao:
+                P = be.attn_oproj(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, L["wo"], Hq, Hkv,
+                                  D)
+            elif merge:
                 # RoPE + KV append inside the attention kernel, its split-K merge inside the o_proj GEMM
                 be.attn_decode_rope(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, attn,
                                     Hq, Hkv, D, defer_merge=True)
@@ -398,7 +404,8 @@ class LlamaModel:
                     be.pf_arm([(L["wo"], pf["rope"], pf["attn"] // 2), (L["wgu"], 0, pf["attn"] // 2)],
                               pf["blocks"])
                 be.attn_decode(q, kc, vc, inp.meta, attn, Hq, Hkv, D)
-            P = be.gemm_part_merge(attn, inp.meta, L["wo"], Hq) if merge else be.gemm_part(attn, L["wo"])
+            if not fused_ao:
+                P = be.gemm_part_merge(attn, inp.meta, L["wo"], Hq) if merge else be.gemm_part(attn, L["wo"])
             if pf:
                 be.pf_arm([(L["wgu"], pf["attn"] // 2, pf["post"])], pf["blocks"])
             xn = reduce_norm(P, L["ln_post"])

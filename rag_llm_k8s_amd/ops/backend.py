@@ -172,6 +172,9 @@ class TorchBackend:
     def part_merge_ok(self, M, meta: AttnMeta, w, Hq, D):
         return False
 
+    def attn_oproj_ok(self, M, meta: AttnMeta, w, Hq, Hkv, D):
+        return False
+
     def prefill_nsplit(self, M, w):
         return 1
 
@@ -312,6 +315,13 @@ class NativeBackend(TorchBackend):
     def part_merge_ok(self, M, meta: AttnMeta, w, Hq, D):
         return (self.enable_part and D == 128 and not self.n.ATTN_FUSED_MERGE
                 and self.n.gemm_part_merge_ok(M, w, Hq, meta.max_parts, meta.ws_o))
+
+    def attn_oproj_ok(self, M, meta: AttnMeta, w, Hq, Hkv, D):
+        return self.enable_part and self.n.attn_oproj_ok(M, w, Hq, Hkv, D, meta.max_parts, meta.ws_o)
+
+    def attn_oproj(self, P, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, w, Hq, Hkv, D):
+        return self.n.attn_oproj(P, positions, cos_t, sin_t, slots, kc, vc, meta.block_tables, meta.kv_lens, Hq, Hkv,
+                                 D, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml, w)
 
     def gemm_part_merge(self, attn_out, meta: AttnMeta, w, Hq):
         return self.n.gemm_part_merge(attn_out, meta.kv_lens, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml,

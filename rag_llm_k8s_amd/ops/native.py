@@ -331,6 +331,68 @@ def gemm_part_merge(attn_out, kv_lens, part_tiles, max_parts, ws_o, ws_ml, Hq, w
     return out
 
 
+# Fused decode attention + o_proj (attention.hip attn_oproj_kernel): one launch in place of
+# attn_decode_rope(defer_merge) -> gemm_part_merge at batch <= 4. RAGK_DECODE_ATTN_OPROJ=0 disables.
+ATTN_OPROJ = os.environ.get("RAGK_DECODE_ATTN_OPROJ", "1") == "1"
+ATTN_OPROJ_KS = int(os.environ.get("RAGK_ATTN_OPROJ_KS", "8"))  # K-slice steps of 64 (4 or 8)
+ATTN_OPROJ_SPIN_US = int(os.environ.get("RAGK_ATTN_OPROJ_SPIN_US", "1000000"))
+_ao_cnt = {}
+
+
+def attn_oproj_ok(M, w, Hq, Hkv, D, max_parts, ws_o):
+    """The fused launch's shape limits: batch <= 4, head dim 128, 4 or 8 query heads per KV head, bf16
+    o_proj weight whose K = Hq * 128 splits into whole 64 * ks slices, <= 64 partitions."""
+    from .fp8 import Fp8Weight
+
+    if not ATTN_OPROJ or isinstance(w, Fp8Weight) or ws_o is None or not (1 <= M <= 4) or D != 128:
+        return False
+    if Hq % Hkv or Hq // Hkv not in (4, 8) or max_parts > 64:
+        return False
+    N, K = w.shape
+    return w.dtype == torch.bfloat16 and K == Hq * D and K % (64 * ATTN_OPROJ_KS) == 0
+
+
+def attn_oproj_counters(device):
+    """The fused launch's counters (attention done, o_proj past its wait, error): zeroed once, re-armed
+    by the kernel itself after every launch (graph replays included)."""
+    key = str(device)
+    if key not in _ao_cnt:
+        _ao_cnt[key] = torch.zeros(16, dtype=torch.int32, device=device)
+    return _ao_cnt[key]
+
+
+def attn_oproj_error(device) -> bool:
+    c = _ao_cnt.get(str(device))
+    return bool(c is not None and int(c[2].item()) != 0)
+
+
+def attn_oproj(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_tables, kv_lens, Hq, Hkv, D, part_tiles,
+               max_parts, ws_o, ws_ml, w, out=None, scale=None):
+    """o_proj split-K partials Po [K / KS, M, N] of the decode attention of the qkv partial slabs P [S, M, ldp]
+    (RoPE + KV append at `slots`, as attn_decode_rope), in ONE launch (attention.hip attn_oproj_kernel): the
+    o_proj blocks stream their weights while the attention blocks stream the KV cache, then merge the
+    partitions of their K-slice and multiply. Same consumer as gemm_part_merge (add_partials_rmsnorm)."""
+    _req(P.dtype == torch.float32 and P.is_contiguous() and P.dim() == 3, "partials")
+    S, B, ldp = P.shape
+    N, K = w.shape
+    _req(attn_oproj_ok(B, w, Hq, Hkv, D, max_parts, ws_o), "fused attention + o_proj shape")
+    _req(kv_lens.numel() == B and positions.numel() == B and slots.numel() == B, "one row per sequence")
+    _req(k_cache.dim() == 4 and k_cache.shape[1] == Hkv and k_cache.shape[2] == 64 and k_cache.shape[3] == D,
+         "paged cache")
+    _req(ws_o.numel() >= B * Hq * max_parts * D and ws_ml.numel() >= B * Hq * max_parts * 2, "partition workspace")
+    ks = ATTN_OPROJ_KS
+    if out is None:
+        out = torch.empty((K // (64 * ks), B, N), dtype=torch.float32, device=P.device)
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    cnt = attn_oproj_counters(P.device)
+    check(_lib.lib().ragk_attn_oproj_fused(
+        P.data_ptr(), S, ldp, positions.data_ptr(), slots.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(),
+        k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0), kv_lens.data_ptr(),
+        ws_o.data_ptr(), ws_ml.data_ptr(), B, Hq, Hkv, D, part_tiles, max_parts, float(scale), w.data_ptr(),
+        w.stride(0), out.data_ptr(), N, ks, cnt.data_ptr(), ATTN_OPROJ_SPIN_US, stream_ptr()), "ragk_attn_oproj_fused")
+    return out
+
+
 SILU_MAX_SLABS = 4  # gemm_part.hip SG_MAXS
 
 

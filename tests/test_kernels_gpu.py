@@ -585,6 +585,58 @@ def test_gemm_part_merge_matches_reduce_then_part(native, kv_lens, target, fp8, 
     assert rel_err(out.cpu(), oracle.cpu()) < 2e-3, rel_err(out.cpu(), oracle.cpu())
 
 
+@pytest.mark.parametrize("kv_lens,target,Hq,Hkv,ks", [([5200], 512, 32, 8, 8), ([70, 3000], 256, 32, 8, 8),
+                                                       ([5200, 64], 256, 32, 8, 4), ([1], 512, 32, 8, 8),
+                                                       ([777, 5300, 65, 2000], 512, 32, 8, 8), ([8100], 512, 32, 8, 4),
+                                                       ([5200], 1024, 4, 1, 4), ([5200, 70], 1024, 8, 1, 8),
+                                                       ([64, 128, 8000], 128, 64, 8, 8)])
+def test_attn_oproj_fused_matches_unfused(native, kv_lens, target, Hq, Hkv, ks):
+    """attention + o_proj in one launch (attn_oproj_kernel: o_proj blocks stream their weights while the
+    attention blocks run, then merge the partitions of their K-slice) == attn_decode_rope followed by
+    gemm_part on the merged output, up to fp32 summation order; same KV-cache contents bit for bit; vs
+    an fp32 oracle. Three launches in a row check that the kernel re-arms its counters. Covers one token,
+    one / many partitions, mixed lengths, M = 1..4, the TP=8 per-rank heads (4 / 1, 8 / 1) and 70B's 64 / 8."""
+    D, S = 128, 8
+    torch.manual_seed(31)
+    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=9)
+    B = len(kv_lens)
+    kc, vc, bt = kc.to(DEV), vc.to(DEV), bt.to(DEV)
+    kvl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    pos = kvl - 1
+    slots = (bt[torch.arange(B, device=DEV), (pos // 64).long()] * 64 + pos % 64).int()
+    P = torch.randn(S, B, (Hq + 2 * Hkv) * D, device=DEV)
+    cos, sin = R.rope_tables(D, 131072, theta=500000.0)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv, target_blocks=target)
+    w = (torch.randn(4096, Hq * D, device=DEV) / math.sqrt(Hq * D)).bfloat16()
+    ws_o = torch.empty((B, Hq, max(mp, 1), D), dtype=torch.float32, device=DEV)
+    ws_ml = torch.empty((B, Hq, max(mp, 1), 2), dtype=torch.float32, device=DEV)
+    old = native.ATTN_OPROJ_KS
+    native.ATTN_OPROJ_KS = ks
+    try:
+        assert native.attn_oproj_ok(B, w, Hq, Hkv, D, mp, ws_o)
+        kc2, vc2 = kc.clone(), vc.clone()
+        ref_attn = torch.empty(B, Hq * D, device=DEV).bfloat16()
+        native.attn_decode_rope(P, pos, cos, sin, slots, kc2, vc2, bt, kvl, ref_attn, Hq, Hkv, D, pt, mp)
+        ref = native.gemm_part(ref_attn, w).sum(0)
+        outs = []
+        for it in range(3):
+            kc3, vc3 = kc.clone(), vc.clone()
+            o = native.attn_oproj(P, pos, cos, sin, slots, kc3, vc3, bt, kvl, Hq, Hkv, D, pt, mp, ws_o, ws_ml, w)
+            assert o.shape == (Hq * D // (64 * ks), B, 4096)
+            outs.append(o.sum(0))
+        torch.cuda.synchronize()
+        assert not native.attn_oproj_error(DEV)
+        assert int(native.attn_oproj_counters(DEV)[:2].abs().sum().item()) == 0  # re-armed
+    finally:
+        native.ATTN_OPROJ_KS = old
+    assert torch.equal(kc3, kc2) and torch.equal(vc3, vc2)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])  # deterministic
+    oracle = ref_attn.float() @ w.float().t()
+    assert rel_err(ref.cpu(), oracle.cpu()) < 1e-4
+    assert rel_err(outs[0].cpu(), oracle.cpu()) < 2e-3, rel_err(outs[0].cpu(), oracle.cpu())
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (3, 6144, 4096), (4, 1280, 8192), (2, 10240, 8192)])
 def test_gemm_part_norm_matches_rmsnorm_then_part(native, M, N, K):
     """gemm_part_norm (RMSNorm applied while staging the activation slice) == rmsnorm_kernel followed
