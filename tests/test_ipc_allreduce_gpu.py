@@ -7,6 +7,7 @@ handle exchanged over gloo -- only the xGMI hop is replaced by local HBM. Oracle
 ranks' inputs in rank order, rounded once (what the kernels compute).
 """
 import os
+import sys
 import socket
 import tempfile
 
@@ -137,7 +138,7 @@ def test_ipc_allreduce_ranks(native, WORLD):
 
 
 # ---------------------------------------------------------------- fused decode reduction
-H_F = 4096
+H_F = int(os.environ.get("RAGK_TEST_FUSED_H", "4096"))  # set per case by the test before spawning
 FUSED_CASES = [(1, 1), (3, 2), (32, 1), (5, 4), (1, 3), (17, 1)]  # (M rows, S slabs): varying grids
 
 
@@ -153,7 +154,8 @@ def _fused_worker(rank, port, d, WORLD):
     from rag_llm_k8s_amd.parallel.ipc_allreduce import IPCAllReduce
 
     ar = IPCAllReduce(None, None, WORLD, rank, "cuda:0", max_bytes=1 << 20, blocks=16, fused_rows=64, fused_h=H_F)
-    res = {}
+    ar.set_fences(os.environ.get("RAGK_TEST_FENCES", "0") == "1")  # the cross-device (xGMI) setting
+    res = {"fences": ar.fences}
     g = torch.Generator().manual_seed(5)
     w = (1 + 0.1 * torch.randn(H_F, generator=g)).bfloat16().cuda()
     try:
@@ -194,16 +196,24 @@ def _fused_worker(rank, port, d, WORLD):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("WORLD", [2, 4, 8])
-def test_fused_allreduce_add_rmsnorm(native, WORLD):
+@pytest.mark.parametrize("WORLD,H,fences", [(2, 4096, 0), (4, 4096, 0), (8, 4096, 0), (8, 8192, 0), (4, 8192, 1),
+                                             (8, 4096, 1)])
+def test_fused_allreduce_add_rmsnorm(native, WORLD, H, fences, monkeypatch):
     """h <- bf16(h + bf16(sum over ranks (rank order) of sum over slabs (slab order) of P)), out = rmsnorm(h):
     the residual stream is exact vs an fp32 oracle, identical on every rank (bit for bit) in both the
-    one-shot and the two-shot mode, for varying row counts, and inside a replayed graph."""
+    one-shot and the two-shot mode, for varying row counts, and inside a replayed graph. H = 8192 is the
+    70B hidden size; fences = 1 runs the system-scope release / acquire barriers that peers on other GPUs
+    get by default (parallel/ipc_allreduce.fences_for)."""
     from rag_llm_k8s_amd.ops import reference as R
 
+    global H_F
+    monkeypatch.setenv("RAGK_TEST_FUSED_H", str(H))
+    monkeypatch.setenv("RAGK_TEST_FENCES", str(fences))
+    monkeypatch.setattr(sys.modules[__name__], "H_F", H)
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
         out = _spawn(_fused_worker, WORLD, d, port)
+    assert all(out[r]["fences"] == bool(fences) for r in range(WORLD))
     w = (1 + 0.1 * torch.randn(H_F, generator=torch.Generator().manual_seed(5))).bfloat16()
 
     def ref(M, S, it, h0):

@@ -7,6 +7,12 @@ all-gather. Reports ms per step (graph replay and in-situ) and, under rocprofv3 
 --stats, launches per step.
 
   python tools/tp_decode_probe.py 1 32        # batch sizes;  TPP_TP=8 TPP_PROMPT=5200 TPP_STEPS=48
+  TPP_MODEL=70b TPP_PREFILL=32768 python tools/tp_decode_probe.py 1 32   # + one 32k-token prefill step
+
+TPP_PREFILL=T: after the decode probes, one prefill step of T tokens (prompts of TPP_PROMPT tokens) is
+timed on the shard. Its bulk row-parallel all-reduces exceed the peer-mapped size limit and go to RCCL
+in a real TP group; here they are skipped (one GPU cannot host an RCCL peer), so the number is the
+shard's compute, and the xGMI time of the step is the bytes printed divided by the link rate.
 """
 import os
 import sys
@@ -66,6 +72,28 @@ def main():
         print("B=%d graph replay only: %.3f ms/step" % (B, (time.perf_counter() - t0) / 20 * 1e3), flush=True)
         del eng
         torch.cuda.empty_cache()
+    T = int(os.environ.get("TPP_PREFILL", "0"))
+    if T:
+        n = -(-T // plen)
+        eng = LLMEngine(m, num_blocks=n * (-(-plen // 64)) + 16, max_batch=max(n, 1), max_prefill_tokens=T,
+                        max_model_len=8192, eos_ids=cfg.eos_token_id, use_graphs=False)
+        gen = torch.Generator().manual_seed(99)
+        p = SamplingParams(max_new_tokens=2, temperature=0.7, top_p=0.9, top_k=50, ignore_eos=True)
+        for rep in range(2):  # the first step warms the kernels
+            for i in range(n):
+                eng.add_request(torch.randint(3, cfg.vocab_size, (min(plen, T - i * plen),), generator=gen).tolist(),
+                                p, seed=i)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            eng.step()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            eng.run_until_done()
+        H = cfg.hidden_size
+        ar_bytes = 2 * cfg.num_hidden_layers * T * H * 2
+        print("prefill step of %d tokens (%d prompts): %.1f ms compute on the shard (%.1f TFLOP/s); a real TP=%d "
+              "step all-reduces %.1f GB of bf16 rows (2 per layer)" % (
+                  T, n, dt * 1e3, 2 * T * w.nbytes() / 2 / dt / 1e12, tp, ar_bytes / 1e9), flush=True)
 
 
 if __name__ == "__main__":
