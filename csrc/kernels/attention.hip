@@ -1553,6 +1553,12 @@ struct OprojArgs {
   int na, nob;               // attention blocks, o_proj blocks
   int* cnt;
   unsigned spin_limit;       // s_memrealtime ticks (100 MHz)
+  // optional residual + RMSNorm tail (add_partials_rmsnorm's math, done by the last o_proj block):
+  // h[M][ldh] += bf16(sum of the slabs) (bf16), xn[M][ldx] = rmsnorm(h) * gamma. h == nullptr: none.
+  bf16_t* h; int ldh;
+  const bf16_t* gamma;
+  bf16_t* xn; int ldx;
+  float eps;
 };
 constexpr int OP_MAXP = 64;  // partitions per (row, head) merged in LDS
 
@@ -1685,20 +1691,100 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[ks], acc, 0, 0, 0);
   }
   const int col = n0 + 16 * wid + fr;
+  const int nslab = o.K / KS;
+  const __amdgpu_buffer_rsrc_t rs_p =
+      __builtin_amdgcn_make_buffer_rsrc(o.P, (short)0, (int)((size_t)nslab * M * o.N * 4), 0x00020000);
   if (fh == 0 && col < o.N) {
-    float* ps = o.P + (size_t)s * M * o.N;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (r < M) ps[(size_t)r * o.N + col] = acc[r];
+    for (int r = 0; r < 4; ++r) {
+      if (r < M) {
+        const int off = (int)((((size_t)s * M + r) * o.N + col) * 4);
+        if (o.h)  // read back by the last block below: write-through
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[r]), rs_p, off, 0, 16);
+        else
+          o.P[off / 4] = acc[r];
+      }
+    }
   }
-  // 5) re-arm: the last o_proj block past its wait resets both counters (every attention block is done
-  //    and every o_proj block has read cnt[0] by then; the next launch is stream-ordered after this one)
+  // 5) arrival ticket (after this block's slab stores have drained): the last o_proj block re-arms both
+  //    counters -- every attention block is done and every o_proj block has read cnt[0] by then; the next
+  //    launch is stream-ordered after this one -- and, with the norm tail, reduces the slabs.
+  int* s_last = reinterpret_cast<int*>(smem);  // the activation slice is dead
+  wait_vmcnt0();
+  __syncthreads();
   if (tid == 0) {
     const int old = __hip_atomic_fetch_add(o.cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == o.nob - 1) {
+    const int last = old == o.nob - 1;
+    if (last) {
       __hip_atomic_store(o.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(o.cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    *s_last = last;
+  }
+  __syncthreads();
+  if (!o.h || !*s_last) return;
+  // 6) residual + RMSNorm of every row (add_partials_rmsnorm_kernel's math; slab order kept)
+  float* red = reinterpret_cast<float*>(smem) + 16;
+  const int nvec = o.N >> 3;
+  for (int r = 0; r < M; ++r) {
+    float v[2][8];  // this thread's two row vectors (H <= 4096; longer rows are re-read from h below)
+    float ss = 0.f;
+    for (int i0 = 0; i0 < nvec; i0 += 512) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int vi = i0 + tid + 256 * i;
+        if (vi >= nvec) continue;
+        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        u32x4 pv[16][2];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int su = min(u, nslab - 1);
+          const int off = (int)((((size_t)su * M + r) * o.N + vi * 8) * 4);
+          pv[u][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_p, off, 0, 16));
+          pv[u][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_p, off + 16, 0, 16));
+        }
+        const u32x4 hv = *reinterpret_cast<const u32x4*>(o.h + (size_t)r * o.ldh + vi * 8);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          if (u < nslab) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              a[e] += __uint_as_float(pv[u][0][e]);
+              a[4 + e] += __uint_as_float(pv[u][1][e]);
+            }
+          }
+        }
+        float hf[8];
+        unpack8(hv, hf);
+        float* vv = v[i];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vv[e] = bf2f(f2bf(hf[e] + bf2f(f2bf(a[e]))));
+        *reinterpret_cast<u32x4*>(o.h + (size_t)r * o.ldh + vi * 8) = pack8(vv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ss += vv[e] * vv[e];
+      }
+    }
+    ss = block_sum(ss, red);
+    const float inv = rsqrtf(ss / (float)o.N + o.eps);
+    for (int i0 = 0; i0 < nvec; i0 += 512) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int vi = i0 + tid + 256 * i;
+        if (vi >= nvec) continue;
+        float hv8[8], wv[8], out8[8];
+        if (nvec <= 512) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hv8[e] = v[i][e];
+        } else {
+          unpack8(*reinterpret_cast<const u32x4*>(o.h + (size_t)r * o.ldh + vi * 8), hv8);
+        }
+        unpack8(*reinterpret_cast<const u32x4*>(o.gamma + vi * 8), wv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) out8[e] = wv[e] * bf2f(f2bf(hv8[e] * inv));
+        *reinterpret_cast<u32x4*>(o.xn + (size_t)r * o.ldx + vi * 8) = pack8(out8);
+      }
+    }
+    __syncthreads();  // red[] reuse by the next row
   }
 }
 
@@ -2015,29 +2101,37 @@ static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* co
 // Fused decode attention (RoPE + KV append from the qkv split-K slabs, as ragk_attn_decode_rope) and
 // o_proj split-K partials (as ragk_gemm_part_merge) in ONE launch: attn_oproj_kernel. B <= 4, D = 128,
 // G in {4, 8}; Wo bf16 [N][Hq * D] (ldw elements); Pout fp32 [K / KS][B][N], KS = 64 * ks_steps
-// (ks_steps 4 or 8). cnt: >= 3 zeroed ints owned by the caller (re-armed by the kernel itself).
+// (ks_steps 4, 8 or 16). cnt: >= 3 zeroed ints owned by the caller (re-armed by the kernel itself).
+// h != nullptr: the residual + RMSNorm tail (h += bf16(sum of slabs), xn = rmsnorm(h) * gamma; the
+// add_partials_rmsnorm consumer) runs in the last o_proj block.
 // part_o / part_ml: the partition workspace (required, also for one partition).
 RAGK_API int ragk_attn_oproj_fused(const float* P, int S, int ldp, const int* positions, const int* slots,
                                    const float* cos_t, const float* sin_t, void* kc, void* vc,
                                    const int* block_tables, int bt_stride, const int* kv_lens, float* part_o,
                                    float* part_ml, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
                                    float scale, const void* Wo, int ldw, float* Pout, int N, int ks_steps, int* cnt,
-                                   unsigned spin_us, hipStream_t st) {
+                                   unsigned spin_us, void* h, int ldh, const void* gamma, void* xn, int ldx,
+                                   float eps, hipStream_t st) {
   if (B <= 0) return 0;
   const int G = Hq / (Hkv > 0 ? Hkv : 1);
   const int K = Hq * D;
   const int KS = 64 * ks_steps;
-  if (B > 4 || D != 128 || Hq % Hkv || (G != 4 && G != 8) || (ks_steps != 4 && ks_steps != 8) || K % KS ||
+  if (B > 4 || D != 128 || Hq % Hkv || (G != 4 && G != 8) || (ks_steps != 4 && ks_steps != 8 && ks_steps != 16) || K % KS ||
       part_tiles < 1 || max_parts < 1 || max_parts > OP_MAXP || S < 1 || ldp < (Hq + 2 * Hkv) * D || !P ||
       !positions || !slots || !cos_t || !sin_t || !part_o || !part_ml || !Wo || !Pout || !cnt || N <= 0 ||
       ldw < K)
+    return (int)hipErrorInvalidValue;
+  // norm tail: the last o_proj block sums <= 16 slabs per row vector (h, gamma, xn: bf16, 16-B rows)
+  if (h && (!gamma || !xn || K / KS > 16 || N % 8 || ldh % 8 || ldx % 8 || ((uintptr_t)h & 15) ||
+            ((uintptr_t)xn & 15) || ((uintptr_t)gamma & 15)))
     return (int)hipErrorInvalidValue;
   DecodeArgs a{nullptr, 0, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, bt_stride, kv_lens,
                part_o, part_ml, nullptr, 0, Hq, Hkv, part_tiles, max_parts,
                scale * 1.4426950408889634f, nullptr, P, (long long)B * ldp, ldp, S, positions, slots, cos_t, sin_t, B};
   const unsigned long long ticks = (unsigned long long)(spin_us ? spin_us : 1000000u) * 100ull;
   OprojArgs o{(const bf16_t*)Wo, ldw, Pout, B, N, K, max_parts * Hkv * B, ((N + 63) / 64) * (K / KS), cnt,
-              (unsigned)(ticks > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : ticks)};
+              (unsigned)(ticks > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : ticks), (bf16_t*)h, ldh, (const bf16_t*)gamma,
+              (bf16_t*)xn, ldx, eps};
   const dim3 grid(o.na + o.nob);
 #define RAGK_AO(GG, NL)                                                                       \
   if (G == GG && 2 * ks_steps == NL) {                                                        \
@@ -2046,8 +2140,10 @@ RAGK_API int ragk_attn_oproj_fused(const float* P, int S, int ldp, const int* po
   }
   RAGK_AO(4, 8)
   RAGK_AO(4, 16)
+  RAGK_AO(4, 32)
   RAGK_AO(8, 8)
   RAGK_AO(8, 16)
+  RAGK_AO(8, 32)
 #undef RAGK_AO
   return (int)hipErrorInvalidValue;
 }

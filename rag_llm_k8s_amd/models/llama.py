@@ -379,13 +379,18 @@ class LlamaModel:
         # batch <= 4: attention and o_proj in ONE launch (attention.hip attn_oproj_kernel) -- the o_proj
         # weight stream overlaps the KV stream instead of following it
         fused_ao = (DECODE_ROPE_FUSED and not pf and be.attn_oproj_ok(M, inp.meta, layers[0]["wo"], Hq, Hkv, D))
+        # ... and, at TP=1, the residual + post-attention norm in its last block (no consumer launch)
+        ao_norm = fused_ao and not tp and be.attn_oproj_norm_ok(layers[0]["wo"])
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
             if fuse_norm:
                 P = be.gemm_part_norm(h, L["ln_in"], c.rms_norm_eps, L["wqkv"])
             else:
                 P = be.gemm_part(xn, L["wqkv"])
-            if fused_ao:
+            if ao_norm:
+                xn = be.attn_oproj(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, L["wo"], Hq,
+                                   Hkv, D, norm=(h, L["ln_post"], c.rms_norm_eps))
+            elif fused_ao:
                 P = be.attn_oproj(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, L["wo"], Hq, Hkv,
                                   D)
             elif merge:
@@ -408,7 +413,8 @@ class LlamaModel:
                 P = be.gemm_part_merge(attn, inp.meta, L["wo"], Hq) if merge else be.gemm_part(attn, L["wo"])
             if pf:
                 be.pf_arm([(L["wgu"], pf["attn"] // 2, pf["post"])], pf["blocks"])
-            xn = reduce_norm(P, L["ln_post"])
+            if not ao_norm:
+                xn = reduce_norm(P, L["ln_post"])
             nxt = layers[li + 1]["ln_in"] if li + 1 < len(layers) else w.norm
             if silu_fused:
                 P = be.gemm_part_silu(be.gemm_part_gu(xn, L["wgu"]), L["wdown"])

@@ -175,6 +175,9 @@ class TorchBackend:
     def attn_oproj_ok(self, M, meta: AttnMeta, w, Hq, Hkv, D):
         return False
 
+    def attn_oproj_norm_ok(self, w):
+        return False
+
     def prefill_nsplit(self, M, w):
         return 1
 
@@ -319,9 +322,12 @@ class NativeBackend(TorchBackend):
     def attn_oproj_ok(self, M, meta: AttnMeta, w, Hq, Hkv, D):
         return self.enable_part and self.n.attn_oproj_ok(M, w, Hq, Hkv, D, meta.max_parts, meta.ws_o)
 
-    def attn_oproj(self, P, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, w, Hq, Hkv, D):
+    def attn_oproj(self, P, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, w, Hq, Hkv, D, norm=None):
         return self.n.attn_oproj(P, positions, cos_t, sin_t, slots, kc, vc, meta.block_tables, meta.kv_lens, Hq, Hkv,
-                                 D, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml, w)
+                                 D, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml, w, norm=norm)
+
+    def attn_oproj_norm_ok(self, w):
+        return self.n.ATTN_OPROJ_NORM and w.shape[1] // (64 * self.n.ATTN_OPROJ_KS) <= 16
 
     def gemm_part_merge(self, attn_out, meta: AttnMeta, w, Hq):
         return self.n.gemm_part_merge(attn_out, meta.kv_lens, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml,

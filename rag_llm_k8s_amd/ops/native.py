@@ -334,7 +334,9 @@ def gemm_part_merge(attn_out, kv_lens, part_tiles, max_parts, ws_o, ws_ml, Hq, w
 # Fused decode attention + o_proj (attention.hip attn_oproj_kernel): one launch in place of
 # attn_decode_rope(defer_merge) -> gemm_part_merge at batch <= 4. RAGK_DECODE_ATTN_OPROJ=0 disables.
 ATTN_OPROJ = os.environ.get("RAGK_DECODE_ATTN_OPROJ", "1") == "1"
-ATTN_OPROJ_KS = int(os.environ.get("RAGK_ATTN_OPROJ_KS", "8"))  # K-slice steps of 64 (4 or 8)
+ATTN_OPROJ_KS = int(os.environ.get("RAGK_ATTN_OPROJ_KS", "8"))  # K-slice steps of 64 (4, 8 or 16)
+# the residual + RMSNorm consumer inside the fused launch (its last o_proj block), TP=1 only
+ATTN_OPROJ_NORM = os.environ.get("RAGK_ATTN_OPROJ_NORM", "1") == "1"
 ATTN_OPROJ_SPIN_US = int(os.environ.get("RAGK_ATTN_OPROJ_SPIN_US", "1000000"))
 _ao_cnt = {}
 
@@ -367,11 +369,13 @@ def attn_oproj_error(device) -> bool:
 
 
 def attn_oproj(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_tables, kv_lens, Hq, Hkv, D, part_tiles,
-               max_parts, ws_o, ws_ml, w, out=None, scale=None):
+               max_parts, ws_o, ws_ml, w, out=None, scale=None, norm=None):
     """o_proj split-K partials Po [K / KS, M, N] of the decode attention of the qkv partial slabs P [S, M, ldp]
     (RoPE + KV append at `slots`, as attn_decode_rope), in ONE launch (attention.hip attn_oproj_kernel): the
     o_proj blocks stream their weights while the attention blocks stream the KV cache, then merge the
-    partitions of their K-slice and multiply. Same consumer as gemm_part_merge (add_partials_rmsnorm)."""
+    partitions of their K-slice and multiply. Same consumer as gemm_part_merge (add_partials_rmsnorm).
+    norm = (h, gamma, eps): the last o_proj block also does that consumer's work -- h += bf16(sum of the
+    slabs) in place, and the function returns xn = rmsnorm(h) * gamma instead of the slabs."""
     _req(P.dtype == torch.float32 and P.is_contiguous() and P.dim() == 3, "partials")
     S, B, ldp = P.shape
     N, K = w.shape
@@ -385,12 +389,21 @@ def attn_oproj(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_tables
         out = torch.empty((K // (64 * ks), B, N), dtype=torch.float32, device=P.device)
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     cnt = attn_oproj_counters(P.device)
+    h = gamma = xn = None
+    eps = 0.0
+    if norm is not None:
+        h, gamma, eps = norm
+        _req(h.dtype == torch.bfloat16 and h.shape == (B, N) and h.stride(1) == 1 and gamma.numel() == N
+             and gamma.is_contiguous() and K // (64 * ks) <= 16, "norm tail: h [B, N] bf16, <= 16 slabs")
+        xn = torch.empty((B, N), dtype=torch.bfloat16, device=P.device)
     check(_lib.lib().ragk_attn_oproj_fused(
         P.data_ptr(), S, ldp, positions.data_ptr(), slots.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(),
         k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0), kv_lens.data_ptr(),
         ws_o.data_ptr(), ws_ml.data_ptr(), B, Hq, Hkv, D, part_tiles, max_parts, float(scale), w.data_ptr(),
-        w.stride(0), out.data_ptr(), N, ks, cnt.data_ptr(), ATTN_OPROJ_SPIN_US, stream_ptr()), "ragk_attn_oproj_fused")
-    return out
+        w.stride(0), out.data_ptr(), N, ks, cnt.data_ptr(), ATTN_OPROJ_SPIN_US, ptr(h), h.stride(0) if h is not None
+        else 0, ptr(gamma), ptr(xn), xn.stride(0) if xn is not None else 0, float(eps), stream_ptr()),
+        "ragk_attn_oproj_fused")
+    return out if norm is None else xn
 
 
 SILU_MAX_SLABS = 4  # gemm_part.hip SG_MAXS

@@ -625,9 +625,23 @@ def test_attn_oproj_fused_matches_unfused(native, kv_lens, target, Hq, Hkv, ks):
             o = native.attn_oproj(P, pos, cos, sin, slots, kc3, vc3, bt, kvl, Hq, Hkv, D, pt, mp, ws_o, ws_ml, w)
             assert o.shape == (Hq * D // (64 * ks), B, 4096)
             outs.append(o.sum(0))
+        # the residual + RMSNorm tail in the last o_proj block == the add_partials_rmsnorm consumer
+        g = (1 + 0.1 * torch.randn(4096, device=DEV)).bfloat16()
+        h0 = torch.randn(B, 4096, device=DEV).bfloat16()
+        norm_ok = Hq * D // (64 * ks) <= 16
+        if norm_ok:
+            h1, h2 = h0.clone(), h0.clone()
+            xn1 = native.attn_oproj(P, pos, cos, sin, slots, kc.clone(), vc.clone(), bt, kvl, Hq, Hkv, D, pt, mp, ws_o,
+                                    ws_ml, w, norm=(h1, g, 1e-5))
+            Ps = native.attn_oproj(P, pos, cos, sin, slots, kc.clone(), vc.clone(), bt, kvl, Hq, Hkv, D, pt, mp, ws_o,
+                                   ws_ml, w)
+            xn2 = native.add_partials_rmsnorm(Ps, h2, g, 1e-5)
         torch.cuda.synchronize()
         assert not native.attn_oproj_error(DEV)
         assert int(native.attn_oproj_counters(DEV)[:2].abs().sum().item()) == 0  # re-armed
+        if norm_ok:
+            assert torch.equal(h1, h2)  # same slab order, same bf16 rounding points
+            assert rel_err(xn1.float().cpu(), xn2.float().cpu()) < 1e-2  # block-sum order differs
     finally:
         native.ATTN_OPROJ_KS = old
     assert torch.equal(kc3, kc2) and torch.equal(vc3, vc2)
