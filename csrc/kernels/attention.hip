@@ -1232,9 +1232,64 @@ __device__ __forceinline__ void decode_signal(int* cnt) {
 // FUSED (attn_oproj_kernel): the partition record is written write-through even for a single-partition
 // sequence (the o_proj blocks merge records only), there is no merge here, and the block signals
 // `fused_cnt` when its records are out -- also when it has no tiles (the counter counts every block).
-template <int D, int G, bool NT = false, bool FUSED = false>
+// qkv slab sum of sum_partials8x2 with write-through (sc1) buffer loads: the slabs were produced by
+// other blocks of the same launch (attn_oproj_kernel's qkv blocks). off1 / off2: byte offsets of the two
+// 8-float runs in slab 0, slab_b: bytes per slab. Same summation order.
+__device__ __forceinline__ void sum_partials8x2_sc1(__amdgpu_buffer_rsrc_t rs, int off1, int off2, int S, int slab_b,
+                                                    float* a, float* b) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) a[e] = b[e] = 0.f;
+  for (int s0 = 0; s0 < S; s0 += PSU) {
+    u32x4 p[PSU][4];
+#pragma unroll
+    for (int u = 0; u < PSU; ++u) {
+      const int o = min(s0 + u, S - 1) * slab_b;
+      p[u][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off1 + o, 0, 16));
+      p[u][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off1 + o + 16, 0, 16));
+      p[u][2] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off2 + o, 0, 16));
+      p[u][3] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off2 + o + 16, 0, 16));
+    }
+#pragma unroll
+    for (int u = 0; u < PSU; ++u) {
+      if (s0 + u < S) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] += __uint_as_float(p[u][0][e]);
+          a[4 + e] += __uint_as_float(p[u][1][e]);
+          b[e] += __uint_as_float(p[u][2][e]);
+          b[4 + e] += __uint_as_float(p[u][3][e]);
+        }
+      }
+    }
+  }
+}
+
+// Bounded poll of an agent-scope counter by one lane (sc1 loads), then the block's barrier. Sets err[0]
+// and gives up (the block computes garbage, never hangs) after `limit` s_memrealtime ticks.
+__device__ __forceinline__ void wait_counter(const int* cnt, int need, int* err, unsigned limit) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+struct QWait {       // attention blocks waiting for the in-launch qkv blocks (QW mode)
+  const int* cnt;    // qkv blocks done
+  int need;
+  int* err;
+  unsigned limit;
+};
+
+template <int D, int G, bool NT = false, bool FUSED = false, bool QW = false>
 __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part, int kvh, int b, char* smem,
-                                                  int* fused_cnt = nullptr) {
+                                                  int* fused_cnt = nullptr, QWait qw = {}) {
   using C = Cfg<D>;
   static_assert(G <= 16, "at most 16 query heads per KV head");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1275,6 +1330,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
                                                                                    32 * s + 8 * fh))
                        : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
   }
+  if constexpr (QW) wait_counter(qw.cnt, qw.need, qw.err, qw.limit);  // the KV prefetch above is in flight
   if (a.qkv_p != nullptr) {
     // q = RoPE(bf16(sum_s P[s][b])) for this KV head's G query heads, one (d, d + D/2) rotate_half
     // pair of 8-vectors per thread (G * D/16 threads, all slab loads of a thread in flight together),
@@ -1284,6 +1340,8 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     constexpr int NV = D / 16;  // pairs per head
     const int pos = a.positions[b];
     const float* prow = a.qkv_p + (size_t)b * a.ldp;
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t rs_qkv = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.qkv_p), (short)0, (int)(a.p_slab * a.S * 4), 0x00020000);
     const float* ct = a.cos_t + (size_t)pos * (D / 2);
     const float* st = a.sin_t + (size_t)pos * (D / 2);
     const int tid = threadIdx.x;
@@ -1293,7 +1351,12 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
       const int g = tid / NV, v = tid % NV;
       const float* ph = prow + (size_t)(kvh * G + g) * D + 8 * v;
       float x1[8], x2[8], o1[8], o2[8];
-      sum_partials8x2(ph, ph + D / 2, a.S, (size_t)a.p_slab, x1, x2);
+      if constexpr (QW) {
+        const int o = (int)((ph - a.qkv_p) * 4);
+        sum_partials8x2_sc1(rs_qkv, o, o + D * 2, a.S, (int)(a.p_slab * 4), x1, x2);
+      } else {
+        sum_partials8x2(ph, ph + D / 2, a.S, (size_t)a.p_slab, x1, x2);
+      }
       rope8(x1, x2, ct + 8 * v, st + 8 * v, o1, o2);
       *reinterpret_cast<u32x4*>(s_q + g * D + 8 * v) = pack8(o1);
       *reinterpret_cast<u32x4*>(s_q + g * D + D / 2 + 8 * v) = pack8(o2);
@@ -1303,7 +1366,12 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
       const size_t kvo = (((size_t)(slot / KT) * a.Hkv + kvh) * KT + (slot % KT)) * D;
       const float* ph = prow + (size_t)(a.Hq + (isv ? a.Hkv : 0) + kvh) * D + 8 * v;
       float x1[8], x2[8];
-      sum_partials8x2(ph, ph + D / 2, a.S, (size_t)a.p_slab, x1, x2);
+      if constexpr (QW) {
+        const int o = (int)((ph - a.qkv_p) * 4);
+        sum_partials8x2_sc1(rs_qkv, o, o + D * 2, a.S, (int)(a.p_slab * 4), x1, x2);
+      } else {
+        sum_partials8x2(ph, ph + D / 2, a.S, (size_t)a.p_slab, x1, x2);
+      }
       bf16_t* dst = (isv ? const_cast<bf16_t*>(a.vc) : const_cast<bf16_t*>(a.kc)) + kvo;
       if (isv) {
         *reinterpret_cast<u32x4*>(dst + 8 * v) = pack8(x1);
@@ -1715,9 +1783,10 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
   if (tid == 0) {
     const int old = __hip_atomic_fetch_add(o.cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == o.nob - 1;
-    if (last) {
+    if (last) {  // (cnt[4]: the 3-role launch's qkv-done counter; every attention block is past its wait)
       __hip_atomic_store(o.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(o.cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o.cnt + 4, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     *s_last = last;
   }
@@ -1788,6 +1857,114 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
   }
 }
 
+// qkv projection blocks of the 3-role launch (attn_oproj_kernel<..., QNLD > 0>): split-K partial slabs
+// P[s][M][N] of rmsnorm(h) . Wqkv^T (gemm_part_norm's math and reduction order: threads sum their row
+// vectors, the 4 wave partials are added in order), 64 output columns x KS per 4-wave block, written
+// through (sc1) for the attention blocks of the same launch, then signalled on cnt[4].
+struct QkvArgs {
+  const bf16_t* W; int ldw;    // [N][K] bf16 (packed q | k | v rows)
+  const bf16_t* h; int ldh;    // [M][K] residual rows (un-normalised)
+  const bf16_t* gamma;         // [K]
+  float eps;
+  float* P;                    // [K / KS][M][N] fp32
+  int M, N, K;
+  int nqb;                     // qkv blocks
+};
+
+template <int NLD>
+__device__ __forceinline__ void qkv_norm_block(const QkvArgs& q, int qb, char* smem, int* cnt) {
+  constexpr int KS = 32 * NLD;
+  constexpr int ROWB = KS * 2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fh = lane >> 4;
+  const int ncb = (q.N + 63) / 64;
+  const int cb = qb % ncb, s = qb / ncb;
+  const int n0 = cb * 64, kbase = s * KS;
+  const int M = q.M;
+  const int nvec = q.K >> 3;  // 16-B vectors per row (K <= 4096: two per thread)
+  // 1) row vectors + the slice's norm weights first (a counted wait retires them before the weights)
+  u32x4 hv[4][2], gv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int vi = min(tid + 256 * i, nvec - 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) hv[r][i] = *reinterpret_cast<const u32x4*>(q.h + (size_t)min(r, M - 1) * q.ldh + vi * 8);
+    gv[i] = *reinterpret_cast<const u32x4*>(q.gamma + min(max(vi * 8, kbase), kbase + KS - 8));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const int wrow = min(n0 + 16 * wid + fr, q.N - 1);
+  const bf16_t* wp = q.W + (size_t)wrow * q.ldw + kbase + 8 * fh;
+  bf16x8 wf[NLD];
+#pragma unroll
+  for (int ks = 0; ks < NLD; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
+  __builtin_amdgcn_s_waitcnt((NLD & 15) | (((NLD >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));  // vmcnt(NLD)
+  __builtin_amdgcn_sched_barrier(0);
+  // 2) RMSNorm statistics (rmsnorm_kernel's order), normalised slice -> LDS (swizzled as the O role's)
+  float* s_red = reinterpret_cast<float*>(smem + 16 * ROWB);  // [4 rows][4 waves]
+  float ss[4];
+  const u32x4 z = {0, 0, 0, 0};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    ss[r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const u32x4 v = tid + 256 * i < nvec ? hv[r][i] : z;
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss[r] += f[e] * f[e];
+    }
+    ss[r] = wave_sum(ss[r]);
+    if (lane == 0) s_red[r * 4 + wid] = ss[r];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (r >= M) break;
+    const float t = ((s_red[r * 4] + s_red[r * 4 + 1]) + s_red[r * 4 + 2]) + s_red[r * 4 + 3];
+    const float inv = rsqrtf(t / (float)q.K + q.eps);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int vi = tid + 256 * i;
+      if (vi < nvec && vi * 8 >= kbase && vi * 8 < kbase + KS) {
+        float f[8], g[8], o[8];
+        unpack8(hv[r][i], f);
+        unpack8(gv[i], g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = g[e] * bf2f(f2bf(f[e] * inv));
+        const int c = vi - kbase / 8;
+        *reinterpret_cast<u32x4*>(smem + r * ROWB + 16 * ((c & ~15) | ((c & 15) ^ (r & 15)))) = pack8(o);
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // raw: __syncthreads() would drain the weight loads (vmcnt(0))
+  __builtin_amdgcn_sched_barrier(0);
+  // 3) MFMA, write-through slab, signal
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NLD; ++ks) {
+    const int chunk = 4 * ks + fh;
+    const bf16x8 xf = *reinterpret_cast<const bf16x8*>(smem + fr * ROWB + 16 * ((chunk & ~15) | ((chunk & 15) ^ (fr & 15))));
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[ks], acc, 0, 0, 0);
+  }
+  const int col = n0 + 16 * wid + fr;
+  const int nslab = q.K / KS;
+  const __amdgpu_buffer_rsrc_t rs_p =
+      __builtin_amdgcn_make_buffer_rsrc(q.P, (short)0, (int)((size_t)nslab * M * q.N * 4), 0x00020000);
+  if (fh == 0 && col < q.N) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r < M)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[r]), rs_p, (int)((((size_t)s * M + r) * q.N + col) * 4),
+                                              0, 16);
+  }
+  decode_signal(cnt + 4);
+}
+
 template <int D, int G, int NLD>
 constexpr int attn_oproj_lds() {
   constexpr int a = decode_lds_bytes<D, G>();
@@ -1795,13 +1972,26 @@ constexpr int attn_oproj_lds() {
   return a > o ? a : o;
 }
 
-template <int D, int G, int NLD>
-__global__ __launch_bounds__(256, 2) void attn_oproj_kernel(DecodeArgs a, OprojArgs o) {
-  __shared__ __attribute__((aligned(16))) char smem[attn_oproj_lds<D, G, NLD>()];
-  const int bid = blockIdx.x;
+// QNLD > 0: the 3-role launch -- blocks [0, nqb) are qkv blocks (qkv_norm_block<QNLD>), then the
+// attention blocks (they prefetch their first KV tile, then wait for every qkv block), then the o_proj
+// blocks. Every wait is on lower-indexed blocks only.
+template <int D, int G, int NLD, int QNLD = 0>
+__global__ __launch_bounds__(256, 2) void attn_oproj_kernel(DecodeArgs a, OprojArgs o, QkvArgs q) {
+  constexpr int lds_q = QNLD > 0 ? 16 * 64 * QNLD + 64 : 0;
+  constexpr int lds = attn_oproj_lds<D, G, NLD>() > lds_q ? attn_oproj_lds<D, G, NLD>() : lds_q;
+  __shared__ __attribute__((aligned(16))) char smem[lds];
+  int bid = blockIdx.x;
+  if constexpr (QNLD > 0) {
+    if (bid < q.nqb) {
+      qkv_norm_block<QNLD>(q, bid, smem, o.cnt);
+      return;
+    }
+    bid -= q.nqb;
+  }
   if (bid < o.na) {
     const int mp = a.max_parts;
-    attn_decode_block<D, G, false, true>(a, bid % mp, (bid / mp) % a.Hkv, bid / (mp * a.Hkv), smem, o.cnt);
+    attn_decode_block<D, G, false, true, (QNLD > 0)>(a, bid % mp, (bid / mp) % a.Hkv, bid / (mp * a.Hkv), smem,
+                                                     o.cnt, QWait{o.cnt + 4, q.nqb, o.cnt + 2, o.spin_limit});
     return;
   }
   oproj_merge_block<D, NLD>(a, o, bid - o.na, smem);
@@ -2133,9 +2323,10 @@ RAGK_API int ragk_attn_oproj_fused(const float* P, int S, int ldp, const int* po
               (unsigned)(ticks > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : ticks), (bf16_t*)h, ldh, (const bf16_t*)gamma,
               (bf16_t*)xn, ldx, eps};
   const dim3 grid(o.na + o.nob);
+  const QkvArgs q{};
 #define RAGK_AO(GG, NL)                                                                       \
   if (G == GG && 2 * ks_steps == NL) {                                                        \
-    hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL>), grid, dim3(256), 0, st, a, o);       \
+    hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL>), grid, dim3(256), 0, st, a, o, q);    \
     return (int)hipGetLastError();                                                            \
   }
   RAGK_AO(4, 8)
@@ -2145,5 +2336,55 @@ RAGK_API int ragk_attn_oproj_fused(const float* P, int S, int ldp, const int* po
   RAGK_AO(8, 16)
   RAGK_AO(8, 32)
 #undef RAGK_AO
+  return (int)hipErrorInvalidValue;
+}
+
+// The 3-role launch: the qkv projection with the input RMSNorm (gemm_part_norm's math) as well --
+// qkv + attention + o_proj (+ the residual / post-attention norm tail) in ONE launch per layer.
+// h [B][ldh] bf16 is the layer input (un-normalised residual), gin its norm weight, Wqkv [Nq][K] bf16
+// (K = 4096), Pq the qkv slab workspace [K / (64 q_ks)][B][Nq] fp32 (q_ks 8 or 16). The post-attention
+// tail (h2 != nullptr) updates h2 (the same residual buffer) in place and writes xn.
+RAGK_API int ragk_qkv_attn_oproj_fused(const void* h, int ldh, const void* gin, float eps_in, const void* Wqkv,
+                                       int ldwq, int Nq, int K, float* Pq, int q_ks, const int* positions,
+                                       const int* slots, const float* cos_t, const float* sin_t, void* kc, void* vc,
+                                       const int* block_tables, int bt_stride, const int* kv_lens, float* part_o,
+                                       float* part_ml, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
+                                       float scale, const void* Wo, int ldw, float* Pout, int N, int ks_steps,
+                                       int* cnt, unsigned spin_us, void* h2, int ldh2, const void* gamma, void* xn,
+                                       int ldx, float eps, hipStream_t st) {
+  if (B <= 0) return 0;
+  const int G = Hq / (Hkv > 0 ? Hkv : 1);
+  const int Ko = Hq * D;
+  const int KS = 64 * ks_steps, QKS = 64 * q_ks;
+  if (B > 4 || D != 128 || Hq % Hkv || (G != 4 && G != 8) || (ks_steps != 4 && ks_steps != 8 && ks_steps != 16) ||
+      Ko % KS || (q_ks != 8 && q_ks != 16) || K > 4096 || K % QKS || Nq != (Hq + 2 * Hkv) * D || ldwq < K ||
+      ldh % 8 || ((uintptr_t)h & 15) || ((uintptr_t)gin & 15) || part_tiles < 1 || max_parts < 1 ||
+      max_parts > OP_MAXP || !h || !gin || !Wqkv || !Pq || !positions || !slots || !cos_t || !sin_t || !part_o ||
+      !part_ml || !Wo || !Pout || !cnt || N <= 0 || ldw < Ko)
+    return (int)hipErrorInvalidValue;
+  if (h2 && (!gamma || !xn || Ko / KS > 16 || N % 8 || ldh2 % 8 || ldx % 8 || ((uintptr_t)h2 & 15) ||
+             ((uintptr_t)xn & 15) || ((uintptr_t)gamma & 15)))
+    return (int)hipErrorInvalidValue;
+  const int S = K / QKS;
+  DecodeArgs a{nullptr, 0, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, bt_stride, kv_lens,
+               part_o, part_ml, nullptr, 0, Hq, Hkv, part_tiles, max_parts,
+               scale * 1.4426950408889634f, nullptr, Pq, (long long)B * Nq, Nq, S, positions, slots, cos_t, sin_t, B};
+  const unsigned long long ticks = (unsigned long long)(spin_us ? spin_us : 1000000u) * 100ull;
+  OprojArgs o{(const bf16_t*)Wo, ldw, Pout, B, N, Ko, max_parts * Hkv * B, ((N + 63) / 64) * (Ko / KS), cnt,
+              (unsigned)(ticks > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : ticks), (bf16_t*)h2, ldh2, (const bf16_t*)gamma,
+              (bf16_t*)xn, ldx, eps};
+  const QkvArgs q{(const bf16_t*)Wqkv, ldwq, (const bf16_t*)h, ldh, (const bf16_t*)gin, eps_in, Pq, B, Nq, K,
+                  ((Nq + 63) / 64) * S};
+  const dim3 grid(q.nqb + o.na + o.nob);
+#define RAGK_QAO(GG, NL, QN)                                                                     \
+  if (G == GG && 2 * ks_steps == NL && 2 * q_ks == QN) {                                         \
+    hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL, QN>), grid, dim3(256), 0, st, a, o, q);   \
+    return (int)hipGetLastError();                                                               \
+  }
+  RAGK_QAO(4, 16, 16)
+  RAGK_QAO(4, 16, 32)
+  RAGK_QAO(8, 16, 16)
+  RAGK_QAO(8, 16, 32)
+#undef RAGK_QAO
   return (int)hipErrorInvalidValue;
 }

@@ -381,13 +381,21 @@ class LlamaModel:
         fused_ao = (DECODE_ROPE_FUSED and not pf and be.attn_oproj_ok(M, inp.meta, layers[0]["wo"], Hq, Hkv, D))
         # ... and, at TP=1, the residual + post-attention norm in its last block (no consumer launch)
         ao_norm = fused_ao and not tp and be.attn_oproj_norm_ok(layers[0]["wo"])
+        # ... and the qkv projection with the input norm as well: the layer's attention half is ONE launch
+        qao = (ao_norm and fuse_norm
+               and be.qkv_attn_oproj_ok(M, inp.meta, layers[0]["wqkv"], layers[0]["wo"], Hq, Hkv, D))
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
-            if fuse_norm:
+            if qao:
+                xn = be.qkv_attn_oproj(h, L["ln_in"], c.rms_norm_eps, L["wqkv"], inp.positions, self.cos, self.sin,
+                                       inp.slots, kc, vc, inp.meta, L["wo"], Hq, Hkv, D, L["ln_post"], c.rms_norm_eps)
+            elif fuse_norm:
                 P = be.gemm_part_norm(h, L["ln_in"], c.rms_norm_eps, L["wqkv"])
             else:
                 P = be.gemm_part(xn, L["wqkv"])
-            if ao_norm:
+            if qao:
+                pass
+            elif ao_norm:
                 xn = be.attn_oproj(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, L["wo"], Hq,
                                    Hkv, D, norm=(h, L["ln_post"], c.rms_norm_eps))
             elif fused_ao:

@@ -178,6 +178,9 @@ class TorchBackend:
     def attn_oproj_norm_ok(self, w):
         return False
 
+    def qkv_attn_oproj_ok(self, M, meta: AttnMeta, wqkv, wo, Hq, Hkv, D):
+        return False
+
     def prefill_nsplit(self, M, w):
         return 1
 
@@ -328,6 +331,15 @@ class NativeBackend(TorchBackend):
 
     def attn_oproj_norm_ok(self, w):
         return self.n.ATTN_OPROJ_NORM and w.shape[1] // (64 * self.n.ATTN_OPROJ_KS) <= 16
+
+    def qkv_attn_oproj_ok(self, M, meta: AttnMeta, wqkv, wo, Hq, Hkv, D):
+        return self.enable_part and self.n.qkv_attn_oproj_ok(M, wqkv, wo, Hq, Hkv, D, meta.max_parts, meta.ws_o)
+
+    def qkv_attn_oproj(self, h, g_in, eps_in, wqkv, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, wo, Hq,
+                       Hkv, D, g_post, eps):
+        return self.n.qkv_attn_oproj(h, g_in, eps_in, wqkv, positions, cos_t, sin_t, slots, kc, vc, meta.block_tables,
+                                     meta.kv_lens, Hq, Hkv, D, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml,
+                                     wo, g_post, eps)
 
     def gemm_part_merge(self, attn_out, meta: AttnMeta, w, Hq):
         return self.n.gemm_part_merge(attn_out, meta.kv_lens, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml,

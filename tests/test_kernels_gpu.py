@@ -651,6 +651,61 @@ def test_attn_oproj_fused_matches_unfused(native, kv_lens, target, Hq, Hkv, ks):
     assert rel_err(outs[0].cpu(), oracle.cpu()) < 2e-3, rel_err(outs[0].cpu(), oracle.cpu())
 
 
+@pytest.mark.parametrize("kv_lens,Hq,Hkv,qks", [([5200], 32, 8, 16), ([70, 3000], 32, 8, 8), ([1], 32, 8, 16),
+                                                 ([777, 5300, 65, 2000], 32, 8, 16), ([5200, 70], 32, 4, 16)])
+def test_qkv_attn_oproj_matches_unfused(native, kv_lens, Hq, Hkv, qks):
+    """The 3-role decode launch (qkv + input RMSNorm, attention + RoPE + KV append, o_proj + residual +
+    post-attention RMSNorm; attention blocks prefetch KV while the qkv weights stream) == rmsnorm ->
+    gemm_part -> attn_decode_rope -> gemm_part -> add_partials_rmsnorm, up to fp32 summation order; the
+    same KV-cache contents; repeated launches re-arm the counters."""
+    D, H = 128, 4096
+    torch.manual_seed(41)
+    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=11)
+    B = len(kv_lens)
+    kc, vc, bt = kc.to(DEV), vc.to(DEV), bt.to(DEV)
+    kvl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    pos = kvl - 1
+    slots = (bt[torch.arange(B, device=DEV), (pos // 64).long()] * 64 + pos % 64).int()
+    cos, sin = R.rope_tables(D, 131072, theta=500000.0)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv, target_blocks=512)
+    Nq = (Hq + 2 * Hkv) * D
+    wqkv = (torch.randn(Nq, H, device=DEV) / math.sqrt(H)).bfloat16()
+    wo = (torch.randn(H, Hq * D, device=DEV) / math.sqrt(Hq * D)).bfloat16()
+    g_in = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16()
+    g_post = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16()
+    h0 = torch.randn(B, H, device=DEV).bfloat16()
+    ws_o = torch.empty((B, Hq, max(mp, 1), D), dtype=torch.float32, device=DEV)
+    ws_ml = torch.empty((B, Hq, max(mp, 1), 2), dtype=torch.float32, device=DEV)
+    # unfused reference chain
+    kc2, vc2, h2 = kc.clone(), vc.clone(), h0.clone()
+    Pq = native.gemm_part(native.rmsnorm(h2, g_in, 1e-5), wqkv)
+    attn = torch.empty(B, Hq * D, device=DEV).bfloat16()
+    native.attn_decode_rope(Pq, pos, cos, sin, slots, kc2, vc2, bt, kvl, attn, Hq, Hkv, D, pt, mp)
+    xn2 = native.add_partials_rmsnorm(native.gemm_part(attn, wo), h2, g_post, 1e-5)
+    old = native.QAO_QKS
+    native.QAO_QKS = qks
+    try:
+        assert native.qkv_attn_oproj_ok(B, wqkv, wo, Hq, Hkv, D, mp, ws_o)
+        res = []
+        for it in range(3):
+            kc1, vc1, h1 = kc.clone(), vc.clone(), h0.clone()
+            xn1 = native.qkv_attn_oproj(h1, g_in, 1e-5, wqkv, pos, cos, sin, slots, kc1, vc1, bt, kvl, Hq, Hkv, D, pt,
+                                        mp, ws_o, ws_ml, wo, g_post, 1e-5)
+            res.append((h1, xn1))
+        torch.cuda.synchronize()
+        assert not native.attn_oproj_error(DEV)
+        assert int(native.attn_oproj_counters(DEV)[:5].abs().sum().item()) == 0  # re-armed
+    finally:
+        native.QAO_QKS = old
+    # k rows appended from differently-ordered fp32 slab sums may differ by 1 bf16 ulp
+    assert rel_err(kc1.float().cpu(), kc2.float().cpu()) < 1e-2 and rel_err(vc1.float().cpu(), vc2.float().cpu()) < 1e-2
+    for h1, xn1 in res:
+        assert torch.equal(h1, res[0][0]) and torch.equal(xn1, res[0][1])  # deterministic
+    assert rel_err(res[0][0].float().cpu(), h2.float().cpu()) < 1e-2
+    assert rel_err(res[0][1].float().cpu(), xn2.float().cpu()) < 2e-2, rel_err(res[0][1].float().cpu(), xn2.float().cpu())
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (3, 6144, 4096), (4, 1280, 8192), (2, 10240, 8192)])
 def test_gemm_part_norm_matches_rmsnorm_then_part(native, M, N, K):
     """gemm_part_norm (RMSNorm applied while staging the activation slice) == rmsnorm_kernel followed
