@@ -1681,16 +1681,28 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
   }
   __syncthreads();
   const int MP = a.max_parts;
-  for (int e = tid; e < M * HPB * MP; e += 256) {
-    const int p = e % MP, j = (e / MP) % HPB, r = e / (MP * HPB);
-    float m = -INFINITY, l = 0.f;
-    if (p < s_np[r]) {
+  {
+    // every (max, sum) load of the thread issued before any is used (indices clamped, masked after):
+    // at most 4 x 4 heads x 64 partitions = 4 per thread
+    constexpr int PER = (4 * HPB * OP_MAXP + 255) / 256;
+    f32x2 ml[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = min(tid + 256 * k, M * HPB * MP - 1);
+      const int p = e % MP, j = (e / MP) % HPB, r = e / (MP * HPB);
       const int pi = ((r * a.Hq + h0 + j) * MP + p) * 8;
-      m = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ml, pi, 0, 16));
-      l = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ml, pi + 4, 0, 16));
+      ml[k] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_ml, pi, 0, 16));
     }
-    s_sc[(r * HPB + j) * OP_MAXP + p] = m;
-    s_l[(r * HPB + j) * OP_MAXP + p] = l;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = tid + 256 * k;
+      if (e < M * HPB * MP) {
+        const int p = e % MP, j = (e / MP) % HPB, r = e / (MP * HPB);
+        const bool ok = p < s_np[r];
+        s_sc[(r * HPB + j) * OP_MAXP + p] = ok ? ml[k][0] : -INFINITY;
+        s_l[(r * HPB + j) * OP_MAXP + p] = ok ? ml[k][1] : 0.f;
+      }
+    }
   }
   __syncthreads();
   if (tid < M * HPB) {
