@@ -1902,7 +1902,7 @@ __device__ __forceinline__ void qkv_norm_block(const QkvArgs& q, int qb, char* s
     const int vi = min(tid + 256 * i, nvec - 1);
 #pragma unroll
     for (int r = 0; r < 4; ++r) hv[r][i] = *reinterpret_cast<const u32x4*>(q.h + (size_t)min(r, M - 1) * q.ldh + vi * 8);
-    gv[i] = *reinterpret_cast<const u32x4*>(q.gamma + min(max(vi * 8, kbase), kbase + KS - 8));
+    gv[i] = *reinterpret_cast<const u32x4*>((q.gamma ? q.gamma : q.h) + min(max(vi * 8, kbase), kbase + KS - 8));
   }
   __builtin_amdgcn_sched_barrier(0);
   const int wrow = min(n0 + 16 * wid + fr, q.N - 1);
@@ -1912,8 +1912,23 @@ __device__ __forceinline__ void qkv_norm_block(const QkvArgs& q, int qb, char* s
   for (int ks = 0; ks < NLD; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
   __builtin_amdgcn_s_waitcnt((NLD & 15) | (((NLD >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));  // vmcnt(NLD)
   __builtin_amdgcn_sched_barrier(0);
-  // 2) RMSNorm statistics (rmsnorm_kernel's order), normalised slice -> LDS (swizzled as the O role's)
+  // 2) RMSNorm statistics (rmsnorm_kernel's order), normalised slice -> LDS (swizzled as the O role's);
+  //    gamma == nullptr: the rows are already normalised (tensor-parallel decode), staged as they are
   float* s_red = reinterpret_cast<float*>(smem + 16 * ROWB);  // [4 rows][4 waves]
+  if (q.gamma == nullptr) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (r >= M) break;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int vi = tid + 256 * i;
+        if (vi < nvec && vi * 8 >= kbase && vi * 8 < kbase + KS) {
+          const int c = vi - kbase / 8;
+          *reinterpret_cast<u32x4*>(smem + r * ROWB + 16 * ((c & ~15) | ((c & 15) ^ (r & 15)))) = hv[r][i];
+        }
+      }
+    }
+  }
   float ss[4];
   const u32x4 z = {0, 0, 0, 0};
 #pragma unroll
@@ -1935,7 +1950,7 @@ __device__ __forceinline__ void qkv_norm_block(const QkvArgs& q, int qb, char* s
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    if (r >= M) break;
+    if (r >= M || q.gamma == nullptr) break;
     const float t = ((s_red[r * 4] + s_red[r * 4 + 1]) + s_red[r * 4 + 2]) + s_red[r * 4 + 3];
     const float inv = rsqrtf(t / (float)q.K + q.eps);
 #pragma unroll
@@ -2354,8 +2369,10 @@ RAGK_API int ragk_attn_oproj_fused(const float* P, int S, int ldp, const int* po
 // The 3-role launch: the qkv projection with the input RMSNorm (gemm_part_norm's math) as well --
 // qkv + attention + o_proj (+ the residual / post-attention norm tail) in ONE launch per layer.
 // h [B][ldh] bf16 is the layer input (un-normalised residual), gin its norm weight, Wqkv [Nq][K] bf16
-// (K = 4096), Pq the qkv slab workspace [K / (64 q_ks)][B][Nq] fp32 (q_ks 8 or 16). The post-attention
-// tail (h2 != nullptr) updates h2 (the same residual buffer) in place and writes xn.
+// (K = 4096), Pq the qkv slab workspace [K / (64 q_ks)][B][Nq] fp32 (q_ks 8 or 16). gin == nullptr: h is
+// already normalised (tensor-parallel decode: the output of the fused cross-rank reduction). The
+// post-attention tail (h2 != nullptr) updates h2 (the same residual buffer) in place and writes xn;
+// without it the o_proj slabs Pout go to the caller's consumer (the cross-rank reduction under TP).
 RAGK_API int ragk_qkv_attn_oproj_fused(const void* h, int ldh, const void* gin, float eps_in, const void* Wqkv,
                                        int ldwq, int Nq, int K, float* Pq, int q_ks, const int* positions,
                                        const int* slots, const float* cos_t, const float* sin_t, void* kc, void* vc,
@@ -2371,7 +2388,7 @@ RAGK_API int ragk_qkv_attn_oproj_fused(const void* h, int ldh, const void* gin, 
   if (B > 4 || D != 128 || Hq % Hkv || (G != 4 && G != 8) || (ks_steps != 4 && ks_steps != 8 && ks_steps != 16) ||
       Ko % KS || (q_ks != 8 && q_ks != 16) || K > 4096 || K % QKS || Nq != (Hq + 2 * Hkv) * D || ldwq < K ||
       ldh % 8 || ((uintptr_t)h & 15) || ((uintptr_t)gin & 15) || part_tiles < 1 || max_parts < 1 ||
-      max_parts > OP_MAXP || !h || !gin || !Wqkv || !Pq || !positions || !slots || !cos_t || !sin_t || !part_o ||
+      max_parts > OP_MAXP || !h || !Wqkv || !Pq || !positions || !slots || !cos_t || !sin_t || !part_o ||
       !part_ml || !Wo || !Pout || !cnt || N <= 0 || ldw < Ko)
     return (int)hipErrorInvalidValue;
   if (h2 && (!gamma || !xn || Ko / KS > 16 || N % 8 || ldh2 % 8 || ldx % 8 || ((uintptr_t)h2 & 15) ||

@@ -384,16 +384,24 @@ class LlamaModel:
         # ... and the qkv projection with the input norm as well: the layer's attention half is ONE launch
         qao = (ao_norm and fuse_norm
                and be.qkv_attn_oproj_ok(M, inp.meta, layers[0]["wqkv"], layers[0]["wo"], Hq, Hkv, D))
+        # tensor parallel: the same launch on the rank's shard, fed by the fused reduction's normed rows
+        # and feeding its o_proj slabs to the next fused reduction
+        qao_tp = (tp and fused_ao
+                  and be.qkv_attn_oproj_ok(M, inp.meta, layers[0]["wqkv"], layers[0]["wo"], Hq, Hkv, D,
+                                           norm_tail=False))
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
             if qao:
                 xn = be.qkv_attn_oproj(h, L["ln_in"], c.rms_norm_eps, L["wqkv"], inp.positions, self.cos, self.sin,
                                        inp.slots, kc, vc, inp.meta, L["wo"], Hq, Hkv, D, L["ln_post"], c.rms_norm_eps)
+            elif qao_tp:
+                P = be.qkv_attn_oproj(xn, None, 0.0, L["wqkv"], inp.positions, self.cos, self.sin, inp.slots, kc, vc,
+                                      inp.meta, L["wo"], Hq, Hkv, D, None, 0.0)
             elif fuse_norm:
                 P = be.gemm_part_norm(h, L["ln_in"], c.rms_norm_eps, L["wqkv"])
             else:
                 P = be.gemm_part(xn, L["wqkv"])
-            if qao:
+            if qao or qao_tp:
                 pass
             elif ao_norm:
                 xn = be.attn_oproj(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, L["wo"], Hq,

@@ -178,7 +178,7 @@ class TorchBackend:
     def attn_oproj_norm_ok(self, w):
         return False
 
-    def qkv_attn_oproj_ok(self, M, meta: AttnMeta, wqkv, wo, Hq, Hkv, D):
+    def qkv_attn_oproj_ok(self, M, meta: AttnMeta, wqkv, wo, Hq, Hkv, D, norm_tail=True):
         return False
 
     def prefill_nsplit(self, M, w):
@@ -332,8 +332,9 @@ class NativeBackend(TorchBackend):
     def attn_oproj_norm_ok(self, w):
         return self.n.ATTN_OPROJ_NORM and w.shape[1] // (64 * self.n.ATTN_OPROJ_KS) <= 16
 
-    def qkv_attn_oproj_ok(self, M, meta: AttnMeta, wqkv, wo, Hq, Hkv, D):
-        return self.enable_part and self.n.qkv_attn_oproj_ok(M, wqkv, wo, Hq, Hkv, D, meta.max_parts, meta.ws_o)
+    def qkv_attn_oproj_ok(self, M, meta: AttnMeta, wqkv, wo, Hq, Hkv, D, norm_tail=True):
+        return self.enable_part and self.n.qkv_attn_oproj_ok(M, wqkv, wo, Hq, Hkv, D, meta.max_parts, meta.ws_o,
+                                                             norm_tail=norm_tail)
 
     def qkv_attn_oproj(self, h, g_in, eps_in, wqkv, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, wo, Hq,
                        Hkv, D, g_post, eps):

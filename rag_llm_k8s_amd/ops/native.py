@@ -412,15 +412,16 @@ QAO = os.environ.get("RAGK_DECODE_QAO", "1") == "1"
 QAO_QKS = int(os.environ.get("RAGK_QAO_QKS", "16"))  # qkv K-slice steps of 64 (8 or 16)
 
 
-def qkv_attn_oproj_ok(M, wqkv, wo, Hq, Hkv, D, max_parts, ws_o):
+def qkv_attn_oproj_ok(M, wqkv, wo, Hq, Hkv, D, max_parts, ws_o, norm_tail=True):
     from .fp8 import Fp8Weight
 
-    if not (QAO and ATTN_OPROJ_NORM) or isinstance(wqkv, Fp8Weight) or not attn_oproj_ok(M, wo, Hq, Hkv, D, max_parts,
-                                                                                          ws_o):
+    if not QAO or (norm_tail and not ATTN_OPROJ_NORM) or isinstance(wqkv, Fp8Weight):
+        return False
+    if not attn_oproj_ok(M, wo, Hq, Hkv, D, max_parts, ws_o):
         return False
     Nq, K = wqkv.shape
     return (wqkv.dtype == torch.bfloat16 and Nq == (Hq + 2 * Hkv) * D and K <= 4096 and K % (64 * QAO_QKS) == 0
-            and ATTN_OPROJ_KS == 8 and wo.shape[1] // (64 * ATTN_OPROJ_KS) <= 16)
+            and ATTN_OPROJ_KS == 8 and (not norm_tail or wo.shape[1] // (64 * ATTN_OPROJ_KS) <= 16))
 
 
 def qkv_attn_oproj(h, g_in, eps_in, wqkv, positions, cos_t, sin_t, slots, k_cache, v_cache, block_tables, kv_lens, Hq,
@@ -429,28 +430,34 @@ def qkv_attn_oproj(h, g_in, eps_in, wqkv, positions, cos_t, sin_t, slots, k_cach
     partials of rmsnorm(h) * g_in (gemm_part_norm's math), then RoPE + KV append + split-K attention (the
     attention blocks prefetch their first KV tile while the qkv weights stream), then o_proj (weights
     prefetched meanwhile) with the residual add into h (in place) and the post-attention RMSNorm in the last
-    block. Returns xn = rmsnorm(h + o_proj(attention)) * g_post."""
+    block. Returns xn = rmsnorm(h + o_proj(attention)) * g_post.
+    Tensor parallel (g_in None, g_post None): h is this rank's already-normalised input rows, and the o_proj
+    split-K slabs [S, M, N] are returned for the cross-rank reduction + residual + norm consumer."""
     B, K = h.shape
     Nq = wqkv.shape[0]
     N = wo.shape[0]
-    _req(qkv_attn_oproj_ok(B, wqkv, wo, Hq, Hkv, D, max_parts, ws_o), "fused qkv + attention + o_proj shape")
-    _req(h.dtype == torch.bfloat16 and h.stride(1) == 1 and h.stride(0) % 8 == 0 and N == K, "residual rows")
+    tail = g_post is not None
+    _req(qkv_attn_oproj_ok(B, wqkv, wo, Hq, Hkv, D, max_parts, ws_o, norm_tail=tail),
+         "fused qkv + attention + o_proj shape")
+    _req(h.dtype == torch.bfloat16 and h.stride(1) == 1 and h.stride(0) % 8 == 0 and (N == K or not tail),
+         "residual rows")
     _req(kv_lens.numel() == B and positions.numel() == B and slots.numel() == B, "one row per sequence")
     _req(ws_o.numel() >= B * Hq * max_parts * D and ws_ml.numel() >= B * Hq * max_parts * 2, "partition workspace")
     qks, ks = QAO_QKS, ATTN_OPROJ_KS
     Pq = torch.empty((K // (64 * qks), B, Nq), dtype=torch.float32, device=h.device)
     Po = torch.empty((wo.shape[1] // (64 * ks), B, N), dtype=torch.float32, device=h.device)
-    xn = torch.empty((B, N), dtype=torch.bfloat16, device=h.device)
+    xn = torch.empty((B, N), dtype=torch.bfloat16, device=h.device) if tail else None
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     cnt = attn_oproj_counters(h.device)
     check(_lib.lib().ragk_qkv_attn_oproj_fused(
-        h.data_ptr(), h.stride(0), g_in.data_ptr(), float(eps_in), wqkv.data_ptr(), wqkv.stride(0), Nq, K,
+        h.data_ptr(), h.stride(0), ptr(g_in), float(eps_in), wqkv.data_ptr(), wqkv.stride(0), Nq, K,
         Pq.data_ptr(), qks, positions.data_ptr(), slots.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(),
         k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0), kv_lens.data_ptr(),
         ws_o.data_ptr(), ws_ml.data_ptr(), B, Hq, Hkv, D, part_tiles, max_parts, float(scale), wo.data_ptr(),
-        wo.stride(0), Po.data_ptr(), N, ks, cnt.data_ptr(), ATTN_OPROJ_SPIN_US, h.data_ptr(), h.stride(0),
-        g_post.data_ptr(), xn.data_ptr(), xn.stride(0), float(eps), stream_ptr()), "ragk_qkv_attn_oproj_fused")
-    return xn
+        wo.stride(0), Po.data_ptr(), N, ks, cnt.data_ptr(), ATTN_OPROJ_SPIN_US, h.data_ptr() if tail else None,
+        h.stride(0) if tail else 0, ptr(g_post), ptr(xn), xn.stride(0) if tail else 0, float(eps), stream_ptr()),
+        "ragk_qkv_attn_oproj_fused")
+    return xn if tail else Po
 
 
 SILU_MAX_SLABS = 4  # gemm_part.hip SG_MAXS

@@ -698,6 +698,16 @@ def test_qkv_attn_oproj_matches_unfused(native, kv_lens, Hq, Hkv, qks):
         assert int(native.attn_oproj_counters(DEV)[:5].abs().sum().item()) == 0  # re-armed
     finally:
         native.QAO_QKS = old
+    # tensor-parallel form: pre-normalised rows in, o_proj slabs out (no norm tail)
+    xin = native.rmsnorm(h0, g_in, 1e-5)
+    old = native.QAO_QKS
+    native.QAO_QKS = qks
+    try:
+        Po = native.qkv_attn_oproj(xin, None, 0.0, wqkv, pos, cos, sin, slots, kc.clone(), vc.clone(), bt, kvl, Hq,
+                                   Hkv, D, pt, mp, ws_o, ws_ml, wo, None, 0.0)
+    finally:
+        native.QAO_QKS = old
+    assert rel_err(Po.sum(0).cpu(), native.gemm_part(attn, wo).sum(0).cpu()) < 2e-2
     # k rows appended from differently-ordered fp32 slab sums may differ by 1 bf16 ulp
     assert rel_err(kc1.float().cpu(), kc2.float().cpu()) < 1e-2 and rel_err(vc1.float().cpu(), vc2.float().cpu()) < 1e-2
     for h1, xn1 in res:
