@@ -239,6 +239,8 @@ class NativeBackend(TorchBackend):
 
         self.n = native
         native._lib.lib()  # fail loudly now if the gfx950 library is missing
+        if torch.device(device).type == "cuda" and torch.cuda.is_available():
+            native.attn_oproj_counters(device)  # before any graph capture
 
     def gemm(self, x, w, bias=None, resid=None, epi="none", out=None, out_f32=False):
         if isinstance(w, Fp8Weight):

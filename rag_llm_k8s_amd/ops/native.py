@@ -354,17 +354,24 @@ def attn_oproj_ok(M, w, Hq, Hkv, D, max_parts, ws_o):
     return w.dtype == torch.bfloat16 and K == Hq * D and K % (64 * ATTN_OPROJ_KS) == 0
 
 
+def _dev_key(device):
+    d = torch.device(device)
+    return d.index if d.index is not None else torch.cuda.current_device()
+
+
 def attn_oproj_counters(device):
-    """The fused launch's counters (attention done, o_proj past its wait, error): zeroed once, re-armed
-    by the kernel itself after every launch (graph replays included)."""
-    key = str(device)
+    """The fused launch's counters (attention done, o_proj past its wait, error, -, qkv done): zeroed once,
+    re-armed by the kernel itself after every launch (graph replays included). Allocated when the native
+    backend is created, never inside a graph capture (the buffer must outlive every graph)."""
+    key = _dev_key(device)
     if key not in _ao_cnt:
-        _ao_cnt[key] = torch.zeros(16, dtype=torch.int32, device=device)
+        _req(not torch.cuda.is_current_stream_capturing(), "fused-launch counters allocated inside a graph capture")
+        _ao_cnt[key] = torch.zeros(16, dtype=torch.int32, device=torch.device("cuda", key))
     return _ao_cnt[key]
 
 
 def attn_oproj_error(device) -> bool:
-    c = _ao_cnt.get(str(device))
+    c = _ao_cnt.get(_dev_key(device))
     return bool(c is not None and int(c[2].item()) != 0)
 
 
