@@ -1222,10 +1222,25 @@ constexpr int decode_lds_bytes() { return 4 * Cfg<D>::TILEB + G * D * 2; }
 // every storing wave has drained its write-through (sc1) stores, then one lane adds to the agent-scope
 // counter the o_proj blocks poll (MI355X_MICROARCH.md "Valid forms": sc1 stores, vmcnt(0), barrier,
 // agent atomic; the consumer polls with sc1 loads and reads the bytes with sc1 loads only).
-__device__ __forceinline__ void decode_signal(int* cnt) {
+// Stage hand-off of the fused launches: arrivals count on ONE counter; the block whose add returns
+// total - 1 (every other producer's stores were drained before its add) raises a done flag in FL_REPL
+// replicas, each on its own 128-B line, and consumers poll the replica of their block index with a long
+// s_sleep -- hundreds of pollers on the counter itself (one line, hammered while it is being
+// incremented) slowed the whole launch (MI355X_MICROARCH.md polling-cost / fanin).
+constexpr int FL_REPL = 16;       // flag replicas
+constexpr int FL_STRIDE = 32;     // ints between replicas (128 B)
+constexpr int FL_A = 64;          // cnt offset of the attention-done flags
+constexpr int FL_Q = FL_A + FL_REPL * FL_STRIDE;  // cnt offset of the qkv-done flags
+constexpr int CNT_INTS = FL_Q + FL_REPL * FL_STRIDE;
+__device__ __forceinline__ void stage_arrive(int* cnt, int total, int* flags) {
   wait_vmcnt0();
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    if (__hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+#pragma unroll
+      for (int k = 0; k < FL_REPL; ++k) __hip_atomic_store(flags + k * FL_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // One split-K partition block of decode attention: partition `part` of KV head `kvh` of sequence `b`.
@@ -1266,11 +1281,12 @@ __device__ __forceinline__ void sum_partials8x2_sc1(__amdgpu_buffer_rsrc_t rs, i
 
 // Bounded poll of an agent-scope counter by one lane (sc1 loads), then the block's barrier. Sets err[0]
 // and gives up (the block computes garbage, never hangs) after `limit` s_memrealtime ticks.
-__device__ __forceinline__ void wait_counter(const int* cnt, int need, int* err, unsigned limit) {
+__device__ __forceinline__ void wait_flag(const int* flags, int* err, unsigned limit) {
   if (threadIdx.x == 0) {
+    const int* f = flags + (blockIdx.x % FL_REPL) * FL_STRIDE;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-      __builtin_amdgcn_s_sleep(1);
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      __builtin_amdgcn_s_sleep(8);
       if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -1280,16 +1296,16 @@ __device__ __forceinline__ void wait_counter(const int* cnt, int need, int* err,
   __syncthreads();
 }
 
+
 struct QWait {       // attention blocks waiting for the in-launch qkv blocks (QW mode)
-  const int* cnt;    // qkv blocks done
-  int need;
+  const int* flags;  // qkv-done flag replicas
   int* err;
   unsigned limit;
 };
 
 template <int D, int G, bool NT = false, bool FUSED = false, bool QW = false>
 __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part, int kvh, int b, char* smem,
-                                                  int* fused_cnt = nullptr, QWait qw = {}) {
+                                                  int* fused_cnt = nullptr, QWait qw = {}, int fused_total = 0) {
   using C = Cfg<D>;
   static_assert(G <= 16, "at most 16 query heads per KV head");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1299,9 +1315,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
   const int pt = decode_part_tiles(n_kt, a);
   const int kt0 = part * pt;
   if (kt0 >= n_kt) {  // block-uniform early exit (before any barrier)
-    if constexpr (FUSED) {
-      if (threadIdx.x == 0) __hip_atomic_fetch_add(fused_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if constexpr (FUSED) stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
     return;
   }
   const int kt1 = min(kt0 + pt, n_kt);
@@ -1330,7 +1344,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
                                                                                    32 * s + 8 * fh))
                        : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
   }
-  if constexpr (QW) wait_counter(qw.cnt, qw.need, qw.err, qw.limit);  // the KV prefetch above is in flight
+  if constexpr (QW) wait_flag(qw.flags, qw.err, qw.limit);  // the KV prefetch above is in flight
   if (a.qkv_p != nullptr) {
     // q = RoPE(bf16(sum_s P[s][b])) for this KV head's G query heads, one (d, d + D/2) rotate_half
     // pair of 8-vectors per thread (G * D/16 threads, all slab loads of a thread in flight together),
@@ -1523,7 +1537,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     }
   }
   if constexpr (FUSED) {
-    decode_signal(fused_cnt);
+    stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
     return;
   }
   if (nparts == 1 || a.counters == nullptr) return;
@@ -1651,18 +1665,9 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
 #pragma unroll
   for (int ks = 0; ks < NLD; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
 
-  // 2) wait for every attention block (one lane polls with sc1 loads; the others wait at the barrier)
-  if (tid == 0) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(o.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < o.na) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > o.spin_limit) {  // never hang: flag it, compute garbage
-        __hip_atomic_store(o.cnt + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
+  // 2) wait for every attention block (one lane polls a done-flag replica; the others wait at the barrier;
+  //    a bounded wait: on timeout the error word is set and the block computes garbage, never hangs)
+  wait_flag(o.cnt + FL_A, o.cnt + 2, o.spin_limit);
 
   // 3) merge the partitions of (row r, head h0 + j): pass 1 the statistics -> per-partition scales and
   //    the merged sum in LDS, pass 2 the partial outputs (all loads of a thread in flight: the scales are
@@ -1795,10 +1800,15 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
   if (tid == 0) {
     const int old = __hip_atomic_fetch_add(o.cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == o.nob - 1;
-    if (last) {  // (cnt[4]: the 3-role launch's qkv-done counter; every attention block is past its wait)
+    if (last) {  // (cnt[4] + the qkv flags: the 3-role launch's; every attention block is past its wait)
       __hip_atomic_store(o.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(o.cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(o.cnt + 4, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < FL_REPL; ++k) {
+        __hip_atomic_store(o.cnt + FL_A + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(o.cnt + FL_Q + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     *s_last = last;
   }
@@ -1989,7 +1999,7 @@ __device__ __forceinline__ void qkv_norm_block(const QkvArgs& q, int qb, char* s
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[r]), rs_p, (int)((((size_t)s * M + r) * q.N + col) * 4),
                                               0, 16);
   }
-  decode_signal(cnt + 4);
+  stage_arrive(cnt + 4, q.nqb, cnt + FL_Q);
 }
 
 template <int D, int G, int NLD>
@@ -2018,7 +2028,7 @@ __global__ __launch_bounds__(256, 2) void attn_oproj_kernel(DecodeArgs a, OprojA
   if (bid < o.na) {
     const int mp = a.max_parts;
     attn_decode_block<D, G, false, true, (QNLD > 0)>(a, bid % mp, (bid / mp) % a.Hkv, bid / (mp * a.Hkv), smem,
-                                                     o.cnt, QWait{o.cnt + 4, q.nqb, o.cnt + 2, o.spin_limit});
+                                                     o.cnt, QWait{o.cnt + FL_Q, o.cnt + 2, o.spin_limit}, o.na);
     return;
   }
   oproj_merge_block<D, NLD>(a, o, bid - o.na, smem);
@@ -2318,7 +2328,8 @@ static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* co
 // Fused decode attention (RoPE + KV append from the qkv split-K slabs, as ragk_attn_decode_rope) and
 // o_proj split-K partials (as ragk_gemm_part_merge) in ONE launch: attn_oproj_kernel. B <= 4, D = 128,
 // G in {4, 8}; Wo bf16 [N][Hq * D] (ldw elements); Pout fp32 [K / KS][B][N], KS = 64 * ks_steps
-// (ks_steps 4, 8 or 16). cnt: >= 3 zeroed ints owned by the caller (re-armed by the kernel itself).
+// (ks_steps 4, 8 or 16). cnt: ragk_attn_oproj_cnt_ints() zeroed ints owned by the caller (re-armed by
+// the kernel itself).
 // h != nullptr: the residual + RMSNorm tail (h += bf16(sum of slabs), xn = rmsnorm(h) * gamma; the
 // add_partials_rmsnorm consumer) runs in the last o_proj block.
 // part_o / part_ml: the partition workspace (required, also for one partition).
@@ -2417,3 +2428,5 @@ RAGK_API int ragk_qkv_attn_oproj_fused(const void* h, int ldh, const void* gin, 
 #undef RAGK_QAO
   return (int)hipErrorInvalidValue;
 }
+
+RAGK_API int ragk_attn_oproj_cnt_ints() { return CNT_INTS; }

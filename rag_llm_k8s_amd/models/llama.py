@@ -378,7 +378,10 @@ class LlamaModel:
                  and be.part_merge_ok(M, inp.meta, layers[0]["wo"], Hq, D))
         # batch <= 4: attention and o_proj in ONE launch (attention.hip attn_oproj_kernel) -- the o_proj
         # weight stream overlaps the KV stream instead of following it
-        fused_ao = (DECODE_ROPE_FUSED and not pf and be.attn_oproj_ok(M, inp.meta, layers[0]["wo"], Hq, Hkv, D))
+        # (never when another process drives this GPU: its waiting blocks could hold the CU slots this
+        # launch's producer blocks need)
+        fused_ao = (DECODE_ROPE_FUSED and not pf and not (tp and getattr(self.comm, "shares_device", False))
+                    and be.attn_oproj_ok(M, inp.meta, layers[0]["wo"], Hq, Hkv, D))
         # ... and, at TP=1, the residual + post-attention norm in its last block (no consumer launch)
         ao_norm = fused_ao and not tp and be.attn_oproj_norm_ok(layers[0]["wo"])
         # ... and the qkv projection with the input norm as well: the layer's attention half is ONE launch

@@ -89,6 +89,7 @@ _SIGS = {
     "ragk_gemm_fp8": [P, I, P, I, P, P, I, P, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_attn_oproj_fused": [P, I, I, P, P, P, P, P, P, P, I, P, P, P, I, I, I, I, I, I, F, P, I, P, I, I, P,
                               ctypes.c_uint, P, I, P, P, I, F, S],
+    "ragk_attn_oproj_cnt_ints": [],
     "ragk_qkv_attn_oproj_fused": [P, I, P, F, P, I, I, I, P, I, P, P, P, P, P, P, P, I, P, P, P, I, I, I, I, I, I, F,
                                   P, I, P, I, I, P, ctypes.c_uint, P, I, P, P, I, F, S],
     # csrc/comm/allreduce.hip (xGMI peer-mapped all-reduce)

@@ -366,7 +366,8 @@ def attn_oproj_counters(device):
     key = _dev_key(device)
     if key not in _ao_cnt:
         _req(not torch.cuda.is_current_stream_capturing(), "fused-launch counters allocated inside a graph capture")
-        _ao_cnt[key] = torch.zeros(16, dtype=torch.int32, device=torch.device("cuda", key))
+        n = int(_lib.lib().ragk_attn_oproj_cnt_ints())
+        _ao_cnt[key] = torch.zeros(max(n, 16), dtype=torch.int32, device=torch.device("cuda", key))
     return _ao_cnt[key]
 
 

@@ -113,6 +113,13 @@ class TPComm:
         peer-mapped path: the fallback is an ordinary all-reduce)."""
         return self.ipc is None or self.ipc.fused_ok(M, H)
 
+    @property
+    def shares_device(self) -> bool:
+        """Another rank of this group drives the same GPU (single-GPU rehearsals)."""
+        return bool(self.ipc is not None and getattr(self.ipc, "shares_device", False)) or (
+            self.ipc is None and str(self.device).startswith("cuda") and self.size > 1
+            and os.environ.get("RAGK_ALLOW_SHARED_DEVICE", "0") == "1")
+
     def all_reduce_async(self, x: torch.Tensor):
         """Start an in-place all-reduce of x; returns a handle whose wait() makes the CURRENT stream
         (GPU) or the host (gloo) wait for it. x must not be touched until then."""
@@ -203,6 +210,8 @@ class TPComm:
 
 
 class SingleRankTPComm:
+    shares_device = False  # one process: the fused decode launches are safe
+
     """One-GPU stand-in for rank `rank` of a `size`-way TP group (probes of a TP shard's step time):
     the model and engine take their TP code paths, and every collective is replaced by a same-sized
     call of the peer-mapped kernels on a ONE-rank communicator (the barrier and the loads hit local

@@ -85,6 +85,10 @@ class IPCAllReduce:
         handles = [r[0] for r in recs]
         self.peer_devices = [r[1] for r in recs]
         self.cross_device = any(d != me[1] for d in self.peer_devices)
+        # another rank drives this same GPU (single-GPU rehearsals): the fused decode launches, whose blocks
+        # wait on other blocks of the same launch, must not run -- other processes' waiting blocks could hold
+        # the CU slots their producers need (ops/native.py attn_oproj)
+        self.shares_device = sum(d == me[1] for d in self.peer_devices) > 1
         self.set_fences(fences_for(self.cross_device))
         joined = ctypes.create_string_buffer(b"".join(handles), hs * size)
         with torch.cuda.device(self.device):
