@@ -1231,7 +1231,8 @@ constexpr int FL_REPL = 16;       // flag replicas
 constexpr int FL_STRIDE = 32;     // ints between replicas (128 B)
 constexpr int FL_A = 64;          // cnt offset of the attention-done flags
 constexpr int FL_Q = FL_A + FL_REPL * FL_STRIDE;  // cnt offset of the qkv-done flags
-constexpr int CNT_INTS = FL_Q + FL_REPL * FL_STRIDE;
+constexpr int CNT_TICKETS = FL_Q + FL_REPL * FL_STRIDE;  // MIA: per (sequence, KV head) merge tickets
+constexpr int CNT_INTS = CNT_TICKETS + 4 * 64;
 __device__ __forceinline__ void stage_arrive(int* cnt, int total, int* flags) {
   wait_vmcnt0();
   __syncthreads();
@@ -1303,7 +1304,18 @@ struct QWait {       // attention blocks waiting for the in-launch qkv blocks (Q
   unsigned limit;
 };
 
-template <int D, int G, bool NT = false, bool FUSED = false, bool QW = false>
+// bf16 pair (d, d + 1) of an attention output row, stored write-through for the o_proj blocks of the
+// same launch (4 B per store: a 2-B write-through store costs ~2x per byte).
+__device__ __forceinline__ void out_pair_sc1(const DecodeArgs& a, int b, int col, float x, float y) {
+  const int nb = a.nb ? a.nb : (int)gridDim.z;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, nb * a.out_stride * 2, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(pk2bf(x, y), rs, (b * a.out_stride + col) * 2, 0, 16);
+}
+
+// MIA (FUSED only): the partitions of a (sequence, KV head) are merged by the last of its partition blocks
+// (ticket counters a.counters) into the bf16 attention output, written through; the o_proj blocks then
+// stage a plain bf16 activation slice instead of each merging the records of its K-slice.
+template <int D, int G, bool NT = false, bool FUSED = false, bool QW = false, bool MIA = false>
 __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part, int kvh, int b, char* smem,
                                                   int* fused_cnt = nullptr, QWait qw = {}, int fused_total = 0) {
   using C = Cfg<D>;
@@ -1502,6 +1514,28 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
 #pragma unroll
     for (int r = 0; r < 4; ++r) so[(wid * 16 + fr) * D + 16 * dt + 4 * fh + r] = o[dt][r];
   __syncthreads();
+  if constexpr (FUSED && MIA) {
+    if (nparts == 1) {  // the block's output is final: bf16 pairs, written through
+      for (int e2 = threadIdx.x; e2 < G * D / 2; e2 += 256) {
+        const int g = (2 * e2) / D, d = (2 * e2) % D;
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[w * 16 + g]);
+        const float Mu = M == -INFINITY ? 0.f : M;
+        float L = 0.f, O0 = 0.f, O1 = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const float sc = exp2f(sm[w * 16 + g] - Mu);
+          L += (sl[w * 64 + g] + sl[w * 64 + g + 16] + sl[w * 64 + g + 32] + sl[w * 64 + g + 48]) * sc;
+          O0 += so[(w * 16 + g) * D + d] * sc;
+          O1 += so[(w * 16 + g) * D + d + 1] * sc;
+        }
+        out_pair_sc1(a, b, (kvh * G + g) * D + d, L > 0.f ? O0 / L : 0.f, L > 0.f ? O1 / L : 0.f);
+      }
+      stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
+      return;
+    }
+  }
   // thread -> (g, d) pairs
   for (int e = threadIdx.x; e < G * D; e += 256) {
     const int g = e / D, d = e % D;
@@ -1536,11 +1570,11 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
       }
     }
   }
-  if constexpr (FUSED) {
+  if constexpr (FUSED && !MIA) {
     stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
     return;
   }
-  if (nparts == 1 || a.counters == nullptr) return;
+  if (!FUSED && (nparts == 1 || a.counters == nullptr)) return;
 
   // ---- fused split-K merge: the last of this (b, kvh)'s nparts partition blocks to finish merges
   // them (same math as attn_decode_reduce_kernel), so the merge costs no extra launch. The partials
@@ -1556,7 +1590,10 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     s_last = (old == nparts - 1);
   }
   __syncthreads();
-  if (!s_last) return;
+  if (!s_last) {
+    if constexpr (FUSED) stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
+    return;
+  }
   asm volatile("" ::: "memory");  // the sc1 loads below stay after the ticket
   float* s_m = reinterpret_cast<float*>(smem);  // [G][nparts] partition max, then its scale
   float* s_l = s_m + G * nparts;                 // [G][nparts] partition sum
@@ -1583,6 +1620,37 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     s_L[g] = L;
   }
   __syncthreads();
+  if constexpr (FUSED) {
+    // pairs (d, d + 1): two 8-byte record loads per partition, one 4-byte write-through output store
+    for (int e2 = threadIdx.x; e2 < G * D / 2; e2 += 256) {
+      const int g = (2 * e2) / D, d = (2 * e2) % D;
+      const int po = (int)(((hb + g) * a.max_parts * D + d) * 4);
+      const float* sc = s_m + g * nparts;
+      float O0 = 0.f, O1 = 0.f;
+      int p = 0;
+      for (; p + 8 <= nparts; p += 8) {
+        f32x2 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          v[i] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_o, po + (p + i) * D * 4, 0, 16));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          O0 += v[i][0] * sc[p + i];
+          O1 += v[i][1] * sc[p + i];
+        }
+      }
+      for (; p < nparts; ++p) {
+        const f32x2 v = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_o, po + p * D * 4, 0, 16));
+        O0 += v[0] * sc[p];
+        O1 += v[1] * sc[p];
+      }
+      const float L = s_L[g];
+      out_pair_sc1(a, b, (kvh * G + g) * D + d, L > 0.f ? O0 / L : 0.f, L > 0.f ? O1 / L : 0.f);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(a.counters + b * a.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
+    return;
+  }
   for (int e = threadIdx.x; e < G * D; e += 256) {
     const int g = e / D, d = e % D;
     const int po = (int)(((hb + g) * a.max_parts * D + d) * 4);  // byte offset of partition 0
@@ -1644,7 +1712,7 @@ struct OprojArgs {
 };
 constexpr int OP_MAXP = 64;  // partitions per (row, head) merged in LDS
 
-template <int D, int NLD>
+template <int D, int NLD, bool MIA = false>
 __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const OprojArgs& o, int ob, char* smem) {
   constexpr int KS = 32 * NLD;          // K-slice (NLD 32-k MFMA steps, one 16-B load each per lane)
   constexpr int ROWB = KS * 2;          // bytes per row of the LDS activation slice
@@ -1668,6 +1736,27 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
   // 2) wait for every attention block (one lane polls a done-flag replica; the others wait at the barrier;
   //    a bounded wait: on timeout the error word is set and the block computes garbage, never hangs)
   wait_flag(o.cnt + FL_A, o.cnt + 2, o.spin_limit);
+  if constexpr (MIA) {
+    // the attention blocks merged the partitions: stage the bf16 rows of this K-slice (write-through loads)
+    const __amdgpu_buffer_rsrc_t rs_x =
+        __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, M * a.out_stride * 2, 0x00020000);
+    constexpr int CPR = KS / 8;  // 16-B chunks per slice row
+    u32x4 xv[(4 * CPR + 255) / 256];
+#pragma unroll
+    for (int i = 0; i < (4 * CPR + 255) / 256; ++i) {
+      const int e = min(tid + 256 * i, M * CPR - 1);
+      const int r = e / CPR, c = e % CPR;
+      xv[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, (r * a.out_stride + kbase + 8 * c) * 2, 0, 16));
+    }
+#pragma unroll
+    for (int i = 0; i < (4 * CPR + 255) / 256; ++i) {
+      const int e = tid + 256 * i;
+      if (e < M * CPR) {
+        const int r = e / CPR, c = e % CPR;
+        *reinterpret_cast<u32x4*>(smem + r * ROWB + 16 * ((c & ~15) | ((c & 15) ^ (r & 15)))) = xv[i];
+      }
+    }
+  } else {
 
   // 3) merge the partitions of (row r, head h0 + j): pass 1 the statistics -> per-partition scales and
   //    the merged sum in LDS, pass 2 the partial outputs (all loads of a thread in flight: the scales are
@@ -1765,6 +1854,7 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
       *reinterpret_cast<uint2*>(smem + r * ROWB + 16 * c + 8 * (d4 & 1)) = w;
     }
   }
+  }  // !MIA
   __syncthreads();
 
   // 4) MFMA over the slice: A = activation rows (fr), B = this wave's weight columns
@@ -2012,7 +2102,7 @@ constexpr int attn_oproj_lds() {
 // QNLD > 0: the 3-role launch -- blocks [0, nqb) are qkv blocks (qkv_norm_block<QNLD>), then the
 // attention blocks (they prefetch their first KV tile, then wait for every qkv block), then the o_proj
 // blocks. Every wait is on lower-indexed blocks only.
-template <int D, int G, int NLD, int QNLD = 0>
+template <int D, int G, int NLD, int QNLD = 0, bool MIA = false>
 __global__ __launch_bounds__(256, 2) void attn_oproj_kernel(DecodeArgs a, OprojArgs o, QkvArgs q) {
   constexpr int lds_q = QNLD > 0 ? 16 * 64 * QNLD + 64 : 0;
   constexpr int lds = attn_oproj_lds<D, G, NLD>() > lds_q ? attn_oproj_lds<D, G, NLD>() : lds_q;
@@ -2027,11 +2117,12 @@ __global__ __launch_bounds__(256, 2) void attn_oproj_kernel(DecodeArgs a, OprojA
   }
   if (bid < o.na) {
     const int mp = a.max_parts;
-    attn_decode_block<D, G, false, true, (QNLD > 0)>(a, bid % mp, (bid / mp) % a.Hkv, bid / (mp * a.Hkv), smem,
-                                                     o.cnt, QWait{o.cnt + FL_Q, o.cnt + 2, o.spin_limit}, o.na);
+    attn_decode_block<D, G, false, true, (QNLD > 0), MIA>(a, bid % mp, (bid / mp) % a.Hkv, bid / (mp * a.Hkv),
+                                                          smem, o.cnt, QWait{o.cnt + FL_Q, o.cnt + 2, o.spin_limit},
+                                                          o.na);
     return;
   }
-  oproj_merge_block<D, NLD>(a, o, bid - o.na, smem);
+  oproj_merge_block<D, NLD, MIA>(a, o, bid - o.na, smem);
 }
 
 // merge split-K partitions: grid (Hq, B), block D threads. The partition statistics are loaded by
@@ -2339,7 +2430,7 @@ RAGK_API int ragk_attn_oproj_fused(const float* P, int S, int ldp, const int* po
                                    float* part_ml, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
                                    float scale, const void* Wo, int ldw, float* Pout, int N, int ks_steps, int* cnt,
                                    unsigned spin_us, void* h, int ldh, const void* gamma, void* xn, int ldx,
-                                   float eps, hipStream_t st) {
+                                   float eps, void* attn_out, hipStream_t st) {
   if (B <= 0) return 0;
   const int G = Hq / (Hkv > 0 ? Hkv : 1);
   const int K = Hq * D;
@@ -2362,10 +2453,18 @@ RAGK_API int ragk_attn_oproj_fused(const float* P, int S, int ldp, const int* po
               (bf16_t*)xn, ldx, eps};
   const dim3 grid(o.na + o.nob);
   const QkvArgs q{};
-#define RAGK_AO(GG, NL)                                                                       \
-  if (G == GG && 2 * ks_steps == NL) {                                                        \
-    hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL>), grid, dim3(256), 0, st, a, o, q);    \
-    return (int)hipGetLastError();                                                            \
+  const bool mia = attn_out != nullptr;  // partitions merged by the attention blocks into attn_out
+  if (mia) {
+    a.out = (bf16_t*)attn_out;
+    a.out_stride = K;
+    a.counters = cnt + CNT_TICKETS;
+    if (B * Hkv > 4 * 64) return (int)hipErrorInvalidValue;
+  }
+#define RAGK_AO(GG, NL)                                                                                \
+  if (G == GG && 2 * ks_steps == NL) {                                                                 \
+    if (mia) hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL, 0, true>), grid, dim3(256), 0, st, a, o, q); \
+    else hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL>), grid, dim3(256), 0, st, a, o, q);         \
+    return (int)hipGetLastError();                                                                     \
   }
   RAGK_AO(4, 8)
   RAGK_AO(4, 16)
@@ -2391,7 +2490,7 @@ RAGK_API int ragk_qkv_attn_oproj_fused(const void* h, int ldh, const void* gin, 
                                        float* part_ml, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
                                        float scale, const void* Wo, int ldw, float* Pout, int N, int ks_steps,
                                        int* cnt, unsigned spin_us, void* h2, int ldh2, const void* gamma, void* xn,
-                                       int ldx, float eps, hipStream_t st) {
+                                       int ldx, float eps, void* attn_out, hipStream_t st) {
   if (B <= 0) return 0;
   const int G = Hq / (Hkv > 0 ? Hkv : 1);
   const int Ko = Hq * D;
@@ -2416,10 +2515,18 @@ RAGK_API int ragk_qkv_attn_oproj_fused(const void* h, int ldh, const void* gin, 
   const QkvArgs q{(const bf16_t*)Wqkv, ldwq, (const bf16_t*)h, ldh, (const bf16_t*)gin, eps_in, Pq, B, Nq, K,
                   ((Nq + 63) / 64) * S};
   const dim3 grid(q.nqb + o.na + o.nob);
-#define RAGK_QAO(GG, NL, QN)                                                                     \
-  if (G == GG && 2 * ks_steps == NL && 2 * q_ks == QN) {                                         \
-    hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL, QN>), grid, dim3(256), 0, st, a, o, q);   \
-    return (int)hipGetLastError();                                                               \
+  const bool mia = attn_out != nullptr;
+  if (mia) {
+    a.out = (bf16_t*)attn_out;
+    a.out_stride = Ko;
+    a.counters = cnt + CNT_TICKETS;
+    if (B * Hkv > 4 * 64) return (int)hipErrorInvalidValue;
+  }
+#define RAGK_QAO(GG, NL, QN)                                                                                 \
+  if (G == GG && 2 * ks_steps == NL && 2 * q_ks == QN) {                                                     \
+    if (mia) hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL, QN, true>), grid, dim3(256), 0, st, a, o, q); \
+    else hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL, QN>), grid, dim3(256), 0, st, a, o, q);          \
+    return (int)hipGetLastError();                                                                           \
   }
   RAGK_QAO(4, 16, 16)
   RAGK_QAO(4, 16, 32)

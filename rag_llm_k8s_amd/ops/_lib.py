@@ -88,10 +88,10 @@ _SIGS = {
     "ragk_quant_fp8_rows": [P, I, P, I, P, I, I, S],
     "ragk_gemm_fp8": [P, I, P, I, P, P, I, P, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_attn_oproj_fused": [P, I, I, P, P, P, P, P, P, P, I, P, P, P, I, I, I, I, I, I, F, P, I, P, I, I, P,
-                              ctypes.c_uint, P, I, P, P, I, F, S],
+                              ctypes.c_uint, P, I, P, P, I, F, P, S],
     "ragk_attn_oproj_cnt_ints": [],
     "ragk_qkv_attn_oproj_fused": [P, I, P, F, P, I, I, I, P, I, P, P, P, P, P, P, P, I, P, P, P, I, I, I, I, I, I, F,
-                                  P, I, P, I, I, P, ctypes.c_uint, P, I, P, P, I, F, S],
+                                  P, I, P, I, I, P, ctypes.c_uint, P, I, P, P, I, F, P, S],
     # csrc/comm/allreduce.hip (xGMI peer-mapped all-reduce)
     "ragk_ar_create": [I, I, ctypes.c_long, I, I, I],
     "ragk_ar_add_rmsnorm": [P, P, I, I, P, I, P, P, I, I, F, I, S],

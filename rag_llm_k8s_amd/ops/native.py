@@ -338,6 +338,20 @@ ATTN_OPROJ_KS = int(os.environ.get("RAGK_ATTN_OPROJ_KS", "8"))  # K-slice steps 
 # the residual + RMSNorm consumer inside the fused launch (its last o_proj block), TP=1 only
 ATTN_OPROJ_NORM = os.environ.get("RAGK_ATTN_OPROJ_NORM", "1") == "1"
 ATTN_OPROJ_SPIN_US = int(os.environ.get("RAGK_ATTN_OPROJ_SPIN_US", "1000000"))
+# where the split-K attention partitions are merged inside the fused launch: 1 = by the last partition
+# block of each (sequence, KV head), into a bf16 row the o_proj blocks stage (once per head);
+# 0 = by every o_proj block for the heads of its K-slice (no extra hand-off, redundant record reads)
+ATTN_OPROJ_MIA = os.environ.get("RAGK_AO_MIA", "1") == "1"
+_ao_ws = {}
+
+
+def _ao_attn_out(B, K, device):
+    """bf16 [B, K] attention-output workspace of the fused launch (MIA); one per (device, shape)."""
+    key = (_dev_key(device), B, K)
+    t = _ao_ws.get(key)
+    if t is None:
+        t = _ao_ws[key] = torch.empty((B, K), dtype=torch.bfloat16, device=torch.device("cuda", key[0]))
+    return t
 _ao_cnt = {}
 
 
@@ -409,8 +423,8 @@ def attn_oproj(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_tables
         k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0), kv_lens.data_ptr(),
         ws_o.data_ptr(), ws_ml.data_ptr(), B, Hq, Hkv, D, part_tiles, max_parts, float(scale), w.data_ptr(),
         w.stride(0), out.data_ptr(), N, ks, cnt.data_ptr(), ATTN_OPROJ_SPIN_US, ptr(h), h.stride(0) if h is not None
-        else 0, ptr(gamma), ptr(xn), xn.stride(0) if xn is not None else 0, float(eps), stream_ptr()),
-        "ragk_attn_oproj_fused")
+        else 0, ptr(gamma), ptr(xn), xn.stride(0) if xn is not None else 0, float(eps),
+        ptr(_ao_attn_out(B, K, P.device)) if ATTN_OPROJ_MIA else None, stream_ptr()), "ragk_attn_oproj_fused")
     return out if norm is None else xn
 
 
@@ -463,7 +477,8 @@ def qkv_attn_oproj(h, g_in, eps_in, wqkv, positions, cos_t, sin_t, slots, k_cach
         k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0), kv_lens.data_ptr(),
         ws_o.data_ptr(), ws_ml.data_ptr(), B, Hq, Hkv, D, part_tiles, max_parts, float(scale), wo.data_ptr(),
         wo.stride(0), Po.data_ptr(), N, ks, cnt.data_ptr(), ATTN_OPROJ_SPIN_US, h.data_ptr() if tail else None,
-        h.stride(0) if tail else 0, ptr(g_post), ptr(xn), xn.stride(0) if tail else 0, float(eps), stream_ptr()),
+        h.stride(0) if tail else 0, ptr(g_post), ptr(xn), xn.stride(0) if tail else 0, float(eps),
+        ptr(_ao_attn_out(B, wo.shape[1], h.device)) if ATTN_OPROJ_MIA else None, stream_ptr()),
         "ragk_qkv_attn_oproj_fused")
     return xn if tail else Po
 
