@@ -7,12 +7,12 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread \
   -k "attn_oproj or gemm_part_merge or attn_decode_rope" > gpurun_out/r4d_fused.log 2>&1 || exit $?
-for mode in "qao:X=1" "ao:RAGK_DECODE_QAO=0" "aonn:RAGK_DECODE_QAO=0 RAGK_ATTN_OPROJ_NORM=0" "unfused:RAGK_DECODE_ATTN_OPROJ=0"; do
+for mode in "qao:X=1" "qao0:RAGK_AO_MIA=0" "ao:RAGK_DECODE_QAO=0" "ao0:RAGK_DECODE_QAO=0 RAGK_AO_MIA=0" "unfused:RAGK_DECODE_ATTN_OPROJ=0"; do
   name=${mode%%:*}; envs=${mode#*:}
   env $envs C1_N=4 timeout -k 10 300 python tools/c1_probe.py > gpurun_out/r4d_c1_$name.log 2>&1 || exit $?
   echo "$name: $(tail -1 gpurun_out/r4d_c1_$name.log)"
 done
-for mode in "qao:X=1" "unfused:RAGK_DECODE_ATTN_OPROJ=0"; do
+for mode in "qao:X=1" "ao:RAGK_DECODE_QAO=0" "unfused:RAGK_DECODE_ATTN_OPROJ=0"; do
   name=${mode%%:*}; envs=${mode#*:}
   mkdir -p gpurun_out/pc1_$name
   env $envs C1_N=2 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pc1_$name -o run \
