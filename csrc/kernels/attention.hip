@@ -1227,6 +1227,15 @@ constexpr int decode_lds_bytes() { return 4 * Cfg<D>::TILEB + G * D * 2; }
 // replicas, each on its own 128-B line, and consumers poll the replica of their block index with a long
 // s_sleep -- hundreds of pollers on the counter itself (one line, hammered while it is being
 // incremented) slowed the whole launch (MI355X_MICROARCH.md polling-cost / fanin).
+// In-kernel stamps of the fused launches (diagnostic instantiation only, tools/fused_stamps.py): lane 0
+// of a block writes s_memrealtime (100 MHz, device-wide) at stage boundaries into g_fused_stamps[block][k].
+__device__ unsigned long long* g_fused_stamps;
+template <bool ST>
+__device__ __forceinline__ void fstamp(int k) {
+  if constexpr (ST) {
+    if (threadIdx.x == 0) g_fused_stamps[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  }
+}
 constexpr int FL_REPL = 16;       // flag replicas
 constexpr int FL_STRIDE = 32;     // ints between replicas (128 B)
 constexpr int FL_A = 64;          // cnt offset of the attention-done flags
@@ -1315,9 +1324,10 @@ __device__ __forceinline__ void out_pair_sc1(const DecodeArgs& a, int b, int col
 // MIA (FUSED only): the partitions of a (sequence, KV head) are merged by the last of its partition blocks
 // (ticket counters a.counters) into the bf16 attention output, written through; the o_proj blocks then
 // stage a plain bf16 activation slice instead of each merging the records of its K-slice.
-template <int D, int G, bool NT = false, bool FUSED = false, bool QW = false, bool MIA = false>
+template <int D, int G, bool NT = false, bool FUSED = false, bool QW = false, bool MIA = false, bool ST = false>
 __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part, int kvh, int b, char* smem,
                                                   int* fused_cnt = nullptr, QWait qw = {}, int fused_total = 0) {
+  fstamp<ST>(0);
   using C = Cfg<D>;
   static_assert(G <= 16, "at most 16 query heads per KV head");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1356,7 +1366,9 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
                                                                                    32 * s + 8 * fh))
                        : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
   }
+  fstamp<ST>(1);
   if constexpr (QW) wait_flag(qw.flags, qw.err, qw.limit);  // the KV prefetch above is in flight
+  fstamp<ST>(2);
   if (a.qkv_p != nullptr) {
     // q = RoPE(bf16(sum_s P[s][b])) for this KV head's G query heads, one (d, d + D/2) rotate_half
     // pair of 8-vectors per thread (G * D/16 threads, all slab loads of a thread in flight together),
@@ -1497,6 +1509,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     }
   }
 
+  fstamp<ST>(3);
   // partition-statistics buffers as write-through (sc1) buffer resources for the fused merge
   const unsigned pbytes = (unsigned)((size_t)(a.nb ? a.nb : (int)gridDim.z) * a.Hq * a.max_parts * 4);
   const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(a.part_o, (short)0, (int)(pbytes * D), 0x00020000);
@@ -1532,7 +1545,9 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
         }
         out_pair_sc1(a, b, (kvh * G + g) * D + d, L > 0.f ? O0 / L : 0.f, L > 0.f ? O1 / L : 0.f);
       }
+      fstamp<ST>(4);
       stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
+      fstamp<ST>(5);
       return;
     }
   }
@@ -1591,7 +1606,9 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
   }
   __syncthreads();
   if (!s_last) {
+    fstamp<ST>(4);
     if constexpr (FUSED) stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
+    fstamp<ST>(5);
     return;
   }
   asm volatile("" ::: "memory");  // the sc1 loads below stay after the ticket
@@ -1648,7 +1665,9 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
       out_pair_sc1(a, b, (kvh * G + g) * D + d, L > 0.f ? O0 / L : 0.f, L > 0.f ? O1 / L : 0.f);
     }
     if (threadIdx.x == 0) __hip_atomic_store(a.counters + b * a.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fstamp<ST>(6);
     stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
+    fstamp<ST>(5);
     return;
   }
   for (int e = threadIdx.x; e < G * D; e += 256) {
@@ -1712,8 +1731,9 @@ struct OprojArgs {
 };
 constexpr int OP_MAXP = 64;  // partitions per (row, head) merged in LDS
 
-template <int D, int NLD, bool MIA = false>
+template <int D, int NLD, bool MIA = false, bool ST = false>
 __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const OprojArgs& o, int ob, char* smem) {
+  fstamp<ST>(0);
   constexpr int KS = 32 * NLD;          // K-slice (NLD 32-k MFMA steps, one 16-B load each per lane)
   constexpr int ROWB = KS * 2;          // bytes per row of the LDS activation slice
   constexpr int HPB = KS / D;           // attention heads in the slice
@@ -1735,7 +1755,9 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
 
   // 2) wait for every attention block (one lane polls a done-flag replica; the others wait at the barrier;
   //    a bounded wait: on timeout the error word is set and the block computes garbage, never hangs)
+  fstamp<ST>(1);
   wait_flag(o.cnt + FL_A, o.cnt + 2, o.spin_limit);
+  fstamp<ST>(2);
   if constexpr (MIA) {
     // the attention blocks merged the partitions: stage the bf16 rows of this K-slice (write-through loads)
     const __amdgpu_buffer_rsrc_t rs_x =
@@ -1857,6 +1879,7 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
   }  // !MIA
   __syncthreads();
 
+  fstamp<ST>(3);
   // 4) MFMA over the slice: A = activation rows (fr), B = this wave's weight columns
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1887,6 +1910,7 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
   int* s_last = reinterpret_cast<int*>(smem);  // the activation slice is dead
   wait_vmcnt0();
   __syncthreads();
+  fstamp<ST>(4);
   if (tid == 0) {
     const int old = __hip_atomic_fetch_add(o.cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == o.nob - 1;
@@ -1903,7 +1927,10 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
     *s_last = last;
   }
   __syncthreads();
-  if (!o.h || !*s_last) return;
+  if (!o.h || !*s_last) {
+    fstamp<ST>(5);
+    return;
+  }
   // 6) residual + RMSNorm of every row (add_partials_rmsnorm_kernel's math; slab order kept)
   float* red = reinterpret_cast<float*>(smem) + 16;
   const int nvec = o.N >> 3;
@@ -1967,6 +1994,7 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
     }
     __syncthreads();  // red[] reuse by the next row
   }
+  fstamp<ST>(6);
 }
 
 // qkv projection blocks of the 3-role launch (attn_oproj_kernel<..., QNLD > 0>): split-K partial slabs
@@ -1983,8 +2011,9 @@ struct QkvArgs {
   int nqb;                     // qkv blocks
 };
 
-template <int NLD>
+template <int NLD, bool ST = false>
 __device__ __forceinline__ void qkv_norm_block(const QkvArgs& q, int qb, char* smem, int* cnt) {
+  fstamp<ST>(0);
   constexpr int KS = 32 * NLD;
   constexpr int ROWB = KS * 2;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2089,7 +2118,9 @@ __device__ __forceinline__ void qkv_norm_block(const QkvArgs& q, int qb, char* s
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[r]), rs_p, (int)((((size_t)s * M + r) * q.N + col) * 4),
                                               0, 16);
   }
+  fstamp<ST>(3);
   stage_arrive(cnt + 4, q.nqb, cnt + FL_Q);
+  fstamp<ST>(5);
 }
 
 template <int D, int G, int NLD>
@@ -2102,7 +2133,7 @@ constexpr int attn_oproj_lds() {
 // QNLD > 0: the 3-role launch -- blocks [0, nqb) are qkv blocks (qkv_norm_block<QNLD>), then the
 // attention blocks (they prefetch their first KV tile, then wait for every qkv block), then the o_proj
 // blocks. Every wait is on lower-indexed blocks only.
-template <int D, int G, int NLD, int QNLD = 0, bool MIA = false>
+template <int D, int G, int NLD, int QNLD = 0, bool MIA = false, bool ST = false>
 __global__ __launch_bounds__(256, 2) void attn_oproj_kernel(DecodeArgs a, OprojArgs o, QkvArgs q) {
   constexpr int lds_q = QNLD > 0 ? 16 * 64 * QNLD + 64 : 0;
   constexpr int lds = attn_oproj_lds<D, G, NLD>() > lds_q ? attn_oproj_lds<D, G, NLD>() : lds_q;
@@ -2110,19 +2141,19 @@ __global__ __launch_bounds__(256, 2) void attn_oproj_kernel(DecodeArgs a, OprojA
   int bid = blockIdx.x;
   if constexpr (QNLD > 0) {
     if (bid < q.nqb) {
-      qkv_norm_block<QNLD>(q, bid, smem, o.cnt);
+      qkv_norm_block<QNLD, ST>(q, bid, smem, o.cnt);
       return;
     }
     bid -= q.nqb;
   }
   if (bid < o.na) {
     const int mp = a.max_parts;
-    attn_decode_block<D, G, false, true, (QNLD > 0), MIA>(a, bid % mp, (bid / mp) % a.Hkv, bid / (mp * a.Hkv),
-                                                          smem, o.cnt, QWait{o.cnt + FL_Q, o.cnt + 2, o.spin_limit},
-                                                          o.na);
+    attn_decode_block<D, G, false, true, (QNLD > 0), MIA, ST>(a, bid % mp, (bid / mp) % a.Hkv, bid / (mp * a.Hkv),
+                                                              smem, o.cnt, QWait{o.cnt + FL_Q, o.cnt + 2, o.spin_limit},
+                                                              o.na);
     return;
   }
-  oproj_merge_block<D, NLD, MIA>(a, o, bid - o.na, smem);
+  oproj_merge_block<D, NLD, MIA, ST>(a, o, bid - o.na, smem);
 }
 
 // merge split-K partitions: grid (Hq, B), block D threads. The partition statistics are loaded by
@@ -2416,6 +2447,10 @@ static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* co
   return (int)hipErrorInvalidValue;
 }
 
+// Diagnostic: the next fused launches (G = 4, ks_steps 8, MIA, q_ks 16 or none) run the stamp build,
+// writing 8 s_memrealtime stamps per block into `stamps` (u64 [grid][8]); nullptr = production build.
+static unsigned long long* g_fused_stamps_host = nullptr;
+
 // Fused decode attention (RoPE + KV append from the qkv split-K slabs, as ragk_attn_decode_rope) and
 // o_proj split-K partials (as ragk_gemm_part_merge) in ONE launch: attn_oproj_kernel. B <= 4, D = 128,
 // G in {4, 8}; Wo bf16 [N][Hq * D] (ldw elements); Pout fp32 [K / KS][B][N], KS = 64 * ks_steps
@@ -2459,6 +2494,10 @@ RAGK_API int ragk_attn_oproj_fused(const float* P, int S, int ldp, const int* po
     a.out_stride = K;
     a.counters = cnt + CNT_TICKETS;
     if (B * Hkv > 4 * 64) return (int)hipErrorInvalidValue;
+  }
+  if (g_fused_stamps_host && mia && G == 4 && ks_steps == 8) {
+    hipLaunchKernelGGL((attn_oproj_kernel<128, 4, 16, 0, true, true>), grid, dim3(256), 0, st, a, o, q);
+    return (int)hipGetLastError();
   }
 #define RAGK_AO(GG, NL)                                                                                \
   if (G == GG && 2 * ks_steps == NL) {                                                                 \
@@ -2522,6 +2561,10 @@ RAGK_API int ragk_qkv_attn_oproj_fused(const void* h, int ldh, const void* gin, 
     a.counters = cnt + CNT_TICKETS;
     if (B * Hkv > 4 * 64) return (int)hipErrorInvalidValue;
   }
+  if (g_fused_stamps_host && mia && G == 4 && ks_steps == 8 && q_ks == 16) {
+    hipLaunchKernelGGL((attn_oproj_kernel<128, 4, 16, 32, true, true>), grid, dim3(256), 0, st, a, o, q);
+    return (int)hipGetLastError();
+  }
 #define RAGK_QAO(GG, NL, QN)                                                                                 \
   if (G == GG && 2 * ks_steps == NL && 2 * q_ks == QN) {                                                     \
     if (mia) hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL, QN, true>), grid, dim3(256), 0, st, a, o, q); \
@@ -2537,3 +2580,8 @@ RAGK_API int ragk_qkv_attn_oproj_fused(const void* h, int ldh, const void* gin, 
 }
 
 RAGK_API int ragk_attn_oproj_cnt_ints() { return CNT_INTS; }
+
+RAGK_API int ragk_fused_set_stamps(unsigned long long* stamps, hipStream_t st) {
+  g_fused_stamps_host = stamps;
+  return (int)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fused_stamps), &stamps, sizeof(stamps), 0, hipMemcpyHostToDevice, st);
+}

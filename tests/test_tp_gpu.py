@@ -125,9 +125,14 @@ def _prefill_decode_logits(model, ids, nxt):
 
 
 def _init(rank, port, world=WORLD):
-    # every rank on cuda:0 on purpose: the distinctness self-test must be told so
+    # every rank on cuda:0 on purpose: the distinctness self-test must be told so. Eight processes with
+    # HIP's default 4 hardware queues each over-subscribe the device's mapped queues, and the scheduler's
+    # time-slicing between a peer-waiting kernel and the queue of the peer it waits for blew the bounded
+    # waits (8-rank engine run, round 4): 2 queues per process keeps every queue mapped (before HIP init).
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", RAGK_TP_CONTROL="gloo", RAGK_ALLOW_SHARED_DEVICE="1")
+    if world >= 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "2"
     from rag_llm_k8s_amd.parallel.dist import init_distributed
 
     return init_distributed(tp=world, backend="gloo")
