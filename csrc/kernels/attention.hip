@@ -1241,7 +1241,8 @@ constexpr int FL_STRIDE = 32;     // ints between replicas (128 B)
 constexpr int FL_A = 64;          // cnt offset of the attention-done flags
 constexpr int FL_Q = FL_A + FL_REPL * FL_STRIDE;  // cnt offset of the qkv-done flags
 constexpr int CNT_TICKETS = FL_Q + FL_REPL * FL_STRIDE;  // MIA: per (sequence, KV head) merge tickets
-constexpr int CNT_INTS = CNT_TICKETS + 4 * 64;
+constexpr int CNT_SS = CNT_TICKETS + 4 * 64;               // v2 o_proj: [4][<= 512] sum-of-squares partials
+constexpr int CNT_INTS = CNT_SS + 4 * 512;
 __device__ __forceinline__ void stage_arrive(int* cnt, int total, int* flags) {
   wait_vmcnt0();
   __syncthreads();
@@ -1612,10 +1613,86 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     return;
   }
   asm volatile("" ::: "memory");  // the sc1 loads below stay after the ticket
+  const size_t hb = (size_t)b * a.Hq + kvh * G;  // first query head of this KV head
+  if constexpr (FUSED) {
+    // Merge on the critical path of the fused launch: each thread's partial-output records of its (head,
+    // d pair)s for the first MCH partitions are requested first, then the (max, sum) statistics (into LDS),
+    // so both are in flight together -- one memory round trip for <= MCH partitions -- and merged in
+    // registers once the per-partition scales are known.
+    constexpr int MCH = 16;
+    constexpr int NPR = (G * D / 2 + 255) / 256;  // (head, pair) items per thread
+    float* s_m = reinterpret_cast<float*>(smem);  // [G][nparts] max -> scale
+    float* s_l = s_m + G * nparts;
+    float* s_L = s_l + G * nparts;
+    f32x2 v[NPR][MCH];
+#pragma unroll
+    for (int k = 0; k < NPR; ++k) {
+      const int e2 = min((int)threadIdx.x + 256 * k, G * D / 2 - 1);
+      const int g = (2 * e2) / D, d = (2 * e2) % D;
+      const int po = (int)(((hb + g) * a.max_parts * D + d) * 4);
+#pragma unroll
+      for (int i = 0; i < MCH; ++i)
+        v[k][i] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_o, po + min(i, nparts - 1) * D * 4, 0, 16));
+    }
+    for (int e = threadIdx.x; e < G * nparts; e += 256) {
+      const int g = e / nparts, p = e % nparts;
+      const f32x2 ml = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_ml, (int)(((hb + g) * a.max_parts + p) * 8), 0, 16));
+      s_m[e] = ml[0];
+      s_l[e] = ml[1];
+    }
+    __syncthreads();
+    if (threadIdx.x < G) {
+      const int g = threadIdx.x;
+      float Mx = -INFINITY;
+      for (int p = 0; p < nparts; ++p) Mx = fmaxf(Mx, s_m[g * nparts + p]);
+      const float Mu = Mx == -INFINITY ? 0.f : Mx;
+      float L = 0.f;
+      for (int p = 0; p < nparts; ++p) {
+        const float sc = exp2f(s_m[g * nparts + p] - Mu);
+        s_m[g * nparts + p] = sc;
+        L += s_l[g * nparts + p] * sc;
+      }
+      s_L[g] = L;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NPR; ++k) {
+      const int e2 = threadIdx.x + 256 * k;
+      if (e2 >= G * D / 2) break;
+      const int g = (2 * e2) / D, d = (2 * e2) % D;
+      const float* sc = s_m + g * nparts;
+      float O0 = 0.f, O1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < MCH; ++i) {
+        const float f = i < nparts ? sc[i] : 0.f;
+        O0 += v[k][i][0] * f;
+        O1 += v[k][i][1] * f;
+      }
+      const int po = (int)(((hb + g) * a.max_parts * D + d) * 4);
+      for (int p0 = MCH; p0 < nparts; p0 += MCH) {  // long contexts: further rounds of MCH records
+        f32x2 w[MCH];
+#pragma unroll
+        for (int i = 0; i < MCH; ++i)
+          w[i] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_o, po + min(p0 + i, nparts - 1) * D * 4, 0, 16));
+#pragma unroll
+        for (int i = 0; i < MCH; ++i) {
+          const float f = p0 + i < nparts ? sc[p0 + i] : 0.f;
+          O0 += w[i][0] * f;
+          O1 += w[i][1] * f;
+        }
+      }
+      const float L = s_L[g];
+      out_pair_sc1(a, b, (kvh * G + g) * D + d, L > 0.f ? O0 / L : 0.f, L > 0.f ? O1 / L : 0.f);
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(a.counters + b * a.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fstamp<ST>(6);
+    stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
+    fstamp<ST>(5);
+    return;
+  }
   float* s_m = reinterpret_cast<float*>(smem);  // [G][nparts] partition max, then its scale
   float* s_l = s_m + G * nparts;                 // [G][nparts] partition sum
   float* s_L = s_l + G * nparts;                 // [G] merged sum
-  const size_t hb = (size_t)b * a.Hq + kvh * G;  // first query head of this KV head
   for (int e = threadIdx.x; e < G * nparts; e += 256) {
     const int g = e / nparts, p = e % nparts;
     const size_t pi = (hb + g) * a.max_parts + p;
@@ -1637,39 +1714,6 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     s_L[g] = L;
   }
   __syncthreads();
-  if constexpr (FUSED) {
-    // pairs (d, d + 1): two 8-byte record loads per partition, one 4-byte write-through output store
-    for (int e2 = threadIdx.x; e2 < G * D / 2; e2 += 256) {
-      const int g = (2 * e2) / D, d = (2 * e2) % D;
-      const int po = (int)(((hb + g) * a.max_parts * D + d) * 4);
-      const float* sc = s_m + g * nparts;
-      float O0 = 0.f, O1 = 0.f;
-      int p = 0;
-      for (; p + 8 <= nparts; p += 8) {
-        f32x2 v[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          v[i] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_o, po + (p + i) * D * 4, 0, 16));
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          O0 += v[i][0] * sc[p + i];
-          O1 += v[i][1] * sc[p + i];
-        }
-      }
-      for (; p < nparts; ++p) {
-        const f32x2 v = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_o, po + p * D * 4, 0, 16));
-        O0 += v[0] * sc[p];
-        O1 += v[1] * sc[p];
-      }
-      const float L = s_L[g];
-      out_pair_sc1(a, b, (kvh * G + g) * D + d, L > 0.f ? O0 / L : 0.f, L > 0.f ? O1 / L : 0.f);
-    }
-    if (threadIdx.x == 0) __hip_atomic_store(a.counters + b * a.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    fstamp<ST>(6);
-    stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
-    fstamp<ST>(5);
-    return;
-  }
   for (int e = threadIdx.x; e < G * D; e += 256) {
     const int g = e / D, d = e % D;
     const int po = (int)(((hb + g) * a.max_parts * D + d) * 4);  // byte offset of partition 0
@@ -1728,6 +1772,7 @@ struct OprojArgs {
   const bf16_t* gamma;
   bf16_t* xn; int ldx;
   float eps;
+  float* ss;                 // v2 tail: [4][nob] per-block sum-of-squares partials
 };
 constexpr int OP_MAXP = 64;  // partitions per (row, head) merged in LDS
 
@@ -2123,6 +2168,150 @@ __device__ __forceinline__ void qkv_norm_block(const QkvArgs& q, int qb, char* s
   fstamp<ST>(5);
 }
 
+// o_proj block of the fused launch, v2 (MIA only): 16 output columns x the FULL K per block, the 4 waves
+// splitting K in quarters (NLQ 16-B weight loads per lane each, all in flight from the block's start), so
+// N / 16 blocks (256 at N = 4096) are resident next to the attention blocks from the first cycle and no
+// split-K slab exists: the block reduces its waves in LDS and finishes its columns itself --
+//   tail (o.h set): h[r][cols] = bf16(h + bf16(o_proj)) written through, per-row sum-of-squares partial
+//     to o.ss[r][block]; the last block (arrival ticket) sums the partials in block order and writes
+//     xn = rmsnorm(h) * gamma;
+//   no tail (tensor parallel): the fp32 partial row o.P[0][r][cols] for the cross-rank reduction.
+template <int D, int NLQ, bool ST = false>
+__device__ __forceinline__ void oproj_full_block(const DecodeArgs& a, const OprojArgs& o, int ob, char* smem) {
+  constexpr int KQ = 32 * NLQ;  // K quarter of one wave
+  constexpr int K = 4 * KQ;
+  constexpr int ROWB = K * 2;   // LDS bytes per activation row (4 rows: M <= 4)
+  fstamp<ST>(0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fh = lane >> 4;
+  const int n0 = ob * 16;
+  const int M = o.M;
+  // 1) this wave's quarter of the block's 16 weight rows, every load in flight
+  const bf16_t* wp = o.W + (size_t)min(n0 + fr, o.N - 1) * o.ldw + wid * KQ + 8 * fh;
+  bf16x8 wf[NLQ];
+#pragma unroll
+  for (int ks = 0; ks < NLQ; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
+  fstamp<ST>(1);
+  // 2) the attention blocks have merged every head into a.out
+  wait_flag(o.cnt + FL_A, o.cnt + 2, o.spin_limit);
+  fstamp<ST>(2);
+  // 3) the M attention rows -> LDS (write-through loads), 16-B chunk c of row r at slot c ^ (r & 15)
+  {
+    const __amdgpu_buffer_rsrc_t rs_x =
+        __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, M * a.out_stride * 2, 0x00020000);
+    constexpr int CPR = K / 8;
+    constexpr int PER = (4 * CPR + 255) / 256;
+    u32x4 xv[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = min(tid + 256 * i, M * CPR - 1);
+      xv[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, ((e / CPR) * a.out_stride + 8 * (e % CPR)) * 2, 0, 16));
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = tid + 256 * i;
+      if (e < M * CPR) {
+        const int r = e / CPR, c = e % CPR;
+        *reinterpret_cast<u32x4*>(smem + r * ROWB + 16 * ((c & ~15) | ((c & 15) ^ (r & 15)))) = xv[i];
+      }
+    }
+  }
+  __syncthreads();
+  fstamp<ST>(3);
+  // 4) MFMA over the wave's K quarter (activation rows >= M alias row fr & 3: their outputs are dropped)
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  const int xr = fr & 3;
+#pragma unroll
+  for (int ks = 0; ks < NLQ; ++ks) {
+    const int chunk = (wid * KQ) / 8 + 4 * ks + fh;
+    const bf16x8 xf = *reinterpret_cast<const bf16x8*>(smem + xr * ROWB + 16 * ((chunk & ~15) | ((chunk & 15) ^ xr)));
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[ks], acc, 0, 0, 0);
+  }
+  // 5) the 4 K quarters summed in wave order (LDS after the activation rows)
+  f32x4* red = reinterpret_cast<f32x4*>(smem + 4 * ROWB);
+  red[wid * 64 + lane] = acc;
+  __syncthreads();
+  int* s_last = reinterpret_cast<int*>(smem + 4 * ROWB + 4 * 64 * 16);
+  float* s_red = reinterpret_cast<float*>(s_last + 4);
+  const int col = n0 + fr;
+  const __amdgpu_buffer_rsrc_t rs_h =
+      __builtin_amdgcn_make_buffer_rsrc(o.h ? o.h : a.out, (short)0, o.h ? M * o.ldh * 2 : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_ss = __builtin_amdgcn_make_buffer_rsrc(o.ss, (short)0, o.ss ? 4 * o.nob * 4 : 0, 0x00020000);
+  if (wid == 0) {
+    f32x4 c = red[lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) c += red[w * 64 + lane];
+    // lane (fr, fh): column n0 + fr, rows 4 fh + r -- rows 0..3 live in the fh == 0 lanes
+    if (!o.h) {
+      if (fh == 0 && col < o.N) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (r < M) o.P[(size_t)r * o.N + col] = c[r];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float hv = bf2f(o.h[(size_t)min(r, M - 1) * o.ldh + min(col, o.N - 1)]);
+        const float v = bf2f(f2bf(hv + bf2f(f2bf(c[r]))));
+        const float vn = __shfl_xor(v, 1, 64);
+        float sq = fh == 0 && col < o.N ? v * v : 0.f;
+        if (r < M && fh == 0 && (fr & 1) == 0 && col < o.N)
+          __builtin_amdgcn_raw_buffer_store_b32(pk2bf(v, vn), rs_h, (r * o.ldh + col) * 2, 0, 16);
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) sq += __shfl_xor(sq, off, 64);
+        if (r < M && lane == 0)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sq), rs_ss, (r * o.nob + ob) * 4, 0, 16);
+      }
+    }
+  }
+  fstamp<ST>(4);
+  // 6) arrival ticket; the last block re-arms the counters and finishes the norm
+  wait_vmcnt0();
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(o.cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == o.nob - 1;
+    if (last) {
+      __hip_atomic_store(o.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o.cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o.cnt + 4, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < FL_REPL; ++k) {
+        __hip_atomic_store(o.cnt + FL_A + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(o.cnt + FL_Q + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    *s_last = last;
+  }
+  __syncthreads();
+  if (!o.h || !*s_last) {
+    fstamp<ST>(5);
+    return;
+  }
+  // per row: sum of squares = the blocks' partials in block order (tree fixed by thread index), then
+  // xn = gamma * bf16(h * rsqrt(mean + eps)); h is re-read write-through (other blocks wrote it)
+  const int nvec = o.N >> 3;
+  for (int r = 0; r < M; ++r) {
+    float ss = 0.f;
+    for (int b2 = tid; b2 < o.nob; b2 += 256)
+      ss += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ss, (r * o.nob + b2) * 4, 0, 16));
+    ss = block_sum(ss, s_red);
+    const float inv = rsqrtf(ss / (float)o.N + o.eps);
+    for (int vi = tid; vi < nvec; vi += 256) {
+      const u32x4 hv = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_h, (r * o.ldh + vi * 8) * 2, 0, 16));
+      float hf[8], wv[8], out8[8];
+      unpack8(hv, hf);
+      unpack8(*reinterpret_cast<const u32x4*>(o.gamma + vi * 8), wv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out8[e] = wv[e] * bf2f(f2bf(hf[e] * inv));
+      *reinterpret_cast<u32x4*>(o.xn + (size_t)r * o.ldx + vi * 8) = pack8(out8);
+    }
+    __syncthreads();  // s_red reuse by the next row
+  }
+  fstamp<ST>(6);
+}
+
 template <int D, int G, int NLD>
 constexpr int attn_oproj_lds() {
   constexpr int a = decode_lds_bytes<D, G>();
@@ -2133,10 +2322,13 @@ constexpr int attn_oproj_lds() {
 // QNLD > 0: the 3-role launch -- blocks [0, nqb) are qkv blocks (qkv_norm_block<QNLD>), then the
 // attention blocks (they prefetch their first KV tile, then wait for every qkv block), then the o_proj
 // blocks. Every wait is on lower-indexed blocks only.
-template <int D, int G, int NLD, int QNLD = 0, bool MIA = false, bool ST = false>
+template <int D, int G, int NLD, int QNLD = 0, bool MIA = false, bool ST = false, bool OV2 = false>
 __global__ __launch_bounds__(256, 2) void attn_oproj_kernel(DecodeArgs a, OprojArgs o, QkvArgs q) {
   constexpr int lds_q = QNLD > 0 ? 16 * 64 * QNLD + 64 : 0;
-  constexpr int lds = attn_oproj_lds<D, G, NLD>() > lds_q ? attn_oproj_lds<D, G, NLD>() : lds_q;
+  constexpr int lds_o = OV2 ? 4 * 4 * 32 * NLD * 2 + 4 * 64 * 16 + 64 : attn_oproj_lds<D, G, NLD>();
+  constexpr int lds_a = decode_lds_bytes<D, G>();
+  constexpr int lds_ao = lds_o > lds_a ? lds_o : lds_a;
+  constexpr int lds = lds_ao > lds_q ? lds_ao : lds_q;
   __shared__ __attribute__((aligned(16))) char smem[lds];
   int bid = blockIdx.x;
   if constexpr (QNLD > 0) {
@@ -2153,7 +2345,10 @@ __global__ __launch_bounds__(256, 2) void attn_oproj_kernel(DecodeArgs a, OprojA
                                                               o.na);
     return;
   }
-  oproj_merge_block<D, NLD, MIA, ST>(a, o, bid - o.na, smem);
+  if constexpr (OV2)
+    oproj_full_block<D, NLD, ST>(a, o, bid - o.na, smem);
+  else
+    oproj_merge_block<D, NLD, MIA, ST>(a, o, bid - o.na, smem);
 }
 
 // merge split-K partitions: grid (Hq, B), block D threads. The partition statistics are loaded by
@@ -2450,6 +2645,12 @@ static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* co
 // Diagnostic: the next fused launches (G = 4, ks_steps 8, MIA, q_ks 16 or none) run the stamp build,
 // writing 8 s_memrealtime stamps per block into `stamps` (u64 [grid][8]); nullptr = production build.
 static unsigned long long* g_fused_stamps_host = nullptr;
+// v2 o_proj role (oproj_full_block): 16-column full-K blocks, no split-K slabs (MIA launches only)
+static int g_ao_v2 = 1;
+RAGK_API int ragk_attn_oproj_set_v2(int on) {
+  g_ao_v2 = on ? 1 : 0;
+  return 0;
+}
 
 // Fused decode attention (RoPE + KV append from the qkv split-K slabs, as ragk_attn_decode_rope) and
 // o_proj split-K partials (as ragk_gemm_part_merge) in ONE launch: attn_oproj_kernel. B <= 4, D = 128,
@@ -2494,6 +2695,24 @@ RAGK_API int ragk_attn_oproj_fused(const float* P, int S, int ldp, const int* po
     a.out_stride = K;
     a.counters = cnt + CNT_TICKETS;
     if (B * Hkv > 4 * 64) return (int)hipErrorInvalidValue;
+  }
+  const int nlq = K / 128;  // v2: 16-B loads per lane of one wave's K quarter
+  if (mia && g_ao_v2 && (nlq == 4 || nlq == 8 || nlq == 16 || nlq == 32) && (N + 15) / 16 <= 512) {
+    o.nob = (N + 15) / 16;
+    o.ss = reinterpret_cast<float*>(cnt + CNT_SS);
+    const dim3 grid2(o.na + o.nob);
+    if (g_fused_stamps_host && G == 4 && nlq == 32) {
+      hipLaunchKernelGGL((attn_oproj_kernel<128, 4, 32, 0, true, true, true>), grid2, dim3(256), 0, st, a, o, q);
+      return (int)hipGetLastError();
+    }
+#define RAGK_AO2(GG, NQ)                                                                                 \
+    if (G == GG && nlq == NQ) {                                                                          \
+      hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NQ, 0, true, false, true>), grid2, dim3(256), 0, st, a, o, q); \
+      return (int)hipGetLastError();                                                                     \
+    }
+    RAGK_AO2(4, 4) RAGK_AO2(4, 8) RAGK_AO2(4, 16) RAGK_AO2(4, 32)
+    RAGK_AO2(8, 4) RAGK_AO2(8, 8) RAGK_AO2(8, 16) RAGK_AO2(8, 32)
+#undef RAGK_AO2
   }
   if (g_fused_stamps_host && mia && G == 4 && ks_steps == 8) {
     hipLaunchKernelGGL((attn_oproj_kernel<128, 4, 16, 0, true, true>), grid, dim3(256), 0, st, a, o, q);
@@ -2560,6 +2779,23 @@ RAGK_API int ragk_qkv_attn_oproj_fused(const void* h, int ldh, const void* gin, 
     a.out_stride = Ko;
     a.counters = cnt + CNT_TICKETS;
     if (B * Hkv > 4 * 64) return (int)hipErrorInvalidValue;
+  }
+  const int nlq = Ko / 128;
+  if (mia && g_ao_v2 && (nlq == 4 || nlq == 8 || nlq == 16 || nlq == 32) && (N + 15) / 16 <= 512) {
+    o.nob = (N + 15) / 16;
+    o.ss = reinterpret_cast<float*>(cnt + CNT_SS);
+    const dim3 grid2(q.nqb + o.na + o.nob);
+    if (g_fused_stamps_host && G == 4 && nlq == 32 && q_ks == 16) {
+      hipLaunchKernelGGL((attn_oproj_kernel<128, 4, 32, 32, true, true, true>), grid2, dim3(256), 0, st, a, o, q);
+      return (int)hipGetLastError();
+    }
+#define RAGK_QAO2(GG, NQ, QN)                                                                                \
+    if (G == GG && nlq == NQ && 2 * q_ks == QN) {                                                          \
+      hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NQ, QN, true, false, true>), grid2, dim3(256), 0, st, a, o, q); \
+      return (int)hipGetLastError();                                                                       \
+    }
+    RAGK_QAO2(4, 32, 16) RAGK_QAO2(4, 32, 32) RAGK_QAO2(4, 4, 32) RAGK_QAO2(8, 32, 32) RAGK_QAO2(8, 8, 32)
+#undef RAGK_QAO2
   }
   if (g_fused_stamps_host && mia && G == 4 && ks_steps == 8 && q_ks == 16) {
     hipLaunchKernelGGL((attn_oproj_kernel<128, 4, 16, 32, true, true>), grid, dim3(256), 0, st, a, o, q);

@@ -91,6 +91,7 @@ _SIGS = {
                               ctypes.c_uint, P, I, P, P, I, F, P, S],
     "ragk_attn_oproj_cnt_ints": [],
     "ragk_fused_set_stamps": [P, S],
+    "ragk_attn_oproj_set_v2": [I],
     "ragk_qkv_attn_oproj_fused": [P, I, P, F, P, I, I, I, P, I, P, P, P, P, P, P, P, I, P, P, P, I, I, I, I, I, I, F,
                                   P, I, P, I, I, P, ctypes.c_uint, P, I, P, P, I, F, P, S],
     # csrc/comm/allreduce.hip (xGMI peer-mapped all-reduce)

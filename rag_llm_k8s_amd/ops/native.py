@@ -342,6 +342,19 @@ ATTN_OPROJ_SPIN_US = int(os.environ.get("RAGK_ATTN_OPROJ_SPIN_US", "1000000"))
 # block of each (sequence, KV head), into a bf16 row the o_proj blocks stage (once per head);
 # 0 = by every o_proj block for the heads of its K-slice (no extra hand-off, redundant record reads)
 ATTN_OPROJ_MIA = os.environ.get("RAGK_AO_MIA", "1") == "1"
+# v2 o_proj role (attention.hip oproj_full_block): 16 output columns x the full K per block, all resident
+# next to the attention blocks, no split-K slabs (the residual / norm, or the TP partial row, written by
+# the blocks themselves). MIA launches with K in {512, ..., 4096} only.
+ATTN_OPROJ_V2 = os.environ.get("RAGK_AO_V2", "1") == "1"
+_ao_v2_set = [None]
+
+
+def _ao_v2(K, N):
+    on = ATTN_OPROJ_MIA and ATTN_OPROJ_V2 and K in (512, 1024, 2048, 4096) and -(-N // 16) <= 512
+    if _ao_v2_set[0] != ATTN_OPROJ_V2:
+        check(_lib.lib().ragk_attn_oproj_set_v2(int(ATTN_OPROJ_V2)), "ragk_attn_oproj_set_v2")
+        _ao_v2_set[0] = ATTN_OPROJ_V2
+    return on
 _ao_ws = {}
 
 
@@ -408,7 +421,7 @@ def attn_oproj(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_tables
     _req(ws_o.numel() >= B * Hq * max_parts * D and ws_ml.numel() >= B * Hq * max_parts * 2, "partition workspace")
     ks = ATTN_OPROJ_KS
     if out is None:
-        out = torch.empty((K // (64 * ks), B, N), dtype=torch.float32, device=P.device)
+        out = torch.empty((1 if _ao_v2(K, N) else K // (64 * ks), B, N), dtype=torch.float32, device=P.device)
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     cnt = attn_oproj_counters(P.device)
     h = gamma = xn = None
@@ -467,7 +480,8 @@ def qkv_attn_oproj(h, g_in, eps_in, wqkv, positions, cos_t, sin_t, slots, k_cach
     _req(ws_o.numel() >= B * Hq * max_parts * D and ws_ml.numel() >= B * Hq * max_parts * 2, "partition workspace")
     qks, ks = QAO_QKS, ATTN_OPROJ_KS
     Pq = torch.empty((K // (64 * qks), B, Nq), dtype=torch.float32, device=h.device)
-    Po = torch.empty((wo.shape[1] // (64 * ks), B, N), dtype=torch.float32, device=h.device)
+    Po = torch.empty((1 if _ao_v2(wo.shape[1], N) else wo.shape[1] // (64 * ks), B, N), dtype=torch.float32,
+                     device=h.device)
     xn = torch.empty((B, N), dtype=torch.bfloat16, device=h.device) if tail else None
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     cnt = attn_oproj_counters(h.device)

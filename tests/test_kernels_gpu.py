@@ -590,8 +590,8 @@ def test_gemm_part_merge_matches_reduce_then_part(native, kv_lens, target, fp8, 
                                                        ([777, 5300, 65, 2000], 512, 32, 8, 8), ([8100], 512, 32, 8, 4),
                                                        ([5200], 1024, 4, 1, 4), ([5200, 70], 1024, 8, 1, 8),
                                                        ([64, 128, 8000], 128, 64, 8, 8)])
-@pytest.mark.parametrize("mia", [True, False])
-def test_attn_oproj_fused_matches_unfused(native, kv_lens, target, Hq, Hkv, ks, mia, monkeypatch):
+@pytest.mark.parametrize("mia,v2", [(True, True), (True, False), (False, False)])
+def test_attn_oproj_fused_matches_unfused(native, kv_lens, target, Hq, Hkv, ks, mia, v2, monkeypatch):
     """attention + o_proj in one launch (attn_oproj_kernel: o_proj blocks stream their weights while the
     attention blocks run, then merge the partitions of their K-slice) == attn_decode_rope followed by
     gemm_part on the merged output, up to fp32 summation order; same KV-cache contents bit for bit; vs
@@ -599,6 +599,7 @@ def test_attn_oproj_fused_matches_unfused(native, kv_lens, target, Hq, Hkv, ks, 
     one / many partitions, mixed lengths, M = 1..4, the TP=8 per-rank heads (4 / 1, 8 / 1) and 70B's 64 / 8."""
     D, S = 128, 8
     monkeypatch.setattr(native, "ATTN_OPROJ_MIA", mia)
+    monkeypatch.setattr(native, "ATTN_OPROJ_V2", v2)
     torch.manual_seed(31)
     kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=9)
     B = len(kv_lens)
@@ -625,7 +626,7 @@ def test_attn_oproj_fused_matches_unfused(native, kv_lens, target, Hq, Hkv, ks, 
         for it in range(3):
             kc3, vc3 = kc.clone(), vc.clone()
             o = native.attn_oproj(P, pos, cos, sin, slots, kc3, vc3, bt, kvl, Hq, Hkv, D, pt, mp, ws_o, ws_ml, w)
-            assert o.shape == (Hq * D // (64 * ks), B, 4096)
+            assert o.shape in ((Hq * D // (64 * ks), B, 4096), (1, B, 4096))
             outs.append(o.sum(0))
         # the residual + RMSNorm tail in the last o_proj block == the add_partials_rmsnorm consumer
         g = (1 + 0.1 * torch.randn(4096, device=DEV)).bfloat16()
@@ -657,14 +658,15 @@ def test_attn_oproj_fused_matches_unfused(native, kv_lens, target, Hq, Hkv, ks, 
 
 @pytest.mark.parametrize("kv_lens,Hq,Hkv,qks", [([5200], 32, 8, 16), ([70, 3000], 32, 8, 8), ([1], 32, 8, 16),
                                                  ([777, 5300, 65, 2000], 32, 8, 16), ([5200, 70], 32, 4, 16)])
-@pytest.mark.parametrize("mia", [True, False])
-def test_qkv_attn_oproj_matches_unfused(native, kv_lens, Hq, Hkv, qks, mia, monkeypatch):
+@pytest.mark.parametrize("mia,v2", [(True, True), (True, False), (False, False)])
+def test_qkv_attn_oproj_matches_unfused(native, kv_lens, Hq, Hkv, qks, mia, v2, monkeypatch):
     """The 3-role decode launch (qkv + input RMSNorm, attention + RoPE + KV append, o_proj + residual +
     post-attention RMSNorm; attention blocks prefetch KV while the qkv weights stream) == rmsnorm ->
     gemm_part -> attn_decode_rope -> gemm_part -> add_partials_rmsnorm, up to fp32 summation order; the
     same KV-cache contents; repeated launches re-arm the counters."""
     D, H = 128, 4096
     monkeypatch.setattr(native, "ATTN_OPROJ_MIA", mia)
+    monkeypatch.setattr(native, "ATTN_OPROJ_V2", v2)
     torch.manual_seed(41)
     kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=11)
     B = len(kv_lens)

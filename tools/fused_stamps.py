@@ -6,7 +6,8 @@ from the launch's first block start, next to the unfused kernels' device times (
   python tools/fused_stamps.py            # B=1; FS_B=4 FS_MODE=qao|ao FS_LEN=5200
 Stamps: attention 0 start, 1 KV prefetch issued, 2 qkv flag seen, 3 main loop done, 4 records out,
 6 merged (last partition of a head), 5 arrived; o_proj 0 start, 1 weights issued, 2 flag seen, 3 slice
-staged, 4 slab stored, 5 end (6 norm tail done); qkv 0 start, 3 slab stored, 5 arrived.
+staged, 4 slab / columns stored, 5 end (6 norm tail done); qkv 0 start, 3 slab stored, 5 arrived.
+RAGK_AO_V2=0 / RAGK_AO_MIA=0 select the older o_proj roles.
 """
 import math
 import os
@@ -82,7 +83,7 @@ def main():
           % (B, L, mode, timed(run), timed(unfused)), flush=True)
     nq = (Nq // 64) * (H // (64 * native.QAO_QKS)) if mode == "qao" else 0
     na = mp * Hkv * B
-    no = (H // 64) * (Hq * D // (64 * native.ATTN_OPROJ_KS))
+    no = (H // 16) if native._ao_v2(Hq * D, H) else (H // 64) * (Hq * D // (64 * native.ATTN_OPROJ_KS))
     st = torch.zeros((nq + na + no, 8), dtype=torch.int64, device=dev)
     lib = native._lib.lib()
     rows = []
