@@ -398,6 +398,14 @@ def attn_oproj_counters(device):
     return _ao_cnt[key]
 
 
+def attn_oproj_armed(device) -> bool:
+    """Every counter, done flag and merge ticket of the fused launches back at zero (the v2 o_proj blocks'
+    sum-of-squares partials at the end of the buffer are scratch and not checked)."""
+    c = attn_oproj_counters(device).clone()
+    c[2] = 0  # error word
+    return int(c[:int(_lib.lib().ragk_attn_oproj_cnt_ints()) - 4 * 512].abs().sum().item()) == 0
+
+
 def attn_oproj_error(device) -> bool:
     c = _ao_cnt.get(_dev_key(device))
     return bool(c is not None and int(c[2].item()) != 0)

@@ -641,9 +641,7 @@ def test_attn_oproj_fused_matches_unfused(native, kv_lens, target, Hq, Hkv, ks, 
             xn2 = native.add_partials_rmsnorm(Ps, h2, g, 1e-5)
         torch.cuda.synchronize()
         assert not native.attn_oproj_error(DEV)
-        cnt = native.attn_oproj_counters(DEV).clone()
-        cnt[2] = 0
-        assert int(cnt.abs().sum().item()) == 0  # counters and done flags re-armed
+        assert native.attn_oproj_armed(DEV)  # counters, done flags and tickets re-armed
         if norm_ok:
             assert torch.equal(h1, h2)  # same slab order, same bf16 rounding points
             assert rel_err(xn1.float().cpu(), xn2.float().cpu()) < 1e-2  # block-sum order differs
@@ -703,9 +701,7 @@ def test_qkv_attn_oproj_matches_unfused(native, kv_lens, Hq, Hkv, qks, mia, v2, 
             res.append((h1, xn1))
         torch.cuda.synchronize()
         assert not native.attn_oproj_error(DEV)
-        cnt = native.attn_oproj_counters(DEV).clone()
-        cnt[2] = 0
-        assert int(cnt.abs().sum().item()) == 0  # counters and done flags re-armed
+        assert native.attn_oproj_armed(DEV)  # counters, done flags and tickets re-armed
     finally:
         native.QAO_QKS = old
     # tensor-parallel form: pre-normalised rows in, o_proj slabs out (no norm tail)
