@@ -1240,7 +1240,8 @@ constexpr int FL_REPL = 16;       // flag replicas
 constexpr int FL_STRIDE = 32;     // ints between replicas (128 B)
 constexpr int FL_A = 64;          // cnt offset of the attention-done flags
 constexpr int FL_Q = FL_A + FL_REPL * FL_STRIDE;  // cnt offset of the qkv-done flags
-constexpr int CNT_TICKETS = FL_Q + FL_REPL * FL_STRIDE;  // MIA: per (sequence, KV head) merge tickets
+constexpr int FL_P = FL_Q + FL_REPL * FL_STRIDE;           // v2: "attention KV prefetch issued" flags
+constexpr int CNT_TICKETS = FL_P + FL_REPL * FL_STRIDE;  // MIA: per (sequence, KV head) merge tickets
 constexpr int CNT_SS = CNT_TICKETS + 4 * 64;               // v2 o_proj: [4][<= 512] sum-of-squares partials
 constexpr int CNT_INTS = CNT_SS + 4 * 512;
 __device__ __forceinline__ void stage_arrive(int* cnt, int total, int* flags) {
@@ -1338,6 +1339,14 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
   const int pt = decode_part_tiles(n_kt, a);
   const int kt0 = part * pt;
   if (kt0 >= n_kt) {  // block-uniform early exit (before any barrier)
+    if constexpr (FUSED && MIA) {
+      if (threadIdx.x == 0 &&
+          __hip_atomic_fetch_add(fused_cnt + 5, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == fused_total - 1) {
+#pragma unroll
+        for (int k = 0; k < FL_REPL; ++k)
+          __hip_atomic_store(fused_cnt + FL_P + k * FL_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     if constexpr (FUSED) stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
     return;
   }
@@ -1368,6 +1377,16 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
                        : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
   }
   fstamp<ST>(1);
+  if constexpr (FUSED && MIA) {
+    // tell the o_proj blocks this block's KV requests are out (their weight stream queues behind them;
+    // nothing is handed off, so no drain): counter cnt[5], flags FL_P
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(fused_cnt + 5, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == fused_total - 1) {
+#pragma unroll
+      for (int k = 0; k < FL_REPL; ++k)
+        __hip_atomic_store(fused_cnt + FL_P + k * FL_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   if constexpr (QW) wait_flag(qw.flags, qw.err, qw.limit);  // the KV prefetch above is in flight
   fstamp<ST>(2);
   if (a.qkv_p != nullptr) {
@@ -1963,10 +1982,12 @@ __device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const Opr
       __hip_atomic_store(o.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(o.cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(o.cnt + 4, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o.cnt + 5, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
       for (int k = 0; k < FL_REPL; ++k) {
         __hip_atomic_store(o.cnt + FL_A + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(o.cnt + FL_Q + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(o.cnt + FL_P + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     *s_last = last;
@@ -2187,7 +2208,17 @@ __device__ __forceinline__ void oproj_full_block(const DecodeArgs& a, const Opro
   const int fr = lane & 15, fh = lane >> 4;
   const int n0 = ob * 16;
   const int M = o.M;
-  // 1) this wave's quarter of the block's 16 weight rows, every load in flight
+  const int col = n0 + fr;
+  // 0) the residual values this block adds to (wave 0, rows 0..3 of column n0 + fr), requested first
+  float hres[4] = {0.f, 0.f, 0.f, 0.f};
+  if (o.h && wid == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) hres[r] = bf2f(o.h[(size_t)min(r, M - 1) * o.ldh + min(col, o.N - 1)]);
+  }
+  // 1) this wave's quarter of the block's 16 weight rows, every load in flight -- issued once every
+  //    attention block has its KV requests out (the weight stream then queues behind them instead of
+  //    delaying the attention's dependent loads)
+  if (o.na > 0) wait_flag(o.cnt + FL_P, o.cnt + 2, o.spin_limit);
   const bf16_t* wp = o.W + (size_t)min(n0 + fr, o.N - 1) * o.ldw + wid * KQ + 8 * fh;
   bf16x8 wf[NLQ];
 #pragma unroll
@@ -2234,7 +2265,6 @@ __device__ __forceinline__ void oproj_full_block(const DecodeArgs& a, const Opro
   __syncthreads();
   int* s_last = reinterpret_cast<int*>(smem + 4 * ROWB + 4 * 64 * 16);
   float* s_red = reinterpret_cast<float*>(s_last + 4);
-  const int col = n0 + fr;
   const __amdgpu_buffer_rsrc_t rs_h =
       __builtin_amdgcn_make_buffer_rsrc(o.h ? o.h : a.out, (short)0, o.h ? M * o.ldh * 2 : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_ss = __builtin_amdgcn_make_buffer_rsrc(o.ss, (short)0, o.ss ? 4 * o.nob * 4 : 0, 0x00020000);
@@ -2252,8 +2282,7 @@ __device__ __forceinline__ void oproj_full_block(const DecodeArgs& a, const Opro
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float hv = bf2f(o.h[(size_t)min(r, M - 1) * o.ldh + min(col, o.N - 1)]);
-        const float v = bf2f(f2bf(hv + bf2f(f2bf(c[r]))));
+        const float v = bf2f(f2bf(hres[r] + bf2f(f2bf(c[r]))));
         const float vn = __shfl_xor(v, 1, 64);
         float sq = fh == 0 && col < o.N ? v * v : 0.f;
         if (r < M && fh == 0 && (fr & 1) == 0 && col < o.N)
@@ -2276,10 +2305,12 @@ __device__ __forceinline__ void oproj_full_block(const DecodeArgs& a, const Opro
       __hip_atomic_store(o.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(o.cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(o.cnt + 4, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(o.cnt + 5, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
       for (int k = 0; k < FL_REPL; ++k) {
         __hip_atomic_store(o.cnt + FL_A + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(o.cnt + FL_Q + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(o.cnt + FL_P + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     *s_last = last;
@@ -2290,19 +2321,35 @@ __device__ __forceinline__ void oproj_full_block(const DecodeArgs& a, const Opro
     return;
   }
   // per row: sum of squares = the blocks' partials in block order (tree fixed by thread index), then
-  // xn = gamma * bf16(h * rsqrt(mean + eps)); h is re-read write-through (other blocks wrote it)
+  // xn = gamma * bf16(h * rsqrt(mean + eps)); h is re-read write-through (other blocks wrote it). The
+  // row's h vectors and gamma are requested together with the partials (one round trip per row, H <= 4096).
   const int nvec = o.N >> 3;
   for (int r = 0; r < M; ++r) {
+    u32x4 hv[2], gv[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int vi = min(tid + 256 * i, nvec - 1);
+      hv[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_h, (r * o.ldh + vi * 8) * 2, 0, 16));
+      gv[i] = *reinterpret_cast<const u32x4*>(o.gamma + vi * 8);
+    }
     float ss = 0.f;
     for (int b2 = tid; b2 < o.nob; b2 += 256)
       ss += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ss, (r * o.nob + b2) * 4, 0, 16));
     ss = block_sum(ss, s_red);
     const float inv = rsqrtf(ss / (float)o.N + o.eps);
     for (int vi = tid; vi < nvec; vi += 256) {
-      const u32x4 hv = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_h, (r * o.ldh + vi * 8) * 2, 0, 16));
+      const int i = (vi - tid) / 256;
+      u32x4 hvv, gvv;
+      if (i < 2) {
+        hvv = i == 0 ? hv[0] : hv[1];
+        gvv = i == 0 ? gv[0] : gv[1];
+      } else {
+        hvv = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_h, (r * o.ldh + vi * 8) * 2, 0, 16));
+        gvv = *reinterpret_cast<const u32x4*>(o.gamma + vi * 8);
+      }
       float hf[8], wv[8], out8[8];
-      unpack8(hv, hf);
-      unpack8(*reinterpret_cast<const u32x4*>(o.gamma + vi * 8), wv);
+      unpack8(hvv, hf);
+      unpack8(gvv, wv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) out8[e] = wv[e] * bf2f(f2bf(hf[e] * inv));
       *reinterpret_cast<u32x4*>(o.xn + (size_t)r * o.ldx + vi * 8) = pack8(out8);
