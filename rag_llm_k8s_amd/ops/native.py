@@ -333,7 +333,10 @@ def gemm_part_merge(attn_out, kv_lens, part_tiles, max_parts, ws_o, ws_ml, Hq, w
 
 # Fused decode attention + o_proj (attention.hip attn_oproj_kernel): one launch in place of
 # attn_decode_rope(defer_merge) -> gemm_part_merge at batch <= 4. RAGK_DECODE_ATTN_OPROJ=0 disables.
-ATTN_OPROJ = os.environ.get("RAGK_DECODE_ATTN_OPROJ", "1") == "1"
+# Off by default: measured slower than the separate kernels at C=1 (3.66 vs 3.53 ms per token; the launch's
+# dependent hand-offs under the shared memory load cost what the kernel boundaries did -- docs/PERF_NOTES.md
+# round 4, profiles/fused_stamps_*_r4.log). Kept, tested, for the A/B and the TP-shard probe.
+ATTN_OPROJ = os.environ.get("RAGK_DECODE_ATTN_OPROJ", "0") == "1"
 ATTN_OPROJ_KS = int(os.environ.get("RAGK_ATTN_OPROJ_KS", "8"))  # K-slice steps of 64 (4, 8 or 16)
 # the residual + RMSNorm consumer inside the fused launch (its last o_proj block), TP=1 only
 ATTN_OPROJ_NORM = os.environ.get("RAGK_ATTN_OPROJ_NORM", "1") == "1"

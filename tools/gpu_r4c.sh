@@ -3,8 +3,7 @@
 #  1. the round-3 bench regression, settled on one box: round-2 HEAD (ab_r2/, a worktree of 28e502e with its
 #     own built libraries) vs HEAD vs HEAD with the 4-wave prefill attention (RAGK_PREFILL_PP=0), 20+5 steps,
 #     alternating;
-#  2. the 70B TP=8 rank-0 shard probe (decode B=1/32 + one 32k-token prefill step);
-#  3. the served path (Flask /generate, C=1 + Poisson).
+#  2. the served path (Flask /generate, C=1 + Poisson).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -19,7 +18,4 @@ for round in 1 2; do
   run head_$round . X=1 || exit $?
   run head_pp0_$round . RAGK_PREFILL_PP=0 || exit $?
 done
-TPP_MODEL=70b TPP_PREFILL=32768 timeout -k 10 400 python -u tools/tp_decode_probe.py 1 32 \
-  > gpurun_out/tp_decode_probe_70b_r4.log 2>&1 || exit $?
-timeout -k 10 300 python -u tools/tp_decode_probe.py 1 32 > gpurun_out/tp_decode_probe_r4.log 2>&1 || exit $?
 timeout -k 10 500 python -u tools/bench_serve.py --c1 20 > gpurun_out/serve_r4.log 2>&1
