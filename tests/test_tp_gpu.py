@@ -126,9 +126,8 @@ def _prefill_decode_logits(model, ids, nxt):
 
 def _init(rank, port, world=WORLD):
     # every rank on cuda:0 on purpose: the distinctness self-test must be told so. Eight processes with
-    # HIP's default 4 hardware queues each over-subscribe the device's mapped queues, and the scheduler's
-    # time-slicing between a peer-waiting kernel and the queue of the peer it waits for blew the bounded
-    # waits (8-rank engine run, round 4): 2 queues per process keeps every queue mapped (before HIP init).
+    # HIP's default 4 hardware queues each over-subscribe the device's mapped queues; 2 queues per process
+    # keeps every queue mapped (set before HIP init) so no peer-waiting kernel waits on an unmapped queue.
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", RAGK_TP_CONTROL="gloo", RAGK_ALLOW_SHARED_DEVICE="1")
     if world >= 8:
@@ -169,6 +168,10 @@ def _tp_worker(rank, port, d, world):
             res["ref_logits"] = _prefill_logits(ref, ids).cpu()
             res["ref_dec_logits"] = _prefill_decode_logits(ref, ids, 77).cpu()
             del ref
+        # the other ranks must not enter the engine's collectives while rank 0 computes the TP=1
+        # reference: their bounded peer waits (5 s) spin on the shared GPU and starve rank 0 -- the
+        # cause of the 8-rank timeouts of round 4 (rank 0 alone took longer than the bound)
+        dist.barrier(group=ctx.tp_cpu_group)
         del sd
         torch.cuda.empty_cache()
 
