@@ -392,6 +392,10 @@ class LlamaModel:
         qao_tp = (tp and fused_ao
                   and be.qkv_attn_oproj_ok(M, inp.meta, layers[0]["wqkv"], layers[0]["wo"], Hq, Hkv, D,
                                            norm_tail=False))
+        # TP=1: the add_partials_rmsnorm consumers of the o_proj / down split-K GEMMs run in those GEMMs'
+        # last blocks (gemm_part.hip TL) -- one launch fewer per norm
+        tail_o = not tp and not pf and not fused_ao and be.part_tail_ok(M, layers[0]["wo"])
+        tail_d = not tp and not pf and not silu_fused and be.part_tail_ok(M, layers[0]["wdown"])
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
             if qao:
@@ -428,11 +432,15 @@ class LlamaModel:
                     be.pf_arm([(L["wo"], pf["rope"], pf["attn"] // 2), (L["wgu"], 0, pf["attn"] // 2)],
                               pf["blocks"])
                 be.attn_decode(q, kc, vc, inp.meta, attn, Hq, Hkv, D)
-            if not fused_ao:
+            if tail_o:
+                # TP=1: the residual add + post-attention norm in the o_proj GEMM's last blocks
+                xn = (be.gemm_part_merge_tail(attn, inp.meta, L["wo"], Hq, h, L["ln_post"], c.rms_norm_eps) if merge
+                      else be.gemm_part_tail(attn, L["wo"], h, L["ln_post"], c.rms_norm_eps))
+            elif not fused_ao:
                 P = be.gemm_part_merge(attn, inp.meta, L["wo"], Hq) if merge else be.gemm_part(attn, L["wo"])
             if pf:
                 be.pf_arm([(L["wgu"], pf["attn"] // 2, pf["post"])], pf["blocks"])
-            if not ao_norm:
+            if not ao_norm and not tail_o:
                 xn = reduce_norm(P, L["ln_post"])
             nxt = layers[li + 1]["ln_in"] if li + 1 < len(layers) else w.norm
             if silu_fused:
@@ -446,6 +454,9 @@ class LlamaModel:
                 be.gemm(a, L["wdown"], resid=h, epi="resid", out=h)
                 if not fuse_norm or li + 1 == len(layers):
                     xn = be.rmsnorm(h, nxt, c.rms_norm_eps)
+                continue
+            if tail_d:
+                xn = be.gemm_part_tail(a, L["wdown"], h, nxt, c.rms_norm_eps)
                 continue
             P = be.gemm_part(a, L["wdown"])
             if pf:

@@ -148,6 +148,16 @@ class TorchBackend:
         h.copy_((h.float() + P.sum(0).to(h.dtype).float()).to(h.dtype))
         return R.rmsnorm(h, w, eps)
 
+    def part_tail_ok(self, M, w):
+        """The split-K GEMM may run its add_partials_rmsnorm consumer in its own last blocks (TP=1)."""
+        return self.enable_part and M <= 64 and not isinstance(w, Fp8Weight)
+
+    def gemm_part_tail(self, x, w, h, gamma, eps):
+        return self.add_partials_rmsnorm(self.gemm_part(x, w), h, gamma, eps)
+
+    def gemm_part_merge_tail(self, attn_out, meta: AttnMeta, w, Hq, h, gamma, eps):
+        return self.add_partials_rmsnorm(self.gemm_part_merge(attn_out, meta, w, Hq), h, gamma, eps)
+
     def rope_kv_partials(self, P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D):
         qkv = P.sum(0).to(q_out.dtype)
         self.rope_kv(qkv, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)
@@ -241,6 +251,7 @@ class NativeBackend(TorchBackend):
         native._lib.lib()  # fail loudly now if the gfx950 library is missing
         if torch.device(device).type == "cuda" and torch.cuda.is_available():
             native.attn_oproj_counters(device)  # before any graph capture
+            native.part_tail_counters(device)
 
     def gemm(self, x, w, bias=None, resid=None, epi="none", out=None, out_f32=False):
         if isinstance(w, Fp8Weight):
@@ -298,6 +309,16 @@ class NativeBackend(TorchBackend):
 
     def add_partials_rmsnorm(self, P, h, w, eps):
         return self.n.add_partials_rmsnorm(P, h, w, eps)
+
+    def part_tail_ok(self, M, w):
+        return self.enable_part and self.n.part_tail_ok(M, w)
+
+    def gemm_part_tail(self, x, w, h, gamma, eps):
+        return self.n.gemm_part_tail(x, w, h, gamma, eps)
+
+    def gemm_part_merge_tail(self, attn_out, meta: AttnMeta, w, Hq, h, gamma, eps):
+        return self.n.gemm_part_merge_tail(attn_out, meta.kv_lens, meta.part_tiles, meta.max_parts, meta.ws_o,
+                                           meta.ws_ml, Hq, w, h, gamma, eps)
 
     def rope_kv_partials(self, P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D):
         self.n.rope_kv_partials(P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)

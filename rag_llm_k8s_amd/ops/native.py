@@ -240,6 +240,98 @@ def gemm_part(x, w, out=None, ks=None):
     return out[:S] if out.dim() == 3 else out
 
 
+# The residual add + RMSNorm consumer of a split-K decode GEMM inside the GEMM's last M blocks
+# (gemm_part.hip TL): TP=1 o_proj and down, every decode batch. RAGK_DECODE_PART_TAIL=0 restores the
+# separate add_partials_rmsnorm launch (default until the sharded-arrival form is measured).
+PART_TAIL = os.environ.get("RAGK_DECODE_PART_TAIL", "0") == "1"
+PART_TAIL_SPIN_US = int(os.environ.get("RAGK_PART_TAIL_SPIN_US", "1000000"))
+_tail_cnt = {}
+
+
+def part_tail_counters(device):
+    """Shard / top arrival counters, done flags, finish counter and timeout word of the tail launches
+    (gemm_part.hip TL_*): zeroed once, re-armed by every launch itself; allocated when the native backend
+    is created, never inside a graph capture."""
+    key = _dev_key(device)
+    if key not in _tail_cnt:
+        _req(not torch.cuda.is_current_stream_capturing(), "tail counters allocated inside a graph capture")
+        n = int(_lib.lib().ragk_gemm_part_tail_ints())
+        _tail_cnt[key] = torch.zeros(n, dtype=torch.int32, device=torch.device("cuda", key))
+    return _tail_cnt[key]
+
+
+def part_tail_armed(device) -> bool:
+    """Every counter and flag back at zero (the timeout word aside)."""
+    c = part_tail_counters(device)
+    return int(c[:-32].abs().sum().item()) == 0
+
+
+def part_tail_error(device) -> bool:
+    c = _tail_cnt.get(_dev_key(device))
+    return bool(c is not None and int(c[-32].item()) != 0)
+
+
+def part_tail_ok(M, w) -> bool:
+    """bf16 weights with N <= 8192 columns, a grid of at least M blocks."""
+    from .fp8 import Fp8Weight
+
+    if not PART_TAIL or isinstance(w, Fp8Weight) or not (1 <= M <= 64):
+        return False
+    N, K = w.shape
+    ks, S = gemm_part_slabs(M, N, K)
+    return S > 0 and N % 8 == 0 and N <= 8192 and -(-N // 64) * S >= 8 * -(-M // 8)
+
+
+def _tail_args(h, gamma, eps, xn, N):
+    _bf16_2d(h, "h")
+    _req(h.shape[1] == N and gamma.numel() == N and gamma.dtype == torch.bfloat16 and gamma.is_contiguous(),
+         "tail residual / norm weights")
+    if xn is None:
+        xn = torch.empty_like(h)
+    _req(xn.shape == h.shape and xn.stride(1) == 1, "tail output rows")
+    cnt = part_tail_counters(h.device)
+    return xn, (h.data_ptr(), h.stride(0), gamma.data_ptr(), xn.data_ptr(), xn.stride(0), float(eps), cnt.data_ptr(),
+                PART_TAIL_SPIN_US * 100)
+
+
+def gemm_part_tail(x, w, h, gamma, eps, xn=None, P=None):
+    """gemm_part + add_partials_rmsnorm in one launch: h += bf16(x @ w^T) (the split-K slabs summed in
+    slab order, rounded once), returns rmsnorm(h) * gamma -- the same values as the two launches."""
+    _bf16_2d(x, "x")
+    _bf16_2d(w, "w")
+    M, K = x.shape
+    N = w.shape[0]
+    _req(w.shape[1] == K and h.shape[0] == M, "gemm_part_tail shape")
+    ks, S = gemm_part_slabs(M, N, K)
+    _req(S > 0, "gemm_part_tail: unsupported K=%d" % K)
+    if P is None:
+        P = torch.empty((S, M, N), dtype=torch.float32, device=x.device)
+    xn, ta = _tail_args(h, gamma, eps, xn, N)
+    check(_lib.lib().ragk_gemm_part_tail(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), P.data_ptr(), M, N, K, ks,
+                                         *ta, stream_ptr()), "ragk_gemm_part_tail")
+    return xn
+
+
+def gemm_part_merge_tail(attn_out, kv_lens, part_tiles, max_parts, ws_o, ws_ml, Hq, w, h, gamma, eps, xn=None):
+    """gemm_part_merge + add_partials_rmsnorm in one launch (batch <= 4 o_proj): returns the normed rows."""
+    M = kv_lens.numel()
+    N, K = w.shape
+    _bf16_2d(w, "w")
+    _req(attn_out.dtype == torch.bfloat16 and attn_out.stride(1) == 1 and attn_out.shape[0] >= M
+         and attn_out.shape[1] == K and h.shape[0] == M, "attention output rows")
+    _req(ws_o is not None and ws_o.dtype == torch.float32 and ws_o.numel() >= M * Hq * max_parts * 128
+         and ws_ml.numel() >= M * Hq * max_parts * 2, "partition workspace")
+    ks, S = gemm_part_slabs(M, N, K)
+    _req(S > 0 and _lib.lib().ragk_gemm_part_merge_ok(M, K, Hq, max_parts, ks), "gemm_part_merge shape")
+    P = torch.empty((S, M, N), dtype=torch.float32, device=attn_out.device)
+    xn, ta = _tail_args(h, gamma, eps, xn, N)
+    check(_lib.lib().ragk_gemm_part_merge_tail(
+        ws_o.data_ptr(), ws_ml.data_ptr(), attn_out.data_ptr(), attn_out.stride(0), kv_lens.data_ptr(), Hq,
+        part_tiles, max_parts, w.data_ptr(), w.stride(0), P.data_ptr(), M, N, K, ks, *ta, stream_ptr()),
+        "ragk_gemm_part_merge_tail")
+    return xn
+
+
 PREFILL_SPLITK = os.environ.get("RAGK_PREFILL_SPLITK", "1") == "1"
 # measured: M = 5.2k (one RAG prompt) 2 slabs win (o_proj + down 760 -> 656 us per layer); a ~2.2k-token
 # tail step with 4 slabs was no faster than unsplit in the bench profile -> split only M >= 4096, 2 slabs

@@ -1051,6 +1051,73 @@ def test_add_partials_rmsnorm(native, S, M, H):
     assert rel_err(y.cpu(), ref) < 4e-3
 
 
+@pytest.mark.parametrize("M", [1, 3, 5, 32, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336), (8192, 8192), (384, 512)])
+def test_gemm_part_tail_matches_part_then_norm(native, M, N, K, monkeypatch):
+    """gemm_part with the add_partials_rmsnorm consumer in its last M blocks (TL) == gemm_part followed by
+    add_partials_rmsnorm, bit for bit (same slabs, same summation orders); three launches in a row check
+    the counters re-arm (and the slabs are still written)."""
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    g = (1 + 0.1 * torch.randn(N, device=DEV)).bfloat16()
+    h0 = torch.randn(M, N, device=DEV).bfloat16()
+    monkeypatch.setattr(native, "PART_TAIL", True)
+    if not native.part_tail_ok(M, w):
+        pytest.skip("shape not supported by the tail launch")
+    h_ref = h0.clone()
+    xn_ref = native.add_partials_rmsnorm(native.gemm_part(x, w), h_ref, g, 1e-5)
+    cnt = native.part_tail_counters(DEV)
+    assert cnt.numel() >= 32 * 12
+    for it in range(3):
+        h = h0.clone()
+        xn = native.gemm_part_tail(x, w, h, g, 1e-5)
+        torch.cuda.synchronize()
+        assert torch.equal(h, h_ref), (it, (h.float() - h_ref.float()).abs().max().item())
+        assert torch.equal(xn, xn_ref), it
+        assert native.part_tail_armed(DEV), cnt.nonzero().flatten().tolist()
+    hr = (h0.float().cpu() + (x.float() @ w.float().t()).cpu().bfloat16().float()).bfloat16()
+    assert rel_err(h_ref.cpu(), hr) < 1e-2
+    assert not native.part_tail_error(DEV)
+
+
+@pytest.mark.parametrize("kv_lens,target", [([5200], 512), ([70, 3000], 256), ([777, 5300, 65, 2000], 512), ([1], 512)])
+def test_gemm_part_merge_tail_matches_separate(native, kv_lens, target):
+    """o_proj with the partition merge AND the residual + norm consumer in one launch == gemm_part_merge
+    followed by add_partials_rmsnorm, bit for bit."""
+    D, S, Hq, Hkv = 128, 8, 32, 8
+    torch.manual_seed(5)
+    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=9)
+    B = len(kv_lens)
+    kc, vc, bt = kc.to(DEV), vc.to(DEV), bt.to(DEV)
+    kvl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    pos = kvl - 1
+    slots = (bt[torch.arange(B, device=DEV), (pos // 64).long()] * 64 + pos % 64).int()
+    P = torch.randn(S, B, (Hq + 2 * Hkv) * D, device=DEV)
+    cos, sin = R.rope_tables(D, 131072, theta=500000.0)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv, target_blocks=target)
+    if mp < 2:
+        pytest.skip("single partition: no merge launch")
+    w = (torch.randn(4096, Hq * D, device=DEV) / math.sqrt(Hq * D)).bfloat16()
+    g = (1 + 0.1 * torch.randn(4096, device=DEV)).bfloat16()
+    h0 = torch.randn(B, 4096, device=DEV).bfloat16()
+    ws_o = torch.empty((B, Hq, mp, D), dtype=torch.float32, device=DEV)
+    ws_ml = torch.empty((B, Hq, mp, 2), dtype=torch.float32, device=DEV)
+    attn = torch.zeros(B, Hq * D, device=DEV).bfloat16()
+    native.attn_decode_rope(P, pos, cos, sin, slots, kc, vc, bt, kvl, attn, Hq, Hkv, D, pt, mp, ws_o=ws_o,
+                            ws_ml=ws_ml, defer_merge=True)
+    h_ref = h0.clone()
+    xn_ref = native.add_partials_rmsnorm(native.gemm_part_merge(attn, kvl, pt, mp, ws_o, ws_ml, Hq, w), h_ref, g, 1e-5)
+    for it in range(3):
+        h = h0.clone()
+        xn = native.gemm_part_merge_tail(attn, kvl, pt, mp, ws_o, ws_ml, Hq, w, h, g, 1e-5)
+        torch.cuda.synchronize()
+        assert torch.equal(h, h_ref) and torch.equal(xn, xn_ref), it
+    assert native.part_tail_armed(DEV)
+    assert not native.part_tail_error(DEV)
+
+
 @pytest.mark.parametrize("S,T", [(4, 33), (9, 32), (16, 1)])  # S > 8: more than one unrolled slab group
 def test_rope_kv_partials(native, S, T):
     torch.manual_seed(12)

@@ -147,12 +147,14 @@ def test_split_k_decode_path_matches_plain_decode(tiny):
     for part in (False, True):
         model = LlamaModel(cfg, w, "cpu", max_positions=512)
         model.be.enable_part = part
-        calls = []
+        calls, tails = [], []
         orig = model.hidden_states_decode_part
         model.hidden_states_decode_part = lambda inp, h: (calls.append(1), orig(inp, h))[1]
+        orig_tail = model.be.gemm_part_tail  # the norm-in-the-GEMM's-tail form (TP=1 o_proj / down)
+        model.be.gemm_part_tail = lambda *a: (tails.append(1), orig_tail(*a))[1]
         eng = LLMEngine(model, num_blocks=32, max_batch=4, max_model_len=512, use_graphs=False)
         outs.append(eng.generate(prompts, params))
-        assert bool(calls) == part
+        assert bool(calls) == part and bool(tails) == part
     assert outs[0] == outs[1]
 
 

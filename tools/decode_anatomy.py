@@ -29,8 +29,14 @@ def main():
     m = L.LlamaModel(cfg, w, dev, max_positions=8192)
     # DA_PF="off,16:128,32:255": decode MALL prefetch configs (MB per window : rider blocks) to A/B
     cfgs = [c for c in os.environ.get("DA_PF", "").split(",") if c] or [None]
-    runs = [(B, c) for c in cfgs for B in Bs]
-    for B, pfc in runs:
+    # DA_TAIL="1,0,1,0": alternate the norm-in-the-GEMM-tail launches (native.PART_TAIL) on / off
+    tails = [t for t in os.environ.get("DA_TAIL", "").split(",") if t] or [None]
+    runs = [(B, c, t) for t in tails for c in cfgs for B in Bs]
+    from rag_llm_k8s_amd.ops import native
+    for B, pfc, tl in runs:
+        if tl is not None:
+            native.PART_TAIL = tl == "1"
+            print("-- part tail %s" % tl, flush=True)
         if pfc is not None:
             L.DECODE_PF = pfc != "off"
             if L.DECODE_PF:
