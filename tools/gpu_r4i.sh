@@ -14,3 +14,7 @@ for t in 1 0; do
   RAGK_DECODE_PART_TAIL=$t C1_N=4 timeout -k 10 300 python tools/c1_probe.py > gpurun_out/r4i_c1_$t.log 2>&1 || exit $?
   echo "tail=$t: $(tail -1 gpurun_out/r4i_c1_$t.log)"
 done
+DA_NT=1,0,1,0 DA_STEPS=48 timeout -k 10 400 python -u tools/decode_anatomy.py 32 > gpurun_out/r4i_nt.log 2>&1 || exit $?
+grep -E "^--|ms/step" gpurun_out/r4i_nt.log
+DA_FM=1,0,1,0 DA_STEPS=48 timeout -k 10 400 python -u tools/decode_anatomy.py 1 32 > gpurun_out/r4i_fm.log 2>&1 || exit $?
+grep -E "^--|ms/step" gpurun_out/r4i_fm.log
