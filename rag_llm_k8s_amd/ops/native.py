@@ -241,8 +241,10 @@ def gemm_part(x, w, out=None, ks=None):
 
 
 # The residual add + RMSNorm consumer of a split-K decode GEMM inside the GEMM's last M blocks
-# (gemm_part.hip TL): TP=1 o_proj and down, every decode batch. RAGK_DECODE_PART_TAIL=0 restores the
-# separate add_partials_rmsnorm launch (default until the sharded-arrival form is measured).
+# (gemm_part.hip TL): TP=1 o_proj and down, every decode batch. Off by default: measured SLOWER than the
+# separate add_partials_rmsnorm launch it replaces (one counter: 3.74-3.81 vs 3.62 ms per step at batch 1,
+# 7.78-7.84 vs 7.54 at batch 32; per-XCD sharded counters: 3.71 vs 3.58 and 7.68 vs 7.57;
+# profiles/decode_tail_ab_r4.log) -- kept, tested bit-exact, for A/B (RAGK_DECODE_PART_TAIL=1).
 PART_TAIL = os.environ.get("RAGK_DECODE_PART_TAIL", "0") == "1"
 PART_TAIL_SPIN_US = int(os.environ.get("RAGK_PART_TAIL_SPIN_US", "1000000"))
 _tail_cnt = {}
@@ -964,6 +966,17 @@ def decode_partitions(max_kv_len, batch, Hkv, target_blocks=None, min_tiles=None
     return min_tiles, mp
 
 
+# Non-temporal K / V loads in the split-K decode attention from this batch up: at batch 32 over 5.2k-token
+# contexts the KV stream (681 MB per layer) is read once per step, and the nt policy keeps it from
+# evicting the L2 / Infinity Cache lines the other kernels reuse: decode step 7.60 -> 7.33 ms in situ
+# (same process, alternating; profiles/decode_nt_ab_r4.log).
+DECODE_NT_MIN_B = int(os.environ.get("RAGK_DECODE_NT_MIN_B", "8"))
+
+
+def _set_decode_nt(B):
+    check(_lib.lib().ragk_attn_decode_set_nt(1 if B >= DECODE_NT_MIN_B else 0), "ragk_attn_decode_set_nt")
+
+
 def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, part_tiles, max_parts, ws_o=None,
                 ws_ml=None, scale=None):
     B = kv_lens.numel()
@@ -982,6 +995,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, par
     if max_parts > 1 and ATTN_FUSED_MERGE and 2 * G * max_parts + 16 <= 4 * 64 * D * 2 // 4:
         cnt = _attn_counters(q.device)
         _req(B * Hkv <= cnt.numel(), "attention ticket buffer too small")
+    _set_decode_nt(B)
     check(_lib.lib().ragk_attn_decode(
         q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
         block_tables.stride(0), kv_lens.data_ptr(), ptr(ws_o), ptr(ws_ml), out.data_ptr(), out.stride(0), B, Hq, Hkv,
@@ -1018,6 +1032,7 @@ def attn_decode_rope(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_
         cnt = _attn_counters(P.device)
         _req(B * Hkv <= cnt.numel(), "attention ticket buffer too small")
     lib = _lib.lib()
+    _set_decode_nt(B)
     if defer_merge:
         lib.ragk_attn_decode_set_defer(1)
     try:
@@ -1034,8 +1049,9 @@ def attn_decode_rope(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_
 
 # split-K decode attention: the last partition block of each (sequence, KV head) merges the partitions
 # (a ticket per pair; zeroed once, reset by the merging block) instead of a separate merge launch
-# Off by default: measured slower at batch 1 (4.41 vs 4.2-4.3 ms per decode step; every partition
-# block's agent-scope release writes back its L2), kept for A/B (tests/test_kernels_gpu.py checks it).
+# Off by default: measured slower at batch 1 (4.41 vs 4.2-4.3 ms per decode step with agent-scope
+# releases; round 4, write-through form: 3.76 / 3.82 vs 3.62 / 3.65 ms at batch 1, neutral at batch 32,
+# profiles/decode_fm_ab_r4.log), kept for A/B (tests/test_kernels_gpu.py checks it).
 ATTN_FUSED_MERGE = os.environ.get("RAGK_ATTN_FUSED_MERGE", "0") == "1"
 _attn_cnt = {}
 

@@ -31,12 +31,12 @@ def main():
     cfgs = [c for c in os.environ.get("DA_PF", "").split(",") if c] or [None]
     # DA_TAIL="1,0,1,0": alternate the norm-in-the-GEMM-tail launches (native.PART_TAIL) on / off
     tails = [t for t in os.environ.get("DA_TAIL", "").split(",") if t] or [None]
-    # DA_NT="0,1,0,1": alternate non-temporal K/V loads in the decode attention (ragk_attn_decode_set_nt)
+    # DA_NT="0,1,0,1": alternate non-temporal K/V loads in the decode attention (native.DECODE_NT_MIN_B)
     nts = [t for t in os.environ.get("DA_NT", "").split(",") if t] or [None]
     # DA_FM="0,1,0,1": alternate the attention's in-kernel split-K merge (native.ATTN_FUSED_MERGE)
     fms = [t for t in os.environ.get("DA_FM", "").split(",") if t] or [None]
     runs = [(B, c, t, nt, fm) for fm in fms for nt in nts for t in tails for c in cfgs for B in Bs]
-    from rag_llm_k8s_amd.ops import _lib, native
+    from rag_llm_k8s_amd.ops import native
     for B, pfc, tl, nt, fm in runs:
         if fm is not None:
             native.ATTN_FUSED_MERGE = fm == "1"
@@ -45,7 +45,7 @@ def main():
             native.PART_TAIL = tl == "1"
             print("-- part tail %s" % tl, flush=True)
         if nt is not None:
-            _lib.lib().ragk_attn_decode_set_nt(int(nt))
+            native.DECODE_NT_MIN_B = 1 if nt == "1" else 1 << 30
             print("-- decode attention nt %s" % nt, flush=True)
         if pfc is not None:
             L.DECODE_PF = pfc != "off"

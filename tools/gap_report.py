@@ -13,8 +13,12 @@ import sys
 from collections import defaultdict
 
 
+def _base(name):
+    return name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+
+
 def kind(name):
-    n = name.split("(")[0]
+    n = _base(name)
     if "gemm_w4" in n or "gemm_pp" in n or "attn_prefill" in n:
         return "prefill"
     if any(k in n for k in ("gemm_part", "gemm_stream", "gemm_skinny", "gemm_dec", "attn_decode", "add_partials",
@@ -24,8 +28,7 @@ def kind(name):
 
 
 def short(name):
-    n = name.split("(")[0]
-    return n.replace("void ", "").replace("(anonymous namespace)::", "")[:60]
+    return _base(name)[:60]
 
 
 def main(path, max_gap_ms=20.0):
@@ -37,6 +40,10 @@ def main(path, max_gap_ms=20.0):
     if not ks:
         print("no kernels")
         return
+    # the serving window: from the first prefill kernel on (weight init / ingest before it are setup)
+    first = next((i for i, k in enumerate(ks) if kind(k[2]) == "prefill"), 0)
+    if "--all" not in sys.argv:
+        ks = ks[first:]
     busy = 0
     cur_s, cur_e, cur_n = ks[0]
     gaps = []
@@ -78,4 +85,5 @@ def main(path, max_gap_ms=20.0):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 20.0)
+    args = [a for a in sys.argv[1:] if a != "--all"]
+    main(args[0], float(args[1]) if len(args) > 1 else 20.0)

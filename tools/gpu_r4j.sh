@@ -10,4 +10,4 @@ f=$(find gpurun_out/prof_gap -name "*kernel_trace.csv" | head -1)
 python tools/gap_report.py "$f" > gpurun_out/gap_report.txt && cat gpurun_out/gap_report.txt
 s=$(find gpurun_out/prof_gap -name "*kernel_stats.csv" | head -1)
 python tools/rocprof_summary.py "$s" 30 > gpurun_out/prof_gap_summary.txt
-rm -f "$f"
+gzip -f "$f"
