@@ -205,7 +205,7 @@ constexpr int SK_WAVES = 8;
 // WV waves per block (default 8; 16 is an A/B option for long-K / few-column shapes such as the
 // batch-1 down projection -- measured slower there: more waves per block lengthen the LDS reduction
 // and the per-block tail more than the extra loads in flight gain).
-template <int MT, int EPI, bool OUT_F32, int WV = SK_WAVES>
+template <int MT, int EPI, bool OUT_F32, int WV = SK_WAVES, int UN = 2>
 __global__ __launch_bounds__(WV * 64) void gemm_skinny_kernel(
     const bf16_t* __restrict__ X, int ldx, const bf16_t* __restrict__ W, int ldw, void* C, int ldc,
     const bf16_t* __restrict__ bias, const bf16_t* resid, int ldr, int M, int N, int K) {
@@ -245,27 +245,42 @@ __global__ __launch_bounds__(WV * 64) void gemm_skinny_kernel(
 
   const int nkb = K >> 7;  // 128-deep K blocks
   const bf16x8 zero = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  for (int kb = wid; kb < nkb; kb += WV) {
-    const int k = kb * 128;
-    bf16x8 wf[NACC][4];
+  // two of the wave's K blocks per iteration, both blocks' weight loads issued before any use (a wave
+  // with one block's 4 loads in flight kept the 256-block batch-1 down projection latency-bound at
+  // ~4.9 TB/s); weights are read once per step -> non-temporal
+  constexpr int U = (PAIR || MT > 1) ? 1 : UN;
+  for (int kb = wid; kb < nkb; kb += U * WV) {
+    bf16x8 wf[U][NACC][4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      wf[0][s] = *reinterpret_cast<const bf16x8*>(w0 + k + 32 * s);
-      if constexpr (PAIR) wf[1][s] = *reinterpret_cast<const bf16x8*>(w1 + k + 32 * s);
+    for (int u = 0; u < U; ++u) {
+      const int k = min(kb + u * WV, nkb - 1) * 128;  // clamped: a missing second block is loaded, not used
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        wf[u][0][s] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w0 + k + 32 * s));
+        if constexpr (PAIR) wf[u][1][s] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w1 + k + 32 * s));
+      }
     }
-    bf16x8 xf[MT][4];
+    bf16x8 xf[U][MT][4];
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        xf[t][s] = xv[t] ? *reinterpret_cast<const bf16x8*>(xr[t] + k + 32 * s) : zero;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int u = 0; u < U; ++u) {
+      const int k = min(kb + u * WV, nkb - 1) * 128;
 #pragma unroll
       for (int t = 0; t < MT; ++t)
 #pragma unroll
-        for (int a = 0; a < NACC; ++a)
-          acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[t][s], wf[a][s], acc[a][t], 0, 0, 0);
+        for (int s = 0; s < 4; ++s)
+          xf[u][t][s] = xv[t] ? *reinterpret_cast<const bf16x8*>(xr[t] + k + 32 * s) : zero;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (kb + u * WV >= nkb) break;  // wave-uniform
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int a = 0; a < NACC; ++a)
+            acc[a][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[u][t][s], wf[u][a][s], acc[a][t], 0, 0, 0);
+    }
   }
 
 #pragma unroll
@@ -466,6 +481,12 @@ hipError_t launch_tile(const void* A, int lda, const void* B, int ldb, void* C, 
 }
 
 static int g_skinny_waves = -1;  // -1: auto (RAGK_SKINNY_WAVES env, else by shape)
+// 128-deep K blocks per wave per iteration of the batch-1 skinny GEMM (A/B knob; 2 = default)
+static int g_skinny_unroll = 2;
+RAGK_API int ragk_gemm_skinny_set_unroll(int u) {
+  g_skinny_unroll = u == 1 ? 1 : 2;
+  return 0;
+}
 RAGK_API int ragk_gemm_skinny_set_waves(int w) {
   g_skinny_waves = (w == 8 || w == 16) ? w : -1;
   return 0;
@@ -487,9 +508,14 @@ hipError_t launch_skinny(const void* X, int ldx, const void* W, int ldw, void* C
                        (const bf16_t*)resid, ldr, M, N, K);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0, st,
-                     (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
-                     (const bf16_t*)resid, ldr, M, N, K);
+  if (g_skinny_unroll == 1)
+    hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, SK_WAVES, 1>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0,
+                       st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
+                       (const bf16_t*)resid, ldr, M, N, K);
+  else
+    hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0, st,
+                       (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
+                       (const bf16_t*)resid, ldr, M, N, K);
   return hipGetLastError();
 }
 

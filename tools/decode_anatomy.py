@@ -35,9 +35,14 @@ def main():
     nts = [t for t in os.environ.get("DA_NT", "").split(",") if t] or [None]
     # DA_FM="0,1,0,1": alternate the attention's in-kernel split-K merge (native.ATTN_FUSED_MERGE)
     fms = [t for t in os.environ.get("DA_FM", "").split(",") if t] or [None]
-    runs = [(B, c, t, nt, fm) for fm in fms for nt in nts for t in tails for c in cfgs for B in Bs]
-    from rag_llm_k8s_amd.ops import native
-    for B, pfc, tl, nt, fm in runs:
+    # DA_SKU="2,1,2,1": K blocks per wave per iteration of the batch-1 skinny GEMM (down projection)
+    skus = [t for t in os.environ.get("DA_SKU", "").split(",") if t] or [None]
+    runs = [(B, c, t, nt, fm, sk) for sk in skus for fm in fms for nt in nts for t in tails for c in cfgs for B in Bs]
+    from rag_llm_k8s_amd.ops import _lib, native
+    for B, pfc, tl, nt, fm, sk in runs:
+        if sk is not None:
+            _lib.lib().ragk_gemm_skinny_set_unroll(int(sk))
+            print("-- skinny unroll %s" % sk, flush=True)
         if fm is not None:
             native.ATTN_FUSED_MERGE = fm == "1"
             print("-- attention fused merge %s" % fm, flush=True)
