@@ -135,7 +135,12 @@ __device__ __forceinline__ void stage_load(const bf16_t* __restrict__ X, int ldx
   }
 }
 
-template <int MT, int EPI, bool OUT_F32, bool FP8, bool NT = false, int ROWS = WROWS>
+// SLAB: split-K partial mode for the decode consumers (add_partials_rmsnorm / rope_kv_partials / the
+// decode attention's qkv staging): every block writes its fp32 partial tile to P[slice][row][col]
+// ([S][M][N], gemm_part's layout) and exits -- no ticket, no in-kernel reduction (the release / acquire
+// of the last-arriver form made the 8-way split down projection 56 us at batch 32; gemm_part's
+// register-streaming blocks need 114 KB of LDS for its activation slice there and run in two rounds).
+template <int MT, int EPI, bool OUT_F32, bool FP8, bool NT = false, int ROWS = WROWS, bool SLAB = false>
 __global__ __launch_bounds__(ST_THREADS, ROWS == 64 ? 2 : 1) void gemm_stream_kernel(
     const bf16_t* __restrict__ X, int ldx, const void* __restrict__ Wv, int ldw, const float* __restrict__ wscale,
     void* C, int ldc, const bf16_t* __restrict__ bias, const bf16_t* resid, int ldr, int M, int N, int K, int S,
@@ -237,6 +242,18 @@ __global__ __launch_bounds__(ST_THREADS, ROWS == 64 ? 2 : 1) void gemm_stream_ke
       for (int r = 0; r < 4; ++r)
         sC[(16 * m + 4 * fh + r) * G::EPI_LD + wid * (ROWS / 4) + 16 * j + fr] = acc[m][j][r];
   __syncthreads();
+  if constexpr (SLAB) {
+    float* ps = reinterpret_cast<float*>(C) + (size_t)slice * M * N;
+    for (int e = tid; e < M * (ROWS / 4); e += ST_THREADS) {
+      const int row = e / (ROWS / 4), c4 = (e % (ROWS / 4)) * 4;
+      const int col = ntile * ROWS + c4;
+      if (col < N) {  // N % 4 == 0 (host check)
+        const float* src = sC + row * G::EPI_LD + c4;
+        *reinterpret_cast<f32x4*>(ps + (size_t)row * N + col) = (f32x4){src[0], src[1], src[2], src[3]};
+      }
+    }
+    return;
+  }
 
   auto finish = [&](int row, int c, float v) {  // c = output column
     if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RESID || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_GELU_TANH)
@@ -353,6 +370,20 @@ int launch_stream(const void* X, int ldx, const void* W, int ldw, const float* w
   return (int)hipGetLastError();
 }
 
+template <int MT>
+int launch_stream_slab(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K, int S, int rows,
+                       hipStream_t st) {
+  const dim3 grid((N + rows - 1) / rows, S);
+  if (rows == 64)
+    hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI_NONE, true, false, true, 64, true>), grid, dim3(ST_THREADS), 0, st,
+                       (const bf16_t*)X, ldx, W, ldw, nullptr, P, N, nullptr, nullptr, 0, M, N, K, S, nullptr, nullptr);
+  else
+    hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI_NONE, true, false, true, WROWS, true>), grid, dim3(ST_THREADS), 0,
+                       st, (const bf16_t*)X, ldx, W, ldw, nullptr, P, N, nullptr, nullptr, 0, M, N, K, S, nullptr,
+                       nullptr);
+  return (int)hipGetLastError();
+}
+
 template <int EPI, bool F32, bool FP8>
 int dispatch_stream(const void* X, int ldx, const void* W, int ldw, const float* wscale, void* C, int ldc,
                     const void* bias, const void* resid, int ldr, int M, int N, int K, int S, float* ws, int* cnt,
@@ -441,4 +472,20 @@ RAGK_API int ragk_gemm_stream(const void* X, int ldx, const void* W, int ldw, co
     default: return (int)hipErrorInvalidValue;
   }
 #undef RAGK_ST_CASE
+}
+
+// Split-K partial slabs P[S][M][N] (fp32) of X[M,K] . W[N,K]^T through the LDS-DMA weight ring (SLAB
+// above): bf16 weights, M <= 64, N % 4 == 0, S | K / 64, rows = 64 (two blocks per CU) or 128.
+RAGK_API int ragk_gemm_stream_part(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K,
+                                   int S, int rows, hipStream_t st) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > 64 || K % 64 || S < 1 || (K / 64) % S || N % 4 || (rows != 64 && rows != 128) || ldx % 8 || ldw % 8)
+    return (int)hipErrorInvalidValue;
+  switch ((M + 15) / 16) {
+    case 1: return launch_stream_slab<1>(X, ldx, W, ldw, P, M, N, K, S, rows, st);
+    case 2: return launch_stream_slab<2>(X, ldx, W, ldw, P, M, N, K, S, rows, st);
+    case 3: return launch_stream_slab<3>(X, ldx, W, ldw, P, M, N, K, S, rows, st);
+    case 4: return launch_stream_slab<4>(X, ldx, W, ldw, P, M, N, K, S, rows, st);
+    default: return (int)hipErrorInvalidValue;
+  }
 }

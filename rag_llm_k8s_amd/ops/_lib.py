@@ -42,6 +42,7 @@ _SIGS = {
     "ragk_gemm_part_merge_ok": [I, I, I, I, I],
     "ragk_gemm_part_tail_ints": [],
     "ragk_gemm_skinny_set_unroll": [I],
+    "ragk_gemm_stream_part": [P, I, P, I, P, I, I, I, I, I, S],
     "ragk_gemm_part_tail": [P, I, P, I, P, I, I, I, I, P, I, P, P, I, F, P, ctypes.c_uint, S],
     "ragk_gemm_part_merge_tail": [P, P, P, I, P, I, I, I, P, I, P, I, I, I, I, P, I, P, P, I, F, P, ctypes.c_uint, S],
     "ragk_gemm_part_silu": [P, I, P, I, P, I, I, I, I, S],

@@ -207,6 +207,47 @@ def gemm_part_norm(h, gamma, eps, w, out=None, ks=None):
     return out
 
 
+# Split-K partial slabs through the LDS-DMA weight ring (gemm_stream.hip SLAB) instead of gemm_part's
+# register-streaming blocks, at decode batches above STREAM_PART_MIN_M: the down projection's 1792-deep
+# activation slice needs 114 KB of LDS per gemm_part block at batch 32 (one block per CU, two rounds).
+STREAM_PART = os.environ.get("RAGK_DECODE_STREAM_PART", "0") == "1"
+STREAM_PART_MIN_M = int(os.environ.get("RAGK_STREAM_PART_MIN_M", "17"))
+
+
+def stream_part_cfg(M, N, K):
+    """(rows, S) of the slab-mode stream GEMM: the most blocks that are co-resident (128-row tiles one
+    block per CU, 64-row tiles two), at least 8 K-steps of 64 per block; (0, 0) if nothing fits."""
+    cus = _cu_count()
+    steps = K // 64
+    best = (0, 0, 0)
+    for rows, per_cu in ((128, 1), (64, 2)):
+        tiles = -(-N // rows)
+        S = 1
+        while tiles * S * 2 <= per_cu * cus and steps % (S * 2) == 0 and steps // (S * 2) >= 8:
+            S *= 2
+        blocks = tiles * S
+        if blocks <= per_cu * cus and (blocks / per_cu, rows) > (best[2], best[0]):
+            best = (rows, S, blocks / per_cu)
+    return best[0], best[1]
+
+
+def gemm_stream_part(x, w, out=None, rows=None, S=None):
+    """Partial slabs P[S, M, N] (fp32) with P.sum(0) = x @ w^T from the LDS-DMA stream GEMM (bf16 weights)."""
+    _bf16_2d(x, "x")
+    _bf16_2d(w, "w")
+    M, K = x.shape
+    N = w.shape[0]
+    _req(w.shape[1] == K and M <= 64 and K % 64 == 0 and N % 4 == 0, "gemm_stream_part shape")
+    r0, s0 = stream_part_cfg(M, N, K)
+    rows, S = rows or r0, S or s0
+    _req(rows in (64, 128) and S >= 1 and (K // 64) % S == 0, "gemm_stream_part config")
+    if out is None:
+        out = torch.empty((S, M, N), dtype=torch.float32, device=x.device)
+    check(_lib.lib().ragk_gemm_stream_part(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), M, N,
+                                           K, S, rows, stream_ptr()), "ragk_gemm_stream_part")
+    return out
+
+
 def gemm_part(x, w, out=None, ks=None):
     """Decode GEMM v5 (csrc/kernels/gemm_part.hip): fp32 split-K partials P[S, M, N] with
     P.sum(0) = x @ w^T. The consumer (add_partials_rmsnorm / rope_kv_partials) does the reduction.
@@ -225,6 +266,9 @@ def gemm_part(x, w, out=None, ks=None):
     M, K = x.shape
     N = wt.shape[0]
     _req(wt.shape[1] == K and M <= 64, "gemm_part shape %s x %s" % (tuple(x.shape), tuple(wt.shape)))
+    if (STREAM_PART and not fp8 and ks is None and out is None and M >= STREAM_PART_MIN_M and K % 64 == 0
+            and N % 4 == 0 and stream_part_cfg(M, N, K)[1] > 0):
+        return gemm_stream_part(x, wt)
     ks, S = gemm_part_slabs(M, N, K, ks)
     _req(S > 0, "gemm_part: unsupported K=%d" % K)
     if out is None:

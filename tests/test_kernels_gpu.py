@@ -1013,6 +1013,22 @@ def test_gemm_part(native, M, N, K):
     assert rel_err(P.sum(0), x.float() @ w.float().t()) < 2e-3
 
 
+@pytest.mark.parametrize("M", [17, 32, 64])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (1000, 1024), (4096, 1792)])
+@pytest.mark.parametrize("rows", [None, 64])
+def test_gemm_stream_part(native, M, N, K, rows):
+    """Split-K slabs from the LDS-DMA stream GEMM (gemm_stream.hip SLAB): P.sum(0) = x @ w^T, [S, M, N]."""
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    r, S = native.stream_part_cfg(M, N, K)
+    if S == 0:
+        pytest.skip("no co-resident split for this shape")
+    P = native.gemm_stream_part(x, w, rows=rows)
+    assert P.shape[1:] == (M, N) and (K // 64) % P.shape[0] == 0
+    assert rel_err(P.sum(0), x.float() @ w.float().t()) < 2e-3
+
+
 @pytest.mark.parametrize("M", [1, 2, 4])
 @pytest.mark.parametrize("I,H", [(1792, 4096), (3584, 4096), (7168, 4096), (3584, 8192), (14336, 4096)])
 def test_gemm_part_silu(native, M, I, H):

@@ -37,9 +37,15 @@ def main():
     fms = [t for t in os.environ.get("DA_FM", "").split(",") if t] or [None]
     # DA_SKU="2,1,2,1": K blocks per wave per iteration of the batch-1 skinny GEMM (down projection)
     skus = [t for t in os.environ.get("DA_SKU", "").split(",") if t] or [None]
-    runs = [(B, c, t, nt, fm, sk) for sk in skus for fm in fms for nt in nts for t in tails for c in cfgs for B in Bs]
+    # DA_SP="1,0,1,0": split-K decode slabs from the LDS-DMA stream GEMM (native.STREAM_PART) or gemm_part
+    sps = [t for t in os.environ.get("DA_SP", "").split(",") if t] or [None]
+    runs = [(B, c, t, nt, fm, sk, sp) for sp in sps for sk in skus for fm in fms for nt in nts for t in tails
+            for c in cfgs for B in Bs]
     from rag_llm_k8s_amd.ops import _lib, native
-    for B, pfc, tl, nt, fm, sk in runs:
+    for B, pfc, tl, nt, fm, sk, sp in runs:
+        if sp is not None:
+            native.STREAM_PART = sp == "1"
+            print("-- stream part %s" % sp, flush=True)
         if sk is not None:
             _lib.lib().ragk_gemm_skinny_set_unroll(int(sk))
             print("-- skinny unroll %s" % sk, flush=True)
