@@ -210,7 +210,9 @@ def gemm_part_norm(h, gamma, eps, w, out=None, ks=None):
 # Split-K partial slabs through the LDS-DMA weight ring (gemm_stream.hip SLAB) instead of gemm_part's
 # register-streaming blocks, at decode batches above STREAM_PART_MIN_M: the down projection's 1792-deep
 # activation slice needs 114 KB of LDS per gemm_part block at batch 32 (one block per CU, two rounds).
-STREAM_PART = os.environ.get("RAGK_DECODE_STREAM_PART", "0") == "1"
+# Batch 32: decode step 7.35 / 7.33 -> 6.91 / 6.98 ms, bench 1568 / 1570 -> 1597 / 1595 tok/s (same box,
+# alternating; profiles/bench_stream_part_ab_r4.log).
+STREAM_PART = os.environ.get("RAGK_DECODE_STREAM_PART", "1") == "1"
 STREAM_PART_MIN_M = int(os.environ.get("RAGK_STREAM_PART_MIN_M", "17"))
 
 
