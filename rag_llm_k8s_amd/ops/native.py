@@ -84,6 +84,7 @@ def use_dec(M, N, K, epi):
 
 STREAM_DEFAULT = os.environ.get("RAGK_STREAM_GEMM", "1") == "1"
 STREAM_MIN_ROWS = int(os.environ.get("RAGK_STREAM_MIN_ROWS", "16384"))
+STREAM_MAX_ROWS = int(os.environ.get("RAGK_STREAM_MAX_ROWS", "32768"))
 
 
 def use_stream(M, N, K, epi, fp8=False):
@@ -92,7 +93,7 @@ def use_stream(M, N, K, epi, fp8=False):
     fp8 2.6 vs 1.5 at M=32) and other 16k-32k-row weights. Below that, the fixed pipeline-fill +
     split-K reduction latencies lose to the register-streaming kernels (profiles/tune_stream_r1.json)."""
     rows = 2 * N if epi == "silu_mul" else N
-    if M > 64 or not (STREAM_MIN_ROWS <= rows < 32768) or K % 128:
+    if M > 64 or not (STREAM_MIN_ROWS <= rows < STREAM_MAX_ROWS) or K % 128:
         return False
     return M > 16 if fp8 else True
 
@@ -213,7 +214,8 @@ def gemm_part_norm(h, gamma, eps, w, out=None, ks=None):
 # Batch 32: decode step 7.35 / 7.33 -> 6.91 / 6.98 ms, bench 1568 / 1570 -> 1597 / 1595 tok/s (same box,
 # alternating; profiles/bench_stream_part_ab_r4.log).
 STREAM_PART = os.environ.get("RAGK_DECODE_STREAM_PART", "1") == "1"
-STREAM_PART_MIN_M = int(os.environ.get("RAGK_STREAM_PART_MIN_M", "17"))
+STREAM_PART_MIN_M = int(os.environ.get("RAGK_STREAM_PART_MIN_M", "5"))  # batch 8 / 16 -3 %, batch 4 +0.6 %
+STREAM_PART_ROWS = int(os.environ.get("RAGK_STREAM_PART_ROWS", "0"))  # 0: by occupancy (ties: 128)
 
 
 def stream_part_cfg(M, N, K):
@@ -223,6 +225,8 @@ def stream_part_cfg(M, N, K):
     steps = K // 64
     best = (0, 0, 0)
     for rows, per_cu in ((128, 1), (64, 2)):
+        if STREAM_PART_ROWS and rows != STREAM_PART_ROWS:
+            continue
         tiles = -(-N // rows)
         S = 1
         while tiles * S * 2 <= per_cu * cus and steps % (S * 2) == 0 and steps // (S * 2) >= 8:
