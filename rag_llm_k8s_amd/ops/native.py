@@ -234,6 +234,10 @@ def stream_part_cfg(M, N, K):
         blocks = tiles * S
         if blocks <= per_cu * cus and (blocks / per_cu, rows) > (best[2], best[0]):
             best = (rows, S, blocks / per_cu)
+    # a grid that fills less than half the CUs (tensor-parallel shards: o_proj K = 512 cannot be split
+    # into 8-step slices) stays on gemm_part, whose 64-column blocks split finer
+    if best[2] < 0.5 * cus:
+        return 0, 0
     return best[0], best[1]
 
 

@@ -1022,9 +1022,8 @@ def test_gemm_stream_part(native, M, N, K, rows):
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
     r, S = native.stream_part_cfg(M, N, K)
-    if S == 0:
-        pytest.skip("no co-resident split for this shape")
-    P = native.gemm_stream_part(x, w, rows=rows)
+    # shapes the policy leaves on gemm_part (grid under half the CUs) still run correctly with an explicit split
+    P = native.gemm_stream_part(x, w, rows=rows or r or 128, S=S or 2)
     assert P.shape[1:] == (M, N) and (K // 64) % P.shape[0] == 0
     assert rel_err(P.sum(0), x.float() @ w.float().t()) < 2e-3
 
