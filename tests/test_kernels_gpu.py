@@ -598,6 +598,7 @@ def test_attn_oproj_fused_matches_unfused(native, kv_lens, target, Hq, Hkv, ks, 
     an fp32 oracle. Three launches in a row check that the kernel re-arms its counters. Covers one token,
     one / many partitions, mixed lengths, M = 1..4, the TP=8 per-rank heads (4 / 1, 8 / 1) and 70B's 64 / 8."""
     D, S = 128, 8
+    monkeypatch.setattr(native, "ATTN_OPROJ", True)  # off by default (slower, PERF_NOTES round 4)
     monkeypatch.setattr(native, "ATTN_OPROJ_MIA", mia)
     monkeypatch.setattr(native, "ATTN_OPROJ_V2", v2)
     torch.manual_seed(31)
@@ -663,6 +664,7 @@ def test_qkv_attn_oproj_matches_unfused(native, kv_lens, Hq, Hkv, qks, mia, v2, 
     gemm_part -> attn_decode_rope -> gemm_part -> add_partials_rmsnorm, up to fp32 summation order; the
     same KV-cache contents; repeated launches re-arm the counters."""
     D, H = 128, 4096
+    monkeypatch.setattr(native, "ATTN_OPROJ", True)  # off by default (slower, PERF_NOTES round 4)
     monkeypatch.setattr(native, "ATTN_OPROJ_MIA", mia)
     monkeypatch.setattr(native, "ATTN_OPROJ_V2", v2)
     torch.manual_seed(41)
@@ -1000,8 +1002,10 @@ def test_gemm_stream_bf16(native, M, N, K):
 @pytest.mark.parametrize("M", [1, 7, 16, 32, 33, 64])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (384, 512), (1000, 1024),
                                  (4096, 1792), (768, 4096), (4096, 512)])  # TP=8 shard down / qkv / o_proj
-def test_gemm_part(native, M, N, K):
-    """Decode GEMM v5: fp32 split-K partial slabs sum to x @ w^T."""
+def test_gemm_part(native, M, N, K, monkeypatch):
+    """Decode GEMM v5: fp32 split-K partial slabs sum to x @ w^T (the register-streaming kernel itself;
+    the stream GEMM's slab mode, which gemm_part dispatches to from batch 5, has its own test)."""
+    monkeypatch.setattr(native, "STREAM_PART", False)
     torch.manual_seed(3)
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
@@ -1078,6 +1082,7 @@ def test_gemm_part_tail_matches_part_then_norm(native, M, N, K, monkeypatch):
     g = (1 + 0.1 * torch.randn(N, device=DEV)).bfloat16()
     h0 = torch.randn(M, N, device=DEV).bfloat16()
     monkeypatch.setattr(native, "PART_TAIL", True)
+    monkeypatch.setattr(native, "STREAM_PART", False)  # the reference is the same gemm_part kernel's slabs
     if not native.part_tail_ok(M, w):
         pytest.skip("shape not supported by the tail launch")
     h_ref = h0.clone()
