@@ -663,6 +663,14 @@ class LLMEngine:
             return
         for b in sizes or self.buckets:
             self._decode_graph(b)
+        # tensor parallel: leave warm-up together. A rank still capturing (host-bound, seconds on a loaded
+        # host) would otherwise keep the others' first collectives spinning in their bounded peer waits.
+        grp = getattr(self.comm, "cpu_group", None)
+        if self.tp_size > 1 and grp is not None:
+            import torch.distributed as dist
+
+            torch.cuda.synchronize()
+            dist.barrier(group=grp)
 
     # ------------------------------------------------------------------ asynchronous decode
     def _decode_inputs_async(self, seqs, B, carried):

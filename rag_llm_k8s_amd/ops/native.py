@@ -216,6 +216,7 @@ def gemm_part_norm(h, gamma, eps, w, out=None, ks=None):
 STREAM_PART = os.environ.get("RAGK_DECODE_STREAM_PART", "1") == "1"
 STREAM_PART_MIN_M = int(os.environ.get("RAGK_STREAM_PART_MIN_M", "5"))  # batch 8 / 16 -3 %, batch 4 +0.6 %
 STREAM_PART_ROWS = int(os.environ.get("RAGK_STREAM_PART_ROWS", "0"))  # 0: by occupancy (ties: 128)
+STREAM_PART_MAX_S = int(os.environ.get("RAGK_STREAM_PART_MAX_S", "64"))  # slabs the consumer sums
 
 
 def stream_part_cfg(M, N, K):
@@ -229,7 +230,8 @@ def stream_part_cfg(M, N, K):
             continue
         tiles = -(-N // rows)
         S = 1
-        while tiles * S * 2 <= per_cu * cus and steps % (S * 2) == 0 and steps // (S * 2) >= 8:
+        while (tiles * S * 2 <= per_cu * cus and steps % (S * 2) == 0 and steps // (S * 2) >= 8
+               and S * 2 <= STREAM_PART_MAX_S):
             S *= 2
         blocks = tiles * S
         if blocks <= per_cu * cus and (blocks / per_cu, rows) > (best[2], best[0]):

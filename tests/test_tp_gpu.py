@@ -149,7 +149,10 @@ def _tp_worker(rank, port, d, world):
     try:
         cfg = _cfg()
         sd = _state_dict(cfg)
-        comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, ctx.device, ctx.tp_cpu_group, ipc_max_bytes=16 << 20)
+        # 8 processes time-slicing one GPU (and 16 host CPUs): a rank can trail the others by seconds, so
+        # the rehearsal's peer waits get a 60 s bound instead of the serving default (5 s)
+        comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, ctx.device, ctx.tp_cpu_group, ipc_max_bytes=16 << 20,
+                      ipc_spin_limit=60_000_000 if world >= 8 else None)
         res["ipc"] = comm.ipc is not None
         _log(rank, world, "comm up (peer-mapped: %s)" % res["ipc"])
         w = LlamaWeights.from_state_dict(cfg, sd, ctx.device, ctx.tp_rank, ctx.tp)
