@@ -31,8 +31,7 @@ def _bf16_2d(t, name):
 PP_MIN_M = int(os.environ.get("RAGK_PP_MIN_M", "1024"))
 PP_VARIANT = int(os.environ.get("RAGK_PP_VARIANT", "2"))
 # large-M kernel: "w4" (default) = 4-wave 128x128-per-wave (gemm_w4.hip, path 6), "pp" = 8-wave
-# ping-pong (path 2). Library GEMMs (hipBLASLt) are never dispatched from here: they are the
-# yardstick of tools/gemm_probe.py (torch.mm) only.
+# ping-pong (path 2); the residual-add projections go to hipBLASLt by default (PREFILL_BLAS below).
 PREFILL_GEMM = os.environ.get("RAGK_PREFILL_GEMM", "w4")
 _pp_variant_set = [None]
 
@@ -106,6 +105,25 @@ def use_pp(M, N, K, epi):
     return N % 128 == 0 if epi == "silu_mul" else N % 8 == 0
 
 
+# Large-M GEMMs through hipBLASLt (torch) instead of gemm_w4, by epilogue. "resid" (default): the
+# residual-add projections (o_proj, down: h += x @ W^T, one in-place addmm with beta = 1 -- a plain
+# BLAS GEMM, one fp32 -> bf16 rounding as in gemm_w4's epilogue). In the bench they ran 8.5 % faster
+# than gemm_w4's residual epilogue kernels (prefill 49.3-49.5 -> 48.2 s over 25 steps, 1586 -> 1613
+# tok/s, same box alternating; profiles/bench_prefill_blas_ab_r4.log), while the qkv projection on
+# hipBLASLt ("plain") was no faster than gemm_w4 (1587 vs 1586) and the fused SiLU*up GEMM has no
+# library form. "none": every large-M GEMM on gemm_w4 (0 library kernels); "plain": no-epilogue GEMMs
+# only; "all": both.
+PREFILL_BLAS = os.environ.get("RAGK_PREFILL_BLAS", "resid")
+
+
+def _gemm_blas(x, w, resid, out, epi):
+    if epi == "resid":
+        if out.data_ptr() == resid.data_ptr() and out.stride() == resid.stride():
+            return out.addmm_(x, w.t())
+        return torch.addmm(resid, x, w.t(), out=out)
+    return torch.mm(x, w.t(), out=out)
+
+
 def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=None):
     """out[M,N] = epi(x[M,K] @ w[N,K]^T). For epi='silu_mul', w is the packed
     gate/up weight [2N, K] (see reference.pack_gate_up) and out has N columns."""
@@ -134,6 +152,10 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
         return out
     L = _lib.lib()
     ldr = resid.stride(0) if resid is not None else 0
+    if (path is None and PREFILL_BLAS != "none" and not out_f32 and bias is None and use_pp(M, N, K, epi)
+            and ((epi == "none" and PREFILL_BLAS in ("plain", "all"))
+                 or (epi == "resid" and PREFILL_BLAS in ("resid", "all")))):
+        return _gemm_blas(x, w, resid, out, epi)
     if path is None and use_pp(M, N, K, epi):
         rows = w.shape[0]
         # gemm_w4 addresses operands with 32-bit buffer offsets
