@@ -483,8 +483,10 @@ hipError_t launch_tile(const void* A, int lda, const void* B, int ldb, void* C, 
 static int g_skinny_waves = -1;  // -1: auto (RAGK_SKINNY_WAVES env, else by shape)
 // 128-deep K blocks per wave per iteration of the batch-1 skinny GEMM (A/B knob; 2 = default)
 static int g_skinny_unroll = 2;
+static bool g_skinny_unroll_set = false;  // set by ragk_gemm_skinny_set_unroll (overrides RAGK_SKINNY_UNROLL)
 RAGK_API int ragk_gemm_skinny_set_unroll(int u) {
   g_skinny_unroll = u == 1 ? 1 : 2;
+  g_skinny_unroll_set = true;
   return 0;
 }
 RAGK_API int ragk_gemm_skinny_set_waves(int w) {
@@ -508,7 +510,11 @@ hipError_t launch_skinny(const void* X, int ldx, const void* W, int ldw, void* C
                        (const bf16_t*)resid, ldr, M, N, K);
     return hipGetLastError();
   }
-  if (g_skinny_unroll == 1)
+  static const int s_unroll_env = [] {
+    const char* v = getenv("RAGK_SKINNY_UNROLL");
+    return v ? atoi(v) : 0;
+  }();
+  if (g_skinny_unroll == 1 || (s_unroll_env == 1 && !g_skinny_unroll_set))
     hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, SK_WAVES, 1>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0,
                        st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
                        (const bf16_t*)resid, ldr, M, N, K);
