@@ -514,7 +514,14 @@ hipError_t launch_skinny(const void* X, int ldx, const void* W, int ldw, void* C
     const char* v = getenv("RAGK_SKINNY_UNROLL");
     return v ? atoi(v) : 0;
   }();
-  if (g_skinny_unroll == 1 || (s_unroll_env == 1 && !g_skinny_unroll_set))
+  // grids of many blocks (the vocab projection: 8016) keep their loads in flight through occupancy; the
+  // unrolled form's extra VGPRs only pay on the few-block shapes (the 256-block down projection)
+  static const int s_unroll_max_blocks = [] {
+    const char* v = getenv("RAGK_SKINNY_UNROLL_MAX_BLOCKS");
+    return v ? atoi(v) : 2048;
+  }();
+  if (g_skinny_unroll == 1 || (s_unroll_env == 1 && !g_skinny_unroll_set) ||
+      (s_unroll_max_blocks > 0 && (N + 15) / 16 > s_unroll_max_blocks))
     hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, SK_WAVES, 1>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0,
                        st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
                        (const bf16_t*)resid, ldr, M, N, K);
