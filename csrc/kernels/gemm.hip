@@ -485,7 +485,7 @@ static int g_skinny_waves = -1;  // -1: auto (RAGK_SKINNY_WAVES env, else by sha
 static int g_skinny_unroll = 2;
 static bool g_skinny_unroll_set = false;  // set by ragk_gemm_skinny_set_unroll (overrides RAGK_SKINNY_UNROLL)
 RAGK_API int ragk_gemm_skinny_set_unroll(int u) {
-  g_skinny_unroll = u == 1 ? 1 : 2;
+  g_skinny_unroll = u == 1 ? 1 : (u == 4 ? 4 : 2);
   g_skinny_unroll_set = true;
   return 0;
 }
@@ -520,9 +520,14 @@ hipError_t launch_skinny(const void* X, int ldx, const void* W, int ldw, void* C
     const char* v = getenv("RAGK_SKINNY_UNROLL_MAX_BLOCKS");
     return v ? atoi(v) : 2048;
   }();
-  if (g_skinny_unroll == 1 || (s_unroll_env == 1 && !g_skinny_unroll_set) ||
-      (s_unroll_max_blocks > 0 && (N + 15) / 16 > s_unroll_max_blocks))
+  const int un = g_skinny_unroll_set ? g_skinny_unroll : (s_unroll_env == 1 || s_unroll_env == 4 ? s_unroll_env
+                                                                                                  : g_skinny_unroll);
+  if (un == 1 || (s_unroll_max_blocks > 0 && (N + 15) / 16 > s_unroll_max_blocks))
     hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, SK_WAVES, 1>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0,
+                       st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
+                       (const bf16_t*)resid, ldr, M, N, K);
+  else if (un == 4 && MT == 1)
+    hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, SK_WAVES, 4>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0,
                        st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
                        (const bf16_t*)resid, ldr, M, N, K);
   else

@@ -39,16 +39,21 @@ def main():
     skus = [t for t in os.environ.get("DA_SKU", "").split(",") if t] or [None]
     # DA_SP="1,0,1,0": split-K decode slabs from the LDS-DMA stream GEMM (native.STREAM_PART) or gemm_part
     sps = [t for t in os.environ.get("DA_SP", "").split(",") if t] or [None]
+    # DA_PAIR="128,64,...": tile rows of the SiLU*up stream GEMM (ragk_gemm_stream_set_pair_rows)
+    pairs = [int(t) for t in os.environ.get("DA_PAIR", "").split(",") if t] or [None]
     # DA_NATIVE="NAME:v1,v2,...": alternate an integer policy global of ops/native.py (e.g.
     # STREAM_PART_MIN_M:1,17,1,17 or STREAM_MAX_ROWS:200000,32768)
     nat_name, nat_vals = None, [None]
     if os.environ.get("DA_NATIVE"):
         nat_name, vals = os.environ["DA_NATIVE"].split(":")
         nat_vals = [int(v) for v in vals.split(",")]
-    runs = [(B, c, t, nt, fm, sk, sp, nv) for nv in nat_vals for sp in sps for sk in skus for fm in fms for nt in nts
-            for t in tails for c in cfgs for B in Bs]
+    runs = [(B, c, t, nt, fm, sk, sp, nv, pr) for pr in pairs for nv in nat_vals for sp in sps for sk in skus
+            for fm in fms for nt in nts for t in tails for c in cfgs for B in Bs]
     from rag_llm_k8s_amd.ops import _lib, native
-    for B, pfc, tl, nt, fm, sk, sp, nv in runs:
+    for B, pfc, tl, nt, fm, sk, sp, nv, pr in runs:
+        if pr is not None:
+            _lib.lib().ragk_gemm_stream_set_pair_rows(pr)
+            print("-- stream pair rows %d" % pr, flush=True)
         if nv is not None:
             setattr(native, nat_name, nv)
             print("-- native.%s = %d" % (nat_name, nv), flush=True)
