@@ -809,7 +809,10 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
 // DIAG (stamp builds only, wrong results): 1 = no softmax chunks in the fast slots, 2 = no fragment reads
 // PRIO_B: static s_setprio 1 for waves 4-7 over the tile loop (MI355X_MICROARCH.md "Two waves per SIMD"
 // item 4: the second-dispatched half loses every arbitration otherwise).
-template <int NW = 4, bool STAMP = false, int DIAG = 0, int PRIO_B = 0>
+// WIDE: the output tile goes through LDS and out as whole 256-B rows (16-B stores, 4 rows per wave
+// instruction) instead of 16 8-B stores per lane into 32 different rows (MI355X_MICROARCH.md: the
+// attention epilogue store tail is store-issue bound).
+template <int NW = 4, bool STAMP = false, int DIAG = 0, int PRIO_B = 0, bool WIDE = false>
 __global__ __launch_bounds__(NW * 64, NW / 4) void attn_prefill_v3_kernel(PrefillArgs a) {
   constexpr int D = 128;
   using C = Cfg<D>;
@@ -1167,6 +1170,32 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void attn_prefill_v3_kernel(Prefil
   const float l = __uint_as_float(lr[0]) + __uint_as_float(lr[1]);
   const float inv = l > 0.f ? 1.f / l : 0.f;
   const int qi = pbase + l32;
+  if constexpr (WIDE) {
+    // every wave is past its last K / V slot read (the loop's barrier count is the same in both groups),
+    // so the ring is free: each wave stages its 32 x 128 bf16 tile (8 KiB, rows of 256 B, 16-B chunk c of
+    // row r at slot c ^ (r & 15)) and stores whole rows
+    __syncthreads();
+    char* so = smem + wid_u * 8192;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int e = 4 * b;
+        const int d = 32 * db + 8 * b + 4 * h;  // 4 values: chunk d / 8, half (d / 4) & 1
+        const int c = (d >> 3) ^ (l32 & 15);
+        *reinterpret_cast<uint2*>(so + l32 * 256 + 16 * c + 8 * ((d >> 2) & 1)) =
+            make_uint2(pk2bf(o[db][e] * inv, o[db][e + 1] * inv), pk2bf(o[db][e + 2] * inv, o[db][e + 3] * inv));
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's own LDS writes, read back by itself
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = 4 * i + (lane >> 4), c = lane & 15;
+      const u32x4 v = *reinterpret_cast<const u32x4*>(so + r * 256 + 16 * (c ^ (r & 15)));
+      if (pbase + r < q_len)
+        *reinterpret_cast<u32x4*>(a.out + (size_t)(q_off + pbase + r) * a.out_stride + hq * D + 8 * c) = v;
+    }
+    return;
+  }
   if (qi < q_len) {
     bf16_t* op = a.out + (size_t)(q_off + qi) * a.out_stride + hq * D + 4 * h;
 #pragma unroll
@@ -2498,6 +2527,7 @@ hipError_t launch_prefill(PrefillArgs a, int n_tiles, hipStream_t st) {
         case 11: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true>), grid, dim3(512), 0, st, a); break;
         case 12: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true, 1>), grid, dim3(512), 0, st, a); break;
         case 14: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, false, 0, 1>), grid, dim3(512), 0, st, a); break;
+        case 15: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, false, 0, 0, true>), grid, dim3(512), 0, st, a); break;
         case 13: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true, 2>), grid, dim3(512), 0, st, a); break;
         default: hipLaunchKernelGGL((attn_prefill_v3_kernel<8>), grid, dim3(512), 0, st, a); break;
       }
@@ -2571,7 +2601,7 @@ RAGK_API int ragk_attn_prefill_qtile(int Hq, int Hkv) {
 // 4 / 8 steps); 5: the stamp build of variant 4 (g_attn_dbg set by ragk_attn_set_dbg); 6: the
 // software-pipelined one-wave-per-SIMD kernel (attn_prefill_v3_kernel, 32-query tiles); 7: its stamps
 RAGK_API int ragk_attn_prefill_set_pp(int v) {
-  if (v < 0 || v > 14) return (int)hipErrorInvalidValue;
+  if (v < 0 || v > 15) return (int)hipErrorInvalidValue;
   g_prefill_pp = v;
   return 0;
 }

@@ -957,8 +957,11 @@ PREFILL_WAVES = int(os.environ.get("RAGK_PREFILL_WAVES", "4"))
 # 0 = the 4-wave kernel; 10 = the software-pipelined 8-wave kernel (attention.hip
 # attn_prefill_v3_kernel: 32x32x16 MFMAs with the online softmax interleaved into the MFMA stream,
 # two 32-query groups sharing each K/V tile; 6-10 % faster, tools/attn_pp_ab.py); 1 / 2 = the
-# barrier-alternated ping-pong kernel and 6 = the one-wave-per-SIMD v3 (A/B only, both slower)
-PREFILL_PP = int(os.environ.get("RAGK_PREFILL_PP", "10"))
+# barrier-alternated ping-pong kernel and 6 = the one-wave-per-SIMD v3 (A/B only, both slower);
+# 15 (default) = 10 with the output tile staged through LDS and stored as whole 256-B rows: bit-identical,
+# 6 x 5.4k 1540 -> 1513 us, one 5.2k prompt 277 -> 271, a 2k chunk over 3k context 177 -> 171
+# (profiles/attn_prefill_wide_epi_r4.log)
+PREFILL_PP = int(os.environ.get("RAGK_PREFILL_PP", "15"))
 # prefill block order (attention.hip prefill_block): 1 = one grid dimension, head group fastest, so the
 # heaviest causal tiles of every head start first and each XCD serves one KV head; 0 = (tile, head) grid
 PREFILL_ORDER = int(os.environ.get("RAGK_PREFILL_ORDER", "1"))

@@ -349,7 +349,7 @@ def test_attn_prefill_paged(native, q_lens, kv_lens, Hq, Hkv):
                                                    ([5, 70], [513, 70], 8, 1), ([1], [1], 4, 1),
                                                    ([64, 65], [64, 200], 4, 1),
                                                    ([2048, 1104], [4096, 5200], 32, 8)])
-@pytest.mark.parametrize("pp", [1, 2, 6, 10])
+@pytest.mark.parametrize("pp", [1, 2, 6, 10, 15])
 def test_attn_prefill_pingpong(native, q_lens, kv_lens, Hq, Hkv, pp):
     """Alternative prefill kernels for the Llama config vs the 4-wave kernel and the fp32 oracle, on
     ragged query tails, chunked prefill (q_len < kv_len), single-tile sequences and 8 query heads per
@@ -366,16 +366,18 @@ def test_attn_prefill_pingpong(native, q_lens, kv_lens, Hq, Hkv, pp):
     args = (q.to(DEV), kc.to(DEV), vc.to(DEV), cu.to(DEV), kvl.to(DEV))
     outs = []
     try:
-        for mode in (0, pp):
+        for mode in (0, pp) + ((10,) if pp == 15 else ()):
             native.set_prefill_waves(4, pp=mode)
             tiles = native.build_prefill_tiles(q_lens, Hq, Hkv)
-            assert (tiles[:, 1] % (64 if mode in (1, 2, 10) else 32) == 0).all()
+            assert (tiles[:, 1] % (64 if mode in (1, 2, 10, 15) else 32) == 0).all()
             out = torch.full((T, Hq * D), float("nan"), device=DEV).bfloat16()
             native.attn_prefill(*args, tiles.to(DEV), out, Hq, Hkv, D, causal=True, paged=True,
                                 block_tables=bt.to(DEV))
             outs.append(out.cpu())
     finally:
         native.set_prefill_waves(native.PREFILL_WAVES)
+    if pp == 15:  # pp 10 with the whole-row epilogue: the same values
+        assert torch.equal(outs[1], outs[2])
     if pp in (1, 2):
         assert torch.equal(outs[0], outs[1])
     else:
