@@ -2528,6 +2528,7 @@ hipError_t launch_prefill(PrefillArgs a, int n_tiles, hipStream_t st) {
         case 12: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true, 1>), grid, dim3(512), 0, st, a); break;
         case 14: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, false, 0, 1>), grid, dim3(512), 0, st, a); break;
         case 15: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, false, 0, 0, true>), grid, dim3(512), 0, st, a); break;
+        case 16: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, false, 0, 1, true>), grid, dim3(512), 0, st, a); break;
         case 13: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true, 2>), grid, dim3(512), 0, st, a); break;
         default: hipLaunchKernelGGL((attn_prefill_v3_kernel<8>), grid, dim3(512), 0, st, a); break;
       }
@@ -2601,7 +2602,7 @@ RAGK_API int ragk_attn_prefill_qtile(int Hq, int Hkv) {
 // 4 / 8 steps); 5: the stamp build of variant 4 (g_attn_dbg set by ragk_attn_set_dbg); 6: the
 // software-pipelined one-wave-per-SIMD kernel (attn_prefill_v3_kernel, 32-query tiles); 7: its stamps
 RAGK_API int ragk_attn_prefill_set_pp(int v) {
-  if (v < 0 || v > 15) return (int)hipErrorInvalidValue;
+  if (v < 0 || v > 16) return (int)hipErrorInvalidValue;
   g_prefill_pp = v;
   return 0;
 }
