@@ -365,8 +365,12 @@ int launch_stream(const void* X, int ldx, const void* W, int ldw, const float* w
     return (int)hipGetLastError();
   }
   const dim3 grid((Nrows + WROWS - 1) / WROWS, S);
-  hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI, F32, FP8>), grid, dim3(ST_THREADS), 0, st, (const bf16_t*)X, ldx,
-                     W, ldw, wscale, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K, S, ws, cnt);
+  if (g_stream_nt && Nrows >= 65536)  // vocab-sized weights, read once per step: non-temporal
+    hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI, F32, FP8, true>), grid, dim3(ST_THREADS), 0, st, (const bf16_t*)X,
+                       ldx, W, ldw, wscale, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K, S, ws, cnt);
+  else
+    hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI, F32, FP8>), grid, dim3(ST_THREADS), 0, st, (const bf16_t*)X, ldx,
+                       W, ldw, wscale, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K, S, ws, cnt);
   return (int)hipGetLastError();
 }
 

@@ -83,7 +83,10 @@ def use_dec(M, N, K, epi):
 
 STREAM_DEFAULT = os.environ.get("RAGK_STREAM_GEMM", "1") == "1"
 STREAM_MIN_ROWS = int(os.environ.get("RAGK_STREAM_MIN_ROWS", "16384"))
-STREAM_MAX_ROWS = int(os.environ.get("RAGK_STREAM_MAX_ROWS", "32768"))
+# vocab-sized weights (>= 32768 rows, the lm_head) go to the stream GEMM (nt weights) only above batch 16:
+# batch 32 6.97 -> 6.94 ms per decode step, batch 4 slower (profiles/decode_lmhead_stream_r4.log)
+STREAM_MAX_ROWS = int(os.environ.get("RAGK_STREAM_MAX_ROWS", "262144"))
+STREAM_VOCAB_MIN_M = int(os.environ.get("RAGK_STREAM_VOCAB_MIN_M", "17"))
 
 
 def use_stream(M, N, K, epi, fp8=False):
@@ -93,6 +96,8 @@ def use_stream(M, N, K, epi, fp8=False):
     split-K reduction latencies lose to the register-streaming kernels (profiles/tune_stream_r1.json)."""
     rows = 2 * N if epi == "silu_mul" else N
     if M > 64 or not (STREAM_MIN_ROWS <= rows < STREAM_MAX_ROWS) or K % 128:
+        return False
+    if rows >= 32768 and M < STREAM_VOCAB_MIN_M:
         return False
     return M > 16 if fp8 else True
 

@@ -1030,6 +1030,22 @@ def test_gemm_part(native, M, N, K, monkeypatch):
     assert rel_err(P.sum(0), x.float() @ w.float().t()) < 2e-3
 
 
+@pytest.mark.parametrize("M", [17, 32])
+def test_gemm_vocab_stream_route(native, M):
+    """Vocab-sized projections above batch 16 run on the stream GEMM (non-temporal weights, fp32 logits):
+    same values as the gemm_dec path within fp32 summation order, and vs an fp32 oracle."""
+    torch.manual_seed(M)
+    N, K = 65536 + 64, 1024
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
+    assert native.use_stream(M, N, K, "none")
+    y = native.gemm(x, w, out_f32=True)
+    ref = x.float() @ w.float().t()
+    assert rel_err(y, ref) < 1e-3
+    assert rel_err(y, native.gemm(x, w, out_f32=True, path=4)) < 1e-4
+    assert not native.use_stream(16, N, K, "none")
+
+
 @pytest.mark.parametrize("M", [17, 32, 64])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (1000, 1024), (4096, 1792)])
 @pytest.mark.parametrize("rows", [None, 64])
