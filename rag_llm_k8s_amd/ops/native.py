@@ -1052,15 +1052,16 @@ def decode_partitions(max_kv_len, batch, Hkv, target_blocks=None, min_tiles=None
     return min_tiles, mp
 
 
-# Non-temporal K / V loads in the split-K decode attention from this batch up: at batch 32 over 5.2k-token
-# contexts the KV stream (681 MB per layer) is read once per step, and the nt policy keeps it from
-# evicting the L2 / Infinity Cache lines the other kernels reuse: decode step 7.60 -> 7.33 ms in situ
-# (same process, alternating; profiles/decode_nt_ab_r4.log).
-DECODE_NT_MIN_B = int(os.environ.get("RAGK_DECODE_NT_MIN_B", "8"))
+# Non-temporal K / V loads in the split-K decode attention once batch x KV heads reaches this: at batch 32
+# over 5.2k-token contexts (TP=1, 8 KV heads) the KV stream (681 MB per layer) is read once per step, and
+# the nt policy keeps it from evicting the L2 / Infinity Cache lines the other kernels reuse: decode step
+# 7.60 -> 7.33 ms (profiles/decode_nt_ab_r4.log); batch 1 / 4 neutral-to-worse, and the TP=8 shard's
+# 1-KV-head stream at batch 32 (85 MB per layer) 2.33 -> 2.40 ms with nt (profiles/tp_nt_ab_r4.log).
+DECODE_NT_MIN_BH = int(os.environ.get("RAGK_DECODE_NT_MIN_BH", "64"))
 
 
-def _set_decode_nt(B):
-    check(_lib.lib().ragk_attn_decode_set_nt(1 if B >= DECODE_NT_MIN_B else 0), "ragk_attn_decode_set_nt")
+def _set_decode_nt(B, Hkv):
+    check(_lib.lib().ragk_attn_decode_set_nt(1 if B * Hkv >= DECODE_NT_MIN_BH else 0), "ragk_attn_decode_set_nt")
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, part_tiles, max_parts, ws_o=None,
@@ -1081,7 +1082,7 @@ def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, par
     if max_parts > 1 and ATTN_FUSED_MERGE and 2 * G * max_parts + 16 <= 4 * 64 * D * 2 // 4:
         cnt = _attn_counters(q.device)
         _req(B * Hkv <= cnt.numel(), "attention ticket buffer too small")
-    _set_decode_nt(B)
+    _set_decode_nt(B, Hkv)
     check(_lib.lib().ragk_attn_decode(
         q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
         block_tables.stride(0), kv_lens.data_ptr(), ptr(ws_o), ptr(ws_ml), out.data_ptr(), out.stride(0), B, Hq, Hkv,
@@ -1118,7 +1119,7 @@ def attn_decode_rope(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_
         cnt = _attn_counters(P.device)
         _req(B * Hkv <= cnt.numel(), "attention ticket buffer too small")
     lib = _lib.lib()
-    _set_decode_nt(B)
+    _set_decode_nt(B, Hkv)
     if defer_merge:
         lib.ragk_attn_decode_set_defer(1)
     try:

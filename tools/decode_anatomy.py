@@ -31,7 +31,7 @@ def main():
     cfgs = [c for c in os.environ.get("DA_PF", "").split(",") if c] or [None]
     # DA_TAIL="1,0,1,0": alternate the norm-in-the-GEMM-tail launches (native.PART_TAIL) on / off
     tails = [t for t in os.environ.get("DA_TAIL", "").split(",") if t] or [None]
-    # DA_NT="0,1,0,1": alternate non-temporal K/V loads in the decode attention (native.DECODE_NT_MIN_B)
+    # DA_NT="0,1,0,1": alternate non-temporal K/V loads in the decode attention (native.DECODE_NT_MIN_BH)
     nts = [t for t in os.environ.get("DA_NT", "").split(",") if t] or [None]
     # DA_FM="0,1,0,1": alternate the attention's in-kernel split-K merge (native.ATTN_FUSED_MERGE)
     fms = [t for t in os.environ.get("DA_FM", "").split(",") if t] or [None]
@@ -70,7 +70,7 @@ def main():
             native.PART_TAIL = tl == "1"
             print("-- part tail %s" % tl, flush=True)
         if nt is not None:
-            native.DECODE_NT_MIN_B = 1 if nt == "1" else 1 << 30
+            native.DECODE_NT_MIN_BH = 1 if nt == "1" else 1 << 30
             print("-- decode attention nt %s" % nt, flush=True)
         if pfc is not None:
             L.DECODE_PF = pfc != "off"
