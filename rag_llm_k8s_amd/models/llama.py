@@ -41,6 +41,10 @@ DECODE_NORM_FUSED = os.environ.get("RAGK_DECODE_NORM_FUSED", "1") == "1"
 # (gemm_part_merge), so the attention's separate merge launch disappears
 DECODE_OPROJ_MERGE = os.environ.get("RAGK_DECODE_OPROJ_MERGE", "1") == "1"
 DECODE_OPROJ_MERGE_MAX_M = int(os.environ.get("RAGK_DECODE_OPROJ_MERGE_MAX_M", "2"))
+# TP=1 batch <= this: o_proj as the register-streaming skinny GEMM with the residual epilogue (writes h),
+# then a plain RMSNorm -- instead of split-K slabs (+ partition merge) and the add_partials_rmsnorm consumer.
+# Off (0): measured slower, batch 1 3.85 vs 3.72 ms per step (profiles/decode_oproj_skinny_ab_r4.log)
+DECODE_OPROJ_SKINNY_MAX_M = int(os.environ.get("RAGK_DECODE_OPROJ_SKINNY_MAX_M", "0"))
 # decode batch <= 4: gate/up as split-K partials, silu(gate) * up formed inside the down GEMM's staging
 # (gemm_part.hip SG): "tp" = under tensor parallelism only (the TP=1 batch <= 4 path keeps the skinny
 # down GEMM with its fused residual), "1" = always, "0" = never
@@ -374,13 +378,15 @@ class LlamaModel:
                       and be.part_silu_ok(M, layers[0]["wgu"], layers[0]["wdown"]))
         fuse_norm = fuse_norm and not silu_fused
         xn = None if fuse_norm else be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
+        o_skinny = not tp and not pf and M <= DECODE_OPROJ_SKINNY_MAX_M
         merge = (DECODE_OPROJ_MERGE and DECODE_ROPE_FUSED and not pf and M <= DECODE_OPROJ_MERGE_MAX_M
-                 and be.part_merge_ok(M, inp.meta, layers[0]["wo"], Hq, D))
+                 and not o_skinny and be.part_merge_ok(M, inp.meta, layers[0]["wo"], Hq, D))
         # batch <= 4: attention and o_proj in ONE launch (attention.hip attn_oproj_kernel) -- the o_proj
         # weight stream overlaps the KV stream instead of following it
         # (never when another process drives this GPU: its waiting blocks could hold the CU slots this
         # launch's producer blocks need)
-        fused_ao = (DECODE_ROPE_FUSED and not pf and not (tp and getattr(self.comm, "shares_device", False))
+        fused_ao = (DECODE_ROPE_FUSED and not pf and not o_skinny
+                    and not (tp and getattr(self.comm, "shares_device", False))
                     and be.attn_oproj_ok(M, inp.meta, layers[0]["wo"], Hq, Hkv, D))
         # ... and, at TP=1, the residual + post-attention norm in its last block (no consumer launch)
         ao_norm = fused_ao and not tp and be.attn_oproj_norm_ok(layers[0]["wo"])
@@ -394,7 +400,7 @@ class LlamaModel:
                                            norm_tail=False))
         # TP=1: the add_partials_rmsnorm consumers of the o_proj / down split-K GEMMs run in those GEMMs'
         # last blocks (gemm_part.hip TL) -- one launch fewer per norm
-        tail_o = not tp and not pf and not fused_ao and be.part_tail_ok(M, layers[0]["wo"])
+        tail_o = not tp and not pf and not fused_ao and not o_skinny and be.part_tail_ok(M, layers[0]["wo"])
         tail_d = not tp and not pf and not silu_fused and be.part_tail_ok(M, layers[0]["wdown"])
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
@@ -432,7 +438,10 @@ class LlamaModel:
                     be.pf_arm([(L["wo"], pf["rope"], pf["attn"] // 2), (L["wgu"], 0, pf["attn"] // 2)],
                               pf["blocks"])
                 be.attn_decode(q, kc, vc, inp.meta, attn, Hq, Hkv, D)
-            if tail_o:
+            if o_skinny:
+                be.gemm(attn, L["wo"], resid=h, epi="resid", out=h)
+                xn = be.rmsnorm(h, L["ln_post"], c.rms_norm_eps)
+            elif tail_o:
                 # TP=1: the residual add + post-attention norm in the o_proj GEMM's last blocks
                 xn = (be.gemm_part_merge_tail(attn, inp.meta, L["wo"], Hq, h, L["ln_post"], c.rms_norm_eps) if merge
                       else be.gemm_part_tail(attn, L["wo"], h, L["ln_post"], c.rms_norm_eps))
@@ -440,7 +449,7 @@ class LlamaModel:
                 P = be.gemm_part_merge(attn, inp.meta, L["wo"], Hq) if merge else be.gemm_part(attn, L["wo"])
             if pf:
                 be.pf_arm([(L["wgu"], pf["attn"] // 2, pf["post"])], pf["blocks"])
-            if not ao_norm and not tail_o:
+            if not ao_norm and not tail_o and not o_skinny:
                 xn = reduce_norm(P, L["ln_post"])
             nxt = layers[li + 1]["ln_in"] if li + 1 < len(layers) else w.norm
             if silu_fused:

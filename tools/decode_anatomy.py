@@ -47,10 +47,18 @@ def main():
     if os.environ.get("DA_NATIVE"):
         nat_name, vals = os.environ["DA_NATIVE"].split(":")
         nat_vals = [int(v) for v in vals.split(",")]
-    runs = [(B, c, t, nt, fm, sk, sp, nv, pr) for pr in pairs for nv in nat_vals for sp in sps for sk in skus
-            for fm in fms for nt in nts for t in tails for c in cfgs for B in Bs]
+    # DA_LLAMA="NAME:v1,v2,...": alternate an integer policy global of models/llama.py
+    ll_name, ll_vals = None, [None]
+    if os.environ.get("DA_LLAMA"):
+        ll_name, vals = os.environ["DA_LLAMA"].split(":")
+        ll_vals = [int(v) for v in vals.split(",")]
+    runs = [(B, c, t, nt, fm, sk, sp, nv, pr, lv) for lv in ll_vals for pr in pairs for nv in nat_vals for sp in sps
+            for sk in skus for fm in fms for nt in nts for t in tails for c in cfgs for B in Bs]
     from rag_llm_k8s_amd.ops import _lib, native
-    for B, pfc, tl, nt, fm, sk, sp, nv, pr in runs:
+    for B, pfc, tl, nt, fm, sk, sp, nv, pr, lv in runs:
+        if lv is not None:
+            setattr(L, ll_name, lv)
+            print("-- llama.%s = %d" % (ll_name, lv), flush=True)
         if pr is not None:
             _lib.lib().ragk_gemm_stream_set_pair_rows(pr)
             print("-- stream pair rows %d" % pr, flush=True)
