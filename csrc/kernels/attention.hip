@@ -1244,8 +1244,8 @@ __device__ __forceinline__ int decode_part_tiles(int n_kt, const DecodeArgs& a) 
 }
 
 // LDS of one decode-attention block: one V tile per wave, then the block's rotated q (G x D bf16).
-template <int D, int G>
-constexpr int decode_lds_bytes() { return 4 * Cfg<D>::TILEB + G * D * 2; }
+template <int D, int G, int NW = 4>
+constexpr int decode_lds_bytes() { return NW * Cfg<D>::TILEB + G * D * 2; }
 
 // Signal of a decode-attention block inside the fused attention + o_proj launch (attn_oproj_kernel):
 // every storing wave has drained its write-through (sc1) stores, then one lane adds to the agent-scope
@@ -1355,9 +1355,14 @@ __device__ __forceinline__ void out_pair_sc1(const DecodeArgs& a, int b, int col
 // MIA (FUSED only): the partitions of a (sequence, KV head) are merged by the last of its partition blocks
 // (ticket counters a.counters) into the bf16 attention output, written through; the o_proj blocks then
 // stage a plain bf16 activation slice instead of each merging the records of its K-slice.
-template <int D, int G, bool NT = false, bool FUSED = false, bool QW = false, bool MIA = false, bool ST = false>
+// NW: waves per block (4; 8 for the batch-32 grid with one partition per sequence: one 8-wave block per
+// CU keeps the same KV bytes in flight as two 4-wave blocks and needs no merge launch)
+template <int D, int G, bool NT = false, bool FUSED = false, bool QW = false, bool MIA = false, bool ST = false,
+          int NW = 4>
 __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part, int kvh, int b, char* smem,
                                                   int* fused_cnt = nullptr, QWait qw = {}, int fused_total = 0) {
+  static_assert(NW == 4 || (NW == 8 && !FUSED), "8-wave blocks: the plain decode kernel only");
+  constexpr int NTH = NW * 64;
   fstamp<ST>(0);
   using C = Cfg<D>;
   static_assert(G <= 16, "at most 16 query heads per KV head");
@@ -1423,7 +1428,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     // pair of 8-vectors per thread (G * D/16 threads, all slab loads of a thread in flight together),
     // staged through LDS; in the block owning the last KV tile, other threads append the new
     // token's k (rotated) and v meanwhile. One barrier covers both.
-    bf16_t* s_q = reinterpret_cast<bf16_t*>(smem + 4 * C::TILEB);
+    bf16_t* s_q = reinterpret_cast<bf16_t*>(smem + NW * C::TILEB);
     constexpr int NV = D / 16;  // pairs per head
     const int pos = a.positions[b];
     const float* prow = a.qkv_p + (size_t)b * a.ldp;
@@ -1489,7 +1494,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
   for (int dt = 0; dt < C::DT; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float m_i = -INFINITY, l_i = 0.f;
 
-  for (int kt = kt0 + wid_u; kt < kt1; kt += 4) {
+  for (int kt = kt0 + wid_u; kt < kt1; kt += NW) {
     bf16x8 kf[4][C::KS];
     if (pre && kt == kt0 + wid_u) {  // requested before the prologue
 #pragma unroll
@@ -1567,8 +1572,8 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
   // ---- combine the 4 waves in LDS ----
   __syncthreads();
   float* sm = reinterpret_cast<float*>(smem);    // [4][16] max
-  float* sl = sm + 4 * 16;                       // [4][64] partial l (per lane)
-  float* so = sl + 4 * 64;                       // [4][16][D] O
+  float* sl = sm + NW * 16;                      // [NW][64] partial l (per lane)
+  float* so = sl + NW * 64;                      // [NW][16][D] O
   if (fh == 0) sm[wid * 16 + fr] = m_i;
   sl[wid * 64 + lane] = l_i;
 #pragma unroll
@@ -1578,15 +1583,15 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
   __syncthreads();
   if constexpr (FUSED && MIA) {
     if (nparts == 1) {  // the block's output is final: bf16 pairs, written through
-      for (int e2 = threadIdx.x; e2 < G * D / 2; e2 += 256) {
+      for (int e2 = threadIdx.x; e2 < G * D / 2; e2 += NTH) {
         const int g = (2 * e2) / D, d = (2 * e2) % D;
         float M = -INFINITY;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[w * 16 + g]);
+        for (int w = 0; w < NW; ++w) M = fmaxf(M, sm[w * 16 + g]);
         const float Mu = M == -INFINITY ? 0.f : M;
         float L = 0.f, O0 = 0.f, O1 = 0.f;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
+        for (int w = 0; w < NW; ++w) {
           const float sc = exp2f(sm[w * 16 + g] - Mu);
           L += (sl[w * 64 + g] + sl[w * 64 + g + 16] + sl[w * 64 + g + 32] + sl[w * 64 + g + 48]) * sc;
           O0 += so[(w * 16 + g) * D + d] * sc;
@@ -1601,15 +1606,15 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     }
   }
   // thread -> (g, d) pairs
-  for (int e = threadIdx.x; e < G * D; e += 256) {
+  for (int e = threadIdx.x; e < G * D; e += NTH) {
     const int g = e / D, d = e % D;
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm[w * 16 + g]);
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, sm[w * 16 + g]);
     const float Mu = M == -INFINITY ? 0.f : M;
     float L = 0.f, O = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const float sc = exp2f(sm[w * 16 + g] - Mu);
       L += (sl[w * 64 + g] + sl[w * 64 + g + 16] + sl[w * 64 + g + 32] + sl[w * 64 + g + 48]) * sc;
       O += so[(w * 16 + g) * D + d] * sc;
@@ -1668,21 +1673,21 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     // so both are in flight together -- one memory round trip for <= MCH partitions -- and merged in
     // registers once the per-partition scales are known.
     constexpr int MCH = 16;
-    constexpr int NPR = (G * D / 2 + 255) / 256;  // (head, pair) items per thread
+    constexpr int NPR = (G * D / 2 + NTH - 1) / NTH;  // (head, pair) items per thread
     float* s_m = reinterpret_cast<float*>(smem);  // [G][nparts] max -> scale
     float* s_l = s_m + G * nparts;
     float* s_L = s_l + G * nparts;
     f32x2 v[NPR][MCH];
 #pragma unroll
     for (int k = 0; k < NPR; ++k) {
-      const int e2 = min((int)threadIdx.x + 256 * k, G * D / 2 - 1);
+      const int e2 = min((int)threadIdx.x + NTH * k, G * D / 2 - 1);
       const int g = (2 * e2) / D, d = (2 * e2) % D;
       const int po = (int)(((hb + g) * a.max_parts * D + d) * 4);
 #pragma unroll
       for (int i = 0; i < MCH; ++i)
         v[k][i] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_o, po + min(i, nparts - 1) * D * 4, 0, 16));
     }
-    for (int e = threadIdx.x; e < G * nparts; e += 256) {
+    for (int e = threadIdx.x; e < G * nparts; e += NTH) {
       const int g = e / nparts, p = e % nparts;
       const f32x2 ml = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_ml, (int)(((hb + g) * a.max_parts + p) * 8), 0, 16));
       s_m[e] = ml[0];
@@ -1705,7 +1710,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < NPR; ++k) {
-      const int e2 = threadIdx.x + 256 * k;
+      const int e2 = threadIdx.x + NTH * k;
       if (e2 >= G * D / 2) break;
       const int g = (2 * e2) / D, d = (2 * e2) % D;
       const float* sc = s_m + g * nparts;
@@ -1741,7 +1746,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
   float* s_m = reinterpret_cast<float*>(smem);  // [G][nparts] partition max, then its scale
   float* s_l = s_m + G * nparts;                 // [G][nparts] partition sum
   float* s_L = s_l + G * nparts;                 // [G] merged sum
-  for (int e = threadIdx.x; e < G * nparts; e += 256) {
+  for (int e = threadIdx.x; e < G * nparts; e += NTH) {
     const int g = e / nparts, p = e % nparts;
     const size_t pi = (hb + g) * a.max_parts + p;
     s_m[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ml, (int)(pi * 8), 0, 16));
@@ -1762,7 +1767,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     s_L[g] = L;
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < G * D; e += 256) {
+  for (int e = threadIdx.x; e < G * D; e += NTH) {
     const int g = e / D, d = e % D;
     const int po = (int)(((hb + g) * a.max_parts * D + d) * 4);  // byte offset of partition 0
     const float* sc = s_m + g * nparts;
@@ -1782,15 +1787,15 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
   if (threadIdx.x == 0) __hip_atomic_store(a.counters + b * a.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int D, int G, bool NT = false>
-__global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeArgs a, PfArgs pf) {
-  __shared__ __attribute__((aligned(16))) char smem[decode_lds_bytes<D, G>()];
+template <int D, int G, bool NT = false, int NW = 4>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attn_decode_kernel(DecodeArgs a, PfArgs pf) {
+  __shared__ __attribute__((aligned(16))) char smem[decode_lds_bytes<D, G, NW>()];
   if ((int)blockIdx.x >= a.max_parts) {  // MALL prefetch rider (block-uniform): x beyond the partitions
     const int ex = gridDim.x - a.max_parts;
     pf_rider(pf, (blockIdx.x - a.max_parts) + ex * (blockIdx.y + gridDim.y * blockIdx.z), ex * gridDim.y * gridDim.z);
     return;
   }
-  attn_decode_block<D, G, NT>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  attn_decode_block<D, G, NT, false, false, false, false, NW>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2645,6 +2650,12 @@ RAGK_API int ragk_attn_prefill_set_order(int order) {
 // K/V cache-policy switch for decode (0 = default, 1 = non-temporal loads; the KV stream is read
 // once per step). A/B in tools/bench_kernels.py --quick.
 static int g_decode_nt = 0;
+// 8-wave single-partition decode attention once batch x KV heads reaches this (0 = never)
+static int g_decode_nw8_min = 0;
+RAGK_API int ragk_attn_decode_set_nw8(int min_pairs) {
+  g_decode_nw8_min = min_pairs > 0 ? min_pairs : 0;
+  return 0;
+}
 RAGK_API int ragk_attn_decode_set_nt(int nt) {
   g_decode_nt = nt ? 1 : 0;
   return 0;
@@ -2700,6 +2711,14 @@ static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* co
   const PfArgs pf = pf_take();
   const int ex = (pf.blocks + Hkv * B - 1) / (Hkv * B);  // rider columns (x beyond max_parts)
   dim3 grid(max_parts + ex, Hkv, B);
+  if (D == 128 && G == 4 && max_parts == 1 && !counters && g_decode_nw8_min > 0 && B * Hkv >= g_decode_nw8_min) {
+    // one partition per sequence over >= 1 block per CU: 8-wave blocks, no merge launch
+    if (g_decode_nt)
+      hipLaunchKernelGGL((attn_decode_kernel<128, 4, true, 8>), grid, dim3(512), 0, st, a, pf);
+    else
+      hipLaunchKernelGGL((attn_decode_kernel<128, 4, false, 8>), grid, dim3(512), 0, st, a, pf);
+    return (int)hipGetLastError();
+  }
 #define RAGK_DC(DD, GG)                                                            \
   if (D == DD && G == GG) {                                                          \
     if (g_decode_nt)                                                                 \

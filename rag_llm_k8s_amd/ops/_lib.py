@@ -37,6 +37,7 @@ _SIGS = {
     "ragk_gemm_part_norm": [P, I, P, F, P, I, P, I, I, I, I, S],
     "ragk_gemm_part_fp8": [P, I, P, I, P, P, I, I, I, I, S],
     "ragk_attn_decode_set_nt": [I],
+    "ragk_attn_decode_set_nw8": [I],
     "ragk_attn_decode_set_defer": [I],
     "ragk_gemm_part_merge": [P, P, P, I, P, I, I, I, P, I, P, P, I, I, I, I, S],
     "ragk_gemm_part_merge_ok": [I, I, I, I, I],

@@ -1048,8 +1048,16 @@ def decode_partitions(max_kv_len, batch, Hkv, target_blocks=None, min_tiles=None
     target_blocks = DECODE_TARGET_BLOCKS if target_blocks is None else target_blocks
     min_tiles = DECODE_MIN_TILES if min_tiles is None else min_tiles
     max_kt = max(1, (max_kv_len + 63) // 64)
+    if DECODE_NW8_MIN_PAIRS > 0 and batch * Hkv >= DECODE_NW8_MIN_PAIRS:
+        return min_tiles, 1  # one 8-wave block per (sequence, KV head), no merge (attention.hip NW = 8)
     mp = max(1, min(-(-target_blocks // (batch * Hkv)), -(-max_kt // min_tiles)))
     return min_tiles, mp
+
+
+# One partition per (sequence, KV head) in 8-wave blocks once batch x KV heads reaches this (>= one block
+# per CU): the same KV bytes in flight as two 4-wave partition blocks, and no merge launch (0 = off).
+# Batch 32: decode step 6.96 -> 6.86-6.90 ms (profiles/decode_nw8_ab_r4.log).
+DECODE_NW8_MIN_PAIRS = int(os.environ.get("RAGK_DECODE_NW8", "256"))
 
 
 # Non-temporal K / V loads in the split-K decode attention once batch x KV heads reaches this: at batch 32
@@ -1061,7 +1069,9 @@ DECODE_NT_MIN_BH = int(os.environ.get("RAGK_DECODE_NT_MIN_BH", "64"))
 
 
 def _set_decode_nt(B, Hkv):
-    check(_lib.lib().ragk_attn_decode_set_nt(1 if B * Hkv >= DECODE_NT_MIN_BH else 0), "ragk_attn_decode_set_nt")
+    L = _lib.lib()
+    check(L.ragk_attn_decode_set_nt(1 if B * Hkv >= DECODE_NT_MIN_BH else 0), "ragk_attn_decode_set_nt")
+    check(L.ragk_attn_decode_set_nw8(DECODE_NW8_MIN_PAIRS), "ragk_attn_decode_set_nw8")
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, part_tiles, max_parts, ws_o=None,

@@ -430,6 +430,37 @@ def test_attn_decode(native, kv_lens, Hq, Hkv, target):
     assert rel_err(out.cpu().reshape(B, Hq, D), ref) < 2e-2
 
 
+@pytest.mark.parametrize("kv_lens,Hq,Hkv", [([5200, 1, 64, 4100], 32, 8), ([65, 3000, 700], 4, 1), ([1], 32, 8),
+                                             ([8100] * 3 + [5], 32, 8)])
+@pytest.mark.parametrize("nt", [0, 1])
+def test_attn_decode_nw8_single_partition(native, kv_lens, Hq, Hkv, nt, monkeypatch):
+    """Single-partition decode attention in 8-wave blocks (attention.hip NW = 8, the batch-32 grid): no merge
+    launch; vs the fp32 oracle and within rounding of the 4-wave split-K kernel, nt loads or not."""
+    D = 128
+    torch.manual_seed(17)
+    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=5)
+    B = len(kv_lens)
+    q = torch.randn(B, Hq * D).bfloat16()
+    kvl = torch.tensor(kv_lens, dtype=torch.int32)
+    args = (q.to(DEV), kc.to(DEV), vc.to(DEV), bt.to(DEV), kvl.to(DEV))
+    pt4, mp4 = native.decode_partitions(max(kv_lens), B, Hkv, target_blocks=512)
+    ref4 = torch.empty(B, Hq * D, device=DEV).bfloat16()
+    native.attn_decode(*args, ref4, Hq, Hkv, D, pt4, mp4)
+    monkeypatch.setattr(native, "DECODE_NW8_MIN_PAIRS", 1)
+    monkeypatch.setattr(native, "DECODE_NT_MIN_BH", 1 if nt else 1 << 30)
+    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv)
+    assert mp == 1
+    out = torch.full((B, Hq * D), float("nan"), device=DEV).bfloat16()
+    native.attn_decode(*args, out, Hq, Hkv, D, pt, mp)
+    torch.cuda.synchronize()
+    cu = torch.arange(B + 1, dtype=torch.int32)
+    ref = R.attention_varlen(q.reshape(B, Hq, D), None, None, cu, kvl, True, 1 / math.sqrt(D),
+                             k_full=lambda s: R.paged_kv_view(kc, bt[s], kv_lens[s], 64),
+                             v_full=lambda s: R.paged_kv_view(vc, bt[s], kv_lens[s], 64))
+    assert rel_err(out.cpu().reshape(B, Hq, D), ref) < 2e-2
+    assert rel_err(out.cpu(), ref4.cpu()) < 1e-2
+
+
 def test_attn_decode_fused_merge_matches_separate_and_resets(native):
     """Split-K decode with the merge fused into the partition kernel (ticket per (sequence, KV head),
     last block merges) == the separate merge launch, bit for bit, and stays so over repeated launches
