@@ -205,7 +205,7 @@ constexpr int SK_WAVES = 8;
 // WV waves per block (default 8; 16 is an A/B option for long-K / few-column shapes such as the
 // batch-1 down projection -- measured slower there: more waves per block lengthen the LDS reduction
 // and the per-block tail more than the extra loads in flight gain).
-template <int MT, int EPI, bool OUT_F32, int WV = SK_WAVES, int UN = 2>
+template <int MT, int EPI, bool OUT_F32, int WV = SK_WAVES, int UN = 2, bool NTW = false>
 __global__ __launch_bounds__(WV * 64) void gemm_skinny_kernel(
     const bf16_t* __restrict__ X, int ldx, const bf16_t* __restrict__ W, int ldw, void* C, int ldc,
     const bf16_t* __restrict__ bias, const bf16_t* resid, int ldr, int M, int N, int K) {
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(WV * 64) void gemm_skinny_kernel(
   const bf16x8 zero = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
   // two of the wave's K blocks per iteration, both blocks' weight loads issued before any use (a wave
   // with one block's 4 loads in flight kept the 256-block batch-1 down projection latency-bound at
-  // ~4.9 TB/s); weights are read once per step -> non-temporal
+  // ~4.9 TB/s); default cache policy (NTW: non-temporal, measured slower here)
   constexpr int U = (PAIR || MT > 1) ? 1 : UN;
   for (int kb = wid; kb < nkb; kb += U * WV) {
     bf16x8 wf[U][NACC][4];
@@ -256,8 +256,13 @@ __global__ __launch_bounds__(WV * 64) void gemm_skinny_kernel(
       const int k = min(kb + u * WV, nkb - 1) * 128;  // clamped: a missing second block is loaded, not used
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        wf[u][0][s] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w0 + k + 32 * s));
-        if constexpr (PAIR) wf[u][1][s] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w1 + k + 32 * s));
+        if constexpr (NTW) {
+          wf[u][0][s] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w0 + k + 32 * s));
+          if constexpr (PAIR) wf[u][1][s] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w1 + k + 32 * s));
+        } else {
+          wf[u][0][s] = *reinterpret_cast<const bf16x8*>(w0 + k + 32 * s);
+          if constexpr (PAIR) wf[u][1][s] = *reinterpret_cast<const bf16x8*>(w1 + k + 32 * s);
+        }
       }
     }
     bf16x8 xf[U][MT][4];
@@ -516,6 +521,12 @@ hipError_t launch_skinny(const void* X, int ldx, const void* W, int ldw, void* C
   }();
   // grids of many blocks (the vocab projection: 8016) keep their loads in flight through occupancy; the
   // unrolled form's extra VGPRs only pay on the few-block shapes (the 256-block down projection)
+  // RAGK_SKINNY_NT=1: non-temporal weight loads (A/B; measured slower at C=1: 3.67 vs 3.59 ms per token,
+  // profiles/c1_skinny_nt_ab_r4.log)
+  static const int s_nt_env = [] {
+    const char* v = getenv("RAGK_SKINNY_NT");
+    return v ? atoi(v) : 0;
+  }();
   static const int s_unroll_max_blocks = [] {
     const char* v = getenv("RAGK_SKINNY_UNROLL_MAX_BLOCKS");
     return v ? atoi(v) : 2048;
@@ -526,6 +537,10 @@ hipError_t launch_skinny(const void* X, int ldx, const void* W, int ldw, void* C
     hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, SK_WAVES, 1>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0,
                        st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
                        (const bf16_t*)resid, ldr, M, N, K);
+  else if (s_nt_env == 1 && MT == 1)  // A/B: two K blocks in flight, non-temporal weight loads
+    hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, SK_WAVES, 2, true>), dim3((N + 15) / 16),
+                       dim3(SK_WAVES * 64), 0, st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc,
+                       (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K);
   else if (un == 4 && MT == 1)
     hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, SK_WAVES, 4>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0,
                        st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
