@@ -487,7 +487,10 @@ hipError_t launch_tile(const void* A, int lda, const void* B, int ldb, void* C, 
 
 static int g_skinny_waves = -1;  // -1: auto (RAGK_SKINNY_WAVES env, else by shape)
 // 128-deep K blocks per wave per iteration of the batch-1 skinny GEMM (A/B knob; 2 = default)
-static int g_skinny_unroll = 2;
+// 1 (default) = the round-3 loop; 2 = two K blocks in flight per wave (A/B: slower at C=1 with default-policy
+// loads, 3.59 vs 3.53 ms per token, profiles/c1_skinny_unroll_plain_ab_r4.log; its earlier apparent win was
+// against the 1-block form WITH non-temporal loads, which costs more than either)
+static int g_skinny_unroll = 1;
 static bool g_skinny_unroll_set = false;  // set by ragk_gemm_skinny_set_unroll (overrides RAGK_SKINNY_UNROLL)
 RAGK_API int ragk_gemm_skinny_set_unroll(int u) {
   g_skinny_unroll = u == 1 ? 1 : (u == 4 ? 4 : 2);
@@ -531,8 +534,8 @@ hipError_t launch_skinny(const void* X, int ldx, const void* W, int ldw, void* C
     const char* v = getenv("RAGK_SKINNY_UNROLL_MAX_BLOCKS");
     return v ? atoi(v) : 2048;
   }();
-  const int un = g_skinny_unroll_set ? g_skinny_unroll : (s_unroll_env == 1 || s_unroll_env == 4 ? s_unroll_env
-                                                                                                  : g_skinny_unroll);
+  const int un = g_skinny_unroll_set ? g_skinny_unroll : (s_unroll_env >= 1 && s_unroll_env <= 4 ? s_unroll_env
+                                                                                                 : g_skinny_unroll);
   if (un == 1 || (s_unroll_max_blocks > 0 && (N + 15) / 16 > s_unroll_max_blocks))
     hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, SK_WAVES, 1>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0,
                        st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
