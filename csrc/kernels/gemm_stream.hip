@@ -378,6 +378,16 @@ template <int MT>
 int launch_stream_slab(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K, int S, int rows,
                        hipStream_t st) {
   const dim3 grid((N + rows - 1) / rows, S);
+  static const int s_nt = [] {  // RAGK_STREAM_PART_NT=0: default-policy weight stream (A/B)
+    const char* v = getenv("RAGK_STREAM_PART_NT");
+    return v ? atoi(v) : 1;
+  }();
+  if (!s_nt) {
+    hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI_NONE, true, false, false, WROWS, true>), grid, dim3(ST_THREADS), 0,
+                       st, (const bf16_t*)X, ldx, W, ldw, nullptr, P, N, nullptr, nullptr, 0, M, N, K, S, nullptr,
+                       nullptr);
+    return (int)hipGetLastError();
+  }
   if (rows == 64)
     hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI_NONE, true, false, true, 64, true>), grid, dim3(ST_THREADS), 0, st,
                        (const bf16_t*)X, ldx, W, ldw, nullptr, P, N, nullptr, nullptr, 0, M, N, K, S, nullptr, nullptr);
