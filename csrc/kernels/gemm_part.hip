@@ -16,6 +16,8 @@
 //     no inter-block synchronisation: the consumer (ragk_add_partials_rmsnorm / rope_kv_partials in
 //     norm.hip) sums the S slabs while doing its own row work, so the reduction costs no extra
 //     launch and no atomics (deterministic).
+#include <stdlib.h>
+
 #include "common.h"
 using namespace ragk;
 
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), MG ? 2 : 1) voi
                                                                   const float* __restrict__ wscale = nullptr,
                                                                   const bf16_t* __restrict__ gamma = nullptr,
                                                                   float eps = 0.f, MergeArgs mg = {},
-                                                                  SiluArgs sg = {}, TailArgs tl = {}) {
+                                                                  SiluArgs sg = {}, TailArgs tl = {}, int wnt = 1) {
   constexpr int KS = NKS * 64;          // K-slice of the block (two halves of NKS k-steps of 32)
   constexpr int XROWS = 16 * MT;
   constexpr int ROWB = KS * 2;          // bytes per LDS row
@@ -421,11 +423,15 @@ __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), MG ? 2 : 1) voi
     const unsigned char* wp = reinterpret_cast<const unsigned char*>(W) + (size_t)wrow * ldw + kbase + kh * (KS / 2) +
                               fh * 16;
 #pragma unroll
-    for (int j = 0; j < NLD; ++j) wf[j] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 64 * j));
+    for (int j = 0; j < NLD; ++j)
+      wf[j] = wnt ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 64 * j))
+                  : *reinterpret_cast<const bf16x8*>(wp + 64 * j);
   } else {
     const bf16_t* wp = W + (size_t)wrow * ldw + kbase + kh * (KS / 2) + fh * 8;
 #pragma unroll
-    for (int ks = 0; ks < NLD; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
+    for (int ks = 0; ks < NLD; ++ks)
+      wf[ks] = wnt ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks))
+                   : *reinterpret_cast<const bf16x8*>(wp + 32 * ks);
   }
   // vmcnt(NLD): the DMA / row loads (older than the NLD weight loads) have landed
   __builtin_amdgcn_s_waitcnt((NLD & 15) | (((NLD >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
@@ -563,6 +569,16 @@ __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), MG ? 2 : 1) voi
   if constexpr (TL) part_tail(tl, P, M, N, K / KS);
 }
 
+// weight-stream cache policy of the split-K decode GEMM: 1 = non-temporal (default), RAGK_PART_NT=0 = default
+// policy (A/B)
+inline int part_nt() {
+  static const int v = [] {
+    const char* e = getenv("RAGK_PART_NT");
+    return e ? (atoi(e) != 0) : 1;
+  }();
+  return v;
+}
+
 template <int MT, bool FP8 = false, int NR = 0, int NV = 1, bool MG = false, bool SG = false, bool TL = false>
 int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K, int ks_steps,
                    hipStream_t st, const float* wscale = nullptr, const void* gamma = nullptr, float eps = 0.f,
@@ -576,7 +592,7 @@ int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int
       hipLaunchKernelGGL((gemm_part_kernel<MT, NK, FP8, NR, NV, MG, SG, TL>), grid, dim3(PT_THREADS + (MG ? MG_THREADS : 0)), \
                          0, st,                                                                             \
                          (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, P, M, N, K, wscale, (const bf16_t*)gamma, \
-                         eps, mg, sg, tl);                                                                  \
+                         eps, mg, sg, tl, part_nt());                                                       \
       break;                                                                                                \
     } else {                                                                                                \
       return (int)hipErrorInvalidValue;                                                                     \
