@@ -1,0 +1,72 @@
+"""CPU tests for the profile post-processing tools (tools/gap_report.py, rocprof_summary.py, pmc_summary.py)
+on small synthetic rocprofv3 CSVs of the same column layout the GPU runs write."""
+import csv
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+
+import gap_report  # noqa: E402
+import pmc_summary  # noqa: E402
+import rocprof_summary  # noqa: E402
+
+
+def _write(path, cols, rows):
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(cols)
+        w.writerows(rows)
+
+
+def test_gap_report_kind_strips_namespace():
+    assert gap_report.kind("void (anonymous namespace)::gemm_part_kernel<4>(float*, int)") == "decode"
+    assert gap_report.kind("void (anonymous namespace)::attn_prefill_kernel<8, false>(...)") == "prefill"
+    assert gap_report.kind("Cijk_Alik_Bljk_BBS_BH") == "other"
+
+
+def test_gap_report_gaps(tmp_path, capsys):
+    us = 1000  # ns
+    rows = [
+        (0, 10 * us, "void (anonymous namespace)::embed_kernel()"),          # setup, dropped (before prefill)
+        (20 * us, 120 * us, "void (anonymous namespace)::gemm_w4_kernel<1>(x)"),
+        (125 * us, 130 * us, "void (anonymous namespace)::gemm_part_kernel<2>(x)"),   # 5 us gap prefill->decode
+        (128 * us, 140 * us, "void (anonymous namespace)::attn_decode_kernel<128>(x)"),  # overlaps, no gap
+        (141 * us, 150 * us, "void (anonymous namespace)::add_partials_rmsnorm(x)"),  # 1 us decode->decode
+        (150 * us + 50_000 * us, 150 * us + 50_010 * us, "void (anonymous namespace)::gemm_part_kernel<2>(x)"),
+    ]
+    p = tmp_path / "run_kernel_trace.csv"
+    _write(p, ["Kernel_Name", "Start_Timestamp", "End_Timestamp"], [(n, s, e) for s, e, n in rows])
+    gap_report.main(str(p), 20.0)
+    out = capsys.readouterr().out
+    assert "5 kernels" in out                      # embed dropped: window starts at the first prefill kernel
+    assert "1 gaps > 20 ms" in out                 # the 50 ms pause is a phase boundary
+    assert "2 gaps <= 20 ms: 0.0 ms" in out        # 5 us + 1 us
+    lines = {ln.split()[0] + ln.split()[1] + ln.split()[2]: ln for ln in out.splitlines() if "->" in ln and "us " not in ln}
+    assert "prefill->decode" in lines and "decode->decode" in lines
+    assert int(lines["prefill->decode"].split()[3]) == 1
+
+
+def test_rocprof_summary(tmp_path, capsys):
+    p = tmp_path / "kernel_stats.csv"
+    _write(p, ["Name", "Calls", "TotalDurationNs", "AverageNs"],
+           [("gemm_part_kernel", 10, 3_000_000, 300_000), ("Cijk_Alik_Bljk", 2, 1_000_000, 500_000)])
+    rocprof_summary.main(str(p))
+    out = capsys.readouterr().out
+    assert "4.0 ms total" in out
+    assert "75.00%" in out and "hipBLASLt (Cijk) kernels: 1" in out
+
+
+def test_pmc_summary(tmp_path, capsys, monkeypatch):
+    d = tmp_path / "pmc" / "host0"
+    d.mkdir(parents=True)
+    cols = ["Dispatch_Id", "Kernel_Name", "Grid_Size", "Workgroup_Size", "Start_Timestamp", "End_Timestamp",
+            "Counter_Name", "Counter_Value"]
+    base = ["7", "void gemm_w4_kernel<1, 2>(x)", "65536", "256", "0", "10000"]
+    _write(d / "run_counter_collection.csv", cols, [
+        base + ["GRBM_GUI_ACTIVE", str(8 * 24000)],           # 24000 cycles over 10 us -> 2.40 GHz
+        base + ["SQ_VALU_MFMA_BUSY_CYCLES", str(1024 * 12000)],  # half the MFMA pipe-cycles busy
+    ])
+    monkeypatch.setattr(sys, "argv", ["pmc_summary.py", str(tmp_path / "pmc")])
+    pmc_summary.main()
+    out = capsys.readouterr().out
+    assert "wg=   256" in out and "clk=2.40GHz" in out and "mfma=50.0%" in out
