@@ -119,6 +119,10 @@ def use_pp(M, N, K, epi):
 # library form. "none": every large-M GEMM on gemm_w4 (0 library kernels); "plain": no-epilogue GEMMs
 # only; "all": both.
 PREFILL_BLAS = os.environ.get("RAGK_PREFILL_BLAS", "resid")
+# Optional K filter for the library route (A/B of the per-projection choice): comma-separated K values
+# (e.g. "4096" = o_proj only, "14336" = down only); empty = every K. Both on the library is best: bench
+# 1638 tok/s vs 1632 (down only) / 1616 (o_proj only) (profiles/bench_blas_ks_ab_r4.log).
+PREFILL_BLAS_KS = {int(k) for k in os.environ.get("RAGK_PREFILL_BLAS_KS", "").split(",") if k.strip()}
 
 
 def _gemm_blas(x, w, resid, out, epi):
@@ -159,7 +163,8 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
     ldr = resid.stride(0) if resid is not None else 0
     if (path is None and PREFILL_BLAS != "none" and not out_f32 and bias is None and use_pp(M, N, K, epi)
             and ((epi == "none" and PREFILL_BLAS in ("plain", "all"))
-                 or (epi == "resid" and PREFILL_BLAS in ("resid", "all")))):
+                 or (epi == "resid" and PREFILL_BLAS in ("resid", "all")))
+            and (not PREFILL_BLAS_KS or K in PREFILL_BLAS_KS)):
         return _gemm_blas(x, w, resid, out, epi)
     if path is None and use_pp(M, N, K, epi):
         rows = w.shape[0]
