@@ -33,6 +33,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "end-to-end RAG query p50 latency + gen tokens/sec, Llama-3.1-8B top-k=4"
+# exit status of a run whose headline line went out but whose TP=N C=1 phase hung / raised
+EXIT_TP_HANG = 3
+EXIT_TP_ERROR = 4
 
 
 def parse():
@@ -126,6 +129,7 @@ def main():
     from rag_llm_k8s_amd.engine.llm_engine import SamplingParams
     from rag_llm_k8s_amd.parallel import dist as D
     from rag_llm_k8s_amd.parallel.comm import TPComm
+    from rag_llm_k8s_amd.utils import faults
     from rag_llm_k8s_amd.utils.workload import build_workload, make_queries
 
     if a.seq_parallel:
@@ -272,25 +276,37 @@ def main():
 
     done = threading.Event()
 
-    def watchdog():  # a hung cross-device phase must not cost the headline line
+    def watchdog():  # a hung cross-device phase must not cost the headline line -- nor look like success
         if not done.wait(a.c1_tp_timeout):
             if res is not None:
                 res.update(p50_latency_c1_tp_ms=None, c1_tp_degree=ctx.world,
                            c1_tp_error="timeout after %.0f s" % a.c1_tp_timeout)
                 emit(res)
-            os._exit(0)
+            sys.stdout.flush()
+            sys.stderr.write("bench.py: TP=%d C=1 phase hung (> %.0f s); exiting %d\n"
+                             % (ctx.world, a.c1_tp_timeout, EXIT_TP_HANG))
+            sys.stderr.flush()
+            os._exit(EXIT_TP_HANG)  # every rank: a stuck peer never reaches the shutdown barrier
 
     threading.Thread(target=watchdog, daemon=True).start()
+    rc = 0
     try:
+        hang = faults.value("bench_tp_hang_s")  # fault injection: the TP phase stalls (tests)
+        if hang:
+            time.sleep(float(hang))
         p50, tt, n, ipc, fences = tp_c1_phase(a, ctx, params)
         tp_res = dict(p50_latency_c1_tp_ms=p50, ttft_c1_tp_p50_ms=tt, c1_tp_degree=ctx.world, c1_tp_queries=n,
                       c1_tp_peer_mapped=ipc, c1_tp_fences=fences)
-    except Exception as e:  # recorded, not fatal: the headline stands on its own
+    except Exception as e:  # the headline line still goes out, but the run's exit status reports the failure
         tp_res = dict(p50_latency_c1_tp_ms=None, c1_tp_degree=ctx.world, c1_tp_error="%s: %s" % (type(e).__name__, e))
+        rc = EXIT_TP_ERROR
     done.set()
     if res is not None:
         res.update(tp_res)
         emit(res)
+    if rc:
+        sys.stdout.flush()
+        os._exit(rc)  # peers may be stuck in the failed collective: no shutdown barrier
     D.shutdown(ctx)
 
 

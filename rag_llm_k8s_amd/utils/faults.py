@@ -13,6 +13,7 @@ real server) can switch on without code changes:
   step_delay_ms=X        every engine step sleeps X ms (request timeouts, step watchdog)
   embed_error            the embedder raises (retrieval failure -> HTTP 500)
   comm_hang_s=X          a TP follower stalls X s before stepping (collective watchdog)
+  bench_tp_hang_s=X      bench.py's TP=N C=1 phase stalls X s (its watchdog must exit non-zero)
 
 `set_faults()` overrides the environment in-process (tests).
 """

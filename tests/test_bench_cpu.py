@@ -17,7 +17,7 @@ def _port():
     return p
 
 
-def _bench(n, *extra):
+def _bench(n, *extra, env_extra=None, rc=0):
     args = ["--gpus", str(n), "--model", "tiny", "--embedder", "tiny", "--chunks", "48", "--chunk-words", "60",
             "--concurrency", "2", "--max-new-tokens", "3", "--steps", "1", "--warmup", "0", "--c1", "1"] + list(extra)
     if n == 1:
@@ -25,10 +25,10 @@ def _bench(n, *extra):
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py"] + args
-    env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", **(env_extra or {}))
     r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert r.returncode == 0 and len(lines) == 1, r.stdout[-3000:]
+    assert r.returncode == rc and len(lines) == 1, (r.returncode, r.stdout[-3000:])
     return json.loads(lines[0])
 
 
@@ -45,3 +45,11 @@ def test_bench_two_ranks_appends_tp_c1():
 def test_bench_one_rank_tp_line_is_the_headline_c1():
     res = _bench(1)
     assert res["c1_tp_degree"] == 1 and res["p50_latency_c1_tp_ms"] == res["p50_latency_c1_ms"]
+
+
+def test_bench_tp_phase_hang_exits_nonzero():
+    """A hung cross-device phase (injected stall > the watchdog bound) still prints the headline line, but
+    the run's exit status says it failed (bench.py EXIT_TP_HANG = 3; torchrun reports a failed child as 1)."""
+    res = _bench(2, "--c1-tp", "1", "--c1-tp-timeout", "5", env_extra={"RAGK_FAULTS": "bench_tp_hang_s=60"}, rc=1)
+    assert res["value"] > 0 and res["p50_latency_c1_tp_ms"] is None
+    assert res["c1_tp_error"].startswith("timeout after 5")
