@@ -54,6 +54,8 @@ class RagConfig:
     max_batch: int = 64  # concurrent sequences in one decode step
     max_model_len: int = 16384
     max_prefill_tokens: int = 32768  # tokens per prefill step (chunked prefill budget)
+    # prompt tokens per step while sequences are decoding (decode-aware budget, TPOT bound; 0 = off)
+    mixed_prefill_tokens: int = 2048
     kv_cache_fraction: float = 0.80  # of free HBM after weights
     kv_cache_blocks: int = 0  # explicit override (64-token blocks)
     embed_batch_tokens: int = 65536
@@ -82,6 +84,7 @@ class RagConfig:
             "INDEX_TYPE": ("index_type", str), "IVF_NLIST": ("ivf_nlist", int), "IVF_NPROBE": ("ivf_nprobe", int),
             "REINGEST_APPEND": ("reingest_append", bool), "MAX_BATCH": ("max_batch", int),
             "MAX_MODEL_LEN": ("max_model_len", int), "MAX_PREFILL_TOKENS": ("max_prefill_tokens", int),
+            "MIXED_PREFILL_TOKENS": ("mixed_prefill_tokens", int),
             "KV_CACHE_FRACTION": ("kv_cache_fraction", float), "KV_CACHE_BLOCKS": ("kv_cache_blocks", int),
             "USE_CUDA_GRAPHS": ("use_cuda_graphs", bool), "LOG_LEVEL": ("log_level", str),
             "TRUNCATE_PROMPT": ("truncate_prompt", str), "REQUEST_TIMEOUT_S": ("request_timeout_s", float),

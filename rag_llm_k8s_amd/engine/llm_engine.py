@@ -96,11 +96,16 @@ class Sequence:
 class LLMEngine:
     def __init__(self, model, num_blocks: int, max_batch: int = 64, max_prefill_tokens: int = 32768,
                  max_model_len: int = 16384, eos_ids=(), use_graphs: bool = True, tp_group=None, top_k_cap: int = 64,
-                 graph_buckets=None):
+                 graph_buckets=None, mixed_prefill_tokens: int = 0):
         self.model = model
         self.device = model.device
         self.max_batch = max_batch
         self.max_prefill_tokens = max_prefill_tokens
+        # Decode-aware prefill budget (served path): a step that carries decoding rows takes at most this
+        # many prompt tokens, so the rows' per-token latency (TPOT) is one short step, not a whole
+        # max_prefill_tokens chunk; with nothing decoding the full budget applies (TTFT, throughput).
+        # 0 = off (offline batch / the headline bench: its wave is throughput-bound).
+        self.mixed_prefill_tokens = int(mixed_prefill_tokens or 0)
         self.max_model_len = max_model_len
         self.eos = set(int(e) for e in eos_ids)
         self.bm = make_block_manager(num_blocks)
@@ -192,7 +197,10 @@ class LLMEngine:
         """Pick (seq, start, n) prefill chunks for this step (`reserve` tokens of the budget are taken
         by decode rows riding along in a mixed step)."""
         chunks = []
-        budget = self.max_prefill_tokens - reserve
+        budget = self.max_prefill_tokens
+        if reserve and self.mixed_prefill_tokens > 0:
+            budget = min(budget, self.mixed_prefill_tokens + reserve)
+        budget -= reserve
         # continue partially-prefilled running sequences first
         for s in self.running:
             if s.computed < len(s.prompt) and budget > 0:

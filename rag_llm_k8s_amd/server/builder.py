@@ -69,7 +69,8 @@ def build_generator(cfg, device, tp_rank=0, tp_size=1, comm=None, tp_group=None)
     cfg.max_model_len = max_len
     blocks = kv_blocks_for(model, cfg, device)
     engine = LLMEngine(model, num_blocks=blocks, max_batch=cfg.max_batch, max_prefill_tokens=cfg.max_prefill_tokens,
-                       max_model_len=max_len, eos_ids=eos, use_graphs=cfg.use_cuda_graphs, tp_group=tp_group)
+                       max_model_len=max_len, eos_ids=eos, use_graphs=cfg.use_cuda_graphs, tp_group=tp_group,
+                       mixed_prefill_tokens=cfg.mixed_prefill_tokens)
     return engine, tok, gen
 
 

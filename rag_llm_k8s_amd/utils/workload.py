@@ -142,7 +142,8 @@ class Workload:
 def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=1000, retrieve_k=4, context_k=4,
                    max_new_tokens=150, max_batch=32, max_model_len=8192, max_prefill_tokens=32768, device="cuda",
                    ctx=None, tp_comm=None, seed=0, use_graphs=True, index_type="flat", kv_blocks=None,
-                   word_vocab=400000, dtype="bf16", index_vectors=0, start_threads=False, ignore_eos=False):
+                   word_vocab=400000, dtype="bf16", index_vectors=0, start_threads=False, ignore_eos=False,
+                   mixed_prefill_tokens=0):
     from ..engine.encoder_engine import EmbeddingEngine
     from ..engine.llm_engine import LLMEngine
     from ..index.store import DocumentStore
@@ -177,7 +178,8 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     blocks = kv_blocks or (max_batch * (-(-max_model_len // 64)) + 16)
     engine = LLMEngine(m, num_blocks=blocks, max_batch=max_batch, max_prefill_tokens=max_prefill_tokens,
                        max_model_len=max_model_len, eos_ids=lcfg.eos_token_id, use_graphs=use_graphs,
-                       tp_group=ctx.tp_group if (ctx is not None and tp_size > 1) else None)
+                       tp_group=ctx.tp_group if (ctx is not None and tp_size > 1) else None,
+                       mixed_prefill_tokens=mixed_prefill_tokens)
     ew = E.EncoderWeights.random(ecfg, device, seed=seed + 1)
     emb = EmbeddingEngine(E.EncoderModel(ecfg, ew, device), enc_tok)
     t["weights_s"] = time.time() - t0
@@ -188,7 +190,8 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     t0 = time.time()
     cfg = RagConfig(device=device, retrieve_k=retrieve_k, context_k=context_k, max_new_tokens=max_new_tokens,
                     max_batch=max_batch, max_model_len=max_model_len, index_path="/tmp/ragk_bench_index",
-                    index_type=index_type, seed=seed, max_prefill_tokens=max_prefill_tokens, ignore_eos=ignore_eos)
+                    index_type=index_type, seed=seed, max_prefill_tokens=max_prefill_tokens, ignore_eos=ignore_eos,
+                    mixed_prefill_tokens=mixed_prefill_tokens)
     n_index = max(n_chunks, index_vectors)
     store = DocumentStore(cfg.index_path, emb.dim, device=device, index_type=index_type,
                           ivf_nlist=4096 if n_index >= 500_000 else 1024)

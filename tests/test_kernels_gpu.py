@@ -41,14 +41,14 @@ def test_gemm_pingpong(native, M, N, K, variant):
         native.set_pp_variant(native.PP_VARIANT)
 
 
-@pytest.mark.parametrize("cont", [1, 0])
+@pytest.mark.parametrize("cont", [2, 1, 0])
 @pytest.mark.parametrize("grid", [8, 16])
 @pytest.mark.parametrize("M,N,K", [(1111, 1024, 256), (513, 4104, 128), (2048, 512, 128), (777, 1280, 384),
                                    (1030, 768, 1024)])
 def test_gemm_w4_persistent(native, M, N, K, grid, cont):
     """Persistent gemm_w4: a few blocks loop over every tile (full and edge tiles, one-K-tile K),
     so the next-tile DMA / register-epilogue overlap and its counted waits run many times per block.
-    cont=1: the continuous K-stream kernel (K/64 >= 4)."""
+    cont=1: the continuous K-stream kernel (K/64 >= 4); cont=2: the same with the three-barrier schedule."""
     native.set_w4_grid(grid)
     native.set_w4_cont(cont)
     try:
@@ -66,15 +66,16 @@ def test_gemm_w4_cont_matches_tile_kernel(native):
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
     r = torch.randn(M, N, device=DEV).bfloat16()
     outs = []
-    for cont in (1, 0):
+    for cont in (2, 1, 0):
         native.set_w4_cont(cont)
         try:
             outs.append((native.gemm(x, w, path=6), native.gemm(x, w, resid=r, epi="resid", path=6),
                          native.gemm(x, w, epi="silu_mul", path=6)))
         finally:
             native.set_w4_cont(-1)
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
 
 
 def test_gemm_large_m_routing(native, monkeypatch):

@@ -184,3 +184,32 @@ def test_mixed_prefill_decode_steps_match_separate_steps(tiny):
         mixed_rows[mixed] = eng.stats.get("mixed_decode_tokens", 0)
     assert outs[True] == outs[False]
     assert mixed_rows[True] > 0 and mixed_rows[False] == 0
+
+
+def test_decode_aware_prefill_budget(tiny):
+    """mixed_prefill_tokens caps the prompt tokens of a step that carries decoding rows (TPOT bound on
+    the served path); a step with nothing decoding takes the full max_prefill_tokens budget (TTFT). Tokens
+    are unchanged by the cap (it only re-chunks the prefill)."""
+    cfg, hf, sd = tiny
+    w = LlamaWeights.from_state_dict(cfg, sd, "cpu")
+    torch.manual_seed(10)
+    short, long_ = torch.randint(3, cfg.vocab_size, (10,)).tolist(), torch.randint(3, cfg.vocab_size, (90,)).tolist()
+    p = SamplingParams(max_new_tokens=12, do_sample=False, ignore_eos=True)
+    outs = {}
+    for cap in (0, 16):
+        model = LlamaModel(cfg, w, "cpu", max_positions=512)
+        eng = LLMEngine(model, num_blocks=64, max_batch=4, max_prefill_tokens=64, max_model_len=512,
+                        use_graphs=False, mixed_prefill_tokens=cap)
+        a = eng.add_request(short, p, seed=1)
+        eng.step()  # nothing decoding yet: the whole short prompt in one step
+        assert a.computed == len(short)
+        b = eng.add_request(long_, p, seed=2)
+        chunks = []
+        while b.computed < len(long_):
+            before = b.computed
+            eng.step()
+            chunks.append(b.computed - before)
+        assert chunks == ([63, 27] if cap == 0 else [16] * 5 + [10]), chunks
+        eng.run_until_done()
+        outs[cap] = (a.out, b.out)
+    assert outs[0] == outs[16]

@@ -77,6 +77,8 @@ def main():
     ap.add_argument("--max-batch", type=int, default=64)
     ap.add_argument("--max-prefill-tokens", type=int, default=8192,
                     help="prefill budget per (mixed) engine step: bounds how long a step can stall decoding requests")
+    ap.add_argument("--mixed-prefill-tokens", type=int, default=2048,
+                    help="decode-aware budget: prompt tokens per step while sequences decode (RagConfig default; 0 = off)")
     ap.add_argument("--c1", type=int, default=20, help="sequential single requests (0 = skip)")
     ap.add_argument("--rate", type=float, default=8.0, help="Poisson arrival rate, requests/s (0 = skip)")
     ap.add_argument("--duration", type=float, default=30.0, help="seconds of Poisson arrivals")
@@ -100,6 +102,7 @@ def main():
     wl = build_workload(model=a.model, embedder=a.embedder, n_chunks=a.chunks, retrieve_k=4, context_k=4,
                         max_new_tokens=a.max_new_tokens, max_batch=a.max_batch, max_prefill_tokens=a.max_prefill_tokens,
                         device=dev, seed=0, use_graphs=dev.startswith("cuda"), start_threads=True, ignore_eos=True,
+                        mixed_prefill_tokens=a.mixed_prefill_tokens,
                         **({"word_vocab": 20000, "chunk_words": 120} if a.model == "tiny" else {}))
     svc = wl.svc
     svc.engine.warmup_graphs() if dev.startswith("cuda") else None
@@ -116,7 +119,7 @@ def main():
            "config": {"model": "Llama-3.1-8B-Instruct" if a.model == "8b" else "llama-tiny",
                       "embedder": "all-MiniLM-L6-v2", "index": "FlatL2 %d vectors" % a.chunks, "retrieve_k": 4,
                       "context_k": 4, "max_new_tokens": a.max_new_tokens, "max_prefill_tokens": a.max_prefill_tokens,
-                      "max_batch": a.max_batch, "dtype": "bf16"},
+                      "mixed_prefill_tokens": a.mixed_prefill_tokens, "max_batch": a.max_batch, "dtype": "bf16"},
            "data": "synthetic (random-init weights; Zipfian pseudo-English corpus)", "setup_s": round(setup_s, 1)}
     if a.c1:
         rs = [post(port, next(qi)) for _ in range(a.c1)]

@@ -32,6 +32,14 @@ def main():
         for p in paths:
             if p == "torch":
                 fns[p] = lambda: torch.matmul(x, w.t())  # noqa: E731
+            elif "c" in p:  # "6c2": gemm_w4 with the continuous-kernel mode set to 2 (set_w4_cont)
+                path, mode = (int(v) for v in p.split("c"))
+
+                def fn(path=path, mode=mode):
+                    N.set_w4_cont(mode)
+                    N.gemm(x, w, resid=r, epi=epi, out=out, path=path)
+                    N.set_w4_cont(-1)
+                fns[p] = fn
             elif "@" in p:  # "6@0": gemm_w4 with the persistent grid set to 0 (one block per tile)
                 path, grid = (int(v) for v in p.split("@"))
 
