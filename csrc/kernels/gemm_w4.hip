@@ -855,12 +855,104 @@ __device__ __forceinline__ void w4_iter_c(char* smem, int g, i32x4 srd_a, i32x4 
   if constexpr (STAMP) stp[4] += __builtin_amdgcn_s_memtime() - t0;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Three-barrier K-tile schedule (w4_iter_h), the instruction placement of hipBLASLt's gfx950 256x256x64
+// kernel as read from its disassembly: per K-tile and wave, 128 MFMAs (m = 8i + j per 32-deep sub-step,
+// the activation fragment a[i] held for 8 MFMAs, the weight fragment b[j] cycling) with
+//   m  0..14 : 8 reads b1[j] (weights, sub-step 1 of tile t), one per 2 MFMAs
+//   m 21/22  : lgkmcnt(0), barrier X        -> every wave is done with the weight half of buffer t&1
+//   m 22..58 : 8 weight DMAs of tile t+2 into it; reads a1[i] at m 24..42 between them
+//   m 51/52  : lgkmcnt(0), barrier Y        -> the activation half of buffer t&1 is free
+//   m 61..125: 8 activation DMAs of tile t+2
+//   m 92/93  : vmcnt(13) (the 13 DMAs of this tile are the youngest), barrier: tile t+1 landed
+//   m 93..124: the 16 F0 reads of tile t+1 (8 weight, then 8 activation fragments, spread)
+//   m 127    : lgkmcnt(0): the next iteration opens on MFMAs whose operands are all in registers.
+// What differs from w4_iter: the reads are never bunched one per MFMA (16 ds_read_b128 per 16-cycle
+// MFMA gap saturate the CU's LDS with four waves), the F0(t+1) reads start 35 MFMAs (not 16) before
+// their first use, and the DMAs start after a barrier that retires only the half of the buffer they
+// overwrite. Reads and DMAs are inline asm so hipcc's waitcnt pass adds nothing: the three waits
+// above are the only ones in the loop (its lgkmcnt(14)s stalled the head of every w4_iter). M0 is
+// set once per DMA group and post-incremented after the next MFMA (no s_nop between M0 and the DMA).
+__device__ __forceinline__ void h_read(bf16x8& d, unsigned addr, int off_imm) {
+  // off_imm is a compile-time constant at every call site (fully unrolled schedule)
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(off_imm) : "memory");
+}
+__device__ __forceinline__ void h_dma(i32x4 srd, int voff, int soff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(srd), "s"(soff) : "memory");
+}
+__device__ __forceinline__ void h_m0_set(unsigned lds) { asm volatile("s_mov_b32 m0, %0" ::"s"(lds) : "memory"); }
+__device__ __forceinline__ void h_m0_inc() { asm volatile("s_add_u32 m0, m0, 0x400" ::: "memory"); }
+
+// DMA slots (MFMA index after which piece q is issued) and read slots of the schedule above
+constexpr int H_DX[8] = {22, 25, 28, 31, 34, 52, 55, 58};     // weight pieces (operand B)
+constexpr int H_DY[8] = {61, 64, 85, 87, 89, 96, 99, 125};    // activation pieces (operand A)
+constexpr int H_RB1[8] = {0, 2, 4, 6, 8, 10, 12, 14};         // b1[j]
+constexpr int H_RA1[8] = {24, 27, 30, 33, 36, 38, 40, 42};    // a1[i]
+constexpr int H_RB0[8] = {93, 94, 95, 97, 98, 100, 101, 102}; // b0[j] of tile t+1
+constexpr int H_RA0[8] = {104, 107, 110, 113, 116, 119, 121, 123};  // a0[i] of tile t+1
+constexpr int H_VM = 13;  // DMAs of this iteration issued before the m = 92 wait
+
+constexpr int h_find(const int (&s)[8], int m) {
+  for (int q = 0; q < 8; ++q)
+    if (s[q] == m) return q;
+  return -1;
+}
+
+// One K-tile of the continuous kernel in the three-barrier schedule. g = running K-tile index (ring
+// slot g & 1); sa / sb = DMA source offsets at K-tile kst (this tile's t+2 or the next tile's 0 / 1);
+// ZERO = the F0 MFMAs start the accumulators (srcC = 0); VMW = the m = 92 vmcnt bound (H_VM plus the
+// vector-memory ops issued between the previous iteration's DMAs and this one's, i.e. an epilogue).
+// rbA / rbB: this lane's read bases (sub-step s, buffer 0) for the activation / weight fragments.
+template <bool ZERO, int VMW>
+__device__ __forceinline__ void w4_iter_h(char* smem, int g, i32x4 srd_a, i32x4 srd_b, const int (&sa)[8],
+                                          const int (&sb)[8], int kst, int wid, const unsigned (&rbA)[2],
+                                          const unsigned (&rbB)[2], f32x4 (&acc)[8][8], bf16x8 (&a0)[8],
+                                          bf16x8 (&b0)[8], bf16x8 (&a1)[8], bf16x8 (&b1)[8]) {
+  static_assert(VMW >= H_VM && VMW <= 63, "vmcnt bound");
+  const unsigned cur = (unsigned)(g & 1) * W_BUF, nxt = (unsigned)((g + 1) & 1) * W_BUF;
+  const unsigned lds_cur = (unsigned)(unsigned long long)(const __attribute__((address_space(3))) char*)smem + cur;
+  const unsigned mX = __builtin_amdgcn_readfirstlane(lds_cur + W_TILE_A + wid * 8192);  // weight pieces
+  const unsigned mY = __builtin_amdgcn_readfirstlane(lds_cur + wid * 8192);             // activation pieces
+  const int kb = kst * WBK * 2;
+  const unsigned rb1 = rbB[1] + cur, ra1 = rbA[1] + cur, rb0 = rbB[0] + nxt, ra0 = rbA[0] + nxt;
+  static_for<128>([&](auto mc) __attribute__((always_inline)) {
+    constexpr int m = decltype(mc)::value;
+    if constexpr (m == 21) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (m == 22 || m == 52) w4_barrier();
+    if constexpr (m == 92) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VMW) : "memory");
+    }
+    if constexpr (m == 93) w4_barrier();
+    if constexpr (m == 51 || m == 127) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // MFMA m
+    if constexpr (m < 64) {
+      if constexpr (ZERO) w4_mfma0(acc, a0, b0, m);
+      else w4_mfma(acc, a0, b0, m);
+    } else {
+      w4_mfma(acc, a1, b1, m - 64);
+    }
+    // post-increment M0 one MFMA after each piece; M0 for a DMA group one MFMA (or more) ahead of its
+    // first piece
+    if constexpr (h_find(H_DX, m - 1) >= 0 || h_find(H_DY, m - 1) >= 0) h_m0_inc();
+    if constexpr (m == 21) h_m0_set(mX);
+    if constexpr (m == 59) h_m0_set(mY);
+    constexpr int qx = h_find(H_DX, m), qy = h_find(H_DY, m);
+    if constexpr (qx >= 0) h_dma(srd_b, sb[qx], kb);
+    if constexpr (qy >= 0) h_dma(srd_a, sa[qy], kb);
+    constexpr int r1b = h_find(H_RB1, m), r1a = h_find(H_RA1, m), r0b = h_find(H_RB0, m), r0a = h_find(H_RA0, m);
+    if constexpr (r1b >= 0) h_read(b1[r1b], rb1, r1b * 2048);
+    if constexpr (r1a >= 0) h_read(a1[r1a], ra1, r1a * 2048);
+    if constexpr (r0b >= 0) h_read(b0[r0b], rb0, r0b * 2048);
+    if constexpr (r0a >= 0) h_read(a0[r0a], ra0, r0a * 2048);
+  });
+}
+
 // Requires K / 64 >= 4 (the launcher falls back to gemm_w4_kernel below that).
 // KSPLIT: split-K over nsplit K-slabs of K columns each in ONE persistent launch -- work item
 // t = z * tiles + tile writes the fp32 partial tile of slab z to C + z * M * ldc (the consumer, e.g.
 // add_partials_rmsnorm, sums the slabs). For prefill shapes whose 256x256 tile count fills only
 // ~1.3 waves of the CUs (o_proj / down at M ~ 5k: 336 tiles on 256 CUs), two slabs make 2.6 waves.
-template <int EPI, bool OUT_F32, bool STAMP = false, bool KSPLIT = false>
+template <int EPI, bool OUT_F32, bool STAMP = false, bool KSPLIT = false, bool H = false>
 __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4c_kernel(const bf16_t* __restrict__ A, int lda,
                                                                  const bf16_t* __restrict__ B, int ldb, void* C,
                                                                  int ldc, const bf16_t* __restrict__ bias,
@@ -911,18 +1003,37 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4c_kernel(const bf16_t* _
   f32x4 acc[8][8];
   unsigned long long stp[5] = {0, 0, 0, 0, 0};
   unsigned long long tl_loop = 0, tl_epi = 0;
+  // w4_iter_h read bases (buffer 0): fragment i / j of sub-step s at base[s] + 2048 i (swizzle independent of i)
+  unsigned rbA[2], rbB[2];
+  {
+    const unsigned l0 = (unsigned)(unsigned long long)(const __attribute__((address_space(3))) char*)smem;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const unsigned cs = (unsigned)(((4 * s2 + fh) ^ ((fr >> 1) & 7)) * 16);
+      rbA[s2] = l0 + (unsigned)((wr * 128 + fr) * 128) + cs;
+      rbB[s2] = l0 + W_TILE_A + (unsigned)((wc * 128 + fr) * 128) + cs;
+    }
+  }
+  constexpr int VMH0 = H_VM + EV > 63 ? 63 : H_VM + EV;
   int g = 0, done = 0;
   for (;;) {
     unsigned long long tt0 = 0;
     if constexpr (STAMP) tt0 = __builtin_amdgcn_s_memtime();
     const int next = tile + (int)gridDim.x;
     const bool has_next = next < nwt;
-    w4_iter_c<true, true, true, VMW0, false>(smem, g, srd_a, srd_b, off_a, off_b, 2, wid, wr, wc, fr, fh, acc, a0,
-                                             b0, a1, b1, stp);
+    if constexpr (H)
+      w4_iter_h<true, VMH0>(smem, g, srd_a, srd_b, off_a, off_b, 2, wid, rbA, rbB, acc, a0, b0, a1, b1);
+    else
+      w4_iter_c<true, true, true, VMW0, false>(smem, g, srd_a, srd_b, off_a, off_b, 2, wid, wr, wc, fr, fh, acc, a0,
+                                               b0, a1, b1, stp);
     ++g;
-    for (int t = 1; t + 2 < nk; ++t, ++g)
-      w4_iter_c<true, true, false, 16, STAMP>(smem, g, srd_a, srd_b, off_a, off_b, t + 2, wid, wr, wc, fr, fh, acc,
-                                              a0, b0, a1, b1, stp);
+    for (int t = 1; t + 2 < nk; ++t, ++g) {
+      if constexpr (H)
+        w4_iter_h<false, H_VM>(smem, g, srd_a, srd_b, off_a, off_b, t + 2, wid, rbA, rbB, acc, a0, b0, a1, b1);
+      else
+        w4_iter_c<true, true, false, 16, STAMP>(smem, g, srd_a, srd_b, off_a, off_b, t + 2, wid, wr, wc, fr, fh, acc,
+                                                a0, b0, a1, b1, stp);
+    }
     // The last two iterations stage (and read the first fragments of) the next tile; on the block's
     // last tile they re-stage this tile's K-tiles 0 / 1 instead (valid addresses, never read), so both
     // cases run the same straight-line code: a branch around the MFMA iterations made the register
@@ -945,12 +1056,19 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4c_kernel(const bf16_t* _
         }
       }
     }
-    w4_iter_c<true, true, false, 16, false>(smem, g, srd_a, srd_b, off_a, off_b, 0, wid, wr, wc, fr, fh, acc, a0, b0,
-                                            a1, b1, stp);
-    ++g;
-    w4_iter_c<true, true, false, 16, false>(smem, g, srd_a, srd_b, off_a, off_b, 1, wid, wr, wc, fr, fh, acc, a0, b0,
-                                            a1, b1, stp);
-    ++g;
+    if constexpr (H) {
+      w4_iter_h<false, H_VM>(smem, g, srd_a, srd_b, off_a, off_b, 0, wid, rbA, rbB, acc, a0, b0, a1, b1);
+      ++g;
+      w4_iter_h<false, H_VM>(smem, g, srd_a, srd_b, off_a, off_b, 1, wid, rbA, rbB, acc, a0, b0, a1, b1);
+      ++g;
+    } else {
+      w4_iter_c<true, true, false, 16, false>(smem, g, srd_a, srd_b, off_a, off_b, 0, wid, wr, wc, fr, fh, acc, a0,
+                                              b0, a1, b1, stp);
+      ++g;
+      w4_iter_c<true, true, false, 16, false>(smem, g, srd_a, srd_b, off_a, off_b, 1, wid, wr, wc, fr, fh, acc, a0,
+                                              b0, a1, b1, stp);
+      ++g;
+    }
     unsigned long long tt1 = 0;
     if constexpr (STAMP) tt1 = __builtin_amdgcn_s_memtime();
     w4_pin_acc(acc);
@@ -1023,13 +1141,14 @@ static int w4_sched_min_k() {
 }
 
 // Continuous K-stream kernel for K < the spread-schedule threshold (RAGK_W4_CONT=0 -> gemm_w4_kernel).
+// 2 = the continuous kernel with the three-barrier schedule (w4_iter_h) for every K.
 static int g_w4_cont = -1;
-static bool w4_cont() {
+static int w4_cont() {
   if (g_w4_cont < 0) {
     const char* e = getenv("RAGK_W4_CONT");
-    g_w4_cont = e ? (atoi(e) != 0) : 1;
+    g_w4_cont = e ? atoi(e) : 1;
   }
-  return g_w4_cont != 0;
+  return g_w4_cont;
 }
 
 template <int EPI, bool F32>
@@ -1037,7 +1156,11 @@ int launch_w4(const void* A, int lda, const void* B, int ldb, void* C, int ldc, 
               int ldr, int M, int N, int K, hipStream_t st) {
   const int nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
   const int grid = w4_grid(nwg);
-  if (K < w4_sched_min_k() && K / WBK >= 4 && w4_cont())
+  if (K / WBK >= 4 && w4_cont() == 2)
+    hipLaunchKernelGGL((gemm_w4c_kernel<EPI, F32, false, false, true>), dim3(grid), dim3(W4_THREADS), 0, st,
+                       (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid,
+                       ldr, M, N, K, nullptr);
+  else if (K < w4_sched_min_k() && K / WBK >= 4 && w4_cont())
     hipLaunchKernelGGL((gemm_w4c_kernel<EPI, F32>), dim3(grid), dim3(W4_THREADS), 0, st, (const bf16_t*)A, lda,
                        (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K,
                        nullptr);
@@ -1064,7 +1187,7 @@ RAGK_API int ragk_gemm_w4_set_grid(int g) {
 // Continuous-K-stream override (tests / A/B): 1 = gemm_w4c_kernel for K < the spread threshold, 0 = off,
 // < 0 = back to RAGK_W4_CONT / the default (on).
 RAGK_API int ragk_gemm_w4_set_cont(int on) {
-  g_w4_cont = on < 0 ? -1 : (on != 0);
+  g_w4_cont = on < 0 ? -1 : on;
   return 0;
 }
 
