@@ -82,6 +82,16 @@ struct ArPeers {
   unsigned spin_limit;       // bound of one peer wait, in s_memrealtime ticks (100 MHz)
 };
 
+// Which wait gave up: the error record names the collective (call site), the peer that never arrived,
+// the block / row slot and the low bits of the epoch (the call index of that slot), so a timeout says
+// WHICH collective of WHICH step stalled on WHICH peer (tests/test_tp_gpu.py, parallel/comm.py).
+enum ArSite : unsigned { AR_SITE_AR_START = 1, AR_SITE_AR_MID = 2, AR_SITE_GATHER = 3, AR_SITE_ROW_START = 4,
+                         AR_SITE_ROW_MID = 5 };
+// record = 1 | site << 1 (3 bits) | peer << 4 (3 bits) | slot << 7 (8 bits) | (epoch & 0xffff) << 15 (bit 31 clear)
+__device__ __forceinline__ unsigned ar_record(unsigned site, int peer, int slot, unsigned ep) {
+  return 1u | (site & 7u) << 1 | ((unsigned)peer & 7u) << 4 | ((unsigned)slot & 255u) << 7 | (ep & 0xffffu) << 15;
+}
+
 __device__ __forceinline__ unsigned ld_sys(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -93,7 +103,7 @@ __device__ __forceinline__ void st_sys(unsigned* p, unsigned v) {
 // slot [b][rank] of every peer's `which` array, wait until all peers published `ep` into mine.
 // Returns false (block-uniform) if a peer did not arrive within the bounded spin: the caller then
 // reads no peer data (the result is garbage either way and the host raises CommError).
-__device__ bool peer_barrier(const ArPeers& P, int rank, int world, int which, unsigned ep) {
+__device__ bool peer_barrier(const ArPeers& P, int rank, int world, int which, unsigned ep, unsigned site) {
   __shared__ int s_ok;
   if (threadIdx.x == 0) s_ok = 1;
   __syncthreads();
@@ -108,8 +118,9 @@ __device__ bool peer_barrier(const ArPeers& P, int rank, int world, int which, u
     while (ld_sys(slot) < ep) {
       __builtin_amdgcn_s_sleep(2);
       if (__builtin_amdgcn_s_memrealtime() - t0 > P.spin_limit) {  // a peer never arrived: report, never hang
-        st_sys(&mf->error, 1u);
-        if (P.host_err) st_sys(P.host_err, 1u);
+        const unsigned rec = ar_record(site, threadIdx.x, b, ep);
+        st_sys(&mf->error, rec);
+        if (P.host_err) st_sys(P.host_err, rec);
         s_ok = 0;
         break;
       }
@@ -144,7 +155,7 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPeers P, int ra
   u32x4* my_stage = reinterpret_cast<u32x4*>(P.base[rank] + stage_off);
   const u32x4* in4 = reinterpret_cast<const u32x4*>(in);
   for (long v = v0 + threadIdx.x; v < v1; v += AR_THREADS) my_stage[v] = in4[v];
-  const bool ok = peer_barrier(P, rank, world, 0, ep);
+  const bool ok = peer_barrier(P, rank, world, 0, ep, AR_SITE_AR_START);
 
   u32x4* out4 = reinterpret_cast<u32x4*>(out);
   if (!ok) {
@@ -175,7 +186,7 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPeers P, int ra
       }
       my_res[v] = pack8(acc);
     }
-    if (peer_barrier(P, rank, world, 1, ep))
+    if (peer_barrier(P, rank, world, 1, ep, AR_SITE_AR_MID))
     for (int p = 0; p < world; ++p) {
       const long t0 = min(v0 + p * sub, v1), t1 = min(t0 + sub, v1);
       for (long v = t0 + threadIdx.x; v < t1; v += AR_THREADS) out4[v] = ld16(P.base[p] + result_off + v * 16);
@@ -212,8 +223,9 @@ __device__ bool row_barrier(const ArPeers& P, int rank, int world, int which, in
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > P.spin_limit) {
         ArFlags* ef = reinterpret_cast<ArFlags*>(P.base[rank]);
-        st_sys(&ef->error, 1u);
-        if (P.host_err) st_sys(P.host_err, 1u);
+        const unsigned rec = ar_record(which ? AR_SITE_ROW_MID : AR_SITE_ROW_START, threadIdx.x, row, ep);
+        st_sys(&ef->error, rec);
+        if (P.host_err) st_sys(P.host_err, rec);
         s_ok = 0;
         break;
       }
@@ -380,7 +392,7 @@ __global__ __launch_bounds__(AR_THREADS) void allgather_kernel(ArPeers P, int ra
   const long v0 = min((long)b * per, n16), v1 = min(v0 + per, n16);
   u32x4* my_stage = reinterpret_cast<u32x4*>(P.base[rank] + stage_off);
   for (long v = v0 + threadIdx.x; v < v1; v += AR_THREADS) my_stage[v] = in[v];
-  if (peer_barrier(P, rank, world, 0, ep))
+  if (peer_barrier(P, rank, world, 0, ep, AR_SITE_GATHER))
   for (int p = 0; p < world; ++p)
     for (long v = v0 + threadIdx.x; v < v1; v += AR_THREADS) out[(long)p * n16 + v] = ld16(P.base[p] + stage_off + v * 16);
   __syncthreads();

@@ -426,319 +426,14 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_prefill_kernel(Prefill
   }
 }
 
-// ------------------------------------------------------------------------------------
-// Ping-pong prefill attention (Llama config: D 128, 4 query heads per KV head, causal, paged
-// cache < 4 GiB). One 8-wave block per CU: waves 0-3 (group A) and 4-7 (group B) each own 32 query
-// rows of the same 4 heads, so wave w and its SIMD partner w + 4 run the same program one segment
-// apart. A segment is the interval between two block barriers; in every segment one group is in
-// its MFMA phase (PV of tile u-1 + QK^T of tile u: 64 MFMAs, LDS fragment reads) while the other
-// is in its VALU phase (online softmax of its tile, the next K or V tile's LDS-DMA). The stamp
-// build of attn_prefill_kernel put a wave at ~4.3k cycles per tile for 1024 cycles of its own
-// MFMAs: the two co-resident waves of a SIMD (independent 4-wave blocks) reached their softmax
-// at the same time and left the matrix pipe idle; here the barrier schedule makes the softmax of
-// one wave and the MFMAs of its partner coincide (MI355X_MICROARCH.md "Two waves per SIMD").
-//
-// K/V ring of 3 slots (tile t in slot t % 3), segment s (A: MFMA phase when s is even, B when odd):
-//   A (MFMA): seg 2u   PV(u-1) + QK(u)       A (VALU): seg 2u+1  softmax(u), DMA K(u+2)
-//   B (MFMA): seg 2u+1 PV(u-1) + QK(u)       B (VALU): seg 2u+2  softmax(u), DMA V(u+2)
-// K(t) is read in segments 2t / 2t+1 and rewritten (as K(t+3)) in 2t+3; V(t) read in 2t+2 / 2t+3,
-// rewritten in 2t+4. The VALU phase ends with vmcnt(4) (only the DMAs it just issued may stay in
-// flight), so every tile lands >= 2 segments after its DMA was issued, before the barrier that
-// precedes its first reader. Prologue: K(0), V(0), K(1). 2n + 2 segments for n KV tiles.
-// Same arithmetic as attn_prefill_kernel (bit-identical outputs).
-constexpr int PP_NS = 3;
-
 template <typename F, int... Is>
 __device__ __forceinline__ void pp_static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
   (f(std::integral_constant<int, Is>{}), ...);
 }
+// f(integral_constant<int, i>) for i = 0..N-1 (compile-time slot indices of a fully unrolled loop)
 template <int N, typename F>
 __device__ __forceinline__ void pp_static_for(F&& f) {
   pp_static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// One MFMA phase: 16 PV steps (d-tile dt = i / 2, key step ks = i % 2; two tr-read pairs per
-// fragment) or 16 QK^T steps (key sub-tile t = j / 4, d-step ks = j % 4; one b128 read). The LDS
-// fragment of step i + PF is requested before the MFMAs of step i and a scheduling fence follows
-// every step, so at most PF + 1 fragments are live. Fragment addresses are the load_vt / load_k
-// images (D = 128: kswz(R) = R & 15, vswz(r) = 2 (r & 7)) rebuilt per phase from an opaque copy of
-// the lane id: loop-invariant per-lane offsets hoisted out of the segment loop spilled (12 VGPRs).
-template <bool PV, int PF>
-__device__ __forceinline__ void pp_mfma_phase(const char* sV, const char* sK, int lane, const bf16x8 (&pb)[2][2],
-                                              const bf16x8 (&qf)[2][Cfg<128>::KS], f32x4 (&o)[Cfg<128>::DT][2],
-                                              f32x4 (&s)[4][2]) {
-  constexpr int N = 16;
-  int ln = lane;
-  asm volatile("" : "+v"(ln));
-  // V^T: rows r0 = 32 ks + 4 h + (i >> 2) and r0 + 16, chunk (2 dt + b) ^ 2 (r0 & 7), half i & 1
-  const int vi = ln & 15, vr = 4 * (ln >> 4) + (vi >> 2);
-  const int vx = vr & 7;
-  const char* vb = sV + vr * 256 + 16 * ((vi >> 1) & 1) + 8 * (vi & 1);
-  // K: row 16 t + fr, chunk (4 s + fh) ^ fr
-  const int fr = ln & 15;
-  const char* kb = sK + fr * 256 + 16 * ((ln >> 4) ^ (fr & 3));
-  const int kx = fr >> 2;
-  auto frag = [&](auto ic) -> bf16x8 {
-    constexpr int i = decltype(ic)::value;
-    if constexpr (PV) {
-      constexpr int dt = i >> 1, ks = i & 1;
-      const char* p = vb + ks * 32 * 256 + 32 * (dt ^ vx);
-      const bf16x4 x0 = tr_read(p), x1 = tr_read(p + 16 * 256);
-      return (bf16x8){x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-    } else {
-      constexpr int t = i >> 2, ks = i & 3;
-      return *reinterpret_cast<const bf16x8*>(kb + t * 16 * 256 + 64 * (ks ^ kx));
-    }
-  };
-  bf16x8 ring[PF + 1];
-  pp_static_for<PF>([&](auto ic) { ring[decltype(ic)::value] = frag(ic); });
-  pp_static_for<N>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-    if constexpr (i + PF < N) ring[(i + PF) % (PF + 1)] = frag(std::integral_constant<int, i + PF>{});
-    const bf16x8 f = ring[i % (PF + 1)];
-    if constexpr (PV) {
-      constexpr int dt = i >> 1, ks = i & 1;
-      o[dt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f, pb[ks][0], o[dt][0], 0, 0, 0);
-      o[dt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f, pb[ks][1], o[dt][1], 0, 0, 0);
-    } else {
-      constexpr int t = i >> 2, ks = i & 3;
-      const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      s[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f, qf[0][ks], ks == 0 ? z : s[t][0], 0, 0, 0);
-      s[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f, qf[1][ks], ks == 0 ? z : s[t][1], 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  });
-}
-
-template <int PRIO_B, int PF = 2, bool STAMP = false>
-__global__ __launch_bounds__(512, 2) void attn_prefill_pp_kernel(PrefillArgs a) {
-  constexpr int D = 128;
-  using C = Cfg<D>;
-  constexpr bool CAUSAL = true;
-  __shared__ __attribute__((aligned(16))) char smem[2 * PP_NS * C::TILEB];  // [K slots][V slots]
-  __shared__ int s_bt[MAX_BT];
-
-  const int lane = threadIdx.x & 63;
-  const int wid_u = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int grp = wid_u >> 2, hs = wid_u & 3;
-  int tix, hg;
-  prefill_block(a, tix, hg);
-  const int seq = a.tiles[2 * tix], q_start = a.tiles[2 * tix + 1];
-  const int G = a.Hq / a.Hkv;
-  const int groups_per_kv = G / 4;
-  const int kvh = hg / groups_per_kv;
-  const int hq = kvh * G + (hg % groups_per_kv) * 4 + hs;
-  const int pbase = q_start + grp * 32;
-
-  const int q_off = a.cu_q[seq];
-  const int q_len = a.cu_q[seq + 1] - q_off;
-  const int kv_len = a.kv_lens[seq];
-  const int ctx0 = kv_len - q_len;
-  const int blk_qmax = min(q_start + 64, q_len) - 1;
-  const int n_keys = min(kv_len, ctx0 + blk_qmax + 1);
-  const int n_kt = (n_keys + KT - 1) / KT;
-  const int wave_pmax = ctx0 + min(pbase + 31, q_len - 1);
-  const int fr = lane & 15, fh = lane >> 4;
-
-  bf16x8 qf[2][C::KS];
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    int qi = pbase + 16 * qt + fr;
-    qi = qi < q_len ? qi : q_len - 1;
-    const bf16_t* qp = a.q + (size_t)(q_off + qi) * a.q_stride + hq * D + 8 * fh;
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s) qf[qt][s] = *reinterpret_cast<const bf16x8*>(qp + 32 * s);
-  }
-  f32x4 o[C::DT][2];
-#pragma unroll
-  for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) o[dt][qt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float m_i[2] = {-INFINITY, -INFINITY}, l_i[2] = {0.f, 0.f};
-  f32x4 s[4][2];
-  bf16x8 pb[2][2];
-
-  const int* bt = a.block_tables + (size_t)seq * a.bt_stride;
-  for (int i = threadIdx.x; i < n_kt; i += 512) s_bt[i] = bt[i];
-
-  // pieces hs, hs + 4, hs + 8, hs + 12 of a 16-piece K / V tile (the wave's share in its group)
-  int koff[4], voff[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int p = hs + 4 * i;
-    const int row = p * C::RPP + lane / C::NC, ph = lane % C::NC;
-    koff[i] = row * C::ROWB + 16 * (ph ^ kswz<D>(row));
-    voff[i] = row * C::ROWB + 16 * (ph ^ vswz<D>(row));
-  }
-  const i32x4 srd_k = make_srd(a.k, a.kv_bytes);
-  const i32x4 srd_v = make_srd(a.v, a.kv_bytes);
-  auto stage = [&](int kt, bool is_v) {
-    const int soff = __builtin_amdgcn_readfirstlane(
-        (int)((unsigned)(s_bt[kt] * a.Hkv + kvh) * (unsigned)(KT * D * 2)));
-    char* base = smem + ((is_v ? PP_NS : 0) + kt % PP_NS) * C::TILEB;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) blds16(is_v ? srd_v : srd_k, is_v ? voff[i] : koff[i], soff, base + (hs + 4 * i) * 1024);
-  };
-  __syncthreads();  // s_bt
-  if (grp == 0) {
-    stage(0, false);
-    stage(0, true);
-  } else if (n_kt > 1) {
-    stage(1, false);
-  }
-  wait_vmcnt0();
-  __syncthreads();
-  if constexpr (PRIO_B) {
-    if (grp == 1) __builtin_amdgcn_s_setprio(1);
-  }
-
-  const float c = a.scale_log2;
-  // MFMA phase of tile u: PV(u-1) (V slot (u-1) % 3) and QK^T(u) (K slot u % 3)
-  auto mfma_phase = [&](int u) {
-    if (u >= 1 && u - 1 < n_kt && (u - 1) * KT <= wave_pmax)
-      pp_mfma_phase<true, PF>(smem + (PP_NS + (u + PP_NS - 1) % PP_NS) * C::TILEB, nullptr, lane, pb, qf, o, s);
-    if (u < n_kt && u * KT <= wave_pmax)
-      pp_mfma_phase<false, PF>(nullptr, smem + (u % PP_NS) * C::TILEB, lane, pb, qf, o, s);
-  };
-  // VALU phase of tile u in segment seg: softmax(u) -> pb (O rescaled), then this segment's DMA
-  // (odd seg: group A stages K((seg + 3) / 2); even: group B stages V(seg / 2 + 1))
-  auto valu_phase = [&](int u, int seg) {
-    const int k0 = u * KT;
-    if (u >= 0 && u < n_kt && k0 <= wave_pmax) {
-      const bool need_mask = (k0 + KT - 1 > ctx0 + pbase) || (k0 + KT > kv_len);
-      float alpha[2];
-      auto softmax = [&](auto mask_tag, const int qt) {
-        constexpr bool MASK = decltype(mask_tag)::value;
-        const int qpos = ctx0 + pbase + 16 * qt + fr;
-        float mx = -INFINITY;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float x = s[t][qt][r];
-            if constexpr (MASK) {
-              const int kj = k0 + 16 * t + 4 * fh + r;
-              const bool ok = kj < kv_len && kj <= qpos;
-              x = ok ? x : -INFINITY;
-              s[t][qt][r] = x;
-            }
-            mx = fmaxf(mx, x);
-          }
-        mx = max_xor16(mx);
-        mx = max_xor32(mx);
-        const float mxs = mx * c;
-        alpha[qt] = 1.f;
-        if (mxs > m_i[qt] + RESCALE_LOG2) {
-          alpha[qt] = m_i[qt] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_i[qt] - mxs);
-          m_i[qt] = mxs;
-        }
-        const float mref = m_i[qt] == -INFINITY ? 0.f : m_i[qt];
-        float ls = 0.f;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float pv = __builtin_amdgcn_exp2f(__builtin_fmaf(s[t][qt][r], c, -mref));
-            s[t][qt][r] = pv;
-            ls += pv;
-          }
-        l_i[qt] = l_i[qt] * alpha[qt] + ls;
-      };
-      if (need_mask) {
-        softmax(std::true_type{}, 0);
-        softmax(std::true_type{}, 1);
-      } else {
-        softmax(std::false_type{}, 0);
-        softmax(std::false_type{}, 1);
-      }
-      if (__builtin_amdgcn_ballot_w64(alpha[0] != 1.f || alpha[1] != 1.f)) {
-#pragma unroll
-        for (int dt = 0; dt < C::DT; ++dt)
-#pragma unroll
-          for (int qt = 0; qt < 2; ++qt) o[dt][qt] *= alpha[qt];
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) pb[ks][qt] = pack_p(s[2 * ks][qt], s[2 * ks + 1][qt]);
-    }
-    const int item = (seg & 1) ? (seg + 3) >> 1 : (seg >> 1) + 1;
-    if (item < n_kt) {
-      stage(item, (seg & 1) == 0);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      wait_vmcnt0();
-    }
-  };
-  // stamp build: per wave [MFMA phase, barrier after it, VALU phase, barrier after it, segments]
-  unsigned long long stp[5] = {0, 0, 0, 0, 0};
-  unsigned long long t0 = 0;
-  auto stamp = [&](int i) {
-    if constexpr (STAMP) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      stp[i] += t - t0;
-      t0 = t;
-    }
-  };
-  auto barrier = [] {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
-  // 2 n_kt + 2 segments, two per iteration; group A: [MFMA(u) | VALU(u)], group B one segment
-  // behind: [VALU(u-1) | MFMA(u)]
-  if (grp == 0) {
-    for (int u = 0; u <= n_kt; ++u) {
-      mfma_phase(u);
-      stamp(0);
-      barrier();
-      stamp(1);
-      valu_phase(u, 2 * u + 1);
-      stamp(2);
-      barrier();
-      stamp(3);
-    }
-  } else {
-    for (int u = 0; u <= n_kt; ++u) {
-      valu_phase(u - 1, 2 * u);
-      stamp(2);
-      barrier();
-      stamp(3);
-      mfma_phase(u);
-      stamp(0);
-      barrier();
-      stamp(1);
-    }
-  }
-  if constexpr (STAMP) {
-    stp[4] = n_kt + 1;
-    if (lane == 0 && g_attn_dbg) {
-      unsigned long long* d = g_attn_dbg + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 8 + wid_u) * 6;
-#pragma unroll
-      for (int i = 0; i < 5; ++i) d[i] = stp[i];
-    }
-  }
-  if constexpr (PRIO_B) {
-    if (grp == 1) __builtin_amdgcn_s_setprio(0);
-  }
-
-#pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    float l = l_i[qt];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    const int qi = pbase + 16 * qt + fr;
-    if (qi < q_len) {
-      bf16_t* op = a.out + (size_t)(q_off + qi) * a.out_stride + hq * D + 4 * fh;
-#pragma unroll
-      for (int dt = 0; dt < C::DT; ++dt) {
-        const f32x4 v = o[dt][qt] * inv;
-        *reinterpret_cast<uint2*>(op + 16 * dt) = make_uint2(pk2bf(v[0], v[1]), pk2bf(v[2], v[3]));
-      }
-    }
-  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1222,8 +917,6 @@ struct DecodeArgs {
   bf16_t* out; int out_stride;
   int Hq, Hkv, part_tiles, max_parts;
   float scale_log2;
-  int* counters;                           // [B][Hkv] zeroed tickets: fused split-K merge (null: separate
-                                           // attn_decode_reduce_kernel launch)
   // Fused RoPE + KV append (null qkv_p: q is read from `q` and the cache already holds the new token).
   // The qkv projection arrives as fp32 split-K partial slabs P[S][B][ldp] (gemm_part.hip); every
   // block sums + rotates its G query heads itself, and the block owning the last KV tile also sums,
@@ -1231,7 +924,6 @@ struct DecodeArgs {
   const float* qkv_p; long long p_slab; int ldp, S;
   const int* positions; const int* slots;
   const float* cos_t; const float* sin_t;
-  int nb;                                  // batch (0: gridDim.z, the 3-D launch)
 };
 
 // Tiles per partition of one sequence: its KV tiles spread evenly over all max_parts partitions
@@ -1247,123 +939,14 @@ __device__ __forceinline__ int decode_part_tiles(int n_kt, const DecodeArgs& a) 
 template <int D, int G, int NW = 4>
 constexpr int decode_lds_bytes() { return NW * Cfg<D>::TILEB + G * D * 2; }
 
-// Signal of a decode-attention block inside the fused attention + o_proj launch (attn_oproj_kernel):
-// every storing wave has drained its write-through (sc1) stores, then one lane adds to the agent-scope
-// counter the o_proj blocks poll (MI355X_MICROARCH.md "Valid forms": sc1 stores, vmcnt(0), barrier,
-// agent atomic; the consumer polls with sc1 loads and reads the bytes with sc1 loads only).
-// Stage hand-off of the fused launches: arrivals count on ONE counter; the block whose add returns
-// total - 1 (every other producer's stores were drained before its add) raises a done flag in FL_REPL
-// replicas, each on its own 128-B line, and consumers poll the replica of their block index with a long
-// s_sleep -- hundreds of pollers on the counter itself (one line, hammered while it is being
-// incremented) slowed the whole launch (MI355X_MICROARCH.md polling-cost / fanin).
-// In-kernel stamps of the fused launches (diagnostic instantiation only, tools/fused_stamps.py): lane 0
-// of a block writes s_memrealtime (100 MHz, device-wide) at stage boundaries into g_fused_stamps[block][k].
-__device__ unsigned long long* g_fused_stamps;
-template <bool ST>
-__device__ __forceinline__ void fstamp(int k) {
-  if constexpr (ST) {
-    if (threadIdx.x == 0) g_fused_stamps[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
-  }
-}
-constexpr int FL_REPL = 16;       // flag replicas
-constexpr int FL_STRIDE = 32;     // ints between replicas (128 B)
-constexpr int FL_A = 64;          // cnt offset of the attention-done flags
-constexpr int FL_Q = FL_A + FL_REPL * FL_STRIDE;  // cnt offset of the qkv-done flags
-constexpr int FL_P = FL_Q + FL_REPL * FL_STRIDE;           // v2: "attention KV prefetch issued" flags
-constexpr int CNT_TICKETS = FL_P + FL_REPL * FL_STRIDE;  // MIA: per (sequence, KV head) merge tickets
-constexpr int CNT_SS = CNT_TICKETS + 4 * 64;               // v2 o_proj: [4][<= 512] sum-of-squares partials
-constexpr int CNT_INTS = CNT_SS + 4 * 512;
-__device__ __forceinline__ void stage_arrive(int* cnt, int total, int* flags) {
-  wait_vmcnt0();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (__hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
-#pragma unroll
-      for (int k = 0; k < FL_REPL; ++k) __hip_atomic_store(flags + k * FL_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 // One split-K partition block of decode attention: partition `part` of KV head `kvh` of sequence `b`.
-// FUSED (attn_oproj_kernel): the partition record is written write-through even for a single-partition
-// sequence (the o_proj blocks merge records only), there is no merge here, and the block signals
-// `fused_cnt` when its records are out -- also when it has no tiles (the counter counts every block).
-// qkv slab sum of sum_partials8x2 with write-through (sc1) buffer loads: the slabs were produced by
-// other blocks of the same launch (attn_oproj_kernel's qkv blocks). off1 / off2: byte offsets of the two
-// 8-float runs in slab 0, slab_b: bytes per slab. Same summation order.
-__device__ __forceinline__ void sum_partials8x2_sc1(__amdgpu_buffer_rsrc_t rs, int off1, int off2, int S, int slab_b,
-                                                    float* a, float* b) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) a[e] = b[e] = 0.f;
-  for (int s0 = 0; s0 < S; s0 += PSU) {
-    u32x4 p[PSU][4];
-#pragma unroll
-    for (int u = 0; u < PSU; ++u) {
-      const int o = min(s0 + u, S - 1) * slab_b;
-      p[u][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off1 + o, 0, 16));
-      p[u][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off1 + o + 16, 0, 16));
-      p[u][2] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off2 + o, 0, 16));
-      p[u][3] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off2 + o + 16, 0, 16));
-    }
-#pragma unroll
-    for (int u = 0; u < PSU; ++u) {
-      if (s0 + u < S) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          a[e] += __uint_as_float(p[u][0][e]);
-          a[4 + e] += __uint_as_float(p[u][1][e]);
-          b[e] += __uint_as_float(p[u][2][e]);
-          b[4 + e] += __uint_as_float(p[u][3][e]);
-        }
-      }
-    }
-  }
-}
-
-// Bounded poll of an agent-scope counter by one lane (sc1 loads), then the block's barrier. Sets err[0]
-// and gives up (the block computes garbage, never hangs) after `limit` s_memrealtime ticks.
-__device__ __forceinline__ void wait_flag(const int* flags, int* err, unsigned limit) {
-  if (threadIdx.x == 0) {
-    const int* f = flags + (blockIdx.x % FL_REPL) * FL_STRIDE;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-      __builtin_amdgcn_s_sleep(8);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-}
-
-
-struct QWait {       // attention blocks waiting for the in-launch qkv blocks (QW mode)
-  const int* flags;  // qkv-done flag replicas
-  int* err;
-  unsigned limit;
-};
-
-// bf16 pair (d, d + 1) of an attention output row, stored write-through for the o_proj blocks of the
-// same launch (4 B per store: a 2-B write-through store costs ~2x per byte).
-__device__ __forceinline__ void out_pair_sc1(const DecodeArgs& a, int b, int col, float x, float y) {
-  const int nb = a.nb ? a.nb : (int)gridDim.z;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, nb * a.out_stride * 2, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b32(pk2bf(x, y), rs, (b * a.out_stride + col) * 2, 0, 16);
-}
-
-// MIA (FUSED only): the partitions of a (sequence, KV head) are merged by the last of its partition blocks
-// (ticket counters a.counters) into the bf16 attention output, written through; the o_proj blocks then
-// stage a plain bf16 activation slice instead of each merging the records of its K-slice.
 // NW: waves per block (4; 8 for the batch-32 grid with one partition per sequence: one 8-wave block per
-// CU keeps the same KV bytes in flight as two 4-wave blocks and needs no merge launch)
-template <int D, int G, bool NT = false, bool FUSED = false, bool QW = false, bool MIA = false, bool ST = false,
-          int NW = 4>
-__device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part, int kvh, int b, char* smem,
-                                                  int* fused_cnt = nullptr, QWait qw = {}, int fused_total = 0) {
-  static_assert(NW == 4 || (NW == 8 && !FUSED), "8-wave blocks: the plain decode kernel only");
+// CU keeps the same KV bytes in flight as two 4-wave blocks and needs no merge launch). A multi-partition
+// sequence writes its partition records; attn_decode_reduce_kernel (or, deferred, the o_proj GEMM's
+// gemm_part_merge) merges them.
+template <int D, int G, bool NT = false, int NW = 4>
+__device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part, int kvh, int b, char* smem) {
   constexpr int NTH = NW * 64;
-  fstamp<ST>(0);
   using C = Cfg<D>;
   static_assert(G <= 16, "at most 16 query heads per KV head");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1372,18 +955,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
   const int n_kt = (kv_len + KT - 1) / KT;
   const int pt = decode_part_tiles(n_kt, a);
   const int kt0 = part * pt;
-  if (kt0 >= n_kt) {  // block-uniform early exit (before any barrier)
-    if constexpr (FUSED && MIA) {
-      if (threadIdx.x == 0 &&
-          __hip_atomic_fetch_add(fused_cnt + 5, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == fused_total - 1) {
-#pragma unroll
-        for (int k = 0; k < FL_REPL; ++k)
-          __hip_atomic_store(fused_cnt + FL_P + k * FL_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if constexpr (FUSED) stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
-    return;
-  }
+  if (kt0 >= n_kt) return;  // block-uniform early exit (before any barrier)
   const int kt1 = min(kt0 + pt, n_kt);
   const int nparts = (n_kt + pt - 1) / pt;
   const int fr = lane & 15, fh = lane >> 4;
@@ -1410,19 +982,6 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
                                                                                    32 * s + 8 * fh))
                        : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
   }
-  fstamp<ST>(1);
-  if constexpr (FUSED && MIA) {
-    // tell the o_proj blocks this block's KV requests are out (their weight stream queues behind them;
-    // nothing is handed off, so no drain): counter cnt[5], flags FL_P
-    if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(fused_cnt + 5, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == fused_total - 1) {
-#pragma unroll
-      for (int k = 0; k < FL_REPL; ++k)
-        __hip_atomic_store(fused_cnt + FL_P + k * FL_STRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if constexpr (QW) wait_flag(qw.flags, qw.err, qw.limit);  // the KV prefetch above is in flight
-  fstamp<ST>(2);
   if (a.qkv_p != nullptr) {
     // q = RoPE(bf16(sum_s P[s][b])) for this KV head's G query heads, one (d, d + D/2) rotate_half
     // pair of 8-vectors per thread (G * D/16 threads, all slab loads of a thread in flight together),
@@ -1432,8 +991,6 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     constexpr int NV = D / 16;  // pairs per head
     const int pos = a.positions[b];
     const float* prow = a.qkv_p + (size_t)b * a.ldp;
-    [[maybe_unused]] const __amdgpu_buffer_rsrc_t rs_qkv = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(a.qkv_p), (short)0, (int)(a.p_slab * a.S * 4), 0x00020000);
     const float* ct = a.cos_t + (size_t)pos * (D / 2);
     const float* st = a.sin_t + (size_t)pos * (D / 2);
     const int tid = threadIdx.x;
@@ -1443,12 +1000,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
       const int g = tid / NV, v = tid % NV;
       const float* ph = prow + (size_t)(kvh * G + g) * D + 8 * v;
       float x1[8], x2[8], o1[8], o2[8];
-      if constexpr (QW) {
-        const int o = (int)((ph - a.qkv_p) * 4);
-        sum_partials8x2_sc1(rs_qkv, o, o + D * 2, a.S, (int)(a.p_slab * 4), x1, x2);
-      } else {
-        sum_partials8x2(ph, ph + D / 2, a.S, (size_t)a.p_slab, x1, x2);
-      }
+      sum_partials8x2(ph, ph + D / 2, a.S, (size_t)a.p_slab, x1, x2);
       rope8(x1, x2, ct + 8 * v, st + 8 * v, o1, o2);
       *reinterpret_cast<u32x4*>(s_q + g * D + 8 * v) = pack8(o1);
       *reinterpret_cast<u32x4*>(s_q + g * D + D / 2 + 8 * v) = pack8(o2);
@@ -1458,12 +1010,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
       const size_t kvo = (((size_t)(slot / KT) * a.Hkv + kvh) * KT + (slot % KT)) * D;
       const float* ph = prow + (size_t)(a.Hq + (isv ? a.Hkv : 0) + kvh) * D + 8 * v;
       float x1[8], x2[8];
-      if constexpr (QW) {
-        const int o = (int)((ph - a.qkv_p) * 4);
-        sum_partials8x2_sc1(rs_qkv, o, o + D * 2, a.S, (int)(a.p_slab * 4), x1, x2);
-      } else {
-        sum_partials8x2(ph, ph + D / 2, a.S, (size_t)a.p_slab, x1, x2);
-      }
+      sum_partials8x2(ph, ph + D / 2, a.S, (size_t)a.p_slab, x1, x2);
       bf16_t* dst = (isv ? const_cast<bf16_t*>(a.vc) : const_cast<bf16_t*>(a.kc)) + kvo;
       if (isv) {
         *reinterpret_cast<u32x4*>(dst + 8 * v) = pack8(x1);
@@ -1563,12 +1110,6 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     }
   }
 
-  fstamp<ST>(3);
-  // partition-statistics buffers as write-through (sc1) buffer resources for the fused merge
-  const unsigned pbytes = (unsigned)((size_t)(a.nb ? a.nb : (int)gridDim.z) * a.Hq * a.max_parts * 4);
-  const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(a.part_o, (short)0, (int)(pbytes * D), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_ml = __builtin_amdgcn_make_buffer_rsrc(a.part_ml, (short)0, (int)(pbytes * 2), 0x00020000);
-
   // ---- combine the 4 waves in LDS ----
   __syncthreads();
   float* sm = reinterpret_cast<float*>(smem);    // [4][16] max
@@ -1581,30 +1122,6 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
 #pragma unroll
     for (int r = 0; r < 4; ++r) so[(wid * 16 + fr) * D + 16 * dt + 4 * fh + r] = o[dt][r];
   __syncthreads();
-  if constexpr (FUSED && MIA) {
-    if (nparts == 1) {  // the block's output is final: bf16 pairs, written through
-      for (int e2 = threadIdx.x; e2 < G * D / 2; e2 += NTH) {
-        const int g = (2 * e2) / D, d = (2 * e2) % D;
-        float M = -INFINITY;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) M = fmaxf(M, sm[w * 16 + g]);
-        const float Mu = M == -INFINITY ? 0.f : M;
-        float L = 0.f, O0 = 0.f, O1 = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-          const float sc = exp2f(sm[w * 16 + g] - Mu);
-          L += (sl[w * 64 + g] + sl[w * 64 + g + 16] + sl[w * 64 + g + 32] + sl[w * 64 + g + 48]) * sc;
-          O0 += so[(w * 16 + g) * D + d] * sc;
-          O1 += so[(w * 16 + g) * D + d + 1] * sc;
-        }
-        out_pair_sc1(a, b, (kvh * G + g) * D + d, L > 0.f ? O0 / L : 0.f, L > 0.f ? O1 / L : 0.f);
-      }
-      fstamp<ST>(4);
-      stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
-      fstamp<ST>(5);
-      return;
-    }
-  }
   // thread -> (g, d) pairs
   for (int e = threadIdx.x; e < G * D; e += NTH) {
     const int g = e / D, d = e % D;
@@ -1620,816 +1137,23 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
       O += so[(w * 16 + g) * D + d] * sc;
     }
     const int hq = kvh * G + g;
-    if (nparts == 1 && !FUSED) {
+    if (nparts == 1) {
       a.out[(size_t)b * a.out_stride + hq * D + d] = f2bf(L > 0.f ? O / L : 0.f);
     } else {
       const size_t pi = ((size_t)b * a.Hq + hq) * a.max_parts + part;
-      if (FUSED || a.counters) {  // write-through (sc1) stores, read back by another CU
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(O), rs_o, (int)((pi * D + d) * 4), 0, 16);
-        if (d == 0) {
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(M), rs_ml, (int)(pi * 8), 0, 16);
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(L), rs_ml, (int)(pi * 8 + 4), 0, 16);
-        }
-      } else {
-        a.part_o[pi * D + d] = O;
-        if (d == 0) {
-          a.part_ml[pi * 2] = M;
-          a.part_ml[pi * 2 + 1] = L;
-        }
+      a.part_o[pi * D + d] = O;
+      if (d == 0) {
+        a.part_ml[pi * 2] = M;
+        a.part_ml[pi * 2 + 1] = L;
       }
     }
   }
-  if constexpr (FUSED && !MIA) {
-    stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
-    return;
-  }
-  if (!FUSED && (nparts == 1 || a.counters == nullptr)) return;
-
-  // ---- fused split-K merge: the last of this (b, kvh)'s nparts partition blocks to finish merges
-  // them (same math as attn_decode_reduce_kernel), so the merge costs no extra launch. The partials
-  // were stored write-through (sc1) and are read back with sc1 loads, so no agent-scope release or
-  // acquire fence is needed for any block -> XCD placement (an L2 write-back per block cost more than
-  // the merge launch it saved).
-  __shared__ int s_last;
-  wait_vmcnt0();  // every storing wave drains its sc1 stores
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(a.counters + b * a.Hkv + kvh, 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (old == nparts - 1);
-  }
-  __syncthreads();
-  if (!s_last) {
-    fstamp<ST>(4);
-    if constexpr (FUSED) stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
-    fstamp<ST>(5);
-    return;
-  }
-  asm volatile("" ::: "memory");  // the sc1 loads below stay after the ticket
-  const size_t hb = (size_t)b * a.Hq + kvh * G;  // first query head of this KV head
-  if constexpr (FUSED) {
-    // Merge on the critical path of the fused launch: each thread's partial-output records of its (head,
-    // d pair)s for the first MCH partitions are requested first, then the (max, sum) statistics (into LDS),
-    // so both are in flight together -- one memory round trip for <= MCH partitions -- and merged in
-    // registers once the per-partition scales are known.
-    constexpr int MCH = 16;
-    constexpr int NPR = (G * D / 2 + NTH - 1) / NTH;  // (head, pair) items per thread
-    float* s_m = reinterpret_cast<float*>(smem);  // [G][nparts] max -> scale
-    float* s_l = s_m + G * nparts;
-    float* s_L = s_l + G * nparts;
-    f32x2 v[NPR][MCH];
-#pragma unroll
-    for (int k = 0; k < NPR; ++k) {
-      const int e2 = min((int)threadIdx.x + NTH * k, G * D / 2 - 1);
-      const int g = (2 * e2) / D, d = (2 * e2) % D;
-      const int po = (int)(((hb + g) * a.max_parts * D + d) * 4);
-#pragma unroll
-      for (int i = 0; i < MCH; ++i)
-        v[k][i] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_o, po + min(i, nparts - 1) * D * 4, 0, 16));
-    }
-    for (int e = threadIdx.x; e < G * nparts; e += NTH) {
-      const int g = e / nparts, p = e % nparts;
-      const f32x2 ml = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_ml, (int)(((hb + g) * a.max_parts + p) * 8), 0, 16));
-      s_m[e] = ml[0];
-      s_l[e] = ml[1];
-    }
-    __syncthreads();
-    if (threadIdx.x < G) {
-      const int g = threadIdx.x;
-      float Mx = -INFINITY;
-      for (int p = 0; p < nparts; ++p) Mx = fmaxf(Mx, s_m[g * nparts + p]);
-      const float Mu = Mx == -INFINITY ? 0.f : Mx;
-      float L = 0.f;
-      for (int p = 0; p < nparts; ++p) {
-        const float sc = exp2f(s_m[g * nparts + p] - Mu);
-        s_m[g * nparts + p] = sc;
-        L += s_l[g * nparts + p] * sc;
-      }
-      s_L[g] = L;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < NPR; ++k) {
-      const int e2 = threadIdx.x + NTH * k;
-      if (e2 >= G * D / 2) break;
-      const int g = (2 * e2) / D, d = (2 * e2) % D;
-      const float* sc = s_m + g * nparts;
-      float O0 = 0.f, O1 = 0.f;
-#pragma unroll
-      for (int i = 0; i < MCH; ++i) {
-        const float f = i < nparts ? sc[i] : 0.f;
-        O0 += v[k][i][0] * f;
-        O1 += v[k][i][1] * f;
-      }
-      const int po = (int)(((hb + g) * a.max_parts * D + d) * 4);
-      for (int p0 = MCH; p0 < nparts; p0 += MCH) {  // long contexts: further rounds of MCH records
-        f32x2 w[MCH];
-#pragma unroll
-        for (int i = 0; i < MCH; ++i)
-          w[i] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_o, po + min(p0 + i, nparts - 1) * D * 4, 0, 16));
-#pragma unroll
-        for (int i = 0; i < MCH; ++i) {
-          const float f = p0 + i < nparts ? sc[p0 + i] : 0.f;
-          O0 += w[i][0] * f;
-          O1 += w[i][1] * f;
-        }
-      }
-      const float L = s_L[g];
-      out_pair_sc1(a, b, (kvh * G + g) * D + d, L > 0.f ? O0 / L : 0.f, L > 0.f ? O1 / L : 0.f);
-    }
-    if (threadIdx.x == 0) __hip_atomic_store(a.counters + b * a.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    fstamp<ST>(6);
-    stage_arrive(fused_cnt, fused_total, fused_cnt + FL_A);
-    fstamp<ST>(5);
-    return;
-  }
-  float* s_m = reinterpret_cast<float*>(smem);  // [G][nparts] partition max, then its scale
-  float* s_l = s_m + G * nparts;                 // [G][nparts] partition sum
-  float* s_L = s_l + G * nparts;                 // [G] merged sum
-  for (int e = threadIdx.x; e < G * nparts; e += NTH) {
-    const int g = e / nparts, p = e % nparts;
-    const size_t pi = (hb + g) * a.max_parts + p;
-    s_m[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ml, (int)(pi * 8), 0, 16));
-    s_l[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ml, (int)(pi * 8 + 4), 0, 16));
-  }
-  __syncthreads();
-  if (threadIdx.x < G) {
-    const int g = threadIdx.x;
-    float Mx = -INFINITY;
-    for (int p = 0; p < nparts; ++p) Mx = fmaxf(Mx, s_m[g * nparts + p]);
-    const float Mu = Mx == -INFINITY ? 0.f : Mx;
-    float L = 0.f;
-    for (int p = 0; p < nparts; ++p) {
-      const float sc = exp2f(s_m[g * nparts + p] - Mu);
-      s_m[g * nparts + p] = sc;
-      L += s_l[g * nparts + p] * sc;
-    }
-    s_L[g] = L;
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < G * D; e += NTH) {
-    const int g = e / D, d = e % D;
-    const int po = (int)(((hb + g) * a.max_parts * D + d) * 4);  // byte offset of partition 0
-    const float* sc = s_m + g * nparts;
-    float O = 0.f;
-    int p = 0;
-    for (; p + 8 <= nparts; p += 8) {  // 8 independent loads in flight
-      float v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_o, po + (p + i) * D * 4, 0, 16));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) O += v[i] * sc[p + i];
-    }
-    for (; p < nparts; ++p) O += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_o, po + p * D * 4, 0, 16)) * sc[p];
-    const float L = s_L[g];
-    a.out[(size_t)b * a.out_stride + (kvh * G + g) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(a.counters + b * a.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int D, int G, bool NT = false, int NW = 4>
-__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attn_decode_kernel(DecodeArgs a, PfArgs pf) {
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attn_decode_kernel(DecodeArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[decode_lds_bytes<D, G, NW>()];
-  if ((int)blockIdx.x >= a.max_parts) {  // MALL prefetch rider (block-uniform): x beyond the partitions
-    const int ex = gridDim.x - a.max_parts;
-    pf_rider(pf, (blockIdx.x - a.max_parts) + ex * (blockIdx.y + gridDim.y * blockIdx.z), ex * gridDim.y * gridDim.z);
-    return;
-  }
-  attn_decode_block<D, G, NT, false, false, false, false, NW>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
-}
-
-// ------------------------------------------------------------------------------------
-// Fused decode attention + o_proj (batch <= 4): one launch instead of attention -> o_proj.
-// ------------------------------------------------------------------------------------
-// Blocks [0, na) are attention partition blocks (attn_decode_block<FUSED>); blocks [na, na + nob) are
-// o_proj split-K blocks. An o_proj block issues its whole weight slice (64 output columns x KS, straight
-// to VGPRs, non-temporal) as soon as it is dispatched -- while the attention blocks still stream the KV
-// cache -- then polls the attention-done counter, merges the split-K partitions of the heads of its
-// K-slice into an LDS activation slice and runs the MFMAs; its fp32 partial slab goes to the
-// add_partials_rmsnorm consumer as gemm_part_merge's does. The o_proj weight stream (33.5 MB per layer
-// at 8B) overlaps the attention instead of following it. Deadlock-free by construction: only o_proj
-// blocks wait, and only on attention blocks, which have lower indices (dispatched first) and never
-// wait; the wait is bounded anyway (error word, never a hang). Counters: cnt[0] attention blocks done,
-// cnt[1] o_proj blocks past their wait (the last one re-arms both for the next layer / replay),
-// cnt[2] error.
-struct OprojArgs {
-  const bf16_t* W; int ldw;  // o_proj weight [N][K] bf16
-  float* P;                  // [K / KS][M][N] fp32 partial slabs
-  int M, N, K;
-  int na, nob;               // attention blocks, o_proj blocks
-  int* cnt;
-  unsigned spin_limit;       // s_memrealtime ticks (100 MHz)
-  // optional residual + RMSNorm tail (add_partials_rmsnorm's math, done by the last o_proj block):
-  // h[M][ldh] += bf16(sum of the slabs) (bf16), xn[M][ldx] = rmsnorm(h) * gamma. h == nullptr: none.
-  bf16_t* h; int ldh;
-  const bf16_t* gamma;
-  bf16_t* xn; int ldx;
-  float eps;
-  float* ss;                 // v2 tail: [4][nob] per-block sum-of-squares partials
-};
-constexpr int OP_MAXP = 64;  // partitions per (row, head) merged in LDS
-
-template <int D, int NLD, bool MIA = false, bool ST = false>
-__device__ __forceinline__ void oproj_merge_block(const DecodeArgs& a, const OprojArgs& o, int ob, char* smem) {
-  fstamp<ST>(0);
-  constexpr int KS = 32 * NLD;          // K-slice (NLD 32-k MFMA steps, one 16-B load each per lane)
-  constexpr int ROWB = KS * 2;          // bytes per row of the LDS activation slice
-  constexpr int HPB = KS / D;           // attention heads in the slice
-  static_assert(KS % D == 0, "slice = whole heads");
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int fr = lane & 15, fh = lane >> 4;
-  const int ncb = (o.N + 63) / 64;
-  const int cb = ob % ncb, s = ob / ncb;
-  const int n0 = cb * 64, kbase = s * KS, h0 = kbase / D;
-  const int M = o.M;
-
-  // 1) the weight slice, all loads in flight before anything else (wave w: columns n0 + 16w + fr)
-  const int wrow = min(n0 + 16 * wid + fr, o.N - 1);
-  const bf16_t* wp = o.W + (size_t)wrow * o.ldw + kbase + 8 * fh;
-  bf16x8 wf[NLD];
-#pragma unroll
-  for (int ks = 0; ks < NLD; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
-
-  // 2) wait for every attention block (one lane polls a done-flag replica; the others wait at the barrier;
-  //    a bounded wait: on timeout the error word is set and the block computes garbage, never hangs)
-  fstamp<ST>(1);
-  wait_flag(o.cnt + FL_A, o.cnt + 2, o.spin_limit);
-  fstamp<ST>(2);
-  if constexpr (MIA) {
-    // the attention blocks merged the partitions: stage the bf16 rows of this K-slice (write-through loads)
-    const __amdgpu_buffer_rsrc_t rs_x =
-        __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, M * a.out_stride * 2, 0x00020000);
-    constexpr int CPR = KS / 8;  // 16-B chunks per slice row
-    u32x4 xv[(4 * CPR + 255) / 256];
-#pragma unroll
-    for (int i = 0; i < (4 * CPR + 255) / 256; ++i) {
-      const int e = min(tid + 256 * i, M * CPR - 1);
-      const int r = e / CPR, c = e % CPR;
-      xv[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, (r * a.out_stride + kbase + 8 * c) * 2, 0, 16));
-    }
-#pragma unroll
-    for (int i = 0; i < (4 * CPR + 255) / 256; ++i) {
-      const int e = tid + 256 * i;
-      if (e < M * CPR) {
-        const int r = e / CPR, c = e % CPR;
-        *reinterpret_cast<u32x4*>(smem + r * ROWB + 16 * ((c & ~15) | ((c & 15) ^ (r & 15)))) = xv[i];
-      }
-    }
-  } else {
-
-  // 3) merge the partitions of (row r, head h0 + j): pass 1 the statistics -> per-partition scales and
-  //    the merged sum in LDS, pass 2 the partial outputs (all loads of a thread in flight: the scales are
-  //    known, so there is no running rescale chain). Records are read write-through (sc1), as written.
-  const unsigned pbytes = (unsigned)((size_t)M * a.Hq * a.max_parts * 4);
-  const __amdgpu_buffer_rsrc_t rs_o = __builtin_amdgcn_make_buffer_rsrc(a.part_o, (short)0, (int)(pbytes * D), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_ml = __builtin_amdgcn_make_buffer_rsrc(a.part_ml, (short)0, (int)(pbytes * 2), 0x00020000);
-  float* s_sc = reinterpret_cast<float*>(smem + 16 * ROWB);  // [M][HPB][OP_MAXP] max, then scale
-  float* s_l = s_sc + 4 * HPB * OP_MAXP;                      // [M][HPB][OP_MAXP] partition sums
-  float* s_il = s_l + 4 * HPB * OP_MAXP;                      // [M][HPB] 1 / merged sum (0 if empty)
-  int* s_np = reinterpret_cast<int*>(s_il + 4 * HPB);         // [M] partitions of row r
-  if (tid < M) {
-    const int n_kt = (a.kv_lens[tid] + KT - 1) / KT;
-    const int pt = decode_part_tiles(n_kt, a);
-    s_np[tid] = (n_kt + pt - 1) / pt;
-  }
-  __syncthreads();
-  const int MP = a.max_parts;
-  {
-    // every (max, sum) load of the thread issued before any is used (indices clamped, masked after):
-    // at most 4 x 4 heads x 64 partitions = 4 per thread
-    constexpr int PER = (4 * HPB * OP_MAXP + 255) / 256;
-    f32x2 ml[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = min(tid + 256 * k, M * HPB * MP - 1);
-      const int p = e % MP, j = (e / MP) % HPB, r = e / (MP * HPB);
-      const int pi = ((r * a.Hq + h0 + j) * MP + p) * 8;
-      ml[k] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_ml, pi, 0, 16));
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = tid + 256 * k;
-      if (e < M * HPB * MP) {
-        const int p = e % MP, j = (e / MP) % HPB, r = e / (MP * HPB);
-        const bool ok = p < s_np[r];
-        s_sc[(r * HPB + j) * OP_MAXP + p] = ok ? ml[k][0] : -INFINITY;
-        s_l[(r * HPB + j) * OP_MAXP + p] = ok ? ml[k][1] : 0.f;
-      }
-    }
-  }
-  __syncthreads();
-  if (tid < M * HPB) {
-    float* sc = s_sc + tid * OP_MAXP;
-    const float* sl = s_l + tid * OP_MAXP;
-    float mx = -INFINITY;
-    for (int p = 0; p < MP; ++p) mx = fmaxf(mx, sc[p]);
-    const float mu = mx == -INFINITY ? 0.f : mx;
-    float L = 0.f;
-    for (int p = 0; p < MP; ++p) {
-      const float f = sc[p] == -INFINITY ? 0.f : exp2f(sc[p] - mu);
-      sc[p] = f;
-      L += sl[p] * f;
-    }
-    s_il[tid] = L > 0.f ? 1.f / L : 0.f;
-  }
-  __syncthreads();
-  // pass 2: task = (row r, head j, 4 dims d4); npg adjacent lanes split a task's partitions
-  const int ntask = M * HPB * (D / 4);
-  int npg = 1;
-  while (npg < 8 && ntask * npg * 2 <= 256) npg *= 2;
-  for (int t0 = 0; t0 < ntask * npg; t0 += 256) {
-    const int tt = t0 + tid;
-    const bool act = tt < ntask * npg;
-    const int task = (act ? tt : 0) / npg, pg = tt % npg;
-    const int d4 = task % (D / 4), j = (task / (D / 4)) % HPB, r = task / ((D / 4) * HPB);
-    const int np = s_np[r];
-    const float* sc = s_sc + (r * HPB + j) * OP_MAXP;
-    const int base = ((r * a.Hq + h0 + j) * MP) * D * 4 + d4 * 16;
-    f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
-    for (int p0 = pg; p0 < np; p0 += 8 * npg) {  // 8 records per thread in flight
-      u32x4 v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int p = min(p0 + i * npg, np - 1);
-        v[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_o, base + p * D * 4, 0, 16));
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float f = p0 + i * npg < np ? sc[p0 + i * npg] : 0.f;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc4[e] += __uint_as_float(v[i][e]) * f;
-      }
-    }
-    for (int off = 1; off < npg; off <<= 1)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc4[e] += __shfl_xor(acc4[e], off, 64);
-    if (act && pg == 0) {
-      const float il = s_il[r * HPB + j];
-      uint2 w;
-      w.x = pk2bf(acc4[0] * il, acc4[1] * il);
-      w.y = pk2bf(acc4[2] * il, acc4[3] * il);
-      const int cc = j * (D / 8) + d4 / 2;  // 16-B chunk of the slice row; 8-B half d4 & 1
-      const int c = (cc & ~15) | ((cc & 15) ^ (r & 15));
-      *reinterpret_cast<uint2*>(smem + r * ROWB + 16 * c + 8 * (d4 & 1)) = w;
-    }
-  }
-  }  // !MIA
-  __syncthreads();
-
-  fstamp<ST>(3);
-  // 4) MFMA over the slice: A = activation rows (fr), B = this wave's weight columns
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < NLD; ++ks) {
-    const int chunk = 4 * ks + fh;
-    const bf16x8 xf = *reinterpret_cast<const bf16x8*>(smem + fr * ROWB + 16 * ((chunk & ~15) | ((chunk & 15) ^ (fr & 15))));
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[ks], acc, 0, 0, 0);
-  }
-  const int col = n0 + 16 * wid + fr;
-  const int nslab = o.K / KS;
-  const __amdgpu_buffer_rsrc_t rs_p =
-      __builtin_amdgcn_make_buffer_rsrc(o.P, (short)0, (int)((size_t)nslab * M * o.N * 4), 0x00020000);
-  if (fh == 0 && col < o.N) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (r < M) {
-        const int off = (int)((((size_t)s * M + r) * o.N + col) * 4);
-        if (o.h)  // read back by the last block below: write-through
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[r]), rs_p, off, 0, 16);
-        else
-          o.P[off / 4] = acc[r];
-      }
-    }
-  }
-  // 5) arrival ticket (after this block's slab stores have drained): the last o_proj block re-arms both
-  //    counters -- every attention block is done and every o_proj block has read cnt[0] by then; the next
-  //    launch is stream-ordered after this one -- and, with the norm tail, reduces the slabs.
-  int* s_last = reinterpret_cast<int*>(smem);  // the activation slice is dead
-  wait_vmcnt0();
-  __syncthreads();
-  fstamp<ST>(4);
-  if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(o.cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == o.nob - 1;
-    if (last) {  // (cnt[4] + the qkv flags: the 3-role launch's; every attention block is past its wait)
-      __hip_atomic_store(o.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(o.cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(o.cnt + 4, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(o.cnt + 5, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-      for (int k = 0; k < FL_REPL; ++k) {
-        __hip_atomic_store(o.cnt + FL_A + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(o.cnt + FL_Q + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(o.cnt + FL_P + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    *s_last = last;
-  }
-  __syncthreads();
-  if (!o.h || !*s_last) {
-    fstamp<ST>(5);
-    return;
-  }
-  // 6) residual + RMSNorm of every row (add_partials_rmsnorm_kernel's math; slab order kept)
-  float* red = reinterpret_cast<float*>(smem) + 16;
-  const int nvec = o.N >> 3;
-  for (int r = 0; r < M; ++r) {
-    float v[2][8];  // this thread's two row vectors (H <= 4096; longer rows are re-read from h below)
-    float ss = 0.f;
-    for (int i0 = 0; i0 < nvec; i0 += 512) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int vi = i0 + tid + 256 * i;
-        if (vi >= nvec) continue;
-        float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        u32x4 pv[16][2];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int su = min(u, nslab - 1);
-          const int off = (int)((((size_t)su * M + r) * o.N + vi * 8) * 4);
-          pv[u][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_p, off, 0, 16));
-          pv[u][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_p, off + 16, 0, 16));
-        }
-        const u32x4 hv = *reinterpret_cast<const u32x4*>(o.h + (size_t)r * o.ldh + vi * 8);
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          if (u < nslab) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              a[e] += __uint_as_float(pv[u][0][e]);
-              a[4 + e] += __uint_as_float(pv[u][1][e]);
-            }
-          }
-        }
-        float hf[8];
-        unpack8(hv, hf);
-        float* vv = v[i];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) vv[e] = bf2f(f2bf(hf[e] + bf2f(f2bf(a[e]))));
-        *reinterpret_cast<u32x4*>(o.h + (size_t)r * o.ldh + vi * 8) = pack8(vv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) ss += vv[e] * vv[e];
-      }
-    }
-    ss = block_sum(ss, red);
-    const float inv = rsqrtf(ss / (float)o.N + o.eps);
-    for (int i0 = 0; i0 < nvec; i0 += 512) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int vi = i0 + tid + 256 * i;
-        if (vi >= nvec) continue;
-        float hv8[8], wv[8], out8[8];
-        if (nvec <= 512) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) hv8[e] = v[i][e];
-        } else {
-          unpack8(*reinterpret_cast<const u32x4*>(o.h + (size_t)r * o.ldh + vi * 8), hv8);
-        }
-        unpack8(*reinterpret_cast<const u32x4*>(o.gamma + vi * 8), wv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) out8[e] = wv[e] * bf2f(f2bf(hv8[e] * inv));
-        *reinterpret_cast<u32x4*>(o.xn + (size_t)r * o.ldx + vi * 8) = pack8(out8);
-      }
-    }
-    __syncthreads();  // red[] reuse by the next row
-  }
-  fstamp<ST>(6);
-}
-
-// qkv projection blocks of the 3-role launch (attn_oproj_kernel<..., QNLD > 0>): split-K partial slabs
-// P[s][M][N] of rmsnorm(h) . Wqkv^T (gemm_part_norm's math and reduction order: threads sum their row
-// vectors, the 4 wave partials are added in order), 64 output columns x KS per 4-wave block, written
-// through (sc1) for the attention blocks of the same launch, then signalled on cnt[4].
-struct QkvArgs {
-  const bf16_t* W; int ldw;    // [N][K] bf16 (packed q | k | v rows)
-  const bf16_t* h; int ldh;    // [M][K] residual rows (un-normalised)
-  const bf16_t* gamma;         // [K]
-  float eps;
-  float* P;                    // [K / KS][M][N] fp32
-  int M, N, K;
-  int nqb;                     // qkv blocks
-};
-
-template <int NLD, bool ST = false>
-__device__ __forceinline__ void qkv_norm_block(const QkvArgs& q, int qb, char* smem, int* cnt) {
-  fstamp<ST>(0);
-  constexpr int KS = 32 * NLD;
-  constexpr int ROWB = KS * 2;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int fr = lane & 15, fh = lane >> 4;
-  const int ncb = (q.N + 63) / 64;
-  const int cb = qb % ncb, s = qb / ncb;
-  const int n0 = cb * 64, kbase = s * KS;
-  const int M = q.M;
-  const int nvec = q.K >> 3;  // 16-B vectors per row (K <= 4096: two per thread)
-  // 1) row vectors + the slice's norm weights first (a counted wait retires them before the weights)
-  u32x4 hv[4][2], gv[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int vi = min(tid + 256 * i, nvec - 1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) hv[r][i] = *reinterpret_cast<const u32x4*>(q.h + (size_t)min(r, M - 1) * q.ldh + vi * 8);
-    gv[i] = *reinterpret_cast<const u32x4*>((q.gamma ? q.gamma : q.h) + min(max(vi * 8, kbase), kbase + KS - 8));
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  const int wrow = min(n0 + 16 * wid + fr, q.N - 1);
-  const bf16_t* wp = q.W + (size_t)wrow * q.ldw + kbase + 8 * fh;
-  bf16x8 wf[NLD];
-#pragma unroll
-  for (int ks = 0; ks < NLD; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
-  __builtin_amdgcn_s_waitcnt((NLD & 15) | (((NLD >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));  // vmcnt(NLD)
-  __builtin_amdgcn_sched_barrier(0);
-  // 2) RMSNorm statistics (rmsnorm_kernel's order), normalised slice -> LDS (swizzled as the O role's);
-  //    gamma == nullptr: the rows are already normalised (tensor-parallel decode), staged as they are
-  float* s_red = reinterpret_cast<float*>(smem + 16 * ROWB);  // [4 rows][4 waves]
-  if (q.gamma == nullptr) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (r >= M) break;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int vi = tid + 256 * i;
-        if (vi < nvec && vi * 8 >= kbase && vi * 8 < kbase + KS) {
-          const int c = vi - kbase / 8;
-          *reinterpret_cast<u32x4*>(smem + r * ROWB + 16 * ((c & ~15) | ((c & 15) ^ (r & 15)))) = hv[r][i];
-        }
-      }
-    }
-  }
-  float ss[4];
-  const u32x4 z = {0, 0, 0, 0};
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    ss[r] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const u32x4 v = tid + 256 * i < nvec ? hv[r][i] : z;
-      float f[8];
-      unpack8(v, f);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) ss[r] += f[e] * f[e];
-    }
-    ss[r] = wave_sum(ss[r]);
-    if (lane == 0) s_red[r * 4 + wid] = ss[r];
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    if (r >= M || q.gamma == nullptr) break;
-    const float t = ((s_red[r * 4] + s_red[r * 4 + 1]) + s_red[r * 4 + 2]) + s_red[r * 4 + 3];
-    const float inv = rsqrtf(t / (float)q.K + q.eps);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int vi = tid + 256 * i;
-      if (vi < nvec && vi * 8 >= kbase && vi * 8 < kbase + KS) {
-        float f[8], g[8], o[8];
-        unpack8(hv[r][i], f);
-        unpack8(gv[i], g);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = g[e] * bf2f(f2bf(f[e] * inv));
-        const int c = vi - kbase / 8;
-        *reinterpret_cast<u32x4*>(smem + r * ROWB + 16 * ((c & ~15) | ((c & 15) ^ (r & 15)))) = pack8(o);
-      }
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // raw: __syncthreads() would drain the weight loads (vmcnt(0))
-  __builtin_amdgcn_sched_barrier(0);
-  // 3) MFMA, write-through slab, signal
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < NLD; ++ks) {
-    const int chunk = 4 * ks + fh;
-    const bf16x8 xf = *reinterpret_cast<const bf16x8*>(smem + fr * ROWB + 16 * ((chunk & ~15) | ((chunk & 15) ^ (fr & 15))));
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[ks], acc, 0, 0, 0);
-  }
-  const int col = n0 + 16 * wid + fr;
-  const int nslab = q.K / KS;
-  const __amdgpu_buffer_rsrc_t rs_p =
-      __builtin_amdgcn_make_buffer_rsrc(q.P, (short)0, (int)((size_t)nslab * M * q.N * 4), 0x00020000);
-  if (fh == 0 && col < q.N) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (r < M)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[r]), rs_p, (int)((((size_t)s * M + r) * q.N + col) * 4),
-                                              0, 16);
-  }
-  fstamp<ST>(3);
-  stage_arrive(cnt + 4, q.nqb, cnt + FL_Q);
-  fstamp<ST>(5);
-}
-
-// o_proj block of the fused launch, v2 (MIA only): 16 output columns x the FULL K per block, the 4 waves
-// splitting K in quarters (NLQ 16-B weight loads per lane each, all in flight from the block's start), so
-// N / 16 blocks (256 at N = 4096) are resident next to the attention blocks from the first cycle and no
-// split-K slab exists: the block reduces its waves in LDS and finishes its columns itself --
-//   tail (o.h set): h[r][cols] = bf16(h + bf16(o_proj)) written through, per-row sum-of-squares partial
-//     to o.ss[r][block]; the last block (arrival ticket) sums the partials in block order and writes
-//     xn = rmsnorm(h) * gamma;
-//   no tail (tensor parallel): the fp32 partial row o.P[0][r][cols] for the cross-rank reduction.
-template <int D, int NLQ, bool ST = false>
-__device__ __forceinline__ void oproj_full_block(const DecodeArgs& a, const OprojArgs& o, int ob, char* smem) {
-  constexpr int KQ = 32 * NLQ;  // K quarter of one wave
-  constexpr int K = 4 * KQ;
-  constexpr int ROWB = K * 2;   // LDS bytes per activation row (4 rows: M <= 4)
-  fstamp<ST>(0);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int fr = lane & 15, fh = lane >> 4;
-  const int n0 = ob * 16;
-  const int M = o.M;
-  const int col = n0 + fr;
-  // 0) the residual values this block adds to (wave 0, rows 0..3 of column n0 + fr), requested first
-  float hres[4] = {0.f, 0.f, 0.f, 0.f};
-  if (o.h && wid == 0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) hres[r] = bf2f(o.h[(size_t)min(r, M - 1) * o.ldh + min(col, o.N - 1)]);
-  }
-  // 1) this wave's quarter of the block's 16 weight rows, every load in flight -- issued once every
-  //    attention block has its KV requests out (the weight stream then queues behind them instead of
-  //    delaying the attention's dependent loads)
-  if (o.na > 0) wait_flag(o.cnt + FL_P, o.cnt + 2, o.spin_limit);
-  const bf16_t* wp = o.W + (size_t)min(n0 + fr, o.N - 1) * o.ldw + wid * KQ + 8 * fh;
-  bf16x8 wf[NLQ];
-#pragma unroll
-  for (int ks = 0; ks < NLQ; ++ks) wf[ks] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wp + 32 * ks));
-  fstamp<ST>(1);
-  // 2) the attention blocks have merged every head into a.out
-  wait_flag(o.cnt + FL_A, o.cnt + 2, o.spin_limit);
-  fstamp<ST>(2);
-  // 3) the M attention rows -> LDS (write-through loads), 16-B chunk c of row r at slot c ^ (r & 15)
-  {
-    const __amdgpu_buffer_rsrc_t rs_x =
-        __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, M * a.out_stride * 2, 0x00020000);
-    constexpr int CPR = K / 8;
-    constexpr int PER = (4 * CPR + 255) / 256;
-    u32x4 xv[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int e = min(tid + 256 * i, M * CPR - 1);
-      xv[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, ((e / CPR) * a.out_stride + 8 * (e % CPR)) * 2, 0, 16));
-    }
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int e = tid + 256 * i;
-      if (e < M * CPR) {
-        const int r = e / CPR, c = e % CPR;
-        *reinterpret_cast<u32x4*>(smem + r * ROWB + 16 * ((c & ~15) | ((c & 15) ^ (r & 15)))) = xv[i];
-      }
-    }
-  }
-  __syncthreads();
-  fstamp<ST>(3);
-  // 4) MFMA over the wave's K quarter (activation rows >= M alias row fr & 3: their outputs are dropped)
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  const int xr = fr & 3;
-#pragma unroll
-  for (int ks = 0; ks < NLQ; ++ks) {
-    const int chunk = (wid * KQ) / 8 + 4 * ks + fh;
-    const bf16x8 xf = *reinterpret_cast<const bf16x8*>(smem + xr * ROWB + 16 * ((chunk & ~15) | ((chunk & 15) ^ xr)));
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf, wf[ks], acc, 0, 0, 0);
-  }
-  // 5) the 4 K quarters summed in wave order (LDS after the activation rows)
-  f32x4* red = reinterpret_cast<f32x4*>(smem + 4 * ROWB);
-  red[wid * 64 + lane] = acc;
-  __syncthreads();
-  int* s_last = reinterpret_cast<int*>(smem + 4 * ROWB + 4 * 64 * 16);
-  float* s_red = reinterpret_cast<float*>(s_last + 4);
-  const __amdgpu_buffer_rsrc_t rs_h =
-      __builtin_amdgcn_make_buffer_rsrc(o.h ? o.h : a.out, (short)0, o.h ? M * o.ldh * 2 : 0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_ss = __builtin_amdgcn_make_buffer_rsrc(o.ss, (short)0, o.ss ? 4 * o.nob * 4 : 0, 0x00020000);
-  if (wid == 0) {
-    f32x4 c = red[lane];
-#pragma unroll
-    for (int w = 1; w < 4; ++w) c += red[w * 64 + lane];
-    // lane (fr, fh): column n0 + fr, rows 4 fh + r -- rows 0..3 live in the fh == 0 lanes
-    if (!o.h) {
-      if (fh == 0 && col < o.N) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (r < M) o.P[(size_t)r * o.N + col] = c[r];
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = bf2f(f2bf(hres[r] + bf2f(f2bf(c[r]))));
-        const float vn = __shfl_xor(v, 1, 64);
-        float sq = fh == 0 && col < o.N ? v * v : 0.f;
-        if (r < M && fh == 0 && (fr & 1) == 0 && col < o.N)
-          __builtin_amdgcn_raw_buffer_store_b32(pk2bf(v, vn), rs_h, (r * o.ldh + col) * 2, 0, 16);
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) sq += __shfl_xor(sq, off, 64);
-        if (r < M && lane == 0)
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sq), rs_ss, (r * o.nob + ob) * 4, 0, 16);
-      }
-    }
-  }
-  fstamp<ST>(4);
-  // 6) arrival ticket; the last block re-arms the counters and finishes the norm
-  wait_vmcnt0();
-  __syncthreads();
-  if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(o.cnt + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == o.nob - 1;
-    if (last) {
-      __hip_atomic_store(o.cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(o.cnt + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(o.cnt + 4, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(o.cnt + 5, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-      for (int k = 0; k < FL_REPL; ++k) {
-        __hip_atomic_store(o.cnt + FL_A + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(o.cnt + FL_Q + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(o.cnt + FL_P + k * FL_STRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    *s_last = last;
-  }
-  __syncthreads();
-  if (!o.h || !*s_last) {
-    fstamp<ST>(5);
-    return;
-  }
-  // per row: sum of squares = the blocks' partials in block order (tree fixed by thread index), then
-  // xn = gamma * bf16(h * rsqrt(mean + eps)); h is re-read write-through (other blocks wrote it). The
-  // row's h vectors and gamma are requested together with the partials (one round trip per row, H <= 4096).
-  const int nvec = o.N >> 3;
-  for (int r = 0; r < M; ++r) {
-    u32x4 hv[2], gv[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int vi = min(tid + 256 * i, nvec - 1);
-      hv[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_h, (r * o.ldh + vi * 8) * 2, 0, 16));
-      gv[i] = *reinterpret_cast<const u32x4*>(o.gamma + vi * 8);
-    }
-    float ss = 0.f;
-    for (int b2 = tid; b2 < o.nob; b2 += 256)
-      ss += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ss, (r * o.nob + b2) * 4, 0, 16));
-    ss = block_sum(ss, s_red);
-    const float inv = rsqrtf(ss / (float)o.N + o.eps);
-    for (int vi = tid; vi < nvec; vi += 256) {
-      const int i = (vi - tid) / 256;
-      u32x4 hvv, gvv;
-      if (i < 2) {
-        hvv = i == 0 ? hv[0] : hv[1];
-        gvv = i == 0 ? gv[0] : gv[1];
-      } else {
-        hvv = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_h, (r * o.ldh + vi * 8) * 2, 0, 16));
-        gvv = *reinterpret_cast<const u32x4*>(o.gamma + vi * 8);
-      }
-      float hf[8], wv[8], out8[8];
-      unpack8(hvv, hf);
-      unpack8(gvv, wv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) out8[e] = wv[e] * bf2f(f2bf(hf[e] * inv));
-      *reinterpret_cast<u32x4*>(o.xn + (size_t)r * o.ldx + vi * 8) = pack8(out8);
-    }
-    __syncthreads();  // s_red reuse by the next row
-  }
-  fstamp<ST>(6);
-}
-
-template <int D, int G, int NLD>
-constexpr int attn_oproj_lds() {
-  constexpr int a = decode_lds_bytes<D, G>();
-  constexpr int o = 16 * 64 * NLD + (2 * 4 * (32 * NLD / D) * OP_MAXP + 4 * (32 * NLD / D) + 4) * 4;
-  return a > o ? a : o;
-}
-
-// QNLD > 0: the 3-role launch -- blocks [0, nqb) are qkv blocks (qkv_norm_block<QNLD>), then the
-// attention blocks (they prefetch their first KV tile, then wait for every qkv block), then the o_proj
-// blocks. Every wait is on lower-indexed blocks only.
-template <int D, int G, int NLD, int QNLD = 0, bool MIA = false, bool ST = false, bool OV2 = false>
-__global__ __launch_bounds__(256, 2) void attn_oproj_kernel(DecodeArgs a, OprojArgs o, QkvArgs q) {
-  constexpr int lds_q = QNLD > 0 ? 16 * 64 * QNLD + 64 : 0;
-  constexpr int lds_o = OV2 ? 4 * 4 * 32 * NLD * 2 + 4 * 64 * 16 + 64 : attn_oproj_lds<D, G, NLD>();
-  constexpr int lds_a = decode_lds_bytes<D, G>();
-  constexpr int lds_ao = lds_o > lds_a ? lds_o : lds_a;
-  constexpr int lds = lds_ao > lds_q ? lds_ao : lds_q;
-  __shared__ __attribute__((aligned(16))) char smem[lds];
-  int bid = blockIdx.x;
-  if constexpr (QNLD > 0) {
-    if (bid < q.nqb) {
-      qkv_norm_block<QNLD, ST>(q, bid, smem, o.cnt);
-      return;
-    }
-    bid -= q.nqb;
-  }
-  if (bid < o.na) {
-    const int mp = a.max_parts;
-    attn_decode_block<D, G, false, true, (QNLD > 0), MIA, ST>(a, bid % mp, (bid / mp) % a.Hkv, bid / (mp * a.Hkv),
-                                                              smem, o.cnt, QWait{o.cnt + FL_Q, o.cnt + 2, o.spin_limit},
-                                                              o.na);
-    return;
-  }
-  if constexpr (OV2)
-    oproj_full_block<D, NLD, ST>(a, o, bid - o.na, smem);
-  else
-    oproj_merge_block<D, NLD, MIA, ST>(a, o, bid - o.na, smem);
+  attn_decode_block<D, G, NT, NW>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 // merge split-K partitions: grid (Hq, B), block D threads. The partition statistics are loaded by
@@ -2497,59 +1221,29 @@ __global__ void attn_decode_reduce_kernel(DecodeArgs a, int D) {
   a.out[(size_t)b * a.out_stride + hq * D + t] = f2bf(L > 0.f ? O / L : 0.f);
 }
 
-// Waves per block when 4 query heads share a KV head (Llama GQA): 8 = two 32-row groups share each
-// K/V tile (half the DMA issue and K/V traffic per wave).
-int g_prefill_waves = 4;
-int g_prefill_prio = 1;  // PRIO variant of the Llama config (D 128, 4 heads per block, causal, paged)
-int g_prefill_buf = 1;   // BUF staging for that config when the cache is < 4 GiB
-// Ping-pong 8-wave kernel for the Llama config (0 off, 1 on, 2 on + static priority for waves 4-7);
-// when on, every 4-heads-per-block config uses 64-query tiles (the 8-wave kernel where the cache
-// is too large for buffer staging).
-int g_prefill_pp = 0;
-
-// Block order (prefill_block): 1 = 1-D grid, head group fastest (default); 0 = 2-D (tile, head group).
-int g_prefill_order = 1;
-
+// Block order (prefill_block): a 1-D grid, head group fastest, so the heaviest causal tiles of every head
+// start first and consecutive blocks (round-robin over the XCDs) put one KV head on each XCD.
+// Kernel per config:
+//   * Llama (D 128, 4 query heads per KV head, causal, paged cache < 4 GiB): the software-pipelined
+//     8-wave kernel with the whole-row LDS epilogue (attn_prefill_v3_kernel<8, ..., WIDE>; 64-query
+//     tiles), tools/attn_pp_ab.py;
+//   * every other 4-heads-per-block config: attn_prefill_kernel with 8 waves (64-query tiles, two 32-row
+//     groups sharing each K/V tile);
+//   * 1 or 2 heads per block (encoders, GPT-2, odd GQA ratios): the 4-wave attn_prefill_kernel.
 template <int D, int GB, bool CAUSAL, bool PAGED>
 hipError_t launch_prefill(PrefillArgs a, int n_tiles, hipStream_t st) {
   const int G = a.Hq / a.Hkv;
   const int n_hg = a.Hkv * (G / GB);
-  a.n_hg = g_prefill_order ? n_hg : 0;
-  const dim3 grid = a.n_hg ? dim3(n_tiles * n_hg) : dim3(n_tiles, n_hg);
+  a.n_hg = n_hg;
+  const dim3 grid(n_tiles * n_hg);
   if constexpr (D == 128 && GB == 4 && CAUSAL && PAGED) {
-    if (g_prefill_pp && a.kv_bytes) {
-      switch (g_prefill_pp) {
-        case 1: hipLaunchKernelGGL((attn_prefill_pp_kernel<0, 2>), grid, dim3(512), 0, st, a); break;
-        case 2: hipLaunchKernelGGL((attn_prefill_pp_kernel<1, 2>), grid, dim3(512), 0, st, a); break;
-        case 3: hipLaunchKernelGGL((attn_prefill_pp_kernel<1, 4>), grid, dim3(512), 0, st, a); break;
-        case 4: hipLaunchKernelGGL((attn_prefill_pp_kernel<1, 8>), grid, dim3(512), 0, st, a); break;
-        case 5: hipLaunchKernelGGL((attn_prefill_pp_kernel<1, 8, true>), grid, dim3(512), 0, st, a); break;
-        case 6: hipLaunchKernelGGL((attn_prefill_v3_kernel<4>), grid, dim3(256), 0, st, a); break;
-        case 7: hipLaunchKernelGGL((attn_prefill_v3_kernel<4, true>), grid, dim3(256), 0, st, a); break;
-        case 8: hipLaunchKernelGGL((attn_prefill_v3_kernel<4, true, 1>), grid, dim3(256), 0, st, a); break;
-        case 9: hipLaunchKernelGGL((attn_prefill_v3_kernel<4, true, 2>), grid, dim3(256), 0, st, a); break;
-        case 10: hipLaunchKernelGGL((attn_prefill_v3_kernel<8>), grid, dim3(512), 0, st, a); break;
-        case 11: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true>), grid, dim3(512), 0, st, a); break;
-        case 12: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true, 1>), grid, dim3(512), 0, st, a); break;
-        case 14: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, false, 0, 1>), grid, dim3(512), 0, st, a); break;
-        case 15: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, false, 0, 0, true>), grid, dim3(512), 0, st, a); break;
-        case 16: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, false, 0, 1, true>), grid, dim3(512), 0, st, a); break;
-        case 13: hipLaunchKernelGGL((attn_prefill_v3_kernel<8, true, 2>), grid, dim3(512), 0, st, a); break;
-        default: hipLaunchKernelGGL((attn_prefill_v3_kernel<8>), grid, dim3(512), 0, st, a); break;
-      }
-      return hipGetLastError();
-    }
-    if (!g_prefill_pp && g_prefill_waves == 4 && g_prefill_prio == 1 && g_prefill_buf && a.kv_bytes) {
-      hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 4, 1, true>), grid, dim3(256), 0, st, a);
+    if (a.kv_bytes) {
+      hipLaunchKernelGGL((attn_prefill_v3_kernel<8, false, 0, 0, true>), grid, dim3(512), 0, st, a);
       return hipGetLastError();
     }
   }
-  if (GB == 4 && (g_prefill_waves == 8 || (g_prefill_pp >= 1 && g_prefill_pp <= 5) || g_prefill_pp >= 10))
+  if constexpr (GB == 4)
     hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 8>), grid, dim3(512), 0, st, a);
-  else if (D == 128 && GB == 4 && CAUSAL && PAGED && g_prefill_prio == 1)
-    hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 4, 1>), grid, dim3(256), 0, st, a);
-  else if (D == 128 && GB == 4 && CAUSAL && PAGED && g_prefill_prio == 2)
-    hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED, false, 4, 2>), grid, dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((attn_prefill_kernel<D, GB, CAUSAL, PAGED>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
@@ -2557,59 +1251,11 @@ hipError_t launch_prefill(PrefillArgs a, int n_tiles, hipStream_t st) {
 
 }  // namespace
 
-// Stamp build of the Llama prefill config (D 128, 4 heads per block, causal, paged): per wave
-// [DMA issue, QK^T, softmax, PV, wait+barrier, tiles] s_memtime sums into dbg[grid][4 waves][6].
-RAGK_API int ragk_attn_prefill_stamp(const void* q, int q_stride, const void* k, const void* v,
-                                     const int* block_tables, int bt_stride, const int* cu_q, const int* kv_lens,
-                                     const int* tiles, int n_tiles, void* out, int out_stride, int Hq, int Hkv,
-                                     float scale, unsigned long long* dbg, hipStream_t st) {
-  if (n_tiles <= 0 || Hq % Hkv || (Hq / Hkv) % 4) return (int)hipErrorInvalidValue;
-  hipMemcpyToSymbolAsync(HIP_SYMBOL(g_attn_dbg), &dbg, sizeof(dbg), 0, hipMemcpyHostToDevice, st);
-  PrefillArgs a{(const bf16_t*)q, q_stride, (const bf16_t*)k, (const bf16_t*)v, 0, block_tables, bt_stride,
-                cu_q, nullptr, kv_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, scale * 1.4426950408889634f};
-  const int G = Hq / Hkv;
-  dim3 grid(n_tiles, Hkv * (G / 4));
-  hipLaunchKernelGGL((attn_prefill_kernel<128, 4, true, true, true>), grid, dim3(256), 0, st, a);
-  return (int)hipGetLastError();
-}
-
-RAGK_API int ragk_attn_set_dbg(unsigned long long* dbg) {
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_dbg), &dbg, sizeof(dbg), 0, hipMemcpyHostToDevice);
-}
-
-RAGK_API int ragk_attn_prefill_set_prio(int v) {
-  if (v < 0 || v > 2) return (int)hipErrorInvalidValue;
-  g_prefill_prio = v;
-  return 0;
-}
-
-RAGK_API int ragk_attn_prefill_set_buf(int v) {
-  g_prefill_buf = v ? 1 : 0;
-  return 0;
-}
-
-// Returns the query positions per block (the host builds `tiles` with this step).
-RAGK_API int ragk_attn_prefill_set_waves(int w) {
-  if (w != 4 && w != 8) return (int)hipErrorInvalidValue;
-  g_prefill_waves = w;
-  return 0;
-}
-
-// (every GB == 4 config follows g_prefill_waves; the host builds tiles with this value)
+// Query rows per block (the host builds `tiles` with this step): 64 for 4 heads per block, else 128 / GB.
 RAGK_API int ragk_attn_prefill_qtile(int Hq, int Hkv) {
   const int G = Hq / Hkv;
   const int GB = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
-  const bool pp64 = (g_prefill_pp >= 1 && g_prefill_pp <= 5) || g_prefill_pp >= 10;
-  return 32 * ((GB == 4 ? (pp64 ? 8 : g_prefill_waves) : 4) / GB);
-}
-
-// 0 off; 1..4 variants (1: fragment prefetch 2 steps; 2: + priority for waves 4-7; 3 / 4: + prefetch
-// 4 / 8 steps); 5: the stamp build of variant 4 (g_attn_dbg set by ragk_attn_set_dbg); 6: the
-// software-pipelined one-wave-per-SIMD kernel (attn_prefill_v3_kernel, 32-query tiles); 7: its stamps
-RAGK_API int ragk_attn_prefill_set_pp(int v) {
-  if (v < 0 || v > 16) return (int)hipErrorInvalidValue;
-  g_prefill_pp = v;
-  return 0;
+  return 32 * ((GB == 4 ? 8 : 4) / GB);
 }
 
 RAGK_API int ragk_attn_prefill(const void* q, int q_stride, const void* k, const void* v, int kv_stride,
@@ -2642,10 +1288,6 @@ RAGK_API int ragk_attn_prefill(const void* q, int q_stride, const void* k, const
   return (int)hipErrorInvalidValue;
 }
 
-RAGK_API int ragk_attn_prefill_set_order(int order) {
-  g_prefill_order = order ? 1 : 0;
-  return 0;
-}
 
 // K/V cache-policy switch for decode (0 = default, 1 = non-temporal loads; the KV stream is read
 // once per step). A/B in tools/bench_kernels.py --quick.
@@ -2661,7 +1303,7 @@ RAGK_API int ragk_attn_decode_set_nt(int nt) {
   return 0;
 }
 
-static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* counters, hipStream_t st);
+static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, hipStream_t st);
 
 // Deferred merge: the next decode-attention launches leave the split-K partitions unmerged (no
 // attn_decode_reduce launch) for a consumer that merges them itself (gemm_part.hip MergeArgs: the
@@ -2675,15 +1317,13 @@ RAGK_API int ragk_attn_decode_set_defer(int on) {
 RAGK_API int ragk_attn_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                               int bt_stride, const int* kv_lens, float* part_o, float* part_ml, void* out,
                               int out_stride, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
-                              float scale, int* counters, hipStream_t st) {
+                              float scale, hipStream_t st) {
   if (B <= 0) return 0;
   if (Hq % Hkv || part_tiles < 1 || max_parts < 1 || max_parts > RED_MAXP) return (int)hipErrorInvalidValue;
-  // fused merge: LDS holds 2 x G x max_parts + G floats of partition statistics (< the 64 KiB V tiles)
-  if (counters && 2 * (Hq / Hkv) * max_parts + 16 > 4 * KT * D * 2 / 4) return (int)hipErrorInvalidValue;
   DecodeArgs a{(const bf16_t*)q, q_stride, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, bt_stride, kv_lens,
                part_o, part_ml, (bf16_t*)out, out_stride, Hq, Hkv, part_tiles, max_parts,
-               scale * 1.4426950408889634f, counters};
-  return launch_attn_decode(a, B, D, max_parts, counters, st);
+               scale * 1.4426950408889634f};
+  return launch_attn_decode(a, B, D, max_parts, st);
 }
 
 // Decode attention fed by the qkv projection's split-K partial slabs P[S][B][ldp] (gemm_part.hip):
@@ -2693,39 +1333,36 @@ RAGK_API int ragk_attn_decode_rope(const float* P, int S, int ldp, const int* po
                                    const float* cos_t, const float* sin_t, void* kc, void* vc,
                                    const int* block_tables, int bt_stride, const int* kv_lens, float* part_o,
                                    float* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D,
-                                   int part_tiles, int max_parts, float scale, int* counters, hipStream_t st) {
+                                   int part_tiles, int max_parts, float scale, hipStream_t st) {
   if (B <= 0) return 0;
   if (Hq % Hkv || part_tiles < 1 || max_parts < 1 || max_parts > RED_MAXP || S < 1 || D % 64 ||
       ldp < (Hq + 2 * Hkv) * D || !P || !positions || !slots || !cos_t || !sin_t)
     return (int)hipErrorInvalidValue;
-  if (counters && 2 * (Hq / Hkv) * max_parts + 16 > 4 * KT * D * 2 / 4) return (int)hipErrorInvalidValue;
   DecodeArgs a{nullptr, 0, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, bt_stride, kv_lens,
                part_o, part_ml, (bf16_t*)out, out_stride, Hq, Hkv, part_tiles, max_parts,
-               scale * 1.4426950408889634f, counters, P, (long long)B * ldp, ldp, S, positions, slots, cos_t, sin_t};
-  return launch_attn_decode(a, B, D, max_parts, counters, st);
+               scale * 1.4426950408889634f, P, (long long)B * ldp, ldp, S, positions, slots, cos_t, sin_t};
+  return launch_attn_decode(a, B, D, max_parts, st);
 }
 
-static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* counters, hipStream_t st) {
+static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, hipStream_t st) {
   const int Hq = a.Hq, Hkv = a.Hkv;
   const int G = Hq / Hkv;
-  const PfArgs pf = pf_take();
-  const int ex = (pf.blocks + Hkv * B - 1) / (Hkv * B);  // rider columns (x beyond max_parts)
-  dim3 grid(max_parts + ex, Hkv, B);
-  if (D == 128 && G == 4 && max_parts == 1 && !counters && g_decode_nw8_min > 0 && B * Hkv >= g_decode_nw8_min) {
+  dim3 grid(max_parts, Hkv, B);
+  if (D == 128 && G == 4 && max_parts == 1 && g_decode_nw8_min > 0 && B * Hkv >= g_decode_nw8_min) {
     // one partition per sequence over >= 1 block per CU: 8-wave blocks, no merge launch
     if (g_decode_nt)
-      hipLaunchKernelGGL((attn_decode_kernel<128, 4, true, 8>), grid, dim3(512), 0, st, a, pf);
+      hipLaunchKernelGGL((attn_decode_kernel<128, 4, true, 8>), grid, dim3(512), 0, st, a);
     else
-      hipLaunchKernelGGL((attn_decode_kernel<128, 4, false, 8>), grid, dim3(512), 0, st, a, pf);
+      hipLaunchKernelGGL((attn_decode_kernel<128, 4, false, 8>), grid, dim3(512), 0, st, a);
     return (int)hipGetLastError();
   }
 #define RAGK_DC(DD, GG)                                                            \
   if (D == DD && G == GG) {                                                          \
     if (g_decode_nt)                                                                 \
-      hipLaunchKernelGGL((attn_decode_kernel<DD, GG, true>), grid, dim3(256), 0, st, a, pf); \
+      hipLaunchKernelGGL((attn_decode_kernel<DD, GG, true>), grid, dim3(256), 0, st, a); \
     else                                                                             \
-      hipLaunchKernelGGL((attn_decode_kernel<DD, GG, false>), grid, dim3(256), 0, st, a, pf); \
-    if (max_parts > 1 && !counters && !g_decode_defer)                               \
+      hipLaunchKernelGGL((attn_decode_kernel<DD, GG, false>), grid, dim3(256), 0, st, a); \
+    if (max_parts > 1 && !g_decode_defer)                                            \
       hipLaunchKernelGGL(attn_decode_reduce_kernel, dim3(Hq, B), dim3(DD), 0, st, a, DD); \
     return (int)hipGetLastError();                                                   \
   }
@@ -2739,182 +1376,3 @@ static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, int* co
   return (int)hipErrorInvalidValue;
 }
 
-// Diagnostic: the next fused launches (G = 4, ks_steps 8, MIA, q_ks 16 or none) run the stamp build,
-// writing 8 s_memrealtime stamps per block into `stamps` (u64 [grid][8]); nullptr = production build.
-static unsigned long long* g_fused_stamps_host = nullptr;
-// v2 o_proj role (oproj_full_block): 16-column full-K blocks, no split-K slabs (MIA launches only)
-static int g_ao_v2 = 1;
-RAGK_API int ragk_attn_oproj_set_v2(int on) {
-  g_ao_v2 = on ? 1 : 0;
-  return 0;
-}
-
-// Fused decode attention (RoPE + KV append from the qkv split-K slabs, as ragk_attn_decode_rope) and
-// o_proj split-K partials (as ragk_gemm_part_merge) in ONE launch: attn_oproj_kernel. B <= 4, D = 128,
-// G in {4, 8}; Wo bf16 [N][Hq * D] (ldw elements); Pout fp32 [K / KS][B][N], KS = 64 * ks_steps
-// (ks_steps 4, 8 or 16). cnt: ragk_attn_oproj_cnt_ints() zeroed ints owned by the caller (re-armed by
-// the kernel itself).
-// h != nullptr: the residual + RMSNorm tail (h += bf16(sum of slabs), xn = rmsnorm(h) * gamma; the
-// add_partials_rmsnorm consumer) runs in the last o_proj block.
-// part_o / part_ml: the partition workspace (required, also for one partition).
-RAGK_API int ragk_attn_oproj_fused(const float* P, int S, int ldp, const int* positions, const int* slots,
-                                   const float* cos_t, const float* sin_t, void* kc, void* vc,
-                                   const int* block_tables, int bt_stride, const int* kv_lens, float* part_o,
-                                   float* part_ml, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
-                                   float scale, const void* Wo, int ldw, float* Pout, int N, int ks_steps, int* cnt,
-                                   unsigned spin_us, void* h, int ldh, const void* gamma, void* xn, int ldx,
-                                   float eps, void* attn_out, hipStream_t st) {
-  if (B <= 0) return 0;
-  const int G = Hq / (Hkv > 0 ? Hkv : 1);
-  const int K = Hq * D;
-  const int KS = 64 * ks_steps;
-  if (B > 4 || D != 128 || Hq % Hkv || (G != 4 && G != 8) || (ks_steps != 4 && ks_steps != 8 && ks_steps != 16) || K % KS ||
-      part_tiles < 1 || max_parts < 1 || max_parts > OP_MAXP || S < 1 || ldp < (Hq + 2 * Hkv) * D || !P ||
-      !positions || !slots || !cos_t || !sin_t || !part_o || !part_ml || !Wo || !Pout || !cnt || N <= 0 ||
-      ldw < K)
-    return (int)hipErrorInvalidValue;
-  // norm tail: the last o_proj block sums <= 16 slabs per row vector (h, gamma, xn: bf16, 16-B rows)
-  if (h && (!gamma || !xn || K / KS > 16 || N % 8 || ldh % 8 || ldx % 8 || ((uintptr_t)h & 15) ||
-            ((uintptr_t)xn & 15) || ((uintptr_t)gamma & 15)))
-    return (int)hipErrorInvalidValue;
-  DecodeArgs a{nullptr, 0, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, bt_stride, kv_lens,
-               part_o, part_ml, nullptr, 0, Hq, Hkv, part_tiles, max_parts,
-               scale * 1.4426950408889634f, nullptr, P, (long long)B * ldp, ldp, S, positions, slots, cos_t, sin_t, B};
-  const unsigned long long ticks = (unsigned long long)(spin_us ? spin_us : 1000000u) * 100ull;
-  OprojArgs o{(const bf16_t*)Wo, ldw, Pout, B, N, K, max_parts * Hkv * B, ((N + 63) / 64) * (K / KS), cnt,
-              (unsigned)(ticks > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : ticks), (bf16_t*)h, ldh, (const bf16_t*)gamma,
-              (bf16_t*)xn, ldx, eps};
-  const dim3 grid(o.na + o.nob);
-  const QkvArgs q{};
-  const bool mia = attn_out != nullptr;  // partitions merged by the attention blocks into attn_out
-  if (mia) {
-    a.out = (bf16_t*)attn_out;
-    a.out_stride = K;
-    a.counters = cnt + CNT_TICKETS;
-    if (B * Hkv > 4 * 64) return (int)hipErrorInvalidValue;
-  }
-  const int nlq = K / 128;  // v2: 16-B loads per lane of one wave's K quarter
-  if (mia && g_ao_v2 && (nlq == 4 || nlq == 8 || nlq == 16 || nlq == 32) && (N + 15) / 16 <= 512) {
-    o.nob = (N + 15) / 16;
-    o.ss = reinterpret_cast<float*>(cnt + CNT_SS);
-    const dim3 grid2(o.na + o.nob);
-    if (g_fused_stamps_host && G == 4 && nlq == 32) {
-      hipLaunchKernelGGL((attn_oproj_kernel<128, 4, 32, 0, true, true, true>), grid2, dim3(256), 0, st, a, o, q);
-      return (int)hipGetLastError();
-    }
-#define RAGK_AO2(GG, NQ)                                                                                 \
-    if (G == GG && nlq == NQ) {                                                                          \
-      hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NQ, 0, true, false, true>), grid2, dim3(256), 0, st, a, o, q); \
-      return (int)hipGetLastError();                                                                     \
-    }
-    RAGK_AO2(4, 4) RAGK_AO2(4, 8) RAGK_AO2(4, 16) RAGK_AO2(4, 32)
-    RAGK_AO2(8, 4) RAGK_AO2(8, 8) RAGK_AO2(8, 16) RAGK_AO2(8, 32)
-#undef RAGK_AO2
-  }
-  if (g_fused_stamps_host && mia && G == 4 && ks_steps == 8) {
-    hipLaunchKernelGGL((attn_oproj_kernel<128, 4, 16, 0, true, true>), grid, dim3(256), 0, st, a, o, q);
-    return (int)hipGetLastError();
-  }
-#define RAGK_AO(GG, NL)                                                                                \
-  if (G == GG && 2 * ks_steps == NL) {                                                                 \
-    if (mia) hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL, 0, true>), grid, dim3(256), 0, st, a, o, q); \
-    else hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL>), grid, dim3(256), 0, st, a, o, q);         \
-    return (int)hipGetLastError();                                                                     \
-  }
-  RAGK_AO(4, 8)
-  RAGK_AO(4, 16)
-  RAGK_AO(4, 32)
-  RAGK_AO(8, 8)
-  RAGK_AO(8, 16)
-  RAGK_AO(8, 32)
-#undef RAGK_AO
-  return (int)hipErrorInvalidValue;
-}
-
-// The 3-role launch: the qkv projection with the input RMSNorm (gemm_part_norm's math) as well --
-// qkv + attention + o_proj (+ the residual / post-attention norm tail) in ONE launch per layer.
-// h [B][ldh] bf16 is the layer input (un-normalised residual), gin its norm weight, Wqkv [Nq][K] bf16
-// (K = 4096), Pq the qkv slab workspace [K / (64 q_ks)][B][Nq] fp32 (q_ks 8 or 16). gin == nullptr: h is
-// already normalised (tensor-parallel decode: the output of the fused cross-rank reduction). The
-// post-attention tail (h2 != nullptr) updates h2 (the same residual buffer) in place and writes xn;
-// without it the o_proj slabs Pout go to the caller's consumer (the cross-rank reduction under TP).
-RAGK_API int ragk_qkv_attn_oproj_fused(const void* h, int ldh, const void* gin, float eps_in, const void* Wqkv,
-                                       int ldwq, int Nq, int K, float* Pq, int q_ks, const int* positions,
-                                       const int* slots, const float* cos_t, const float* sin_t, void* kc, void* vc,
-                                       const int* block_tables, int bt_stride, const int* kv_lens, float* part_o,
-                                       float* part_ml, int B, int Hq, int Hkv, int D, int part_tiles, int max_parts,
-                                       float scale, const void* Wo, int ldw, float* Pout, int N, int ks_steps,
-                                       int* cnt, unsigned spin_us, void* h2, int ldh2, const void* gamma, void* xn,
-                                       int ldx, float eps, void* attn_out, hipStream_t st) {
-  if (B <= 0) return 0;
-  const int G = Hq / (Hkv > 0 ? Hkv : 1);
-  const int Ko = Hq * D;
-  const int KS = 64 * ks_steps, QKS = 64 * q_ks;
-  if (B > 4 || D != 128 || Hq % Hkv || (G != 4 && G != 8) || (ks_steps != 4 && ks_steps != 8 && ks_steps != 16) ||
-      Ko % KS || (q_ks != 8 && q_ks != 16) || K > 4096 || K % QKS || Nq != (Hq + 2 * Hkv) * D || ldwq < K ||
-      ldh % 8 || ((uintptr_t)h & 15) || ((uintptr_t)gin & 15) || part_tiles < 1 || max_parts < 1 ||
-      max_parts > OP_MAXP || !h || !Wqkv || !Pq || !positions || !slots || !cos_t || !sin_t || !part_o ||
-      !part_ml || !Wo || !Pout || !cnt || N <= 0 || ldw < Ko)
-    return (int)hipErrorInvalidValue;
-  if (h2 && (!gamma || !xn || Ko / KS > 16 || N % 8 || ldh2 % 8 || ldx % 8 || ((uintptr_t)h2 & 15) ||
-             ((uintptr_t)xn & 15) || ((uintptr_t)gamma & 15)))
-    return (int)hipErrorInvalidValue;
-  const int S = K / QKS;
-  DecodeArgs a{nullptr, 0, (const bf16_t*)kc, (const bf16_t*)vc, block_tables, bt_stride, kv_lens,
-               part_o, part_ml, nullptr, 0, Hq, Hkv, part_tiles, max_parts,
-               scale * 1.4426950408889634f, nullptr, Pq, (long long)B * Nq, Nq, S, positions, slots, cos_t, sin_t, B};
-  const unsigned long long ticks = (unsigned long long)(spin_us ? spin_us : 1000000u) * 100ull;
-  OprojArgs o{(const bf16_t*)Wo, ldw, Pout, B, N, Ko, max_parts * Hkv * B, ((N + 63) / 64) * (Ko / KS), cnt,
-              (unsigned)(ticks > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : ticks), (bf16_t*)h2, ldh2, (const bf16_t*)gamma,
-              (bf16_t*)xn, ldx, eps};
-  const QkvArgs q{(const bf16_t*)Wqkv, ldwq, (const bf16_t*)h, ldh, (const bf16_t*)gin, eps_in, Pq, B, Nq, K,
-                  ((Nq + 63) / 64) * S};
-  const dim3 grid(q.nqb + o.na + o.nob);
-  const bool mia = attn_out != nullptr;
-  if (mia) {
-    a.out = (bf16_t*)attn_out;
-    a.out_stride = Ko;
-    a.counters = cnt + CNT_TICKETS;
-    if (B * Hkv > 4 * 64) return (int)hipErrorInvalidValue;
-  }
-  const int nlq = Ko / 128;
-  if (mia && g_ao_v2 && (nlq == 4 || nlq == 8 || nlq == 16 || nlq == 32) && (N + 15) / 16 <= 512) {
-    o.nob = (N + 15) / 16;
-    o.ss = reinterpret_cast<float*>(cnt + CNT_SS);
-    const dim3 grid2(q.nqb + o.na + o.nob);
-    if (g_fused_stamps_host && G == 4 && nlq == 32 && q_ks == 16) {
-      hipLaunchKernelGGL((attn_oproj_kernel<128, 4, 32, 32, true, true, true>), grid2, dim3(256), 0, st, a, o, q);
-      return (int)hipGetLastError();
-    }
-#define RAGK_QAO2(GG, NQ, QN)                                                                                \
-    if (G == GG && nlq == NQ && 2 * q_ks == QN) {                                                          \
-      hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NQ, QN, true, false, true>), grid2, dim3(256), 0, st, a, o, q); \
-      return (int)hipGetLastError();                                                                       \
-    }
-    RAGK_QAO2(4, 32, 16) RAGK_QAO2(4, 32, 32) RAGK_QAO2(4, 4, 32) RAGK_QAO2(8, 32, 32) RAGK_QAO2(8, 8, 32)
-#undef RAGK_QAO2
-  }
-  if (g_fused_stamps_host && mia && G == 4 && ks_steps == 8 && q_ks == 16) {
-    hipLaunchKernelGGL((attn_oproj_kernel<128, 4, 16, 32, true, true>), grid, dim3(256), 0, st, a, o, q);
-    return (int)hipGetLastError();
-  }
-#define RAGK_QAO(GG, NL, QN)                                                                                 \
-  if (G == GG && 2 * ks_steps == NL && 2 * q_ks == QN) {                                                     \
-    if (mia) hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL, QN, true>), grid, dim3(256), 0, st, a, o, q); \
-    else hipLaunchKernelGGL((attn_oproj_kernel<128, GG, NL, QN>), grid, dim3(256), 0, st, a, o, q);          \
-    return (int)hipGetLastError();                                                                           \
-  }
-  RAGK_QAO(4, 16, 16)
-  RAGK_QAO(4, 16, 32)
-  RAGK_QAO(8, 16, 16)
-  RAGK_QAO(8, 16, 32)
-#undef RAGK_QAO
-  return (int)hipErrorInvalidValue;
-}
-
-RAGK_API int ragk_attn_oproj_cnt_ints() { return CNT_INTS; }
-
-RAGK_API int ragk_fused_set_stamps(unsigned long long* stamps, hipStream_t st) {
-  g_fused_stamps_host = stamps;
-  return (int)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_fused_stamps), &stamps, sizeof(stamps), 0, hipMemcpyHostToDevice, st);
-}

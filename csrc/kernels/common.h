@@ -251,54 +251,6 @@ __device__ __forceinline__ void blds16(i32x4 srd, int voff, int soff, void* lds_
   ragk_raw_buffer_load_lds(srd, (__attribute__((address_space(3))) unsigned*)lds_wave_base, 16, voff, soff, 0, 0);
 }
 
-// ---- MALL prefetch riders (rationale: prefetch.hip). A latency-bound decode kernel (rope/KV write,
-// split-K attention at small batch, residual+norm consumers) leaves HBM nearly idle; extra "rider"
-// blocks appended to its grid read up to two byte ranges of the weights the NEXT GEMMs stream, once,
-// with the allocating cache policy, so those GEMMs find them in the MALL. Armed per launch from the
-// host (ragk_pf_arm): the next rider-capable launch on this thread takes the armed ranges.
-struct PfArgs {
-  const u32x4* p0 = nullptr;
-  long long n0 = 0;  // 16-B units
-  const u32x4* p1 = nullptr;
-  long long n1 = 0;
-  unsigned* sink = nullptr;
-  int blocks = 0;    // rider blocks (0 = none)
-};
-
-inline PfArgs& pf_slot() {
-  static thread_local PfArgs s;
-  return s;
-}
-// host: the armed ranges for this launch (cleared)
-inline PfArgs pf_take() {
-  PfArgs a = pf_slot();
-  pf_slot() = PfArgs();
-  if (!a.sink || a.n0 + a.n1 <= 0) a.blocks = 0;
-  return a;
-}
-
-// device: rider r of nr streams its share of [p0, p0 + n0) ++ [p1, p1 + n1), 8 independent 16-B loads
-// per lane in flight; the XOR of the data is stored only when it equals a runtime key (keeps the loads
-// live; a hit is a harmless write to the sink). Vector loads and stores only.
-__device__ __forceinline__ void pf_rider(const PfArgs& a, int r, int nr) {
-  const long long tot = a.n0 + a.n1;
-  const long long per = (tot + nr - 1) / nr;
-  const long long b0 = (long long)r * per;
-  const long long b1 = b0 + per < tot ? b0 + per : tot;
-  const int nt = blockDim.x;
-  unsigned acc = 0;
-  for (long long i = b0 + threadIdx.x; i < b1; i += (long long)nt * 8) {
-    u32x4 v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const long long k = i + (long long)j * nt;
-      v[j] = k < b1 ? (k < a.n0 ? a.p0[k] : a.p1[k - a.n0]) : (u32x4){0u, 0u, 0u, 0u};
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc ^= v[j][0] ^ v[j][3];
-  }
-  if (acc == (unsigned)(a.n0 ^ 0x9e3779b9u)) a.sink[r & 4095] = acc;
-}
 
 
 // ---- lane-level bitonic networks over (value, id) pairs held one per lane of a wave (ascending by

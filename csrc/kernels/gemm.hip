@@ -202,13 +202,14 @@ __global__ __launch_bounds__(TILE_THREADS, 2) void gemm_tile_kernel(
 // ------------------------------------------------------------------------------------
 constexpr int SK_WAVES = 8;
 
-// WV waves per block (default 8; 16 is an A/B option for long-K / few-column shapes such as the
-// batch-1 down projection -- measured slower there: more waves per block lengthen the LDS reduction
-// and the per-block tail more than the extra loads in flight gain).
-template <int MT, int EPI, bool OUT_F32, int WV = SK_WAVES, int UN = 2, bool NTW = false>
-__global__ __launch_bounds__(WV * 64) void gemm_skinny_kernel(
+// (16 waves per block measured slower on the batch-1 down projection: more waves lengthen the LDS
+// reduction and the per-block tail more than the extra loads in flight gain; two K blocks in flight per
+// wave and non-temporal weight loads were slower at C=1 too -- profiles/c1_skinny_*_ab_r4.log.)
+template <int MT, int EPI, bool OUT_F32>
+__global__ __launch_bounds__(SK_WAVES * 64) void gemm_skinny_kernel(
     const bf16_t* __restrict__ X, int ldx, const bf16_t* __restrict__ W, int ldw, void* C, int ldc,
     const bf16_t* __restrict__ bias, const bf16_t* resid, int ldr, int M, int N, int K) {
+  constexpr int WV = SK_WAVES;
   constexpr bool PAIR = (EPI == EPI_SILU_MUL);
   constexpr int NACC = PAIR ? 2 : 1;
   __shared__ __attribute__((aligned(16))) f32x4 red[WV][NACC * MT][64];
@@ -245,10 +246,7 @@ __global__ __launch_bounds__(WV * 64) void gemm_skinny_kernel(
 
   const int nkb = K >> 7;  // 128-deep K blocks
   const bf16x8 zero = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
-  // two of the wave's K blocks per iteration, both blocks' weight loads issued before any use (a wave
-  // with one block's 4 loads in flight kept the 256-block batch-1 down projection latency-bound at
-  // ~4.9 TB/s); default cache policy (NTW: non-temporal, measured slower here)
-  constexpr int U = (PAIR || MT > 1) ? 1 : UN;
+  constexpr int U = 1;  // K blocks per wave per iteration (default cache policy for the weights)
   for (int kb = wid; kb < nkb; kb += U * WV) {
     bf16x8 wf[U][NACC][4];
 #pragma unroll
@@ -256,13 +254,8 @@ __global__ __launch_bounds__(WV * 64) void gemm_skinny_kernel(
       const int k = min(kb + u * WV, nkb - 1) * 128;  // clamped: a missing second block is loaded, not used
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        if constexpr (NTW) {
-          wf[u][0][s] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w0 + k + 32 * s));
-          if constexpr (PAIR) wf[u][1][s] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(w1 + k + 32 * s));
-        } else {
-          wf[u][0][s] = *reinterpret_cast<const bf16x8*>(w0 + k + 32 * s);
-          if constexpr (PAIR) wf[u][1][s] = *reinterpret_cast<const bf16x8*>(w1 + k + 32 * s);
-        }
+        wf[u][0][s] = *reinterpret_cast<const bf16x8*>(w0 + k + 32 * s);
+        if constexpr (PAIR) wf[u][1][s] = *reinterpret_cast<const bf16x8*>(w1 + k + 32 * s);
       }
     }
     bf16x8 xf[U][MT][4];
@@ -485,73 +478,12 @@ hipError_t launch_tile(const void* A, int lda, const void* B, int ldb, void* C, 
   return hipGetLastError();
 }
 
-static int g_skinny_waves = -1;  // -1: auto (RAGK_SKINNY_WAVES env, else by shape)
-// 128-deep K blocks per wave per iteration of the batch-1 skinny GEMM (A/B knob; 2 = default)
-// 1 (default) = the round-3 loop; 2 = two K blocks in flight per wave (A/B: slower at C=1 with default-policy
-// loads, 3.59 vs 3.53 ms per token, profiles/c1_skinny_unroll_plain_ab_r4.log; its earlier apparent win was
-// against the 1-block form WITH non-temporal loads, which costs more than either)
-static int g_skinny_unroll = 1;
-static bool g_skinny_unroll_set = false;  // set by ragk_gemm_skinny_set_unroll (overrides RAGK_SKINNY_UNROLL)
-RAGK_API int ragk_gemm_skinny_set_unroll(int u) {
-  g_skinny_unroll = u == 1 ? 1 : (u == 4 ? 4 : 2);
-  g_skinny_unroll_set = true;
-  return 0;
-}
-RAGK_API int ragk_gemm_skinny_set_waves(int w) {
-  g_skinny_waves = (w == 8 || w == 16) ? w : -1;
-  return 0;
-}
-
 template <int MT, int EPI, bool F32>
 hipError_t launch_skinny(const void* X, int ldx, const void* W, int ldw, void* C, int ldc, const void* bias,
                          const void* resid, int ldr, int M, int N, int K, hipStream_t st) {
-  static const int s_env = [] {
-    const char* v = getenv("RAGK_SKINNY_WAVES");
-    return v ? atoi(v) : 0;
-  }();
-  int wv = g_skinny_waves > 0 ? g_skinny_waves : (s_env == 8 || s_env == 16 ? s_env : 0);
-  // auto = 8: 16 waves measured slower on the batch-1 down projection (decode step 3.66 -> 3.74 ms)
-  if (wv == 0) wv = 8;
-  if (wv == 16 && MT == 1) {
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, 16>), dim3((N + 15) / 16), dim3(16 * 64), 0, st,
-                       (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
-                       (const bf16_t*)resid, ldr, M, N, K);
-    return hipGetLastError();
-  }
-  static const int s_unroll_env = [] {
-    const char* v = getenv("RAGK_SKINNY_UNROLL");
-    return v ? atoi(v) : 0;
-  }();
-  // grids of many blocks (the vocab projection: 8016) keep their loads in flight through occupancy; the
-  // unrolled form's extra VGPRs only pay on the few-block shapes (the 256-block down projection)
-  // RAGK_SKINNY_NT=1: non-temporal weight loads (A/B; measured slower at C=1: 3.67 vs 3.59 ms per token,
-  // profiles/c1_skinny_nt_ab_r4.log)
-  static const int s_nt_env = [] {
-    const char* v = getenv("RAGK_SKINNY_NT");
-    return v ? atoi(v) : 0;
-  }();
-  static const int s_unroll_max_blocks = [] {
-    const char* v = getenv("RAGK_SKINNY_UNROLL_MAX_BLOCKS");
-    return v ? atoi(v) : 2048;
-  }();
-  const int un = g_skinny_unroll_set ? g_skinny_unroll : (s_unroll_env >= 1 && s_unroll_env <= 4 ? s_unroll_env
-                                                                                                 : g_skinny_unroll);
-  if (un == 1 || (s_unroll_max_blocks > 0 && (N + 15) / 16 > s_unroll_max_blocks))
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, SK_WAVES, 1>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0,
-                       st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
-                       (const bf16_t*)resid, ldr, M, N, K);
-  else if (s_nt_env == 1 && MT == 1)  // A/B: two K blocks in flight, non-temporal weight loads
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, SK_WAVES, 2, true>), dim3((N + 15) / 16),
-                       dim3(SK_WAVES * 64), 0, st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc,
-                       (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K);
-  else if (un == 4 && MT == 1)
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32, SK_WAVES, 4>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0,
-                       st, (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
-                       (const bf16_t*)resid, ldr, M, N, K);
-  else
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0, st,
-                       (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
-                       (const bf16_t*)resid, ldr, M, N, K);
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, EPI, F32>), dim3((N + 15) / 16), dim3(SK_WAVES * 64), 0, st,
+                     (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, C, ldc, (const bf16_t*)bias,
+                     (const bf16_t*)resid, ldr, M, N, K);
   return hipGetLastError();
 }
 

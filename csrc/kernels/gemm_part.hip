@@ -104,166 +104,14 @@ struct SiluArgs {
   int S1;
 };
 
-// TL (TP=1 o_proj / down at any decode batch): the consumer of the slabs -- h += bf16(sum of slabs),
-// xn = rmsnorm(h) * gamma, add_partials_rmsnorm_kernel's exact math -- runs inside the launch, in M of its
-// blocks, instead of a separate launch (one kernel boundary and one launch ramp fewer per norm).
-// Every block writes its slab write-through (sc1), drains it and arrives on the counter of its shard
-// (blockIdx % 8: the XCD the dispatcher put it on; placement is a speed matter only). One device-scope
-// counter for all ~512 arrivals serialises them (~12 ns each, MI355X_MICROARCH.md "fanin": ~6 us per
-// launch, measured here as a net LOSS vs the separate launch); eight shards run their fan-ins in
-// parallel, and the last arriver of each shard arrives on the top counter, whose last arriver raises the
-// done flag (TL_REPL replicas, one 128-B line each). The last ceil(M / 8) arrivers of shard x own rows
-// x, x + 8, ...: they prefetch the row's residual and norm weights, wait (bounded, one polling lane) for
-// the done flag, sum the row's slabs with write-through loads in slab order and finish the row. The
-// flag raiser and every row block arrive on a finish counter once their stores have drained; the
-// last of those M + 1 arrivals re-arms everything (nobody polls or writes any word by then; the next
-// launch is stream-ordered). A wait that runs out sets the error word (the row is computed from
-// whatever is there; the host turns the word into an error, never a hang).
-struct TailArgs {
-  bf16_t* h;             // [M][ldh] residual rows, updated in place
-  int ldh;
-  const bf16_t* gamma;   // [N] norm weights
-  bf16_t* xn;            // [M][ldx] normalised rows
-  int ldx;
-  float eps;
-  int* cnt;              // TL_INTS ints, zero before the first launch (the launch leaves them zero)
-  unsigned spin_limit;   // s_memrealtime ticks (100 MHz)
-};
-constexpr int TL_THREADS = PT_THREADS;  // threads that own row vectors (add_partials_rmsnorm's PNT)
-constexpr int TL_SH = 8, TL_LINE = 32;  // shards; ints per 128-B line
-constexpr int TL_TOP = TL_SH * TL_LINE;
-constexpr int TL_REPL = 8;
-constexpr int TL_DONE = TL_TOP + TL_LINE;
-constexpr int TL_FIN = TL_DONE + TL_REPL * TL_LINE;
-constexpr int TL_ERR = TL_FIN + TL_LINE;
-constexpr int TL_INTS = TL_ERR + TL_LINE;
-
-__device__ __forceinline__ void part_tail(const TailArgs& tl, const float* P, int M, int N, int S) {
-  __shared__ int s_row;
-  __shared__ float s_tred[(PT_THREADS + MG_THREADS) / 64];
-  wait_vmcnt0();
-  __syncthreads();
-  const int tid = threadIdx.x;
-  const int total = gridDim.x * gridDim.y;
-  const int bid = blockIdx.y * gridDim.x + blockIdx.x;
-  const int x = bid % TL_SH;
-  const int nx = (total - x + TL_SH - 1) / TL_SH;  // blocks of shard x (host: total >= 8 * ceil(M / 8))
-  const int kx = (M + TL_SH - 1) / TL_SH;         // row slots per shard
-  if (tid == 0) {
-    int row = -1;
-    const int t = __hip_atomic_fetch_add(tl.cnt + x * TL_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == nx - 1 &&
-        __hip_atomic_fetch_add(tl.cnt + TL_TOP, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == TL_SH - 1) {
-#pragma unroll
-      for (int k = 0; k < TL_REPL; ++k)
-        __hip_atomic_store(tl.cnt + TL_DONE + k * TL_LINE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      wait_vmcnt0();
-      __hip_atomic_fetch_add(tl.cnt + TL_FIN, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (t >= nx - kx) {
-      const int r = (t - (nx - kx)) * TL_SH + x;
-      row = r < M ? r : -1;
-    }
-    s_row = row;
-  }
-  __syncthreads();
-  const int row = s_row;
-  if (row < 0) return;  // block-uniform
-  constexpr int MAXV = 2;  // H <= 8192
-  const int nvec = N >> 3;
-  const bool own = tid < TL_THREADS;
-  bf16_t* hr = tl.h + (size_t)row * tl.ldh;
-  u32x4 hv[MAXV], gv[MAXV];
-#pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int vi = min(tid % TL_THREADS + i * TL_THREADS, nvec - 1);
-    hv[i] = *reinterpret_cast<const u32x4*>(hr + vi * 8);
-    gv[i] = *reinterpret_cast<const u32x4*>(tl.gamma + vi * 8);
-  }
-  if (tid == 0) {
-    const int* f = tl.cnt + TL_DONE + (bid % TL_REPL) * TL_LINE;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-      __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > tl.spin_limit) {
-        __hip_atomic_store(tl.cnt + TL_ERR, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(P), (short)0,
-                                                                      S * M * N * 4, 0x00020000);
-  float v[MAXV][8];
-  float ss = 0.f;
-#pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int vi = tid + i * TL_THREADS;
-    if (own && vi < nvec) {
-      // slab order 0..S-1 into one accumulator (add_slabs8's order), PSU slabs' loads in flight at once
-      float a[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) a[e] = 0.f;
-      const int base = (row * N + vi * 8) * 4;
-      for (int s0 = 0; s0 < S; s0 += PSU) {
-        u32x4 p[PSU][2];
-#pragma unroll
-        for (int u = 0; u < PSU; ++u) {
-          const int o = base + min(s0 + u, S - 1) * M * N * 4;
-          p[u][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 16));
-          p[u][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16, 0, 16));
-        }
-#pragma unroll
-        for (int u = 0; u < PSU; ++u) {
-          if (s0 + u < S) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              a[e] += __uint_as_float(p[u][0][e]);
-              a[4 + e] += __uint_as_float(p[u][1][e]);
-            }
-          }
-        }
-      }
-      unpack8(hv[i], v[i]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[i][e] = bf2f(f2bf(v[i][e] + bf2f(f2bf(a[e]))));
-      *reinterpret_cast<u32x4*>(hr + vi * 8) = pack8(v[i]);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) ss += v[i][e] * v[i][e];
-    }
-  }
-  ss = block_sum(ss, s_tred);  // waves beyond TL_THREADS add zeros after the owners' partials
-  const float inv = rsqrtf(ss / (float)N + tl.eps);
-#pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int vi = tid + i * TL_THREADS;
-    if (own && vi < nvec) {
-      float wv[8], o[8];
-      unpack8(gv[i], wv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = wv[e] * bf2f(f2bf(v[i][e] * inv));
-      *reinterpret_cast<u32x4*>(tl.xn + (size_t)row * tl.ldx + vi * 8) = pack8(o);
-    }
-  }
-  if (tid == 0 && __hip_atomic_fetch_add(tl.cnt + TL_FIN, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == M) {
-#pragma unroll
-    for (int k = 0; k < TL_SH; ++k) __hip_atomic_store(tl.cnt + k * TL_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(tl.cnt + TL_TOP, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int k = 0; k < TL_REPL; ++k)
-      __hip_atomic_store(tl.cnt + TL_DONE + k * TL_LINE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(tl.cnt + TL_FIN, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-template <int MT, int NKS, bool FP8 = false, int NR = 0, int NV = 1, bool MG = false, bool SG = false, bool TL = false>
+template <int MT, int NKS, bool FP8 = false, int NR = 0, int NV = 1, bool MG = false, bool SG = false>
 __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), MG ? 2 : 1) void gemm_part_kernel(const bf16_t* __restrict__ X, int ldx,
                                                                   const bf16_t* __restrict__ W, int ldw,
                                                                   float* __restrict__ P, int M, int N, int K,
                                                                   const float* __restrict__ wscale = nullptr,
                                                                   const bf16_t* __restrict__ gamma = nullptr,
                                                                   float eps = 0.f, MergeArgs mg = {},
-                                                                  SiluArgs sg = {}, TailArgs tl = {}, int wnt = 1) {
+                                                                  SiluArgs sg = {}, int wnt = 1) {
   constexpr int KS = NKS * 64;          // K-slice of the block (two halves of NKS k-steps of 32)
   constexpr int XROWS = 16 * MT;
   constexpr int ROWB = KS * 2;          // bytes per LDS row
@@ -555,44 +403,26 @@ __global__ __launch_bounds__(PT_THREADS + (MG ? MG_THREADS : 0), MG ? 2 : 1) voi
       for (int r = 0; r < 4; ++r) {
         const int row = 16 * t + 4 * fh + r;
         const float val = FP8 ? (acc[t][r] + o[r]) * sc : acc[t][r] + o[r];
-        if constexpr (TL) {  // read back by the tail blocks: write-through
-          if (row < M && col < N) {
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(P, (short)0, (K / KS) * M * N * 4, 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val), rs, ((s * M + row) * N + col) * 4, 0, 16);
-          }
-        } else {
-          if (row < M && col < N) ps[(size_t)row * N + col] = val;
-        }
+        if (row < M && col < N) ps[(size_t)row * N + col] = val;
       }
     }
   }
-  if constexpr (TL) part_tail(tl, P, M, N, K / KS);
 }
 
-// weight-stream cache policy of the split-K decode GEMM: 1 = non-temporal (default), RAGK_PART_NT=0 = default
-// policy (A/B)
-inline int part_nt() {
-  static const int v = [] {
-    const char* e = getenv("RAGK_PART_NT");
-    return e ? (atoi(e) != 0) : 1;
-  }();
-  return v;
-}
-
-template <int MT, bool FP8 = false, int NR = 0, int NV = 1, bool MG = false, bool SG = false, bool TL = false>
+template <int MT, bool FP8 = false, int NR = 0, int NV = 1, bool MG = false, bool SG = false>
 int launch_part_mt(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K, int ks_steps,
                    hipStream_t st, const float* wscale = nullptr, const void* gamma = nullptr, float eps = 0.f,
-                   MergeArgs mg = {}, SiluArgs sg = {}, TailArgs tl = {}) {
+                   MergeArgs mg = {}, SiluArgs sg = {}) {
   const int KS = ks_steps * 64;
   const dim3 grid((N + PT_NB - 1) / PT_NB, K / KS);
 #define RAGK_PART(NK)                                                                                       \
   case NK:                                                                                                  \
     if constexpr (16 * MT * NK * 64 * 2 <= 128 * 1024 && (16 * MT * NK * 64 * 2) % 8192 == 0 &&           \
                   (NR == 0 || NK == 8 || NK == 16) && (!MG || NK == 4 || NK == 8) && (!SG || NK <= 16)) {   \
-      hipLaunchKernelGGL((gemm_part_kernel<MT, NK, FP8, NR, NV, MG, SG, TL>), grid, dim3(PT_THREADS + (MG ? MG_THREADS : 0)), \
+      hipLaunchKernelGGL((gemm_part_kernel<MT, NK, FP8, NR, NV, MG, SG>), grid, dim3(PT_THREADS + (MG ? MG_THREADS : 0)), \
                          0, st,                                                                             \
                          (const bf16_t*)X, ldx, (const bf16_t*)W, ldw, P, M, N, K, wscale, (const bf16_t*)gamma, \
-                         eps, mg, sg, tl, part_nt());                                                       \
+                         eps, mg, sg, 1);  /* non-temporal weight stream */                                                       \
       break;                                                                                                \
     } else {                                                                                                \
       return (int)hipErrorInvalidValue;                                                                     \
@@ -732,50 +562,3 @@ RAGK_API int ragk_gemm_part_merge_ok(int M, int K, int Hq, int max_parts, int ks
   return (max_parts + npg - 1) / npg <= MG_MAXPP;
 }
 
-// TL: the same GEMMs with the residual add + RMSNorm consumer in their last M blocks (part_tail above):
-// h[M][ldh] += bf16(sum of the slabs), xn[M][ldx] = rmsnorm(h) * gamma; P still receives the slabs.
-// cnt: >= 3 ints, zero before the first launch (the launch leaves them zero). bf16 weights, N % 8 == 0,
-// N <= 8192, grid >= M blocks.
-static bool part_tail_args_ok(int M, int N, int K, int ks_steps, const void* h, const void* gamma, const void* xn,
-                              const int* cnt) {
-  if (!h || !gamma || !xn || !cnt || N % 8 || N > 8 * TL_THREADS * 2) return false;
-  const int blocks = ((N + PT_NB - 1) / PT_NB) * (K / (64 * ks_steps));
-  return blocks >= TL_SH * ((M + TL_SH - 1) / TL_SH) && (long long)(K / (64 * ks_steps)) * M * N * 4 < (1LL << 31);
-}
-
-RAGK_API int ragk_gemm_part_tail_ints() { return TL_INTS; }
-
-RAGK_API int ragk_gemm_part_tail(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K,
-                                 int ks_steps, void* h, int ldh, const void* gamma, void* xn, int ldxn, float eps,
-                                 int* cnt, unsigned spin_limit, hipStream_t st) {
-  if (M <= 0) return 0;
-  if (M > 64 || ks_steps <= 0 || K % (64 * ks_steps) != 0 || !part_tail_args_ok(M, N, K, ks_steps, h, gamma, xn, cnt))
-    return (int)hipErrorInvalidValue;
-  const int mt = (M + 15) / 16;
-  if (16 * mt * ks_steps * 64 * 2 > 128 * 1024) return (int)hipErrorInvalidValue;
-  const TailArgs tl{(bf16_t*)h, ldh, (const bf16_t*)gamma, (bf16_t*)xn, ldxn, eps, cnt, spin_limit};
-#define RAGK_PT(T) return launch_part_mt<T, false, 0, 1, false, false, true>(X, ldx, W, ldw, P, M, N, K, ks_steps, st, \
-                                                                             nullptr, nullptr, 0.f, {}, {}, tl)
-  switch (mt) {
-    case 1: RAGK_PT(1);
-    case 2: RAGK_PT(2);
-    case 3: RAGK_PT(3);
-    case 4: RAGK_PT(4);
-    default: return (int)hipErrorInvalidValue;
-  }
-#undef RAGK_PT
-}
-
-RAGK_API int ragk_gemm_part_merge_tail(const float* part_o, const float* part_ml, const void* out, int out_stride,
-                                       const int* kv_lens, int Hq, int part_tiles, int max_parts, const void* W, int ldw,
-                                       float* P, int M, int N, int K, int ks_steps, void* h, int ldh, const void* gamma,
-                                       void* xn, int ldxn, float eps, int* cnt, unsigned spin_limit, hipStream_t st) {
-  if (M <= 0) return 0;
-  if (!ragk_gemm_part_merge_ok(M, K, Hq, max_parts, ks_steps) || !part_o || !part_ml || !out || !kv_lens ||
-      part_tiles < 1 || !part_tail_args_ok(M, N, K, ks_steps, h, gamma, xn, cnt))
-    return (int)hipErrorInvalidValue;
-  const MergeArgs mg{part_o, part_ml, (const bf16_t*)out, out_stride, kv_lens, Hq, part_tiles, max_parts};
-  const TailArgs tl{(bf16_t*)h, ldh, (const bf16_t*)gamma, (bf16_t*)xn, ldxn, eps, cnt, spin_limit};
-  return launch_part_mt<1, false, 0, 1, true, false, true>(out, out_stride, W, ldw, P, M, N, K, ks_steps, st, nullptr,
-                                                           nullptr, 0.f, mg, {}, tl);
-}

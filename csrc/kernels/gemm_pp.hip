@@ -231,172 +231,16 @@ __global__ __launch_bounds__(PP_THREADS, 1) void gemm_pp_kernel(const bf16_t* __
 }
 
 
-// ------------------------------------------------------------------------------------------------
-// Variant 4 (experimental, A/B only): same 256x256 tile, waves and ping-pong, but 32-deep K-tiles
-// in a 4-buffer ring (4 x 32 KiB). Each K-tile's DMA is issued 6 barrier intervals (3 K-tiles)
-// before its first read instead of 2; waits are counted (vmcnt(8) = the two younger tiles may stay
-// in flight), never 0 in steady state. Measured 8-13 % SLOWER than variant 2 on Llama-8B prefill
-// shapes (1.17-1.26 vs 1.23-1.38 PF at M=16384): DMA latency was not the limiter, and the halved
-// MFMA bursts (32 per interval) add barrier overhead. Kept for A/B (RAGK_PP_VARIANT=4).
-//   group 0: READ(t) at global interval 2t, COMPUTE(t) at 2t+1, issues tile t+3 in READ(t);
-//   group 1: one interval behind, issues tile t+4 in COMPUTE(t);
-//   both halves of tile X are issued in global interval 2X-6, after group 1's READ(X-4) (the
-//   buffer's previous tile) ended with lgkmcnt(0) + barrier; each wave retires its part of tile X
-//   by the barrier that ends global interval 2X-1.
-// 64-B LDS rows: chunk c of row R sits in 16-B slot c ^ ((R>>1)&3) -- conflict-free for the
-// ds_read_b128 lane groups ({0-3,12-15,20-27}, ...).
-// ------------------------------------------------------------------------------------------------
-constexpr int P4K = 32;
-constexpr int P4_TILE = 256 * P4K * 2;  // 16 KiB per operand tile
-constexpr int P4_BUF = 2 * P4_TILE;     // 32 KiB per K-tile
-constexpr int P4_NB = 4;
-constexpr int P4_LDS = (P4_NB * P4_BUF > PEPI_BYTES) ? P4_NB * P4_BUF : PEPI_BYTES;
-
-__device__ __forceinline__ int swz4(int row, int chunk) { return chunk ^ ((row >> 1) & 3); }
-
-// one K-tile = 32 pieces of 16 rows x 64 B (A: 0-15, B: 16-31); wave w stages pieces 4w..4w+3
-__device__ __forceinline__ void pp4_stage(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ B,
-                                          int ldb, int m0, int M, int n0, int N, int k0, char* buf, int wid,
-                                          int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = wid * 4 + i;
-    const bool isA = q < 16;
-    const int r = (q & 15) * 16 + (lane >> 2);
-    const int c = swz4(r, lane & 3);
-    const bf16_t* g = isA ? A : B;
-    const int ld = isA ? lda : ldb;
-    const int rv = isA ? M : N;
-    int gr = (isA ? m0 : n0) + r;
-    gr = gr < rv ? gr : rv - 1;
-    glds16(g + (size_t)gr * ld + k0 + c * 8, buf + q * 1024);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  __builtin_amdgcn_s_waitcnt((N & 15) | (((N >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
-}
-
-// wait for tile `x`'s own DMA, given the newest tile this wave has issued
-__device__ __forceinline__ void pp4_wait(int x, int newest) {
-  const int younger = newest - x;  // tiles issued after x (each 4 glds per wave)
-  if (younger >= 2) wait_vm<8>();
-  else if (younger == 1) wait_vm<4>();
-  else wait_vm<0>();
-}
-
-template <int EPI, bool OUT_F32>
-__global__ __launch_bounds__(PP_THREADS, 1) void gemm_pp4_kernel(const bf16_t* __restrict__ A, int lda,
-                                                                 const bf16_t* __restrict__ B, int ldb, void* C,
-                                                                 int ldc, const bf16_t* __restrict__ bias,
-                                                                 const bf16_t* resid, int ldr, int M, int N, int K) {
-  __shared__ __attribute__((aligned(16))) char smem[P4_LDS];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wid >> 2, wq = wid & 3;
-  const int fr = lane & 15, fh = lane >> 4;
-
-  const int tiles_m = (M + PBM - 1) / PBM, tiles_n = (N + PBN - 1) / PBN;
-  const int nwg = tiles_m * tiles_n;
-  const int logical = xcd_remap(blockIdx.x, nwg);
-  const int group = logical / (PGROUP_M * tiles_n);
-  const int first_m = group * PGROUP_M;
-  const int gm = min(tiles_m - first_m, PGROUP_M);
-  const int in_group = logical % (PGROUP_M * tiles_n);
-  const int m0 = (first_m + in_group % gm) * PBM;
-  const int n0 = (in_group / gm) * PBN;
-  const int nk = K / P4K;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  bf16x8 af[8], bfr[4];
-
-  auto stage = [&](int x) {
-    pp4_stage(A, lda, B, ldb, m0, M, n0, N, x * P4K, smem + (x % P4_NB) * P4_BUF, wid, lane);
-  };
-  // prologue: tiles 0..2 by everyone, tile 3 by group 1 (group 0 issues it in READ(0))
-  int newest = -1;
-#pragma unroll
-  for (int x = 0; x < 3; ++x)
-    if (x < nk) {
-      stage(x);
-      newest = x;
-    }
-  if (grp == 1 && 3 < nk) {
-    stage(3);
-    newest = 3;
-  }
-  pp4_wait(0, newest);
-  barrier_raw();                // boundary 0
-  if (grp == 1) barrier_raw();  // group 1 runs one interval behind
-
-  for (int t = 0; t < nk; ++t) {
-    // ---------------- READ segment: fragments of tile t ---------------------------------
-    const char* sa = smem + (t % P4_NB) * P4_BUF;
-    const char* sb = sa + P4_TILE;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int R = grp * 128 + 16 * i + fr;
-      af[i] = *reinterpret_cast<const bf16x8*>(sa + R * 64 + 16 * swz4(R, fh));
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int R = wq * 64 + 16 * j + fr;
-      bfr[j] = *reinterpret_cast<const bf16x8*>(sb + R * 64 + 16 * swz4(R, fh));
-    }
-    if (grp == 0 && t + 3 < nk) {
-      stage(t + 3);
-      newest = t + 3;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (grp == 1 && t + 1 < nk) pp4_wait(t + 1, newest);  // group 1's interval 2t+1 ends here
-    barrier_raw();
-    // ---------------- COMPUTE segment: 32 MFMAs -----------------------------------------
-    if (grp == 1 && t + 4 < nk) {
-      stage(t + 4);
-      newest = t + 4;
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    if (grp == 0 && t + 1 < nk) pp4_wait(t + 1, newest);  // group 0's interval 2t+1 ends here
-    barrier_raw();
-  }
-  if (grp == 0) barrier_raw();  // match group 1's extra barrier
-  wait_vmcnt0();
-  pp_epilogue<EPI, OUT_F32>(acc, smem, tid, grp, wq, fr, fh, m0, n0, C, ldc, bias, resid, ldr, M, N);
-}
-
-int g_pp_variant = 2;  // 2: 2 x 64-deep buffers, 4: 4 x 32-deep ring (ragk_gemm_pp_set_variant)
-
 template <int EPI, bool F32>
 int launch_pp(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias, const void* resid,
               int ldr, int M, int N, int K, hipStream_t st) {
   const int nwg = ((M + PBM - 1) / PBM) * ((N + PBN - 1) / PBN);
-  if (g_pp_variant == 4)
-    hipLaunchKernelGGL((gemm_pp4_kernel<EPI, F32>), dim3(nwg), dim3(PP_THREADS), 0, st, (const bf16_t*)A, lda,
-                       (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K);
-  else
-    hipLaunchKernelGGL((gemm_pp_kernel<EPI, F32>), dim3(nwg), dim3(PP_THREADS), 0, st, (const bf16_t*)A, lda,
-                       (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, F32>), dim3(nwg), dim3(PP_THREADS), 0, st, (const bf16_t*)A, lda,
+                     (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K);
   return (int)hipGetLastError();
 }
 
 }  // namespace
-
-RAGK_API int ragk_gemm_pp_set_variant(int v) {
-  if (v != 2 && v != 4) return (int)hipErrorInvalidValue;
-  g_pp_variant = v;
-  return 0;
-}
 
 // N = output columns (for EPI_SILU_MUL the weight has 2N rows, N % 128 == 0). Requires K % 64 == 0.
 RAGK_API int ragk_gemm_pp(const void* A, int lda, const void* B, int ldb, void* C, int ldc, const void* bias,

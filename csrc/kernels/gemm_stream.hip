@@ -378,16 +378,7 @@ template <int MT>
 int launch_stream_slab(const void* X, int ldx, const void* W, int ldw, float* P, int M, int N, int K, int S, int rows,
                        hipStream_t st) {
   const dim3 grid((N + rows - 1) / rows, S);
-  static const int s_nt = [] {  // RAGK_STREAM_PART_NT=0: default-policy weight stream (A/B)
-    const char* v = getenv("RAGK_STREAM_PART_NT");
-    return v ? atoi(v) : 1;
-  }();
-  if (!s_nt) {
-    hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI_NONE, true, false, false, WROWS, true>), grid, dim3(ST_THREADS), 0,
-                       st, (const bf16_t*)X, ldx, W, ldw, nullptr, P, N, nullptr, nullptr, 0, M, N, K, S, nullptr,
-                       nullptr);
-    return (int)hipGetLastError();
-  }
+  // non-temporal weight stream (each weight byte is read once per step)
   if (rows == 64)
     hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI_NONE, true, false, true, 64, true>), grid, dim3(ST_THREADS), 0, st,
                        (const bf16_t*)X, ldx, W, ldw, nullptr, P, N, nullptr, nullptr, 0, M, N, K, S, nullptr, nullptr);
@@ -427,19 +418,10 @@ RAGK_API int ragk_gemm_stream_set_pair_rows(int rows) {
 }
 
 RAGK_API int ragk_gemm_stream_splits(int N, int K, int epi, int fp8) {
-  static const int s_env = [] {
-    const char* v = getenv("RAGK_STREAM_S");
-    return v ? atoi(v) : 0;
-  }();
   const int Nrows = epi == EPI_SILU_MUL ? 2 * N : N;
   const int rows = stream_rows(epi);
   const int tiles = (Nrows + rows - 1) / rows;
   const int steps = K / (fp8 ? 128 : 64);
-  if (s_env > 0) {
-    int S = s_env;
-    while (S > 1 && steps % S) S >>= 1;
-    return S;
-  }
   int S = 1;
   const int slots = rows == 64 ? 640 : 320;  // 64-row tiles: two blocks per CU
   while (tiles * S * 2 <= slots && steps % (S * 2) == 0 && steps / (S * 2) >= 8) S *= 2;

@@ -354,12 +354,8 @@ constexpr int PNT = 512;
 __global__ __launch_bounds__(PNT) void add_partials_rmsnorm_kernel(const float* __restrict__ P, int S, int M,
                                                                    bf16_t* h, int ldh,
                                                                    const bf16_t* __restrict__ w, bf16_t* out,
-                                                                   int ldo, int H, float eps, PfArgs pf) {
+                                                                   int ldo, int H, float eps) {
   __shared__ float red[PNT / 64];
-  if ((int)blockIdx.x >= M) {  // MALL prefetch rider (block-uniform)
-    pf_rider(pf, blockIdx.x - M, gridDim.x - M);
-    return;
-  }
   const int row = blockIdx.x;
   bf16_t* hr = h + (size_t)row * ldh;
   constexpr int MAXV = 2;  // up to 2 x 8 x 512 = 8192 columns in registers
@@ -418,12 +414,7 @@ __global__ __launch_bounds__(NT) void rope_kv_partials_kernel(const float* __res
                                                               const float* __restrict__ cos_t,
                                                               const float* __restrict__ sin_t,
                                                               const int* __restrict__ slots, bf16_t* kc, bf16_t* vc,
-                                                              int Hq, int Hkv, int D, int BS, PfArgs pf) {
-  if ((int)blockIdx.x >= T) {  // MALL prefetch rider (block-uniform)
-    const int ex = gridDim.x - T;
-    pf_rider(pf, (blockIdx.x - T) + ex * blockIdx.y, ex * gridDim.y);
-    return;
-  }
+                                                              int Hq, int Hkv, int D, int BS) {
   const int t = blockIdx.x, hg = blockIdx.y, ngroups = gridDim.y;
   const int pos = positions[t];
   const int slot = slots ? slots[t] : -1;
@@ -549,9 +540,8 @@ RAGK_API int ragk_add_partials_rmsnorm(const float* P, int S, int M, void* h, in
                                        int ldo, int H, float eps, hipStream_t st) {
   if (M <= 0) return 0;
   if (H % 8 || H > 8 * PNT * 2 || S < 1) return (int)hipErrorInvalidValue;
-  const PfArgs pf = pf_take();
-  hipLaunchKernelGGL(add_partials_rmsnorm_kernel, dim3(M + pf.blocks), dim3(PNT), 0, st, P, S, M, (bf16_t*)h, ldh,
-                     (const bf16_t*)w, (bf16_t*)out, ldo, H, eps, pf);
+  hipLaunchKernelGGL(add_partials_rmsnorm_kernel, dim3(M), dim3(PNT), 0, st, P, S, M, (bf16_t*)h, ldh,
+                     (const bf16_t*)w, (bf16_t*)out, ldo, H, eps);
   return (int)hipGetLastError();
 }
 
@@ -565,9 +555,7 @@ RAGK_API int ragk_rope_kv_partials(const float* P, int S, int T, int ldp, void* 
   // at least one wave of (head, 8-column) items per block
   const int items = (Hq + 2 * Hkv) * (D / 16);
   const int groups = std::max(1, std::min((items + 63) / 64, std::max(4, (512 + T - 1) / T)));
-  const PfArgs pf = pf_take();
-  const int ex = (pf.blocks + groups - 1) / groups;  // rider columns (x beyond T), spread over the groups
-  hipLaunchKernelGGL(rope_kv_partials_kernel, dim3(T + ex, groups), dim3(NT), 0, st, P, S, T, ldp, (bf16_t*)q_out,
-                     ldq, positions, cos_t, sin_t, slots, (bf16_t*)kc, (bf16_t*)vc, Hq, Hkv, D, BS, pf);
+  hipLaunchKernelGGL(rope_kv_partials_kernel, dim3(T, groups), dim3(NT), 0, st, P, S, T, ldp, (bf16_t*)q_out,
+                     ldq, positions, cos_t, sin_t, slots, (bf16_t*)kc, (bf16_t*)vc, Hq, Hkv, D, BS);
   return (int)hipGetLastError();
 }

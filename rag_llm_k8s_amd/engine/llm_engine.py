@@ -40,8 +40,8 @@ from .kv_manager import BLOCK, make_block_manager
 # threshold-filtered lane networks, merged by the sampler's lane network); larger batches use 7
 # radix-select chunks (topk_lds). tools/sampler_bench.py: top-k + sample 21.0 us at batch 1 (7 chunks:
 # 40.1), 33.6 us at batch 32 (7 chunks: 41.2) -- profiles/sampler_bench_r3.log
-SMALL_BATCH_TOPK_MAX_B = int(os.environ.get("RAGK_TOPK_SMALL_B", "64"))
-SMALL_BATCH_TOPK_CHUNK = int(os.environ.get("RAGK_TOPK_SMALL_CHUNK", "4096"))
+SMALL_BATCH_TOPK_MAX_B = 64
+SMALL_BATCH_TOPK_CHUNK = 4096
 
 log = logging.getLogger(__name__)
 
@@ -126,7 +126,7 @@ class LLMEngine:
         self.K = top_k_cap
         self._warned_topk = False
         # TP prefill steps of at least this many tokens run as 2 micro-batches with async all-reduces
-        self.tp_overlap_min_tokens = int(os.environ.get("RAGK_TP_OVERLAP_MIN", "1024"))
+        self.tp_overlap_min_tokens = 1024
         self.is_cuda = self.device.type == "cuda"
         self.use_graphs = use_graphs and self.is_cuda
         self.buckets = sorted(set(graph_buckets or [b for b in (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 192, 256)

@@ -25,30 +25,14 @@ import torch
 from ..ops.backend import AttnMeta, get_backend
 from ..ops.reference import pack_gate_up, rope_tables
 
-# decode MALL prefetch (LlamaModel._pf_plan): on/off, MB per latency window, rider blocks, and the
-# batch size up to which the split-K attention counts as latency-bound
-DECODE_PF = os.environ.get("RAGK_DECODE_PF", "0") == "1"
-DECODE_PF_MB = int(os.environ.get("RAGK_DECODE_PF_MB", "16"))
-DECODE_PF_BLOCKS = int(os.environ.get("RAGK_DECODE_PF_BLOCKS", "128"))
-DECODE_PF_SMALL_BATCH = int(os.environ.get("RAGK_DECODE_PF_SMALL", "8"))
 # decode batches up to this size run the down projection on the register-streaming GEMM (fused residual)
-DECODE_DOWN_SKINNY_MAX_M = int(os.environ.get("RAGK_DECODE_DOWN_SKINNY_MAX_M", "4"))
-# decode: RoPE + KV append done by the attention kernel from the qkv partial slabs (attn_decode_rope)
-DECODE_ROPE_FUSED = os.environ.get("RAGK_DECODE_ROPE_FUSED", "1") == "1"
-# decode batch <= DECODE_DOWN_SKINNY_MAX_M: input RMSNorm inside the qkv split-K GEMM (gemm_part_norm)
-DECODE_NORM_FUSED = os.environ.get("RAGK_DECODE_NORM_FUSED", "1") == "1"
-# decode batch <= 4: the o_proj split-K GEMM merges the attention's split-K partitions itself
-# (gemm_part_merge), so the attention's separate merge launch disappears
-DECODE_OPROJ_MERGE = os.environ.get("RAGK_DECODE_OPROJ_MERGE", "1") == "1"
-DECODE_OPROJ_MERGE_MAX_M = int(os.environ.get("RAGK_DECODE_OPROJ_MERGE_MAX_M", "2"))
-# TP=1 batch <= this: o_proj as the register-streaming skinny GEMM with the residual epilogue (writes h),
-# then a plain RMSNorm -- instead of split-K slabs (+ partition merge) and the add_partials_rmsnorm consumer.
-# Off (0): measured slower, batch 1 3.85 vs 3.72 ms per step (profiles/decode_oproj_skinny_ab_r4.log)
-DECODE_OPROJ_SKINNY_MAX_M = int(os.environ.get("RAGK_DECODE_OPROJ_SKINNY_MAX_M", "0"))
-# decode batch <= 4: gate/up as split-K partials, silu(gate) * up formed inside the down GEMM's staging
-# (gemm_part.hip SG): "tp" = under tensor parallelism only (the TP=1 batch <= 4 path keeps the skinny
-# down GEMM with its fused residual), "1" = always, "0" = never
-DECODE_SILU_FUSED = os.environ.get("RAGK_DECODE_SILU_FUSED", "tp")  # batch 4: 2 merge rounds, slower
+DECODE_DOWN_SKINNY_MAX_M = 4
+# decode batch <= DECODE_OPROJ_MERGE_MAX_M: the o_proj split-K GEMM merges the attention's split-K
+# partitions itself (gemm_part_merge), so the attention's separate merge launch disappears
+DECODE_OPROJ_MERGE_MAX_M = 2
+# decode batch <= 4 under tensor parallelism: gate/up as split-K partials, silu(gate) * up formed inside
+# the down GEMM's staging (gemm_part.hip SG); the TP=1 batch <= 4 path keeps the skinny down GEMM with
+# its fused residual (batch 4 at TP=1: 2 merge rounds, slower)
 
 
 @dataclass
@@ -325,19 +309,6 @@ class LlamaModel:
             return False
         return self.be.part_ok(M, L["wqkv"]) and self.be.part_ok(M, L["wo"]) and self.be.part_ok(M, L["wdown"])
 
-    def _pf_plan(self, M):
-        """MALL prefetch plan of a decode step at batch M (csrc/kernels/prefetch.hip, common.h pf_rider):
-        bytes of the next GEMM's weights that rider blocks of each latency-bound kernel pull into the
-        Infinity Cache. At small batch the split-K attention is latency-bound too and carries riders; at
-        large batch it streams the KV cache at full bandwidth (and would evict what was prefetched
-        before it), so only the post-attention consumers carry them. RAGK_DECODE_PF=0 disables."""
-        if not DECODE_PF or self.device.type != "cuda":
-            return None
-        mb = 1 << 20
-        small = M <= DECODE_PF_SMALL_BATCH
-        return dict(rope=DECODE_PF_MB * mb if small else 0, attn=2 * DECODE_PF_MB * mb if small else 0,
-                    post=DECODE_PF_MB * mb, blocks=DECODE_PF_BLOCKS)
-
     def hidden_states_decode_part(self, inp: StepInput, h):
         """Decode step with the split-K partial GEMM (csrc/kernels/gemm_part.hip) for the three
         small-N projections: qkv / o_proj / down write fp32 partial slabs and the following row
@@ -366,91 +337,22 @@ class LlamaModel:
             return be.add_partials_rmsnorm(P, h, gamma, c.rms_norm_eps)
 
         attn = torch.empty((M, Hq * D), dtype=h.dtype, device=h.device)
-        q = torch.empty((M, Hq * D), dtype=h.dtype, device=h.device)
         layers = w.layers
-        pf = None if tp else self._pf_plan(M)
         # batch <= 4: the input norm runs inside the qkv GEMM (gemm_part_norm) -- one launch fewer per layer
-        fuse_norm = (DECODE_NORM_FUSED and M <= DECODE_DOWN_SKINNY_MAX_M and not pf and not tp
-                     and be.part_norm_ok(M, layers[0]["wqkv"]))
+        fuse_norm = M <= DECODE_DOWN_SKINNY_MAX_M and not tp and be.part_norm_ok(M, layers[0]["wqkv"])
         # batch <= 4 (TP): silu(gate) * up inside the down GEMM; the down partials then go through the
         # reduce + norm consumer, so the next layer's input norm is not fused into its qkv GEMM
-        silu_fused = (not pf and (DECODE_SILU_FUSED == "1" or (DECODE_SILU_FUSED == "tp" and tp))
-                      and be.part_silu_ok(M, layers[0]["wgu"], layers[0]["wdown"]))
-        fuse_norm = fuse_norm and not silu_fused
+        silu_fused = tp and be.part_silu_ok(M, layers[0]["wgu"], layers[0]["wdown"])
         xn = None if fuse_norm else be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
-        o_skinny = not tp and not pf and M <= DECODE_OPROJ_SKINNY_MAX_M
-        merge = (DECODE_OPROJ_MERGE and DECODE_ROPE_FUSED and not pf and M <= DECODE_OPROJ_MERGE_MAX_M
-                 and not o_skinny and be.part_merge_ok(M, inp.meta, layers[0]["wo"], Hq, D))
-        # batch <= 4: attention and o_proj in ONE launch (attention.hip attn_oproj_kernel) -- the o_proj
-        # weight stream overlaps the KV stream instead of following it
-        # (never when another process drives this GPU: its waiting blocks could hold the CU slots this
-        # launch's producer blocks need)
-        fused_ao = (DECODE_ROPE_FUSED and not pf and not o_skinny
-                    and not (tp and getattr(self.comm, "shares_device", False))
-                    and be.attn_oproj_ok(M, inp.meta, layers[0]["wo"], Hq, Hkv, D))
-        # ... and, at TP=1, the residual + post-attention norm in its last block (no consumer launch)
-        ao_norm = fused_ao and not tp and be.attn_oproj_norm_ok(layers[0]["wo"])
-        # ... and the qkv projection with the input norm as well: the layer's attention half is ONE launch
-        qao = (ao_norm and fuse_norm
-               and be.qkv_attn_oproj_ok(M, inp.meta, layers[0]["wqkv"], layers[0]["wo"], Hq, Hkv, D))
-        # tensor parallel: the same launch on the rank's shard, fed by the fused reduction's normed rows
-        # and feeding its o_proj slabs to the next fused reduction
-        qao_tp = (tp and fused_ao
-                  and be.qkv_attn_oproj_ok(M, inp.meta, layers[0]["wqkv"], layers[0]["wo"], Hq, Hkv, D,
-                                           norm_tail=False))
-        # TP=1: the add_partials_rmsnorm consumers of the o_proj / down split-K GEMMs run in those GEMMs'
-        # last blocks (gemm_part.hip TL) -- one launch fewer per norm
-        tail_o = not tp and not pf and not fused_ao and not o_skinny and be.part_tail_ok(M, layers[0]["wo"])
-        tail_d = not tp and not pf and not silu_fused and be.part_tail_ok(M, layers[0]["wdown"])
+        merge = M <= DECODE_OPROJ_MERGE_MAX_M and be.part_merge_ok(M, inp.meta, layers[0]["wo"], Hq, D)
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
-            if qao:
-                xn = be.qkv_attn_oproj(h, L["ln_in"], c.rms_norm_eps, L["wqkv"], inp.positions, self.cos, self.sin,
-                                       inp.slots, kc, vc, inp.meta, L["wo"], Hq, Hkv, D, L["ln_post"], c.rms_norm_eps)
-            elif qao_tp:
-                P = be.qkv_attn_oproj(xn, None, 0.0, L["wqkv"], inp.positions, self.cos, self.sin, inp.slots, kc, vc,
-                                      inp.meta, L["wo"], Hq, Hkv, D, None, 0.0)
-            elif fuse_norm:
-                P = be.gemm_part_norm(h, L["ln_in"], c.rms_norm_eps, L["wqkv"])
-            else:
-                P = be.gemm_part(xn, L["wqkv"])
-            if qao or qao_tp:
-                pass
-            elif ao_norm:
-                xn = be.attn_oproj(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, L["wo"], Hq,
-                                   Hkv, D, norm=(h, L["ln_post"], c.rms_norm_eps))
-            elif fused_ao:
-                P = be.attn_oproj(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, L["wo"], Hq, Hkv,
-                                  D)
-            elif merge:
-                # RoPE + KV append inside the attention kernel, its split-K merge inside the o_proj GEMM
-                be.attn_decode_rope(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, attn,
-                                    Hq, Hkv, D, defer_merge=True)
-            elif DECODE_ROPE_FUSED and not pf:
-                # RoPE + KV append inside the attention kernel (one launch fewer per layer)
-                be.attn_decode_rope(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, attn,
-                                    Hq, Hkv, D)
-            else:
-                if pf and pf["rope"]:
-                    be.pf_arm([(L["wo"], 0, pf["rope"])], pf["blocks"])
-                be.rope_kv_partials(P, q, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
-                if pf and pf["attn"]:
-                    be.pf_arm([(L["wo"], pf["rope"], pf["attn"] // 2), (L["wgu"], 0, pf["attn"] // 2)],
-                              pf["blocks"])
-                be.attn_decode(q, kc, vc, inp.meta, attn, Hq, Hkv, D)
-            if o_skinny:
-                be.gemm(attn, L["wo"], resid=h, epi="resid", out=h)
-                xn = be.rmsnorm(h, L["ln_post"], c.rms_norm_eps)
-            elif tail_o:
-                # TP=1: the residual add + post-attention norm in the o_proj GEMM's last blocks
-                xn = (be.gemm_part_merge_tail(attn, inp.meta, L["wo"], Hq, h, L["ln_post"], c.rms_norm_eps) if merge
-                      else be.gemm_part_tail(attn, L["wo"], h, L["ln_post"], c.rms_norm_eps))
-            elif not fused_ao:
-                P = be.gemm_part_merge(attn, inp.meta, L["wo"], Hq) if merge else be.gemm_part(attn, L["wo"])
-            if pf:
-                be.pf_arm([(L["wgu"], pf["attn"] // 2, pf["post"])], pf["blocks"])
-            if not ao_norm and not tail_o and not o_skinny:
-                xn = reduce_norm(P, L["ln_post"])
+            P = be.gemm_part_norm(h, L["ln_in"], c.rms_norm_eps, L["wqkv"]) if fuse_norm else be.gemm_part(xn, L["wqkv"])
+            # RoPE + KV append inside the attention kernel; at batch <= 2 its split-K merge inside the o_proj GEMM
+            be.attn_decode_rope(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, attn, Hq, Hkv, D,
+                                defer_merge=merge)
+            P = be.gemm_part_merge(attn, inp.meta, L["wo"], Hq) if merge else be.gemm_part(attn, L["wo"])
+            xn = reduce_norm(P, L["ln_post"])
             nxt = layers[li + 1]["ln_in"] if li + 1 < len(layers) else w.norm
             if silu_fused:
                 P = be.gemm_part_silu(be.gemm_part_gu(xn, L["wgu"]), L["wdown"])
@@ -464,13 +366,7 @@ class LlamaModel:
                 if not fuse_norm or li + 1 == len(layers):
                     xn = be.rmsnorm(h, nxt, c.rms_norm_eps)
                 continue
-            if tail_d:
-                xn = be.gemm_part_tail(a, L["wdown"], h, nxt, c.rms_norm_eps)
-                continue
             P = be.gemm_part(a, L["wdown"])
-            if pf:
-                be.pf_arm([(layers[li + 1]["wqkv"] if li + 1 < len(layers) else w.lm_head, 0, pf["post"])],
-                          pf["blocks"])
             xn = reduce_norm(P, nxt)
         if inp.logits_idx is not None:
             xn = be.gather_rows(xn, inp.logits_idx)

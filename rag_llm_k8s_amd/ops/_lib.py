@@ -23,13 +23,8 @@ _SIGS = {
     "ragk_gemm": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_path": [I, P, I, P, I, P, I, P, P, I, I, I, I, I, S],
     "ragk_gemm_pp": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
-    "ragk_gemm_pp_set_variant": [I],
     "ragk_gemm_w4_set_grid": [I],
-    "ragk_gemm_w4_set_cont": [I],
-    "ragk_attn_prefill_set_prio": [I],
-    "ragk_attn_prefill_set_buf": [I],
     "ragk_gemm_stream_set_nt": [I],
-    "ragk_gemm_skinny_set_waves": [I],
     "ragk_gemm_stream_set_pair_rows": [I],
     "ragk_gemm_w4": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_w4_splitk": [P, I, P, I, P, I, I, I, I, S],
@@ -41,19 +36,9 @@ _SIGS = {
     "ragk_attn_decode_set_defer": [I],
     "ragk_gemm_part_merge": [P, P, P, I, P, I, I, I, P, I, P, P, I, I, I, I, S],
     "ragk_gemm_part_merge_ok": [I, I, I, I, I],
-    "ragk_gemm_part_tail_ints": [],
-    "ragk_gemm_skinny_set_unroll": [I],
     "ragk_gemm_stream_part": [P, I, P, I, P, I, I, I, I, I, S],
-    "ragk_gemm_part_tail": [P, I, P, I, P, I, I, I, I, P, I, P, P, I, F, P, ctypes.c_uint, S],
-    "ragk_gemm_part_merge_tail": [P, P, P, I, P, I, I, I, P, I, P, I, I, I, I, P, I, P, P, I, F, P, ctypes.c_uint, S],
     "ragk_gemm_part_silu": [P, I, P, I, P, I, I, I, I, S],
     "ragk_gemm_part_silu_ok": [I, I, I, I],
-    "ragk_attn_prefill_set_waves": [I],
-    "ragk_attn_prefill_set_pp": [I],
-    "ragk_attn_prefill_set_order": [I],
-    "ragk_attn_set_dbg": [P],
-    "ragk_attn_prefill_stamp": [P, I, P, P, P, I, P, P, P, I, P, I, I, I, F, P, S],
-    "ragk_gemm_w4_diag": [I, I, P, I, P, I, P, I, I, I, I, P, S],
     "ragk_gemm_part_ksteps": [I, I, I],
     "ragk_gemm_part_set_min_blocks": [I],
     "ragk_add_partials_rmsnorm": [P, I, I, P, I, P, P, I, I, F, S],
@@ -71,8 +56,8 @@ _SIGS = {
     "ragk_gather_rows": [P, I, P, P, I, I, I, S],
     "ragk_attn_prefill_qtile": [I, I],
     "ragk_attn_prefill": [P, I, P, P, I, P, I, P, P, P, P, I, P, I, I, I, I, I, I, F, S],
-    "ragk_attn_decode": [P, I, P, P, P, I, P, P, P, P, I, I, I, I, I, I, I, F, P, S],
-    "ragk_attn_decode_rope": [P, I, I, P, P, P, P, P, P, P, I, P, P, P, P, I, I, I, I, I, I, I, F, P, S],
+    "ragk_attn_decode": [P, I, P, P, P, I, P, P, P, P, I, I, I, I, I, I, I, F, S],
+    "ragk_attn_decode_rope": [P, I, I, P, P, P, P, P, P, P, I, P, P, P, P, I, I, I, I, I, I, I, F, S],
     "ragk_topk_candidates": [P, I, I, I, I, I, I, P, P, S],
     "ragk_sample_candidates": [P, P, I, I, P, P, P, P, P, P, P, S],
     "ragk_sample_candidates_lists": [P, P, I, I, I, P, P, P, P, P, P, P, S],
@@ -83,23 +68,12 @@ _SIGS = {
     "ragk_ivf_search": [P, I, I, P, I, P, I, P, P, P, I, P, P, P, P, S],
     "ragk_kmeans_assign": [P, I, I, P, P, I, P, P, P, S],
     "ragk_l2_scatter": [P, I, I, P, P, I, S],
-    "ragk_prefetch": [P, ctypes.c_longlong, I, P, S],
-    "ragk_spin_us": [I, S],
-    "ragk_spin_prefetch": [I, P, ctypes.c_longlong, I, P, S],
-    "ragk_pf_arm": [P, ctypes.c_longlong, P, ctypes.c_longlong, I, P],
     "ragk_l2_append": [P, I, I, I, P, I, S],
     "ragk_l2_gather": [P, I, I, P, I, P, S],
     "ragk_gemm_stream": [P, I, P, I, P, P, I, P, P, I, I, I, I, I, I, I, P, P, S],
     "ragk_gemm_stream_splits": [I, I, I, I],
     "ragk_quant_fp8_rows": [P, I, P, I, P, I, I, S],
     "ragk_gemm_fp8": [P, I, P, I, P, P, I, P, P, I, P, P, I, I, I, I, I, I, S],
-    "ragk_attn_oproj_fused": [P, I, I, P, P, P, P, P, P, P, I, P, P, P, I, I, I, I, I, I, F, P, I, P, I, I, P,
-                              ctypes.c_uint, P, I, P, P, I, F, P, S],
-    "ragk_attn_oproj_cnt_ints": [],
-    "ragk_fused_set_stamps": [P, S],
-    "ragk_attn_oproj_set_v2": [I],
-    "ragk_qkv_attn_oproj_fused": [P, I, P, F, P, I, I, I, P, I, P, P, P, P, P, P, P, I, P, P, P, I, I, I, I, I, I, F,
-                                  P, I, P, I, I, P, ctypes.c_uint, P, I, P, P, I, F, P, S],
     # csrc/comm/allreduce.hip (xGMI peer-mapped all-reduce)
     "ragk_ar_create": [I, I, ctypes.c_long, I, I, I],
     "ragk_ar_add_rmsnorm": [P, P, I, I, P, I, P, P, I, I, F, I, S],

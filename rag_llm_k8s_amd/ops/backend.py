@@ -117,9 +117,6 @@ class TorchBackend:
     def part_ok(self, M, w):
         return self.enable_part and M <= 64
 
-    def pf_arm(self, ranges, blocks):
-        """MALL prefetch hint for the next decode kernel (GPU only; nothing to do here)."""
-
     def gemm_part(self, x, w):
         wf = w.dequant() if isinstance(w, Fp8Weight) else w.float()
         return (x.float() @ wf.t()).unsqueeze(0)
@@ -148,16 +145,6 @@ class TorchBackend:
         h.copy_((h.float() + P.sum(0).to(h.dtype).float()).to(h.dtype))
         return R.rmsnorm(h, w, eps)
 
-    def part_tail_ok(self, M, w):
-        """The split-K GEMM may run its add_partials_rmsnorm consumer in its own last blocks (TP=1)."""
-        return self.enable_part and M <= 64 and not isinstance(w, Fp8Weight)
-
-    def gemm_part_tail(self, x, w, h, gamma, eps):
-        return self.add_partials_rmsnorm(self.gemm_part(x, w), h, gamma, eps)
-
-    def gemm_part_merge_tail(self, attn_out, meta: AttnMeta, w, Hq, h, gamma, eps):
-        return self.add_partials_rmsnorm(self.gemm_part_merge(attn_out, meta, w, Hq), h, gamma, eps)
-
     def rope_kv_partials(self, P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D):
         qkv = P.sum(0).to(q_out.dtype)
         self.rope_kv(qkv, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)
@@ -174,21 +161,13 @@ class TorchBackend:
         out.copy_(o.reshape(T, Hq * D))
         return out
 
-    def attn_decode_rope(self, P, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, out, Hq, Hkv, D):
+    def attn_decode_rope(self, P, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, out, Hq, Hkv, D,
+                         defer_merge=False):
         q = torch.empty((P.shape[1], Hq * D), dtype=out.dtype, device=out.device)
         self.rope_kv_partials(P, q, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)
         return self.attn_decode(q, kc, vc, meta, out, Hq, Hkv, D)
 
     def part_merge_ok(self, M, meta: AttnMeta, w, Hq, D):
-        return False
-
-    def attn_oproj_ok(self, M, meta: AttnMeta, w, Hq, Hkv, D):
-        return False
-
-    def attn_oproj_norm_ok(self, w):
-        return False
-
-    def qkv_attn_oproj_ok(self, M, meta: AttnMeta, wqkv, wo, Hq, Hkv, D, norm_tail=True):
         return False
 
     def prefill_nsplit(self, M, w):
@@ -249,9 +228,6 @@ class NativeBackend(TorchBackend):
 
         self.n = native
         native._lib.lib()  # fail loudly now if the gfx950 library is missing
-        if torch.device(device).type == "cuda" and torch.cuda.is_available():
-            native.attn_oproj_counters(device)  # before any graph capture
-            native.part_tail_counters(device)
 
     def gemm(self, x, w, bias=None, resid=None, epi="none", out=None, out_f32=False):
         if isinstance(w, Fp8Weight):
@@ -304,21 +280,8 @@ class NativeBackend(TorchBackend):
     def gemm_part_silu(self, pgu, w):
         return self.n.gemm_part_silu(pgu, w)
 
-    def pf_arm(self, ranges, blocks):
-        self.n.pf_arm(ranges, blocks)
-
     def add_partials_rmsnorm(self, P, h, w, eps):
         return self.n.add_partials_rmsnorm(P, h, w, eps)
-
-    def part_tail_ok(self, M, w):
-        return self.enable_part and self.n.part_tail_ok(M, w)
-
-    def gemm_part_tail(self, x, w, h, gamma, eps):
-        return self.n.gemm_part_tail(x, w, h, gamma, eps)
-
-    def gemm_part_merge_tail(self, attn_out, meta: AttnMeta, w, Hq, h, gamma, eps):
-        return self.n.gemm_part_merge_tail(attn_out, meta.kv_lens, meta.part_tiles, meta.max_parts, meta.ws_o,
-                                           meta.ws_ml, Hq, w, h, gamma, eps)
 
     def rope_kv_partials(self, P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D):
         self.n.rope_kv_partials(P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)
@@ -342,28 +305,8 @@ class NativeBackend(TorchBackend):
         return self.n.gemm_splitk(x, w, nsplit)
 
     def part_merge_ok(self, M, meta: AttnMeta, w, Hq, D):
-        return (self.enable_part and D == 128 and not self.n.ATTN_FUSED_MERGE
+        return (self.enable_part and D == 128
                 and self.n.gemm_part_merge_ok(M, w, Hq, meta.max_parts, meta.ws_o))
-
-    def attn_oproj_ok(self, M, meta: AttnMeta, w, Hq, Hkv, D):
-        return self.enable_part and self.n.attn_oproj_ok(M, w, Hq, Hkv, D, meta.max_parts, meta.ws_o)
-
-    def attn_oproj(self, P, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, w, Hq, Hkv, D, norm=None):
-        return self.n.attn_oproj(P, positions, cos_t, sin_t, slots, kc, vc, meta.block_tables, meta.kv_lens, Hq, Hkv,
-                                 D, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml, w, norm=norm)
-
-    def attn_oproj_norm_ok(self, w):
-        return self.n.ATTN_OPROJ_NORM and w.shape[1] // (64 * self.n.ATTN_OPROJ_KS) <= 16
-
-    def qkv_attn_oproj_ok(self, M, meta: AttnMeta, wqkv, wo, Hq, Hkv, D, norm_tail=True):
-        return self.enable_part and self.n.qkv_attn_oproj_ok(M, wqkv, wo, Hq, Hkv, D, meta.max_parts, meta.ws_o,
-                                                             norm_tail=norm_tail)
-
-    def qkv_attn_oproj(self, h, g_in, eps_in, wqkv, positions, cos_t, sin_t, slots, kc, vc, meta: AttnMeta, wo, Hq,
-                       Hkv, D, g_post, eps):
-        return self.n.qkv_attn_oproj(h, g_in, eps_in, wqkv, positions, cos_t, sin_t, slots, kc, vc, meta.block_tables,
-                                     meta.kv_lens, Hq, Hkv, D, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml,
-                                     wo, g_post, eps)
 
     def gemm_part_merge(self, attn_out, meta: AttnMeta, w, Hq):
         return self.n.gemm_part_merge(attn_out, meta.kv_lens, meta.part_tiles, meta.max_parts, meta.ws_o, meta.ws_ml,

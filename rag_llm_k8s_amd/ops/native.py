@@ -28,18 +28,8 @@ def _bf16_2d(t, name):
 
 
 # ----------------------------------------------------------------------------- GEMM
-PP_MIN_M = int(os.environ.get("RAGK_PP_MIN_M", "1024"))
-PP_VARIANT = int(os.environ.get("RAGK_PP_VARIANT", "2"))
-# large-M kernel: "w4" (default) = 4-wave 128x128-per-wave (gemm_w4.hip, path 6), "pp" = 8-wave
-# ping-pong (path 2); the residual-add projections go to hipBLASLt by default (PREFILL_BLAS below).
-PREFILL_GEMM = os.environ.get("RAGK_PREFILL_GEMM", "w4")
-_pp_variant_set = [None]
-
-
-def set_pp_variant(v):
-    """2: two 64-deep K buffers; 4: four 32-deep buffers, 3-tile-deep DMA (gemm_pp.hip)."""
-    check(_lib.lib().ragk_gemm_pp_set_variant(int(v)), "ragk_gemm_pp_set_variant")
-    _pp_variant_set[0] = int(v)
+# large-M GEMMs (prefill) go to the 256x256 MFMA kernels from this many rows
+PP_MIN_M = 1024
 
 
 def set_w4_grid(g):
@@ -48,20 +38,10 @@ def set_w4_grid(g):
     check(_lib.lib().ragk_gemm_w4_set_grid(int(g)), "ragk_gemm_w4_set_grid")
 
 
-def set_skinny_waves(w):
-    """Waves per block of the skinny decode GEMM (one row tile): 8, 16, or -1 = auto (8;
-    RAGK_SKINNY_WAVES overrides). 16 measured slower on the batch-1 down projection."""
-    check(_lib.lib().ragk_gemm_skinny_set_waves(int(w)), "ragk_gemm_skinny_set_waves")
 
 
-def set_w4_cont(on):
-    """gemm_w4 continuous K-stream kernel (K < 8192): 1 = on (default), 0 = the per-tile-prologue
-    kernel, -1 = back to RAGK_W4_CONT / the default."""
-    check(_lib.lib().ragk_gemm_w4_set_cont(int(on)), "ragk_gemm_w4_set_cont")
-
-
-DEC_DEFAULT = os.environ.get("RAGK_DEC_GEMM", "1") == "1"
-DEC_WS_BYTES = int(os.environ.get("RAGK_DEC_WS_MB", "96")) << 20
+DEC_DEFAULT = True
+DEC_WS_BYTES = 96 << 20
 _dec_ws = {}
 
 
@@ -81,12 +61,12 @@ def use_dec(M, N, K, epi):
     return 16 < M <= 64 and N >= 32768 and K % 256 == 0 and epi != "silu_mul"
 
 
-STREAM_DEFAULT = os.environ.get("RAGK_STREAM_GEMM", "1") == "1"
-STREAM_MIN_ROWS = int(os.environ.get("RAGK_STREAM_MIN_ROWS", "16384"))
+STREAM_DEFAULT = True
+STREAM_MIN_ROWS = 16384
 # vocab-sized weights (>= 32768 rows, the lm_head) go to the stream GEMM (nt weights) only above batch 16:
 # batch 32 6.97 -> 6.94 ms per decode step, batch 4 slower (profiles/decode_lmhead_stream_r4.log)
-STREAM_MAX_ROWS = int(os.environ.get("RAGK_STREAM_MAX_ROWS", "262144"))
-STREAM_VOCAB_MIN_M = int(os.environ.get("RAGK_STREAM_VOCAB_MIN_M", "17"))
+STREAM_MAX_ROWS = 262144
+STREAM_VOCAB_MIN_M = 17
 
 
 def use_stream(M, N, K, epi, fp8=False):
@@ -105,7 +85,7 @@ def use_stream(M, N, K, epi, fp8=False):
 def use_pp(M, N, K, epi):
     """Large-M GEMMs go to a 256x256 MFMA kernel: gemm_w4.hip (default, 4 waves x 128x128, 9-16 %
     faster on the Llama-8B prefill shapes, profiles/gemm_w4_r1.txt) or the 8-wave ping-pong gemm_pp.hip."""
-    if M < PP_MIN_M or K % 64:
+    if M < PP_MIN_M or K % 64 or K < 192:  # gemm_w4's continuous ring needs three K-tiles per tile
         return False
     return N % 128 == 0 if epi == "silu_mul" else N % 8 == 0
 
@@ -119,10 +99,6 @@ def use_pp(M, N, K, epi):
 # library form. "none": every large-M GEMM on gemm_w4 (0 library kernels); "plain": no-epilogue GEMMs
 # only; "all": both.
 PREFILL_BLAS = os.environ.get("RAGK_PREFILL_BLAS", "resid")
-# Optional K filter for the library route (A/B of the per-projection choice): comma-separated K values
-# (e.g. "4096" = o_proj only, "14336" = down only); empty = every K. Both on the library is best: bench
-# 1638 tok/s vs 1632 (down only) / 1616 (o_proj only) (profiles/bench_blas_ks_ab_r4.log).
-PREFILL_BLAS_KS = {int(k) for k in os.environ.get("RAGK_PREFILL_BLAS_KS", "").split(",") if k.strip()}
 
 
 def _gemm_blas(x, w, resid, out, epi):
@@ -163,14 +139,13 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
     ldr = resid.stride(0) if resid is not None else 0
     if (path is None and PREFILL_BLAS != "none" and not out_f32 and bias is None and use_pp(M, N, K, epi)
             and ((epi == "none" and PREFILL_BLAS in ("plain", "all"))
-                 or (epi == "resid" and PREFILL_BLAS in ("resid", "all")))
-            and (not PREFILL_BLAS_KS or K in PREFILL_BLAS_KS)):
+                 or (epi == "resid" and PREFILL_BLAS in ("resid", "all")))):
         return _gemm_blas(x, w, resid, out, epi)
     if path is None and use_pp(M, N, K, epi):
         rows = w.shape[0]
         # gemm_w4 addresses operands with 32-bit buffer offsets
         fits = x.stride(0) * M * 2 < 2 ** 31 and w.stride(0) * rows * 2 < 2 ** 31
-        path = 6 if (PREFILL_GEMM == "w4" and fits) else 2
+        path = 6 if fits else 2  # gemm_pp (8-wave ping-pong, 64-bit addressing): operands past 2 GiB
     if path is None and STREAM_DEFAULT and use_stream(M, N, K, epi):
         path = 5
     if path is None and DEC_DEFAULT and use_dec(M, N, K, epi):
@@ -187,8 +162,6 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
                              ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), S, ws.data_ptr(), cnt.data_ptr(),
                              stream_ptr())
     elif path == 2:
-        if _pp_variant_set[0] is None:
-            set_pp_variant(PP_VARIANT)
         rc = L.ragk_gemm_pp(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0),
                             ptr(bias), ptr(resid), ldr, M, N, K, e, int(out_f32), stream_ptr())
     elif path == 6:
@@ -204,7 +177,7 @@ def gemm(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False, path=
     return out
 
 
-PART_MIN_BLOCKS = int(os.environ.get("RAGK_PART_MIN_BLOCKS", "512"))
+PART_MIN_BLOCKS = 512
 _part_cfg = [False]
 
 
@@ -245,10 +218,10 @@ def gemm_part_norm(h, gamma, eps, w, out=None, ks=None):
 # activation slice needs 114 KB of LDS per gemm_part block at batch 32 (one block per CU, two rounds).
 # Batch 32: decode step 7.35 / 7.33 -> 6.91 / 6.98 ms, bench 1568 / 1570 -> 1597 / 1595 tok/s (same box,
 # alternating; profiles/bench_stream_part_ab_r4.log).
-STREAM_PART = os.environ.get("RAGK_DECODE_STREAM_PART", "1") == "1"
-STREAM_PART_MIN_M = int(os.environ.get("RAGK_STREAM_PART_MIN_M", "5"))  # batch 8 / 16 -3 %, batch 4 +0.6 %
-STREAM_PART_ROWS = int(os.environ.get("RAGK_STREAM_PART_ROWS", "0"))  # 0: by occupancy (ties: 128)
-STREAM_PART_MAX_S = int(os.environ.get("RAGK_STREAM_PART_MAX_S", "64"))  # slabs the consumer sums
+STREAM_PART = True
+STREAM_PART_MIN_M = 5  # batch 8 / 16 -3 %, batch 4 +0.6 %
+STREAM_PART_ROWS = 0  # 0: by occupancy (ties: 128)
+STREAM_PART_MAX_S = 64  # slabs the consumer sums
 
 
 def stream_part_cfg(M, N, K):
@@ -328,104 +301,10 @@ def gemm_part(x, w, out=None, ks=None):
     return out[:S] if out.dim() == 3 else out
 
 
-# The residual add + RMSNorm consumer of a split-K decode GEMM inside the GEMM's last M blocks
-# (gemm_part.hip TL): TP=1 o_proj and down, every decode batch. Off by default: measured SLOWER than the
-# separate add_partials_rmsnorm launch it replaces (one counter: 3.74-3.81 vs 3.62 ms per step at batch 1,
-# 7.78-7.84 vs 7.54 at batch 32; per-XCD sharded counters: 3.71 vs 3.58 and 7.68 vs 7.57;
-# profiles/decode_tail_ab_r4.log) -- kept, tested bit-exact, for A/B (RAGK_DECODE_PART_TAIL=1).
-PART_TAIL = os.environ.get("RAGK_DECODE_PART_TAIL", "0") == "1"
-PART_TAIL_SPIN_US = int(os.environ.get("RAGK_PART_TAIL_SPIN_US", "1000000"))
-_tail_cnt = {}
-
-
-def part_tail_counters(device):
-    """Shard / top arrival counters, done flags, finish counter and timeout word of the tail launches
-    (gemm_part.hip TL_*): zeroed once, re-armed by every launch itself; allocated when the native backend
-    is created, never inside a graph capture."""
-    key = _dev_key(device)
-    if key not in _tail_cnt:
-        _req(not torch.cuda.is_current_stream_capturing(), "tail counters allocated inside a graph capture")
-        n = int(_lib.lib().ragk_gemm_part_tail_ints())
-        _tail_cnt[key] = torch.zeros(n, dtype=torch.int32, device=torch.device("cuda", key))
-    return _tail_cnt[key]
-
-
-def part_tail_armed(device) -> bool:
-    """Every counter and flag back at zero (the timeout word aside)."""
-    c = part_tail_counters(device)
-    return int(c[:-32].abs().sum().item()) == 0
-
-
-def part_tail_error(device) -> bool:
-    c = _tail_cnt.get(_dev_key(device))
-    return bool(c is not None and int(c[-32].item()) != 0)
-
-
-def part_tail_ok(M, w) -> bool:
-    """bf16 weights with N <= 8192 columns, a grid of at least M blocks."""
-    from .fp8 import Fp8Weight
-
-    if not PART_TAIL or isinstance(w, Fp8Weight) or not (1 <= M <= 64):
-        return False
-    N, K = w.shape
-    ks, S = gemm_part_slabs(M, N, K)
-    return S > 0 and N % 8 == 0 and N <= 8192 and -(-N // 64) * S >= 8 * -(-M // 8)
-
-
-def _tail_args(h, gamma, eps, xn, N):
-    _bf16_2d(h, "h")
-    _req(h.shape[1] == N and gamma.numel() == N and gamma.dtype == torch.bfloat16 and gamma.is_contiguous(),
-         "tail residual / norm weights")
-    if xn is None:
-        xn = torch.empty_like(h)
-    _req(xn.shape == h.shape and xn.stride(1) == 1, "tail output rows")
-    cnt = part_tail_counters(h.device)
-    return xn, (h.data_ptr(), h.stride(0), gamma.data_ptr(), xn.data_ptr(), xn.stride(0), float(eps), cnt.data_ptr(),
-                PART_TAIL_SPIN_US * 100)
-
-
-def gemm_part_tail(x, w, h, gamma, eps, xn=None, P=None):
-    """gemm_part + add_partials_rmsnorm in one launch: h += bf16(x @ w^T) (the split-K slabs summed in
-    slab order, rounded once), returns rmsnorm(h) * gamma -- the same values as the two launches."""
-    _bf16_2d(x, "x")
-    _bf16_2d(w, "w")
-    M, K = x.shape
-    N = w.shape[0]
-    _req(w.shape[1] == K and h.shape[0] == M, "gemm_part_tail shape")
-    ks, S = gemm_part_slabs(M, N, K)
-    _req(S > 0, "gemm_part_tail: unsupported K=%d" % K)
-    if P is None:
-        P = torch.empty((S, M, N), dtype=torch.float32, device=x.device)
-    xn, ta = _tail_args(h, gamma, eps, xn, N)
-    check(_lib.lib().ragk_gemm_part_tail(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), P.data_ptr(), M, N, K, ks,
-                                         *ta, stream_ptr()), "ragk_gemm_part_tail")
-    return xn
-
-
-def gemm_part_merge_tail(attn_out, kv_lens, part_tiles, max_parts, ws_o, ws_ml, Hq, w, h, gamma, eps, xn=None):
-    """gemm_part_merge + add_partials_rmsnorm in one launch (batch <= 4 o_proj): returns the normed rows."""
-    M = kv_lens.numel()
-    N, K = w.shape
-    _bf16_2d(w, "w")
-    _req(attn_out.dtype == torch.bfloat16 and attn_out.stride(1) == 1 and attn_out.shape[0] >= M
-         and attn_out.shape[1] == K and h.shape[0] == M, "attention output rows")
-    _req(ws_o is not None and ws_o.dtype == torch.float32 and ws_o.numel() >= M * Hq * max_parts * 128
-         and ws_ml.numel() >= M * Hq * max_parts * 2, "partition workspace")
-    ks, S = gemm_part_slabs(M, N, K)
-    _req(S > 0 and _lib.lib().ragk_gemm_part_merge_ok(M, K, Hq, max_parts, ks), "gemm_part_merge shape")
-    P = torch.empty((S, M, N), dtype=torch.float32, device=attn_out.device)
-    xn, ta = _tail_args(h, gamma, eps, xn, N)
-    check(_lib.lib().ragk_gemm_part_merge_tail(
-        ws_o.data_ptr(), ws_ml.data_ptr(), attn_out.data_ptr(), attn_out.stride(0), kv_lens.data_ptr(), Hq,
-        part_tiles, max_parts, w.data_ptr(), w.stride(0), P.data_ptr(), M, N, K, ks, *ta, stream_ptr()),
-        "ragk_gemm_part_merge_tail")
-    return xn
-
-
-PREFILL_SPLITK = os.environ.get("RAGK_PREFILL_SPLITK", "1") == "1"
+PREFILL_SPLITK = True
 # measured: M = 5.2k (one RAG prompt) 2 slabs win (o_proj + down 760 -> 656 us per layer); a ~2.2k-token
 # tail step with 4 slabs was no faster than unsplit in the bench profile -> split only M >= 4096, 2 slabs
-PREFILL_SPLITK_MIN_M = int(os.environ.get("RAGK_PREFILL_SPLITK_MIN_M", "4096"))
+PREFILL_SPLITK_MIN_M = 4096
 _n_cus = [0]
 
 
@@ -459,7 +338,7 @@ def prefill_nsplit(M, N, K):
 
 
 def gemm_splitk(x, w, nsplit, out=None):
-    """fp32 split-K slabs P[nsplit, M, N] with P.sum(0) = x @ w^T, one persistent gemm_w4c launch
+    """fp32 split-K slabs P[nsplit, M, N] with P.sum(0) = x @ w^T, one persistent gemm_w4 launch
     (csrc/kernels/gemm_w4.hip KSPLIT); consumed by add_partials_rmsnorm (residual add + norm)."""
     _bf16_2d(x, "x")
     _bf16_2d(w, "w")
@@ -511,183 +390,6 @@ def gemm_part_merge(attn_out, kv_lens, part_tiles, max_parts, ws_o, ws_ml, Hq, w
         part_tiles, max_parts, wt.data_ptr(), wt.stride(0), w.scale.data_ptr() if fp8 else None, out.data_ptr(), M, N,
         K, ks, stream_ptr()), "ragk_gemm_part_merge")
     return out
-
-
-# Fused decode attention + o_proj (attention.hip attn_oproj_kernel): one launch in place of
-# attn_decode_rope(defer_merge) -> gemm_part_merge at batch <= 4. RAGK_DECODE_ATTN_OPROJ=0 disables.
-# Off by default: measured slower than the separate kernels at C=1 (3.66 vs 3.53 ms per token; the launch's
-# dependent hand-offs under the shared memory load cost what the kernel boundaries did -- docs/PERF_NOTES.md
-# round 4, profiles/fused_stamps_*_r4.log). Kept, tested, for the A/B and the TP-shard probe.
-ATTN_OPROJ = os.environ.get("RAGK_DECODE_ATTN_OPROJ", "0") == "1"
-ATTN_OPROJ_KS = int(os.environ.get("RAGK_ATTN_OPROJ_KS", "8"))  # K-slice steps of 64 (4, 8 or 16)
-# the residual + RMSNorm consumer inside the fused launch (its last o_proj block), TP=1 only
-ATTN_OPROJ_NORM = os.environ.get("RAGK_ATTN_OPROJ_NORM", "1") == "1"
-ATTN_OPROJ_SPIN_US = int(os.environ.get("RAGK_ATTN_OPROJ_SPIN_US", "1000000"))
-# where the split-K attention partitions are merged inside the fused launch: 1 = by the last partition
-# block of each (sequence, KV head), into a bf16 row the o_proj blocks stage (once per head);
-# 0 = by every o_proj block for the heads of its K-slice (no extra hand-off, redundant record reads)
-ATTN_OPROJ_MIA = os.environ.get("RAGK_AO_MIA", "1") == "1"
-# v2 o_proj role (attention.hip oproj_full_block): 16 output columns x the full K per block, all resident
-# next to the attention blocks, no split-K slabs (the residual / norm, or the TP partial row, written by
-# the blocks themselves). MIA launches with K in {512, ..., 4096} only.
-ATTN_OPROJ_V2 = os.environ.get("RAGK_AO_V2", "1") == "1"
-_ao_v2_set = [None]
-
-
-def _ao_v2(K, N):
-    on = ATTN_OPROJ_MIA and ATTN_OPROJ_V2 and K in (512, 1024, 2048, 4096) and -(-N // 16) <= 512
-    if _ao_v2_set[0] != ATTN_OPROJ_V2:
-        check(_lib.lib().ragk_attn_oproj_set_v2(int(ATTN_OPROJ_V2)), "ragk_attn_oproj_set_v2")
-        _ao_v2_set[0] = ATTN_OPROJ_V2
-    return on
-_ao_ws = {}
-
-
-def _ao_attn_out(B, K, device):
-    """bf16 [B, K] attention-output workspace of the fused launch (MIA); one per (device, shape)."""
-    key = (_dev_key(device), B, K)
-    t = _ao_ws.get(key)
-    if t is None:
-        t = _ao_ws[key] = torch.empty((B, K), dtype=torch.bfloat16, device=torch.device("cuda", key[0]))
-    return t
-_ao_cnt = {}
-
-
-def attn_oproj_ok(M, w, Hq, Hkv, D, max_parts, ws_o):
-    """The fused launch's shape limits: batch <= 4, head dim 128, 4 or 8 query heads per KV head, bf16
-    o_proj weight whose K = Hq * 128 splits into whole 64 * ks slices, <= 64 partitions."""
-    from .fp8 import Fp8Weight
-
-    if not ATTN_OPROJ or isinstance(w, Fp8Weight) or ws_o is None or not (1 <= M <= 4) or D != 128:
-        return False
-    if Hq % Hkv or Hq // Hkv not in (4, 8) or max_parts > 64:
-        return False
-    N, K = w.shape
-    return w.dtype == torch.bfloat16 and K == Hq * D and K % (64 * ATTN_OPROJ_KS) == 0
-
-
-def _dev_key(device):
-    d = torch.device(device)
-    return d.index if d.index is not None else torch.cuda.current_device()
-
-
-def attn_oproj_counters(device):
-    """The fused launch's counters (attention done, o_proj past its wait, error, -, qkv done): zeroed once,
-    re-armed by the kernel itself after every launch (graph replays included). Allocated when the native
-    backend is created, never inside a graph capture (the buffer must outlive every graph)."""
-    key = _dev_key(device)
-    if key not in _ao_cnt:
-        _req(not torch.cuda.is_current_stream_capturing(), "fused-launch counters allocated inside a graph capture")
-        n = int(_lib.lib().ragk_attn_oproj_cnt_ints())
-        _ao_cnt[key] = torch.zeros(max(n, 16), dtype=torch.int32, device=torch.device("cuda", key))
-    return _ao_cnt[key]
-
-
-def attn_oproj_armed(device) -> bool:
-    """Every counter, done flag and merge ticket of the fused launches back at zero (the v2 o_proj blocks'
-    sum-of-squares partials at the end of the buffer are scratch and not checked)."""
-    c = attn_oproj_counters(device).clone()
-    c[2] = 0  # error word
-    return int(c[:int(_lib.lib().ragk_attn_oproj_cnt_ints()) - 4 * 512].abs().sum().item()) == 0
-
-
-def attn_oproj_error(device) -> bool:
-    c = _ao_cnt.get(_dev_key(device))
-    return bool(c is not None and int(c[2].item()) != 0)
-
-
-def attn_oproj(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_tables, kv_lens, Hq, Hkv, D, part_tiles,
-               max_parts, ws_o, ws_ml, w, out=None, scale=None, norm=None):
-    """o_proj split-K partials Po [K / KS, M, N] of the decode attention of the qkv partial slabs P [S, M, ldp]
-    (RoPE + KV append at `slots`, as attn_decode_rope), in ONE launch (attention.hip attn_oproj_kernel): the
-    o_proj blocks stream their weights while the attention blocks stream the KV cache, then merge the
-    partitions of their K-slice and multiply. Same consumer as gemm_part_merge (add_partials_rmsnorm).
-    norm = (h, gamma, eps): the last o_proj block also does that consumer's work -- h += bf16(sum of the
-    slabs) in place, and the function returns xn = rmsnorm(h) * gamma instead of the slabs."""
-    _req(P.dtype == torch.float32 and P.is_contiguous() and P.dim() == 3, "partials")
-    S, B, ldp = P.shape
-    N, K = w.shape
-    _req(attn_oproj_ok(B, w, Hq, Hkv, D, max_parts, ws_o), "fused attention + o_proj shape")
-    _req(kv_lens.numel() == B and positions.numel() == B and slots.numel() == B, "one row per sequence")
-    _req(k_cache.dim() == 4 and k_cache.shape[1] == Hkv and k_cache.shape[2] == 64 and k_cache.shape[3] == D,
-         "paged cache")
-    _req(ws_o.numel() >= B * Hq * max_parts * D and ws_ml.numel() >= B * Hq * max_parts * 2, "partition workspace")
-    ks = ATTN_OPROJ_KS
-    if out is None:
-        out = torch.empty((1 if _ao_v2(K, N) else K // (64 * ks), B, N), dtype=torch.float32, device=P.device)
-    scale = 1.0 / math.sqrt(D) if scale is None else scale
-    cnt = attn_oproj_counters(P.device)
-    h = gamma = xn = None
-    eps = 0.0
-    if norm is not None:
-        h, gamma, eps = norm
-        _req(h.dtype == torch.bfloat16 and h.shape == (B, N) and h.stride(1) == 1 and gamma.numel() == N
-             and gamma.is_contiguous() and K // (64 * ks) <= 16, "norm tail: h [B, N] bf16, <= 16 slabs")
-        xn = torch.empty((B, N), dtype=torch.bfloat16, device=P.device)
-    check(_lib.lib().ragk_attn_oproj_fused(
-        P.data_ptr(), S, ldp, positions.data_ptr(), slots.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(),
-        k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0), kv_lens.data_ptr(),
-        ws_o.data_ptr(), ws_ml.data_ptr(), B, Hq, Hkv, D, part_tiles, max_parts, float(scale), w.data_ptr(),
-        w.stride(0), out.data_ptr(), N, ks, cnt.data_ptr(), ATTN_OPROJ_SPIN_US, ptr(h), h.stride(0) if h is not None
-        else 0, ptr(gamma), ptr(xn), xn.stride(0) if xn is not None else 0, float(eps),
-        ptr(_ao_attn_out(B, K, P.device)) if ATTN_OPROJ_MIA else None, stream_ptr()), "ragk_attn_oproj_fused")
-    return out if norm is None else xn
-
-
-# The 3-role launch (qkv with the input norm + attention + o_proj + post-attention norm tail) at TP=1,
-# batch <= 4: RAGK_DECODE_QAO=0 falls back to gemm_part_norm + the 2-role launch.
-QAO = os.environ.get("RAGK_DECODE_QAO", "1") == "1"
-QAO_QKS = int(os.environ.get("RAGK_QAO_QKS", "16"))  # qkv K-slice steps of 64 (8 or 16)
-
-
-def qkv_attn_oproj_ok(M, wqkv, wo, Hq, Hkv, D, max_parts, ws_o, norm_tail=True):
-    from .fp8 import Fp8Weight
-
-    if not QAO or (norm_tail and not ATTN_OPROJ_NORM) or isinstance(wqkv, Fp8Weight):
-        return False
-    if not attn_oproj_ok(M, wo, Hq, Hkv, D, max_parts, ws_o):
-        return False
-    Nq, K = wqkv.shape
-    return (wqkv.dtype == torch.bfloat16 and Nq == (Hq + 2 * Hkv) * D and K <= 4096 and K % (64 * QAO_QKS) == 0
-            and ATTN_OPROJ_KS == 8 and (not norm_tail or wo.shape[1] // (64 * ATTN_OPROJ_KS) <= 16))
-
-
-def qkv_attn_oproj(h, g_in, eps_in, wqkv, positions, cos_t, sin_t, slots, k_cache, v_cache, block_tables, kv_lens, Hq,
-                   Hkv, D, part_tiles, max_parts, ws_o, ws_ml, wo, g_post, eps, scale=None):
-    """One decode layer's attention half in ONE launch (attention.hip attn_oproj_kernel, 3 roles): qkv split-K
-    partials of rmsnorm(h) * g_in (gemm_part_norm's math), then RoPE + KV append + split-K attention (the
-    attention blocks prefetch their first KV tile while the qkv weights stream), then o_proj (weights
-    prefetched meanwhile) with the residual add into h (in place) and the post-attention RMSNorm in the last
-    block. Returns xn = rmsnorm(h + o_proj(attention)) * g_post.
-    Tensor parallel (g_in None, g_post None): h is this rank's already-normalised input rows, and the o_proj
-    split-K slabs [S, M, N] are returned for the cross-rank reduction + residual + norm consumer."""
-    B, K = h.shape
-    Nq = wqkv.shape[0]
-    N = wo.shape[0]
-    tail = g_post is not None
-    _req(qkv_attn_oproj_ok(B, wqkv, wo, Hq, Hkv, D, max_parts, ws_o, norm_tail=tail),
-         "fused qkv + attention + o_proj shape")
-    _req(h.dtype == torch.bfloat16 and h.stride(1) == 1 and h.stride(0) % 8 == 0 and (N == K or not tail),
-         "residual rows")
-    _req(kv_lens.numel() == B and positions.numel() == B and slots.numel() == B, "one row per sequence")
-    _req(ws_o.numel() >= B * Hq * max_parts * D and ws_ml.numel() >= B * Hq * max_parts * 2, "partition workspace")
-    qks, ks = QAO_QKS, ATTN_OPROJ_KS
-    Pq = torch.empty((K // (64 * qks), B, Nq), dtype=torch.float32, device=h.device)
-    Po = torch.empty((1 if _ao_v2(wo.shape[1], N) else wo.shape[1] // (64 * ks), B, N), dtype=torch.float32,
-                     device=h.device)
-    xn = torch.empty((B, N), dtype=torch.bfloat16, device=h.device) if tail else None
-    scale = 1.0 / math.sqrt(D) if scale is None else scale
-    cnt = attn_oproj_counters(h.device)
-    check(_lib.lib().ragk_qkv_attn_oproj_fused(
-        h.data_ptr(), h.stride(0), ptr(g_in), float(eps_in), wqkv.data_ptr(), wqkv.stride(0), Nq, K,
-        Pq.data_ptr(), qks, positions.data_ptr(), slots.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(),
-        k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0), kv_lens.data_ptr(),
-        ws_o.data_ptr(), ws_ml.data_ptr(), B, Hq, Hkv, D, part_tiles, max_parts, float(scale), wo.data_ptr(),
-        wo.stride(0), Po.data_ptr(), N, ks, cnt.data_ptr(), ATTN_OPROJ_SPIN_US, h.data_ptr() if tail else None,
-        h.stride(0) if tail else 0, ptr(g_post), ptr(xn), xn.stride(0) if tail else 0, float(eps),
-        ptr(_ao_attn_out(B, wo.shape[1], h.device)) if ATTN_OPROJ_MIA else None, stream_ptr()),
-        "ragk_qkv_attn_oproj_fused")
-    return xn if tail else Po
 
 
 SILU_MAX_SLABS = 4  # gemm_part.hip SG_MAXS
@@ -784,7 +486,7 @@ def quant_fp8_rows(x, q=None, scale=None):
     return q, scale
 
 
-FP8_DEC_STREAM = os.environ.get("RAGK_FP8_DEC", "auto") != "regs"
+FP8_DEC_STREAM = True
 
 
 def gemm_fp8(x, w, bias=None, resid=None, epi="none", out=None, out_f32=False):
@@ -962,44 +664,13 @@ def gather_rows(x, idx, out=None):
 
 
 # ----------------------------------------------------------------------------- attention
-PREFILL_WAVES = int(os.environ.get("RAGK_PREFILL_WAVES", "4"))
-# prefill attention kernel for the Llama config (D 128, 4 query heads per KV head, causal, paged):
-# 0 = the 4-wave kernel; 10 = the software-pipelined 8-wave kernel (attention.hip
-# attn_prefill_v3_kernel: 32x32x16 MFMAs with the online softmax interleaved into the MFMA stream,
-# two 32-query groups sharing each K/V tile; 6-10 % faster, tools/attn_pp_ab.py); 1 / 2 = the
-# barrier-alternated ping-pong kernel and 6 = the one-wave-per-SIMD v3 (A/B only, both slower);
-# 15 (default) = 10 with the output tile staged through LDS and stored as whole 256-B rows: bit-identical,
-# 6 x 5.4k 1540 -> 1513 us, one 5.2k prompt 277 -> 271, a 2k chunk over 3k context 177 -> 171
-# (profiles/attn_prefill_wide_epi_r4.log)
-PREFILL_PP = int(os.environ.get("RAGK_PREFILL_PP", "15"))
-# prefill block order (attention.hip prefill_block): 1 = one grid dimension, head group fastest, so the
-# heaviest causal tiles of every head start first and each XCD serves one KV head; 0 = (tile, head) grid
-PREFILL_ORDER = int(os.environ.get("RAGK_PREFILL_ORDER", "1"))
-_prefill_waves_set = [None]
-
-
-def set_prefill_waves(w, pp=None):
-    """Waves per prefill-attention block when 4 query heads share a KV head (4 or 8), and the
-    ping-pong kernel mode (64-query tiles when on). Tile lists built before a change are invalid."""
-    check(_lib.lib().ragk_attn_prefill_set_waves(int(w)), "ragk_attn_prefill_set_waves")
-    pp = PREFILL_PP if pp is None else int(pp)
-    check(_lib.lib().ragk_attn_prefill_set_pp(pp), "ragk_attn_prefill_set_pp")
-    check(_lib.lib().ragk_attn_prefill_set_order(PREFILL_ORDER), "ragk_attn_prefill_set_order")
-    _prefill_waves_set[0] = int(w)
-
-
 def prefill_qtile(Hq, Hkv):
-    """Query rows per prefill-attention block (the tile list must be built with the kernel's value)."""
-    if not torch.cuda.is_available():  # CPU engine: tiles are unused by the torch backend
-        G = Hq // Hkv
-        GB = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
-        # the library's predicate (attention.hip ragk_attn_prefill_qtile): 64-query tiles for the
-        # ping-pong / v3 modes 1..5 and >= 10, else the configured waves per block
-        pp64 = 1 <= PREFILL_PP <= 5 or PREFILL_PP >= 10
-        return 32 * ((8 if pp64 else PREFILL_WAVES) // GB if GB == 4 else 4 // GB)
-    if _prefill_waves_set[0] is None:
-        set_prefill_waves(PREFILL_WAVES)
-    return _lib.lib().ragk_attn_prefill_qtile(Hq, Hkv)
+    """Query rows per prefill-attention block (the tile list must be built with the kernel's value):
+    64 when 4 query heads share a KV head (the 8-wave kernels, two 32-row groups per K/V tile), else
+    128 / heads-per-block (attention.hip ragk_attn_prefill_qtile)."""
+    G = Hq // Hkv
+    GB = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
+    return 32 * ((8 if GB == 4 else 4) // GB)
 
 
 def build_prefill_tiles(q_lens, Hq, Hkv):
@@ -1040,8 +711,8 @@ def attn_prefill(q, k, v, cu_q, kv_lens, tiles, out, Hq, Hkv, D, causal=True, pa
     return out
 
 
-DECODE_TARGET_BLOCKS = int(os.environ.get("RAGK_DECODE_BLOCKS", "512"))
-DECODE_MIN_TILES = int(os.environ.get("RAGK_DECODE_MIN_TILES", "4"))
+DECODE_TARGET_BLOCKS = 512
+DECODE_MIN_TILES = 4
 
 
 def decode_partitions(max_kv_len, batch, Hkv, target_blocks=None, min_tiles=None):
@@ -1062,7 +733,7 @@ def decode_partitions(max_kv_len, batch, Hkv, target_blocks=None, min_tiles=None
 # One partition per (sequence, KV head) in 8-wave blocks once batch x KV heads reaches this (>= one block
 # per CU): the same KV bytes in flight as two 4-wave partition blocks, and no merge launch (0 = off).
 # Batch 32: decode step 6.96 -> 6.86-6.90 ms (profiles/decode_nw8_ab_r4.log).
-DECODE_NW8_MIN_PAIRS = int(os.environ.get("RAGK_DECODE_NW8", "256"))
+DECODE_NW8_MIN_PAIRS = 256
 
 
 # Non-temporal K / V loads in the split-K decode attention once batch x KV heads reaches this: at batch 32
@@ -1070,7 +741,7 @@ DECODE_NW8_MIN_PAIRS = int(os.environ.get("RAGK_DECODE_NW8", "256"))
 # the nt policy keeps it from evicting the L2 / Infinity Cache lines the other kernels reuse: decode step
 # 7.60 -> 7.33 ms (profiles/decode_nt_ab_r4.log); batch 1 / 4 neutral-to-worse, and the TP=8 shard's
 # 1-KV-head stream at batch 32 (85 MB per layer) 2.33 -> 2.40 ms with nt (profiles/tp_nt_ab_r4.log).
-DECODE_NT_MIN_BH = int(os.environ.get("RAGK_DECODE_NT_MIN_BH", "64"))
+DECODE_NT_MIN_BH = 64
 
 
 def _set_decode_nt(B, Hkv):
@@ -1093,15 +764,11 @@ def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, par
             ws_ml = torch.empty((B, Hq, max_parts, 2), dtype=torch.float32, device=q.device)
         _req(ws_o.numel() >= B * Hq * max_parts * D and ws_ml.numel() >= B * Hq * max_parts * 2, "workspace")
     scale = 1.0 / math.sqrt(D) if scale is None else scale
-    cnt = None
-    if max_parts > 1 and ATTN_FUSED_MERGE and 2 * G * max_parts + 16 <= 4 * 64 * D * 2 // 4:
-        cnt = _attn_counters(q.device)
-        _req(B * Hkv <= cnt.numel(), "attention ticket buffer too small")
     _set_decode_nt(B, Hkv)
     check(_lib.lib().ragk_attn_decode(
         q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(),
         block_tables.stride(0), kv_lens.data_ptr(), ptr(ws_o), ptr(ws_ml), out.data_ptr(), out.stride(0), B, Hq, Hkv,
-        D, part_tiles, max_parts, float(scale), ptr(cnt), stream_ptr()), "ragk_attn_decode")
+        D, part_tiles, max_parts, float(scale), stream_ptr()), "ragk_attn_decode")
     return out
 
 
@@ -1127,12 +794,8 @@ def attn_decode_rope(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_
             ws_ml = torch.empty((B, Hq, max_parts, 2), dtype=torch.float32, device=P.device)
         _req(ws_o.numel() >= B * Hq * max_parts * D and ws_ml.numel() >= B * Hq * max_parts * 2, "workspace")
     scale = 1.0 / math.sqrt(D) if scale is None else scale
-    cnt = None
-    if defer_merge:  # the partitions stay unmerged for gemm_part_merge (no reduce launch, no fused merge)
+    if defer_merge:  # the partitions stay unmerged for gemm_part_merge (no reduce launch)
         _req(max_parts > 1 and ws_o is not None, "deferred merge needs a partition workspace")
-    elif max_parts > 1 and ATTN_FUSED_MERGE and 2 * (Hq // Hkv) * max_parts + 16 <= 4 * 64 * D * 2 // 4:
-        cnt = _attn_counters(P.device)
-        _req(B * Hkv <= cnt.numel(), "attention ticket buffer too small")
     lib = _lib.lib()
     _set_decode_nt(B, Hkv)
     if defer_merge:
@@ -1142,27 +805,11 @@ def attn_decode_rope(P, positions, cos_t, sin_t, slots, k_cache, v_cache, block_
             P.data_ptr(), S, ldp, positions.data_ptr(), slots.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(),
             k_cache.data_ptr(), v_cache.data_ptr(), block_tables.data_ptr(), block_tables.stride(0),
             kv_lens.data_ptr(), ptr(ws_o), ptr(ws_ml), out.data_ptr(), out.stride(0), B, Hq, Hkv, D, part_tiles,
-            max_parts, float(scale), ptr(cnt), stream_ptr()), "ragk_attn_decode_rope")
+            max_parts, float(scale), stream_ptr()), "ragk_attn_decode_rope")
     finally:
         if defer_merge:
             lib.ragk_attn_decode_set_defer(0)
     return out
-
-
-# split-K decode attention: the last partition block of each (sequence, KV head) merges the partitions
-# (a ticket per pair; zeroed once, reset by the merging block) instead of a separate merge launch
-# Off by default: measured slower at batch 1 (4.41 vs 4.2-4.3 ms per decode step with agent-scope
-# releases; round 4, write-through form: 3.76 / 3.82 vs 3.62 / 3.65 ms at batch 1, neutral at batch 32,
-# profiles/decode_fm_ab_r4.log), kept for A/B (tests/test_kernels_gpu.py checks it).
-ATTN_FUSED_MERGE = os.environ.get("RAGK_ATTN_FUSED_MERGE", "0") == "1"
-_attn_cnt = {}
-
-
-def _attn_counters(device):
-    key = str(device)
-    if key not in _attn_cnt:
-        _attn_cnt[key] = torch.zeros(1 << 16, dtype=torch.int32, device=device)
-    return _attn_cnt[key]
 
 
 # ----------------------------------------------------------------------------- sampling
@@ -1193,7 +840,7 @@ def topk_candidates(logits, K, vocab_offset=0, max_cand=512, chunks=None, cand_v
 
 
 # candidate lists rank-merged in the sampler (no full sort) when rows ask for top_k <= 64
-SAMPLE_LIST_MERGE = os.environ.get("RAGK_SAMPLE_LIST_MERGE", "1") == "1"
+SAMPLE_LIST_MERGE = True
 
 
 def sample_candidates(cand_v, cand_i, temps, top_ks, top_ps, seeds, steps, out_tok=None, out_lp=None, list_len=None):
@@ -1340,45 +987,3 @@ def l2_append(xt, cap, n0, x):
           "ragk_l2_append")
 
 
-# ----------------------------------------------------------------------------- MALL prefetch
-_pf_sink = {}
-
-
-def prefetch(t, nbytes=None, blocks=64):
-    """Read the first `nbytes` of tensor `t` once with the allocating cache policy (csrc/kernels/
-    prefetch.hip) so a following kernel finds them in the MALL. Reads only."""
-    key = str(t.device)
-    if key not in _pf_sink:
-        _pf_sink[key] = torch.zeros(4096, dtype=torch.int32, device=t.device)
-    nb = t.numel() * t.element_size() if nbytes is None else min(int(nbytes), t.numel() * t.element_size())
-    _req(t.data_ptr() % 16 == 0 and blocks <= 4096, "16-B aligned, <= 4096 blocks")
-    check(_lib.lib().ragk_prefetch(t.data_ptr(), nb, int(blocks), _pf_sink[key].data_ptr(), stream_ptr()),
-          "ragk_prefetch")
-
-
-def pf_arm(ranges, blocks):
-    """Arm the next rider-capable launch (rope_kv_partials / attn_decode / add_partials_rmsnorm) on this
-    thread with up to two (tensor, byte_offset, nbytes) weight ranges to pull into the MALL with
-    `blocks` extra rider blocks (csrc/kernels/common.h pf_rider). Ranges are clipped to the tensors."""
-    args = []
-    dev = None
-    for t, off, nb in list(ranges)[:2]:
-        if hasattr(t, "w8"):  # Fp8Weight: the e4m3 byte matrix
-            t = t.w8
-        total = t.numel() * t.element_size()
-        off = min(int(off), total) & ~15
-        nb = (min(int(nb), total - off)) & ~15
-        if nb > 0:
-            args.append((t.data_ptr() + off, nb))
-            dev = t.device
-    if not args or blocks <= 0:
-        return
-    key = str(dev)
-    if key not in _pf_sink:
-        _pf_sink[key] = torch.zeros(4096, dtype=torch.int32, device=dev)
-    (p0, b0), (p1, b1) = args[0], (args[1] if len(args) > 1 else (None, 0))
-    check(_lib.lib().ragk_pf_arm(p0, b0, p1, b1, int(blocks), _pf_sink[key].data_ptr()), "ragk_pf_arm")
-
-
-def spin_us(us):
-    check(_lib.lib().ragk_spin_us(int(us), stream_ptr()), "ragk_spin_us")

@@ -68,7 +68,10 @@ class TPComm:
         """Raise CommError if a peer-mapped collective gave up waiting for a peer (cheap: reads a
         pinned host word). Once raised, every later call raises too."""
         if self.broken is None and self.ipc is not None and self.ipc.error():
-            self.broken = "peer-mapped collective timed out waiting for a peer (rank %d)" % self.rank
+            from .ipc_allreduce import describe_error
+
+            self.broken = "peer-mapped collective timed out on rank %d: %s" % (
+                self.rank, describe_error(self.ipc.error_record()))
             log.critical(self.broken)
         if self.broken is not None:
             raise CommError(self.broken)

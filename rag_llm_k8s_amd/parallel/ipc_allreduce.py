@@ -22,16 +22,16 @@ import torch.distributed as dist
 from ..ops import _lib
 from ..ops._lib import check, stream_ptr
 
-ONE_SHOT_MAX = int(os.environ.get("RAGK_AR_ONESHOT_MAX", str(512 << 10)))
+ONE_SHOT_MAX = 512 << 10
 SPIN_LIMIT = int(os.environ.get("RAGK_AR_TIMEOUT_US", "0"))  # 0 = kernel default (5 s per peer wait)
-MAX_BYTES = int(os.environ.get("RAGK_AR_MAX_BYTES", str(8 << 20)))
-BLOCKS = int(os.environ.get("RAGK_AR_BLOCKS", "64"))
+MAX_BYTES = 8 << 20
+BLOCKS = 64
 # fused decode reduction (ar_add_rmsnorm): row slots and max hidden size of the row area
-FUSED_ROWS = int(os.environ.get("RAGK_AR_FUSED_ROWS", "256"))
-FUSED_H = int(os.environ.get("RAGK_AR_FUSED_H", "8192"))
+FUSED_ROWS = 256
+FUSED_H = 8192
 # one-shot (every rank reads every peer's fp32 row) while the total read stays below this; two-shot
 # (reduce-scatter of column slices + gather of the bf16 slices, 2 barriers) above it
-FUSED_ONESHOT_BYTES = int(os.environ.get("RAGK_AR_FUSED_ONESHOT_BYTES", str(512 << 10)))
+FUSED_ONESHOT_BYTES = 512 << 10
 
 
 def fences_for(cross_device: bool, env=None) -> bool:
@@ -183,9 +183,27 @@ class IPCAllReduce:
     def error(self) -> bool:
         """True if a peer failed to arrive within the kernel's bounded spin (comm watchdog). Reads the
         pinned host word (no device sync); falls back to a device read."""
+        return self.error_record() != 0
+
+    def error_record(self) -> int:
+        """The error record of a failed peer wait (0 = healthy; see describe_error)."""
         if self._err_word is not None:
-            return self._err_word.value != 0
-        return self.L.ragk_ar_error(self.h) != 0
+            return int(self._err_word.value)
+        return max(0, int(self.L.ragk_ar_error(self.h)))
+
+
+SITES = {1: "all-reduce (start barrier)", 2: "all-reduce (two-shot mid barrier)", 3: "all-gather",
+         4: "fused reduce+norm row (start barrier)", 5: "fused reduce+norm row (two-shot mid barrier)"}
+
+
+def describe_error(rec: int) -> str:
+    """Decode an error record of csrc/comm/allreduce.hip (ar_record): 1 | site << 1 | peer << 4 |
+    block-or-row << 7 | (epoch & 0xffff) << 15."""
+    if not rec:
+        return "no error"
+    site, peer, slot, ep = (rec >> 1) & 7, (rec >> 4) & 7, (rec >> 7) & 255, (rec >> 15) & 0xFFFF
+    what = SITES.get(site, "site %d" % site)
+    return "%s, block/row %d, call %d (mod 65536): peer rank %d never arrived" % (what, slot, ep, peer)
 
     def close(self):
         if getattr(self, "h", None):

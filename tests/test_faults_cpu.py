@@ -193,3 +193,16 @@ def test_fault_spec_parsing(monkeypatch):
     assert faults.active("embed_error") and faults.value("missing_shard") == "3"
     monkeypatch.setenv("RAGK_FAULTS", "")
     assert faults.faults() == {}
+
+
+def test_peer_wait_error_record_decodes():
+    """The comm watchdog's error word (csrc/comm/allreduce.hip ar_record) names the collective, the peer
+    that never arrived, the block / row slot and the call index; CommError carries the decoded text."""
+    from rag_llm_k8s_amd.parallel.ipc_allreduce import describe_error
+
+    rec = 1 | 4 << 1 | 6 << 4 | 3 << 7 | 1234 << 15
+    assert describe_error(rec) == ("fused reduce+norm row (start barrier), block/row 3, call 1234 (mod 65536): "
+                                   "peer rank 6 never arrived")
+    assert describe_error(1 | 1 << 1 | 1 << 4 | 1 << 15).startswith("all-reduce (start barrier), block/row 0, call 1")
+    assert describe_error(0) == "no error"
+    assert rec < 2 ** 31  # ragk_ar_error returns it as a non-negative int

@@ -243,3 +243,40 @@ def test_fused_allreduce_add_rmsnorm(native, WORLD, H, fences, monkeypatch):
         for r in range(WORLD):
             assert torch.equal(out[r]["graph"][it][0], want)
     assert all(out[r]["error"] is False for r in range(WORLD))
+
+
+# ---------------------------------------------------------------- watchdog error record
+def _timeout_worker(rank, port, d, WORLD=2):
+    """Rank 1 skips the collectives: rank 0's bounded peer waits give up and record which one."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    torch.cuda.set_device(0)
+    from rag_llm_k8s_amd.parallel.ipc_allreduce import IPCAllReduce, describe_error
+
+    ar = IPCAllReduce(None, None, WORLD, rank, "cuda:0", max_bytes=1 << 20, blocks=8, fused_rows=8, fused_h=512,
+                      spin_limit=200000)  # 0.2 s per peer wait
+    res = {}
+    try:
+        if rank == 0:
+            x = torch.ones(8 * 512, dtype=torch.bfloat16, device="cuda")
+            ar.all_reduce(x, mode=0)  # call 1 of every block: peer 1 never arrives
+            torch.cuda.synchronize()
+            res["rec"] = ar.error_record()
+            res["text"] = describe_error(res["rec"])
+    finally:
+        torch.cuda.synchronize()
+        dist.barrier()
+        ar.close()
+        torch.save(res, os.path.join(d, "r%d.pt" % rank))
+        dist.destroy_process_group()
+
+
+def test_ipc_timeout_error_record(native):
+    """A peer that never arrives: the waiting rank's error word names the collective (start barrier of the
+    all-reduce), the peer (rank 1), the block and the call index -- what CommError reports."""
+    with tempfile.TemporaryDirectory() as d:
+        out = _spawn(_timeout_worker, 2, d, _free_port())
+    rec = out[0]["rec"]
+    assert rec & 1, rec
+    assert (rec >> 1) & 7 == 1 and (rec >> 4) & 7 == 1 and (rec >> 7) & 255 < 8 and (rec >> 15) & 0xFFFF == 1, rec
+    assert "peer rank 1 never arrived" in out[0]["text"] and "all-reduce (start barrier)" in out[0]["text"]

@@ -28,54 +28,56 @@ def test_gemm_plain(native, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 256, 128), (300, 1024, 768), (1111, 6144, 4096), (256, 256, 128),
-                                   (2049, 512, 1024), (513, 4104, 256), (260, 768, 384)])
-@pytest.mark.parametrize("variant", [2, 4, "w4"])
-def test_gemm_pingpong(native, M, N, K, variant):
-    if variant == "w4":  # 4-wave 128x128-per-wave kernel (gemm_w4.hip)
+                                   (2049, 512, 1024), (513, 4104, 256), (260, 768, 384), (700, 1024, 192)])
+@pytest.mark.parametrize("kernel", ["pp", "w4"])
+def test_gemm_pingpong(native, M, N, K, kernel):
+    """The two 256x256 large-M kernels: gemm_w4 (4 waves, the prefill default, K >= 192) and gemm_pp (8-wave
+    ping-pong, 64-bit addressing: the fallback for operands past 2 GiB)."""
+    if kernel == "w4":
+        if K < 192:
+            pytest.skip("gemm_w4 needs three K-tiles per tile")
         _check_pingpong(native, M, N, K, path=6)
         return
-    native.set_pp_variant(variant)
-    try:
-        _check_pingpong(native, M, N, K)
-    finally:
-        native.set_pp_variant(native.PP_VARIANT)
+    _check_pingpong(native, M, N, K, path=2)
 
 
-@pytest.mark.parametrize("cont", [2, 1, 0])
 @pytest.mark.parametrize("grid", [8, 16])
-@pytest.mark.parametrize("M,N,K", [(1111, 1024, 256), (513, 4104, 128), (2048, 512, 128), (777, 1280, 384),
+@pytest.mark.parametrize("M,N,K", [(1111, 1024, 256), (513, 4104, 192), (2048, 512, 192), (777, 1280, 384),
                                    (1030, 768, 1024)])
-def test_gemm_w4_persistent(native, M, N, K, grid, cont):
-    """Persistent gemm_w4: a few blocks loop over every tile (full and edge tiles, one-K-tile K),
-    so the next-tile DMA / register-epilogue overlap and its counted waits run many times per block.
-    cont=1: the continuous K-stream kernel (K/64 >= 4); cont=2: the same with the three-barrier schedule."""
+def test_gemm_w4_persistent(native, M, N, K, grid):
+    """Persistent gemm_w4: a few blocks loop over every tile (full and edge tiles, the shortest ring of
+    three K-tiles), so the next-tile staging inside the K-stream, the register epilogue and the counted
+    waits around it run many times per block."""
     native.set_w4_grid(grid)
-    native.set_w4_cont(cont)
     try:
         _check_pingpong(native, M, N, K, path=6)
     finally:
         native.set_w4_grid(-1)
-        native.set_w4_cont(-1)
 
 
-def test_gemm_w4_cont_matches_tile_kernel(native):
-    """Both persistent kernels sum the K-tiles in the same order: bit-identical outputs."""
+def test_gemm_w4_grid_independent(native):
+    """A tile's K-loop and epilogue do not depend on which block computes it or how many tiles the block
+    streams before it: every grid (one block per tile, 8 / 24 blocks, one per CU) gives bit-identical
+    outputs, for the plain, residual (in place), SiLU*up, bias+GELU and fp32 split-K forms."""
     torch.manual_seed(23)
     M, N, K = 1300, 1536, 640
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
     r = torch.randn(M, N, device=DEV).bfloat16()
+    b = torch.randn(N, device=DEV).bfloat16()
     outs = []
-    for cont in (2, 1, 0):
-        native.set_w4_cont(cont)
+    for grid in (-1, 0, 8, 24):
+        native.set_w4_grid(grid)
         try:
-            outs.append((native.gemm(x, w, path=6), native.gemm(x, w, resid=r, epi="resid", path=6),
-                         native.gemm(x, w, epi="silu_mul", path=6)))
+            h = r.clone()
+            native.gemm(x, w, resid=h, epi="resid", out=h, path=6)
+            outs.append((native.gemm(x, w, path=6), h, native.gemm(x, w, epi="silu_mul", path=6),
+                         native.gemm(x, w, bias=b, epi="bias_gelu", path=6), native.gemm_splitk(x, w, 2)))
         finally:
-            native.set_w4_cont(-1)
+            native.set_w4_grid(-1)
     for o in outs[1:]:
-        for a, b in zip(outs[0], o):
-            assert torch.equal(a, b)
+        for a, c in zip(outs[0], o):
+            assert torch.equal(a, c)
 
 
 def test_gemm_large_m_routing(native, monkeypatch):
@@ -88,7 +90,7 @@ def test_gemm_large_m_routing(native, monkeypatch):
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
     r = torch.randn(M, N, device=DEV).bfloat16()
-    assert native.PREFILL_GEMM == "w4" and native.PREFILL_BLAS == "resid"
+    assert native.PREFILL_BLAS == "resid"
     assert torch.equal(native.gemm(x, w), native.gemm(x, w, path=6))
     h = r.clone()
     native.gemm(x, w, resid=h, epi="resid", out=h)
@@ -113,7 +115,7 @@ def _check_pingpong(native, M, N, K, path=2):
     r = torch.randn(M, N, device=DEV).bfloat16()
     y = native.gemm(x, w, path=path)
     assert rel_err(y, x.float() @ w.float().t()) < 1e-2
-    for epi in ["bias", "resid", "bias_resid", "bias_gelu"]:
+    for epi in ["bias", "resid", "bias_resid", "bias_gelu", "gelu", "bias_gelu_tanh"]:
         y = native.gemm(x, w, bias=b, resid=r, epi=epi, path=path)
         assert rel_err(y.cpu(), R.linear(x.cpu(), w.cpu(), b.cpu(), r.cpu(), epi=epi)) < 1e-2, epi
     yf = native.gemm(x, w, out_f32=True, path=path)
@@ -148,23 +150,16 @@ def test_gemm_decode_v3(native, M, N, K):
 
 
 @pytest.mark.parametrize("M", [1, 4, 13])
-def test_gemm_skinny_wave_variants(native, M):
-    """Skinny decode GEMM (ragk_gemm routing at M <= 16) with 8 and 16 waves per block: same result
-    (K-blocks strided over the waves; the 16-wave variant serves long-K shapes like down_proj)."""
+def test_gemm_skinny_long_k(native, M):
+    """Skinny decode GEMM (ragk_gemm routing at M <= 16) on the long-K down projection shape with the
+    residual epilogue (K-blocks strided over the block's 8 waves)."""
     torch.manual_seed(22)
     N, K = 4096, 14336
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
     r = torch.randn(M, N, device=DEV).bfloat16()
     ref = x.float() @ w.float().t() + r.float()
-    outs = []
-    for wv in (8, 16):
-        native.set_skinny_waves(wv)
-        try:
-            outs.append(native.gemm(x, w, resid=r, epi="resid"))
-        finally:
-            native.set_skinny_waves(-1)
-        assert rel_err(outs[-1], ref) < 1e-2
+    assert rel_err(native.gemm(x, w, resid=r, epi="resid"), ref) < 1e-2
 
 
 @pytest.mark.parametrize("path", [0, 1])
@@ -324,39 +319,16 @@ def _paged_setup(lens, Hkv, D, seed=0):
 
 
 @pytest.mark.parametrize("q_lens,kv_lens,Hq,Hkv", [([37], [37], 8, 2), ([100, 64, 1], [100, 300, 129], 32, 8),
-                                                   ([200], [200], 4, 4), ([5, 70], [513, 70], 8, 1),
-                                                   # 5.2k RAG prompt, chunked prefill at 8B heads: later chunks
-                                                   # have q_len < kv_len, 82 KV blocks (> 80)
-                                                   ([2048, 1104], [4096, 5200], 32, 8)])
-def test_attn_prefill_paged(native, q_lens, kv_lens, Hq, Hkv):
-    D = 128
-    torch.manual_seed(9)
-    kc, vc, bt = _paged_setup(kv_lens, Hkv, D)
-    T = sum(q_lens)
-    q = torch.randn(T, Hq * D).bfloat16()
-    cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(q_lens), 0)), dtype=torch.int32)
-    kvl = torch.tensor(kv_lens, dtype=torch.int32)
-    tiles = native.build_prefill_tiles(q_lens, Hq, Hkv)
-    out = torch.empty(T, Hq * D, device=DEV).bfloat16()
-    native.attn_prefill(q.to(DEV), kc.to(DEV), vc.to(DEV), cu.to(DEV), kvl.to(DEV), tiles.to(DEV), out, Hq, Hkv, D,
-                        causal=True, paged=True, block_tables=bt.to(DEV))
-    ref = R.attention_varlen(q.reshape(T, Hq, D), None, None, cu, kvl, True, 1 / math.sqrt(D),
-                             k_full=lambda s: R.paged_kv_view(kc, bt[s], kv_lens[s], 64),
-                             v_full=lambda s: R.paged_kv_view(vc, bt[s], kv_lens[s], 64))
-    assert rel_err(out.cpu().reshape(T, Hq, D), ref) < 2e-2
-
-
-@pytest.mark.parametrize("q_lens,kv_lens,Hq,Hkv", [([37], [37], 8, 2), ([100, 64, 1], [100, 300, 129], 32, 8),
                                                    ([5, 70], [513, 70], 8, 1), ([1], [1], 4, 1),
                                                    ([64, 65], [64, 200], 4, 1),
                                                    ([2048, 1104], [4096, 5200], 32, 8)])
-@pytest.mark.parametrize("pp", [1, 2, 6, 10, 15])
-def test_attn_prefill_pingpong(native, q_lens, kv_lens, Hq, Hkv, pp):
-    """Alternative prefill kernels for the Llama config vs the 4-wave kernel and the fp32 oracle, on
-    ragged query tails, chunked prefill (q_len < kv_len), single-tile sequences and 8 query heads per
-    KV head. pp 1 / 2: 8-wave ping-pong (64-query tiles, 3-slot K/V ring), bit-identical (same MFMA
-    and softmax order). pp 6: software-pipelined one-wave-per-SIMD kernel (32x32x16 MFMAs: another
-    fp32 summation order, so within bf16 rounding of the 4-wave kernel)."""
+@pytest.mark.parametrize("big_cache", [False, True])
+def test_attn_prefill_llama_kernels(native, q_lens, kv_lens, Hq, Hkv, big_cache):
+    """The Llama prefill kernels vs the fp32 oracle on ragged query tails, chunked prefill (q_len <
+    kv_len), single-tile sequences and 4 / 8 query heads per KV head: the software-pipelined 8-wave
+    kernel (attn_prefill_v3_kernel, per-layer cache < 4 GiB: buffer-descriptor K/V staging) and, with a
+    cache of >= 4 GiB per layer (big_cache: the same blocks placed at the top of an 8 GiB pair), the
+    8-wave attn_prefill_kernel. 64-query tiles for 4 heads per block."""
     D = 128
     torch.manual_seed(19)
     kc, vc, bt = _paged_setup(kv_lens, Hkv, D)
@@ -364,29 +336,27 @@ def test_attn_prefill_pingpong(native, q_lens, kv_lens, Hq, Hkv, pp):
     q = torch.randn(T, Hq * D).bfloat16()
     cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(q_lens), 0)), dtype=torch.int32)
     kvl = torch.tensor(kv_lens, dtype=torch.int32)
-    args = (q.to(DEV), kc.to(DEV), vc.to(DEV), cu.to(DEV), kvl.to(DEV))
-    outs = []
-    try:
-        for mode in (0, pp) + ((10,) if pp == 15 else ()):
-            native.set_prefill_waves(4, pp=mode)
-            tiles = native.build_prefill_tiles(q_lens, Hq, Hkv)
-            assert (tiles[:, 1] % (64 if mode in (1, 2, 10, 15) else 32) == 0).all()
-            out = torch.full((T, Hq * D), float("nan"), device=DEV).bfloat16()
-            native.attn_prefill(*args, tiles.to(DEV), out, Hq, Hkv, D, causal=True, paged=True,
-                                block_tables=bt.to(DEV))
-            outs.append(out.cpu())
-    finally:
-        native.set_prefill_waves(native.PREFILL_WAVES)
-    if pp == 15:  # pp 10 with the whole-row epilogue: the same values
-        assert torch.equal(outs[1], outs[2])
-    if pp in (1, 2):
-        assert torch.equal(outs[0], outs[1])
+    if big_cache:  # >= 4 GiB of blocks per cache: the kernel cannot address it with 32-bit buffer offsets
+        nblk = -(-(4 << 30) // (Hkv * 64 * D * 2)) + kc.shape[0]
+        off = nblk - kc.shape[0]
+        kd = torch.empty((nblk, Hkv, 64, D), dtype=torch.bfloat16, device=DEV)
+        vd = torch.empty_like(kd)
+        kd[off:] = kc.to(DEV)
+        vd[off:] = vc.to(DEV)
+        btd = (bt + off).to(DEV)
     else:
-        assert rel_err(outs[1], outs[0]) < 1e-2
+        kd, vd, btd = kc.to(DEV), vc.to(DEV), bt.to(DEV)
+    tiles = native.build_prefill_tiles(q_lens, Hq, Hkv)
+    if (Hq // Hkv) % 4 == 0:
+        assert (tiles[:, 1] % 64 == 0).all()
+    out = torch.full((T, Hq * D), float("nan"), device=DEV).bfloat16()
+    native.attn_prefill(q.to(DEV), kd, vd, cu.to(DEV), kvl.to(DEV), tiles.to(DEV), out, Hq, Hkv, D, causal=True,
+                        paged=True, block_tables=btd)
     ref = R.attention_varlen(q.reshape(T, Hq, D), None, None, cu, kvl, True, 1 / math.sqrt(D),
                              k_full=lambda s: R.paged_kv_view(kc, bt[s], kv_lens[s], 64),
                              v_full=lambda s: R.paged_kv_view(vc, bt[s], kv_lens[s], 64))
-    assert rel_err(outs[1].reshape(T, Hq, D), ref) < 2e-2
+    assert rel_err(out.cpu().reshape(T, Hq, D), ref) < 2e-2
+    del kd, vd
 
 
 @pytest.mark.parametrize("D,H", [(32, 12), (64, 16)])
@@ -460,37 +430,6 @@ def test_attn_decode_nw8_single_partition(native, kv_lens, Hq, Hkv, nt, monkeypa
                              v_full=lambda s: R.paged_kv_view(vc, bt[s], kv_lens[s], 64))
     assert rel_err(out.cpu().reshape(B, Hq, D), ref) < 2e-2
     assert rel_err(out.cpu(), ref4.cpu()) < 1e-2
-
-
-def test_attn_decode_fused_merge_matches_separate_and_resets(native):
-    """Split-K decode with the merge fused into the partition kernel (ticket per (sequence, KV head),
-    last block merges) == the separate merge launch, bit for bit, and stays so over repeated launches
-    (the merging block resets its ticket, as a replayed hipGraph needs)."""
-    D, Hq, Hkv = 128, 32, 8
-    kv_lens = [5200, 1, 64, 65, 3000, 700]
-    torch.manual_seed(13)
-    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=4)
-    B = len(kv_lens)
-    q = torch.randn(B, Hq * D).bfloat16().to(DEV)
-    kc, vc, bt = kc.to(DEV), vc.to(DEV), bt.to(DEV)
-    kvl = torch.tensor(kv_lens, dtype=torch.int32).to(DEV)
-    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv, target_blocks=1024)
-    assert mp > 1
-    outs = {}
-    for fused in (False, True):
-        native.ATTN_FUSED_MERGE = fused
-        try:
-            runs = []
-            for _ in range(3):
-                out = torch.empty(B, Hq * D, device=DEV).bfloat16()
-                native.attn_decode(q, kc, vc, bt, kvl, out, Hq, Hkv, D, pt, mp)
-                runs.append(out.cpu())
-        finally:
-            native.ATTN_FUSED_MERGE = False
-        assert all(torch.equal(runs[0], r) for r in runs[1:])
-        outs[fused] = runs[0]
-    assert torch.equal(outs[True], outs[False])
-    assert int(native._attn_counters(DEV)[:B * Hkv].abs().sum()) == 0
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (4, 1), (8, 1)])
@@ -628,145 +567,6 @@ def test_gemm_part_merge_matches_reduce_then_part(native, kv_lens, target, fp8, 
     oracle = ref_attn.float() @ wd.t()
     assert rel_err(ref.cpu(), oracle.cpu()) < 1e-4
     assert rel_err(out.cpu(), oracle.cpu()) < 2e-3, rel_err(out.cpu(), oracle.cpu())
-
-
-@pytest.mark.parametrize("kv_lens,target,Hq,Hkv,ks", [([5200], 512, 32, 8, 8), ([70, 3000], 256, 32, 8, 8),
-                                                       ([5200, 64], 256, 32, 8, 4), ([1], 512, 32, 8, 8),
-                                                       ([777, 5300, 65, 2000], 512, 32, 8, 8), ([8100], 512, 32, 8, 4),
-                                                       ([5200], 1024, 4, 1, 4), ([5200, 70], 1024, 8, 1, 8),
-                                                       ([64, 128, 8000], 128, 64, 8, 8)])
-@pytest.mark.parametrize("mia,v2", [(True, True), (True, False), (False, False)])
-def test_attn_oproj_fused_matches_unfused(native, kv_lens, target, Hq, Hkv, ks, mia, v2, monkeypatch):
-    """attention + o_proj in one launch (attn_oproj_kernel: o_proj blocks stream their weights while the
-    attention blocks run, then merge the partitions of their K-slice) == attn_decode_rope followed by
-    gemm_part on the merged output, up to fp32 summation order; same KV-cache contents bit for bit; vs
-    an fp32 oracle. Three launches in a row check that the kernel re-arms its counters. Covers one token,
-    one / many partitions, mixed lengths, M = 1..4, the TP=8 per-rank heads (4 / 1, 8 / 1) and 70B's 64 / 8."""
-    D, S = 128, 8
-    monkeypatch.setattr(native, "ATTN_OPROJ", True)  # off by default (slower, PERF_NOTES round 4)
-    monkeypatch.setattr(native, "ATTN_OPROJ_MIA", mia)
-    monkeypatch.setattr(native, "ATTN_OPROJ_V2", v2)
-    torch.manual_seed(31)
-    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=9)
-    B = len(kv_lens)
-    kc, vc, bt = kc.to(DEV), vc.to(DEV), bt.to(DEV)
-    kvl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
-    pos = kvl - 1
-    slots = (bt[torch.arange(B, device=DEV), (pos // 64).long()] * 64 + pos % 64).int()
-    P = torch.randn(S, B, (Hq + 2 * Hkv) * D, device=DEV)
-    cos, sin = R.rope_tables(D, 131072, theta=500000.0)
-    cos, sin = cos.to(DEV), sin.to(DEV)
-    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv, target_blocks=target)
-    w = (torch.randn(4096, Hq * D, device=DEV) / math.sqrt(Hq * D)).bfloat16()
-    ws_o = torch.empty((B, Hq, max(mp, 1), D), dtype=torch.float32, device=DEV)
-    ws_ml = torch.empty((B, Hq, max(mp, 1), 2), dtype=torch.float32, device=DEV)
-    old = native.ATTN_OPROJ_KS
-    native.ATTN_OPROJ_KS = ks
-    try:
-        assert native.attn_oproj_ok(B, w, Hq, Hkv, D, mp, ws_o)
-        kc2, vc2 = kc.clone(), vc.clone()
-        ref_attn = torch.empty(B, Hq * D, device=DEV).bfloat16()
-        native.attn_decode_rope(P, pos, cos, sin, slots, kc2, vc2, bt, kvl, ref_attn, Hq, Hkv, D, pt, mp)
-        ref = native.gemm_part(ref_attn, w).sum(0)
-        outs = []
-        for it in range(3):
-            kc3, vc3 = kc.clone(), vc.clone()
-            o = native.attn_oproj(P, pos, cos, sin, slots, kc3, vc3, bt, kvl, Hq, Hkv, D, pt, mp, ws_o, ws_ml, w)
-            assert o.shape in ((Hq * D // (64 * ks), B, 4096), (1, B, 4096))
-            outs.append(o.sum(0))
-        # the residual + RMSNorm tail in the last o_proj block == the add_partials_rmsnorm consumer
-        g = (1 + 0.1 * torch.randn(4096, device=DEV)).bfloat16()
-        h0 = torch.randn(B, 4096, device=DEV).bfloat16()
-        norm_ok = Hq * D // (64 * ks) <= 16
-        if norm_ok:
-            h1, h2 = h0.clone(), h0.clone()
-            xn1 = native.attn_oproj(P, pos, cos, sin, slots, kc.clone(), vc.clone(), bt, kvl, Hq, Hkv, D, pt, mp, ws_o,
-                                    ws_ml, w, norm=(h1, g, 1e-5))
-            Ps = native.attn_oproj(P, pos, cos, sin, slots, kc.clone(), vc.clone(), bt, kvl, Hq, Hkv, D, pt, mp, ws_o,
-                                   ws_ml, w)
-            xn2 = native.add_partials_rmsnorm(Ps, h2, g, 1e-5)
-        torch.cuda.synchronize()
-        assert not native.attn_oproj_error(DEV)
-        assert native.attn_oproj_armed(DEV)  # counters, done flags and tickets re-armed
-        if norm_ok:
-            assert torch.equal(h1, h2)  # same slab order, same bf16 rounding points
-            assert rel_err(xn1.float().cpu(), xn2.float().cpu()) < 1e-2  # block-sum order differs
-    finally:
-        native.ATTN_OPROJ_KS = old
-    assert torch.equal(kc3, kc2) and torch.equal(vc3, vc2)
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])  # deterministic
-    oracle = ref_attn.float() @ w.float().t()
-    assert rel_err(ref.cpu(), oracle.cpu()) < 1e-4
-    assert rel_err(outs[0].cpu(), oracle.cpu()) < 2e-3, rel_err(outs[0].cpu(), oracle.cpu())
-
-
-@pytest.mark.parametrize("kv_lens,Hq,Hkv,qks", [([5200], 32, 8, 16), ([70, 3000], 32, 8, 8), ([1], 32, 8, 16),
-                                                 ([777, 5300, 65, 2000], 32, 8, 16), ([5200, 70], 32, 4, 16)])
-@pytest.mark.parametrize("mia,v2", [(True, True), (True, False), (False, False)])
-def test_qkv_attn_oproj_matches_unfused(native, kv_lens, Hq, Hkv, qks, mia, v2, monkeypatch):
-    """The 3-role decode launch (qkv + input RMSNorm, attention + RoPE + KV append, o_proj + residual +
-    post-attention RMSNorm; attention blocks prefetch KV while the qkv weights stream) == rmsnorm ->
-    gemm_part -> attn_decode_rope -> gemm_part -> add_partials_rmsnorm, up to fp32 summation order; the
-    same KV-cache contents; repeated launches re-arm the counters."""
-    D, H = 128, 4096
-    monkeypatch.setattr(native, "ATTN_OPROJ", True)  # off by default (slower, PERF_NOTES round 4)
-    monkeypatch.setattr(native, "ATTN_OPROJ_MIA", mia)
-    monkeypatch.setattr(native, "ATTN_OPROJ_V2", v2)
-    torch.manual_seed(41)
-    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=11)
-    B = len(kv_lens)
-    kc, vc, bt = kc.to(DEV), vc.to(DEV), bt.to(DEV)
-    kvl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
-    pos = kvl - 1
-    slots = (bt[torch.arange(B, device=DEV), (pos // 64).long()] * 64 + pos % 64).int()
-    cos, sin = R.rope_tables(D, 131072, theta=500000.0)
-    cos, sin = cos.to(DEV), sin.to(DEV)
-    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv, target_blocks=512)
-    Nq = (Hq + 2 * Hkv) * D
-    wqkv = (torch.randn(Nq, H, device=DEV) / math.sqrt(H)).bfloat16()
-    wo = (torch.randn(H, Hq * D, device=DEV) / math.sqrt(Hq * D)).bfloat16()
-    g_in = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16()
-    g_post = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16()
-    h0 = torch.randn(B, H, device=DEV).bfloat16()
-    ws_o = torch.empty((B, Hq, max(mp, 1), D), dtype=torch.float32, device=DEV)
-    ws_ml = torch.empty((B, Hq, max(mp, 1), 2), dtype=torch.float32, device=DEV)
-    # unfused reference chain
-    kc2, vc2, h2 = kc.clone(), vc.clone(), h0.clone()
-    Pq = native.gemm_part(native.rmsnorm(h2, g_in, 1e-5), wqkv)
-    attn = torch.empty(B, Hq * D, device=DEV).bfloat16()
-    native.attn_decode_rope(Pq, pos, cos, sin, slots, kc2, vc2, bt, kvl, attn, Hq, Hkv, D, pt, mp)
-    xn2 = native.add_partials_rmsnorm(native.gemm_part(attn, wo), h2, g_post, 1e-5)
-    old = native.QAO_QKS
-    native.QAO_QKS = qks
-    try:
-        assert native.qkv_attn_oproj_ok(B, wqkv, wo, Hq, Hkv, D, mp, ws_o)
-        res = []
-        for it in range(3):
-            kc1, vc1, h1 = kc.clone(), vc.clone(), h0.clone()
-            xn1 = native.qkv_attn_oproj(h1, g_in, 1e-5, wqkv, pos, cos, sin, slots, kc1, vc1, bt, kvl, Hq, Hkv, D, pt,
-                                        mp, ws_o, ws_ml, wo, g_post, 1e-5)
-            res.append((h1, xn1))
-        torch.cuda.synchronize()
-        assert not native.attn_oproj_error(DEV)
-        assert native.attn_oproj_armed(DEV)  # counters, done flags and tickets re-armed
-    finally:
-        native.QAO_QKS = old
-    # tensor-parallel form: pre-normalised rows in, o_proj slabs out (no norm tail)
-    xin = native.rmsnorm(h0, g_in, 1e-5)
-    old = native.QAO_QKS
-    native.QAO_QKS = qks
-    try:
-        Po = native.qkv_attn_oproj(xin, None, 0.0, wqkv, pos, cos, sin, slots, kc.clone(), vc.clone(), bt, kvl, Hq,
-                                   Hkv, D, pt, mp, ws_o, ws_ml, wo, None, 0.0)
-    finally:
-        native.QAO_QKS = old
-    assert rel_err(Po.sum(0).cpu(), native.gemm_part(attn, wo).sum(0).cpu()) < 2e-2
-    # k rows appended from differently-ordered fp32 slab sums may differ by 1 bf16 ulp
-    assert rel_err(kc1.float().cpu(), kc2.float().cpu()) < 1e-2 and rel_err(vc1.float().cpu(), vc2.float().cpu()) < 1e-2
-    for h1, xn1 in res:
-        assert torch.equal(h1, res[0][0]) and torch.equal(xn1, res[0][1])  # deterministic
-    assert rel_err(res[0][0].float().cpu(), h2.float().cpu()) < 1e-2
-    assert rel_err(res[0][1].float().cpu(), xn2.float().cpu()) < 2e-2, rel_err(res[0][1].float().cpu(), xn2.float().cpu())
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (3, 6144, 4096), (4, 1280, 8192), (2, 10240, 8192)])
@@ -1129,74 +929,6 @@ def test_add_partials_rmsnorm(native, S, M, H):
     assert (h.cpu().float() - h_ref.float()).abs().max().item() <= 0.0625
     assert rel_err(h.cpu(), h_ref) < 1e-3
     assert rel_err(y.cpu(), ref) < 4e-3
-
-
-@pytest.mark.parametrize("M", [1, 3, 5, 32, 64])
-@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336), (8192, 8192), (384, 512)])
-def test_gemm_part_tail_matches_part_then_norm(native, M, N, K, monkeypatch):
-    """gemm_part with the add_partials_rmsnorm consumer in its last M blocks (TL) == gemm_part followed by
-    add_partials_rmsnorm, bit for bit (same slabs, same summation orders); three launches in a row check
-    the counters re-arm (and the slabs are still written)."""
-    torch.manual_seed(M + N + K)
-    x = torch.randn(M, K, device=DEV).bfloat16()
-    w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
-    g = (1 + 0.1 * torch.randn(N, device=DEV)).bfloat16()
-    h0 = torch.randn(M, N, device=DEV).bfloat16()
-    monkeypatch.setattr(native, "PART_TAIL", True)
-    monkeypatch.setattr(native, "STREAM_PART", False)  # the reference is the same gemm_part kernel's slabs
-    if not native.part_tail_ok(M, w):
-        pytest.skip("shape not supported by the tail launch")
-    h_ref = h0.clone()
-    xn_ref = native.add_partials_rmsnorm(native.gemm_part(x, w), h_ref, g, 1e-5)
-    cnt = native.part_tail_counters(DEV)
-    assert cnt.numel() >= 32 * 12
-    for it in range(3):
-        h = h0.clone()
-        xn = native.gemm_part_tail(x, w, h, g, 1e-5)
-        torch.cuda.synchronize()
-        assert torch.equal(h, h_ref), (it, (h.float() - h_ref.float()).abs().max().item())
-        assert torch.equal(xn, xn_ref), it
-        assert native.part_tail_armed(DEV), cnt.nonzero().flatten().tolist()
-    hr = (h0.float().cpu() + (x.float() @ w.float().t()).cpu().bfloat16().float()).bfloat16()
-    assert rel_err(h_ref.cpu(), hr) < 1e-2
-    assert not native.part_tail_error(DEV)
-
-
-@pytest.mark.parametrize("kv_lens,target", [([5200], 512), ([70, 3000], 256), ([777, 5300, 65, 2000], 512), ([1], 512)])
-def test_gemm_part_merge_tail_matches_separate(native, kv_lens, target):
-    """o_proj with the partition merge AND the residual + norm consumer in one launch == gemm_part_merge
-    followed by add_partials_rmsnorm, bit for bit."""
-    D, S, Hq, Hkv = 128, 8, 32, 8
-    torch.manual_seed(5)
-    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=9)
-    B = len(kv_lens)
-    kc, vc, bt = kc.to(DEV), vc.to(DEV), bt.to(DEV)
-    kvl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
-    pos = kvl - 1
-    slots = (bt[torch.arange(B, device=DEV), (pos // 64).long()] * 64 + pos % 64).int()
-    P = torch.randn(S, B, (Hq + 2 * Hkv) * D, device=DEV)
-    cos, sin = R.rope_tables(D, 131072, theta=500000.0)
-    cos, sin = cos.to(DEV), sin.to(DEV)
-    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv, target_blocks=target)
-    if mp < 2:
-        pytest.skip("single partition: no merge launch")
-    w = (torch.randn(4096, Hq * D, device=DEV) / math.sqrt(Hq * D)).bfloat16()
-    g = (1 + 0.1 * torch.randn(4096, device=DEV)).bfloat16()
-    h0 = torch.randn(B, 4096, device=DEV).bfloat16()
-    ws_o = torch.empty((B, Hq, mp, D), dtype=torch.float32, device=DEV)
-    ws_ml = torch.empty((B, Hq, mp, 2), dtype=torch.float32, device=DEV)
-    attn = torch.zeros(B, Hq * D, device=DEV).bfloat16()
-    native.attn_decode_rope(P, pos, cos, sin, slots, kc, vc, bt, kvl, attn, Hq, Hkv, D, pt, mp, ws_o=ws_o,
-                            ws_ml=ws_ml, defer_merge=True)
-    h_ref = h0.clone()
-    xn_ref = native.add_partials_rmsnorm(native.gemm_part_merge(attn, kvl, pt, mp, ws_o, ws_ml, Hq, w), h_ref, g, 1e-5)
-    for it in range(3):
-        h = h0.clone()
-        xn = native.gemm_part_merge_tail(attn, kvl, pt, mp, ws_o, ws_ml, Hq, w, h, g, 1e-5)
-        torch.cuda.synchronize()
-        assert torch.equal(h, h_ref) and torch.equal(xn, xn_ref), it
-    assert native.part_tail_armed(DEV)
-    assert not native.part_tail_error(DEV)
 
 
 @pytest.mark.parametrize("S,T", [(4, 33), (9, 32), (16, 1)])  # S > 8: more than one unrolled slab group

@@ -150,8 +150,8 @@ def test_split_k_decode_path_matches_plain_decode(tiny):
         calls, tails = [], []
         orig = model.hidden_states_decode_part
         model.hidden_states_decode_part = lambda inp, h: (calls.append(1), orig(inp, h))[1]
-        orig_tail = model.be.gemm_part_tail  # the norm-in-the-GEMM's-tail form (TP=1 o_proj / down)
-        model.be.gemm_part_tail = lambda *a: (tails.append(1), orig_tail(*a))[1]
+        orig_red = model.be.add_partials_rmsnorm  # the split-K slabs' reduce + residual + norm consumer
+        model.be.add_partials_rmsnorm = lambda *a: (tails.append(1), orig_red(*a))[1]
         eng = LLMEngine(model, num_blocks=32, max_batch=4, max_model_len=512, use_graphs=False)
         outs.append(eng.generate(prompts, params))
         assert bool(calls) == part and bool(tails) == part

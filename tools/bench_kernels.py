@@ -48,16 +48,13 @@ def main():
             w = (torch.randn(wn, K, device=dev) / math.sqrt(K)).bfloat16()
             r = torch.randn(M, N_, device=dev).bfloat16() if epi == "resid" else None
             out = torch.empty(M, N_, device=dev).bfloat16()
-            N.set_pp_variant(4)
-            t4 = timeit(lambda: N.gemm(x, w, resid=r, epi=epi, out=out, path=2))
-            N.set_pp_variant(2)
-            t = timeit(lambda: N.gemm(x, w, resid=r, epi=epi, out=out, path=2))
+            t = timeit(lambda: N.gemm(x, w, resid=r, epi=epi, out=out, path=6))
             t0 = timeit(lambda: N.gemm(x, w, resid=r, epi=epi, out=out, path=0))
             w8 = F8.quantize_weight(w)
             t8 = timeit(lambda: N.gemm_fp8(x, w8, resid=r, epi=epi, out=out))
             flops = 2 * M * wn * K
             tt = timeit(lambda: torch.matmul(x, w.t()))
-            rows.append(dict(kind="gemm_prefill", name=name, M=M, N=wn, K=K, pp_us=t * 1e6, pp_tflops=flops / t / 1e12, pp4_tflops=flops / t4 / 1e12,
+            rows.append(dict(kind="gemm_prefill", name=name, M=M, N=wn, K=K, pp_us=t * 1e6, pp_tflops=flops / t / 1e12,
                              tile128_tflops=flops / t0 / 1e12, fp8_w8a8_tflops=flops / t8 / 1e12,
                              torch_us=tt * 1e6, torch_tflops=flops / tt / 1e12))
             print(rows[-1], flush=True)

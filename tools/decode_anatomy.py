@@ -27,18 +27,8 @@ def main():
     dev = "cuda:0"
     w = L.LlamaWeights.random(cfg, dev, seed=0)
     m = L.LlamaModel(cfg, w, dev, max_positions=8192)
-    # DA_PF="off,16:128,32:255": decode MALL prefetch configs (MB per window : rider blocks) to A/B
-    cfgs = [c for c in os.environ.get("DA_PF", "").split(",") if c] or [None]
-    # DA_TAIL="1,0,1,0": alternate the norm-in-the-GEMM-tail launches (native.PART_TAIL) on / off
-    tails = [t for t in os.environ.get("DA_TAIL", "").split(",") if t] or [None]
     # DA_NT="0,1,0,1": alternate non-temporal K/V loads in the decode attention (native.DECODE_NT_MIN_BH)
     nts = [t for t in os.environ.get("DA_NT", "").split(",") if t] or [None]
-    # DA_FM="0,1,0,1": alternate the attention's in-kernel split-K merge (native.ATTN_FUSED_MERGE)
-    fms = [t for t in os.environ.get("DA_FM", "").split(",") if t] or [None]
-    # DA_SKU="2,1,2,1": K blocks per wave per iteration of the batch-1 skinny GEMM (down projection)
-    skus = [t for t in os.environ.get("DA_SKU", "").split(",") if t] or [None]
-    # DA_SP="1,0,1,0": split-K decode slabs from the LDS-DMA stream GEMM (native.STREAM_PART) or gemm_part
-    sps = [t for t in os.environ.get("DA_SP", "").split(",") if t] or [None]
     # DA_PAIR="128,64,...": tile rows of the SiLU*up stream GEMM (ragk_gemm_stream_set_pair_rows)
     pairs = [int(t) for t in os.environ.get("DA_PAIR", "").split(",") if t] or [None]
     # DA_NATIVE="NAME:v1,v2,...": alternate an integer policy global of ops/native.py (e.g.
@@ -52,10 +42,9 @@ def main():
     if os.environ.get("DA_LLAMA"):
         ll_name, vals = os.environ["DA_LLAMA"].split(":")
         ll_vals = [int(v) for v in vals.split(",")]
-    runs = [(B, c, t, nt, fm, sk, sp, nv, pr, lv) for lv in ll_vals for pr in pairs for nv in nat_vals for sp in sps
-            for sk in skus for fm in fms for nt in nts for t in tails for c in cfgs for B in Bs]
+    runs = [(B, nt, nv, pr, lv) for lv in ll_vals for pr in pairs for nv in nat_vals for nt in nts for B in Bs]
     from rag_llm_k8s_amd.ops import _lib, native
-    for B, pfc, tl, nt, fm, sk, sp, nv, pr, lv in runs:
+    for B, nt, nv, pr, lv in runs:
         if lv is not None:
             setattr(L, ll_name, lv)
             print("-- llama.%s = %d" % (ll_name, lv), flush=True)
@@ -65,27 +54,9 @@ def main():
         if nv is not None:
             setattr(native, nat_name, nv)
             print("-- native.%s = %d" % (nat_name, nv), flush=True)
-        if sp is not None:
-            native.STREAM_PART = sp == "1"
-            print("-- stream part %s" % sp, flush=True)
-        if sk is not None:
-            _lib.lib().ragk_gemm_skinny_set_unroll(int(sk))
-            print("-- skinny unroll %s" % sk, flush=True)
-        if fm is not None:
-            native.ATTN_FUSED_MERGE = fm == "1"
-            print("-- attention fused merge %s" % fm, flush=True)
-        if tl is not None:
-            native.PART_TAIL = tl == "1"
-            print("-- part tail %s" % tl, flush=True)
         if nt is not None:
             native.DECODE_NT_MIN_BH = 1 if nt == "1" else 1 << 30
             print("-- decode attention nt %s" % nt, flush=True)
-        if pfc is not None:
-            L.DECODE_PF = pfc != "off"
-            if L.DECODE_PF:
-                mbs, blk = pfc.split(":")
-                L.DECODE_PF_MB, L.DECODE_PF_BLOCKS = int(mbs), int(blk)
-            print("-- decode prefetch %s" % pfc, flush=True)
         eng = LLMEngine(m, num_blocks=B * 128 + 16, max_batch=B, max_prefill_tokens=32768, max_model_len=8192,
                         eos_ids=cfg.eos_token_id, graph_buckets=[B])
         eng.warmup_graphs([B])

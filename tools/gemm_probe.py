@@ -36,17 +36,6 @@ def main():
             elif p == "blas":  # the library route of ops.native (resid: in-place addmm, beta = 1)
                 h = r.clone() if r is not None else None
                 fns[p] = lambda h=h: N._gemm_blas(x, w, h, h if h is not None else out, epi)  # noqa: E731
-            elif "c" in p:  # "6c2" / "6c2@128": gemm_w4 with the continuous-kernel mode 2 (set_w4_cont)
-                pm, _, grid = p.partition("@")
-                path, mode = (int(v) for v in pm.split("c"))
-
-                def fn(path=path, mode=mode, grid=int(grid or -1)):
-                    N.set_w4_cont(mode)
-                    N.set_w4_grid(grid)
-                    N.gemm(x, w, resid=r, epi=epi, out=out, path=path)
-                    N.set_w4_cont(-1)
-                    N.set_w4_grid(-1)
-                fns[p] = fn
             elif "@" in p:  # "6@0": gemm_w4 with the persistent grid set to 0 (one block per tile)
                 path, grid = (int(v) for v in p.split("@"))
 
