@@ -343,7 +343,10 @@ __device__ __forceinline__ void w4_epilogue_reg(const f32x4 (&acc)[8][8], int wr
 //   m 61..125: 8 activation DMAs of tile t+2
 //   m 92/93  : vmcnt(13) (the 13 DMAs of this tile are the youngest), barrier: tile t+1 landed
 //   m 93..123: the 16 F0 reads of tile t+1 (8 weight, then 8 activation fragments, spread)
-//   m 127    : lgkmcnt(0): the next iteration opens on MFMAs whose operands are all in registers.
+// and no drain at the end of the K-tile: the next iteration waits for exactly the F0 fragments each of
+// its first MFMAs needs (lgkmcnt(7) before m 0 = b0[0..7] and a0[0] landed; 10 before m 8: a0[1]; 13
+// before m 16: a0[2]; the m 21 drain covers the rest), so the last F0 reads of a K-tile get 20+ MFMAs
+// instead of 4 to land (an lgkmcnt(0) before the last MFMA exposed their latency every K-tile).
 // M0 is set once per DMA group and post-incremented after the next MFMA (no s_nop between M0 and DMA).
 __device__ __forceinline__ void h_read(bf16x8& d, unsigned addr, int off_imm) {
   // off_imm is a compile-time constant at every call site (fully unrolled schedule)
@@ -373,10 +376,11 @@ constexpr int h_find(const int (&s)[8], int m) {
 // One K-tile. g = running K-tile index (ring slot g & 1); sa / sb = DMA source offsets at K-tile kst
 // (this tile's t+2 or the next tile's 0 / 1); ZERO = the F0 MFMAs start the accumulators (srcC = 0);
 // VMW = the m = 92 vmcnt bound (H_VM plus the vector-memory ops issued between the previous
-// iteration's DMAs and this one's, i.e. an epilogue). rbA / rbB: this lane's read bases (sub-step s,
-// buffer 0) of the activation / weight fragments; fragment i at + 2048 i (the swizzle of row
-// 16 i + fr does not depend on i).
-template <bool ZERO, int VMW>
+// iteration's DMAs and this one's, i.e. an epilogue). F0 = issue the 16 F0 reads of K-tile t+1 (false:
+// the caller issues them itself, w4_read_f0). rbA / rbB: this lane's read bases (sub-step s, buffer 0)
+// of the activation / weight fragments; fragment i at + 2048 i (the swizzle of row 16 i + fr does not
+// depend on i).
+template <bool ZERO, int VMW, bool F0 = true>
 __device__ __forceinline__ void w4_iter_h(char* smem, int g, i32x4 srd_a, i32x4 srd_b, const int (&sa)[8],
                                           const int (&sb)[8], int kst, int wid, const unsigned (&rbA)[2],
                                           const unsigned (&rbB)[2], f32x4 (&acc)[8][8], bf16x8 (&a0)[8],
@@ -390,7 +394,10 @@ __device__ __forceinline__ void w4_iter_h(char* smem, int g, i32x4 srd_a, i32x4 
   const unsigned rb1 = rbB[1] + cur, ra1 = rbA[1] + cur, rb0 = rbB[0] + nxt, ra0 = rbA[0] + nxt;
   static_for<128>([&](auto mc) __attribute__((always_inline)) {
     constexpr int m = decltype(mc)::value;
-    if constexpr (m == 21 || m == 51 || m == 127) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (m == 0) asm volatile("s_waitcnt lgkmcnt(7)" ::: "memory");
+    if constexpr (m == 8) asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory");
+    if constexpr (m == 16) asm volatile("s_waitcnt lgkmcnt(13)" ::: "memory");
+    if constexpr (m == 21 || m == 51) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr (m == 22 || m == 52) w4_barrier();
     if constexpr (m == 92) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VMW) : "memory");
     if constexpr (m == 93) w4_barrier();
@@ -410,8 +417,24 @@ __device__ __forceinline__ void w4_iter_h(char* smem, int g, i32x4 srd_a, i32x4 
     constexpr int r1b = h_find(H_RB1, m), r1a = h_find(H_RA1, m), r0b = h_find(H_RB0, m), r0a = h_find(H_RA0, m);
     if constexpr (r1b >= 0) h_read(b1[r1b], rb1, r1b * 2048);
     if constexpr (r1a >= 0) h_read(a1[r1a], ra1, r1a * 2048);
-    if constexpr (r0b >= 0) h_read(b0[r0b], rb0, r0b * 2048);
-    if constexpr (r0a >= 0) h_read(a0[r0a], ra0, r0a * 2048);
+    if constexpr (F0 && r0b >= 0) h_read(b0[r0b], rb0, r0b * 2048);
+    if constexpr (F0 && r0a >= 0) h_read(a0[r0a], ra0, r0a * 2048);
+  });
+}
+
+// The F0 reads of the K-tile in ring slot g & 1, in w4_iter_h's order (the 8 weight fragments, then the
+// 8 activation fragments), left in flight for the next w4_iter_h's counted waits.
+__device__ __forceinline__ void w4_read_f0(int g, const unsigned (&rbA)[2], const unsigned (&rbB)[2],
+                                           bf16x8 (&a0)[8], bf16x8 (&b0)[8]) {
+  const unsigned buf = (unsigned)(g & 1) * W_BUF;
+  const unsigned rb0 = rbB[0] + buf, ra0 = rbA[0] + buf;
+  static_for<8>([&](auto jc) __attribute__((always_inline)) {
+    constexpr int j = decltype(jc)::value;
+    h_read(b0[j], rb0, j * 2048);
+  });
+  static_for<8>([&](auto ic) __attribute__((always_inline)) {
+    constexpr int i = decltype(ic)::value;
+    h_read(a0[i], ra0, i * 2048);
   });
 }
 
@@ -456,6 +479,12 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
   // epilogue vector-memory ops younger than the next tile's K-tile-1 DMA at its first vmcnt
   constexpr int EV = w4_epi_vmem<EPI, OUT_F32>();
   constexpr int VMH0 = H_VM + EV > 63 ? 63 : H_VM + EV;
+  // The next tile's F0 fragments are read before the epilogue (in the last K-tile, hidden under its
+  // MFMAs) only where the epilogue leaves room for their 64 registers: with the bias, GELU or fp32
+  // residual epilogues the allocator spilled them to scratch straight after the asm read issued, i.e.
+  // before the data landed (tools/isa_lds_hazard.py checks every instantiation for that). Those read
+  // them after the epilogue instead.
+  constexpr bool LATE_F0 = !(EPI == EPI_NONE || EPI == EPI_SILU_MUL || (EPI == EPI_RESID && !OUT_F32));
 
   int tile = blockIdx.x;
   int z = KSPLIT ? tile / nwg : 0;
@@ -527,8 +556,10 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
     }
     w4_iter_h<false, H_VM>(smem, g, srd_a, srd_b, off_a, off_b, 0, wid, rbA, rbB, acc, a0, b0, a1, b1);
     ++g;
-    w4_iter_h<false, H_VM>(smem, g, srd_a, srd_b, off_a, off_b, 1, wid, rbA, rbB, acc, a0, b0, a1, b1);
+    w4_iter_h<false, H_VM, !LATE_F0>(smem, g, srd_a, srd_b, off_a, off_b, 1, wid, rbA, rbB, acc, a0, b0, a1, b1);
     ++g;
+    // the epilogue is compiler-scheduled code: it may move any register, so no asm read is in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     w4_pin_acc(acc);
     void* Cz = KSPLIT ? (void*)(reinterpret_cast<float*>(C) + (size_t)z * M * ldc) : C;
     if (m0 + WBM <= M && n0 + WBN <= N) {
@@ -544,8 +575,10 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
     asm volatile("s_nop 7" ::: "memory");
     if (!has_next) {
       __builtin_amdgcn_s_waitcnt(0x0F70);  // the re-staged K-tiles land before the block's LDS is released
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // and the last (unused) F0 reads
       break;
     }
+    if constexpr (LATE_F0) w4_read_f0(g, rbA, rbB, a0, b0);
     tile = next;
     m0 = nm0;
     n0 = nn0;

@@ -191,6 +191,17 @@ class IPCAllReduce:
             return int(self._err_word.value)
         return max(0, int(self.L.ragk_ar_error(self.h)))
 
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.ragk_ar_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
 
 SITES = {1: "all-reduce (start barrier)", 2: "all-reduce (two-shot mid barrier)", 3: "all-gather",
          4: "fused reduce+norm row (start barrier)", 5: "fused reduce+norm row (two-shot mid barrier)"}
@@ -204,14 +215,3 @@ def describe_error(rec: int) -> str:
     site, peer, slot, ep = (rec >> 1) & 7, (rec >> 4) & 7, (rec >> 7) & 255, (rec >> 15) & 0xFFFF
     what = SITES.get(site, "site %d" % site)
     return "%s, block/row %d, call %d (mod 65536): peer rank %d never arrived" % (what, slot, ep, peer)
-
-    def close(self):
-        if getattr(self, "h", None):
-            self.L.ragk_ar_destroy(self.h)
-            self.h = None
-
-    def __del__(self):  # pragma: no cover - interpreter shutdown order
-        try:
-            self.close()
-        except Exception:
-            pass

@@ -28,7 +28,7 @@ def test_gemm_plain(native, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 256, 128), (300, 1024, 768), (1111, 6144, 4096), (256, 256, 128),
-                                   (2049, 512, 1024), (513, 4104, 256), (260, 768, 384), (700, 1024, 192)])
+                                   (2049, 512, 1024), (513, 4104, 256), (260, 768, 384), (700, 1024, 384)])
 @pytest.mark.parametrize("kernel", ["pp", "w4"])
 def test_gemm_pingpong(native, M, N, K, kernel):
     """The two 256x256 large-M kernels: gemm_w4 (4 waves, the prefill default, K >= 192) and gemm_pp (8-wave
@@ -42,11 +42,10 @@ def test_gemm_pingpong(native, M, N, K, kernel):
 
 
 @pytest.mark.parametrize("grid", [8, 16])
-@pytest.mark.parametrize("M,N,K", [(1111, 1024, 256), (513, 4104, 192), (2048, 512, 192), (777, 1280, 384),
+@pytest.mark.parametrize("M,N,K", [(1111, 1024, 256), (513, 4104, 256), (2048, 512, 256), (777, 1280, 384),
                                    (1030, 768, 1024)])
 def test_gemm_w4_persistent(native, M, N, K, grid):
-    """Persistent gemm_w4: a few blocks loop over every tile (full and edge tiles, the shortest ring of
-    three K-tiles), so the next-tile staging inside the K-stream, the register epilogue and the counted
+    """Persistent gemm_w4: a few blocks loop over every tile (full and edge tiles, rings of 4-16 K-tiles), so the next-tile staging inside the K-stream, the register epilogue and the counted
     waits around it run many times per block."""
     native.set_w4_grid(grid)
     try:
@@ -878,11 +877,13 @@ def test_gemm_vocab_stream_route(native, M):
     assert not native.use_stream(16, N, K, "none")
 
 
-@pytest.mark.parametrize("M", [17, 32, 64])
+@pytest.mark.parametrize("M", [5, 8, 16, 17, 32, 64])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (1000, 1024), (4096, 1792)])
 @pytest.mark.parametrize("rows", [None, 64])
 def test_gemm_stream_part(native, M, N, K, rows):
-    """Split-K slabs from the LDS-DMA stream GEMM (gemm_stream.hip SLAB): P.sum(0) = x @ w^T, [S, M, N]."""
+    """Split-K slabs from the LDS-DMA stream GEMM (gemm_stream.hip SLAB): P.sum(0) = x @ w^T, [S, M, N].
+    M = 5..16 is the one-row-tile instantiation (activation rows padded below 16) that decode batches
+    from STREAM_PART_MIN_M up take by default."""
     torch.manual_seed(M + N)
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
@@ -891,6 +892,14 @@ def test_gemm_stream_part(native, M, N, K, rows):
     P = native.gemm_stream_part(x, w, rows=rows or r or 128, S=S or 2)
     assert P.shape[1:] == (M, N) and (K // 64) % P.shape[0] == 0
     assert rel_err(P.sum(0), x.float() @ w.float().t()) < 2e-3
+    if rows is None:  # the register-streaming gemm_part that the slabs replace agrees
+        old = native.STREAM_PART
+        native.STREAM_PART = False
+        try:
+            Q = native.gemm_part(x, w)
+        finally:
+            native.STREAM_PART = old
+        assert rel_err(P.sum(0), Q.sum(0)) < 1e-4
 
 
 @pytest.mark.parametrize("M", [1, 2, 4])

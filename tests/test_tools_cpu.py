@@ -4,7 +4,10 @@ import csv
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+import pytest
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 import gap_report  # noqa: E402
 import pmc_summary  # noqa: E402
@@ -70,3 +73,35 @@ def test_pmc_summary(tmp_path, capsys, monkeypatch):
     pmc_summary.main()
     out = capsys.readouterr().out
     assert "wg=   256" in out and "clk=2.40GHz" in out and "mfma=50.0%" in out
+
+
+def test_isa_lds_hazard_model():
+    """The asm-wait checker: a register of an LDS read touched before its lgkmcnt retires it is a
+    hazard (the spill gemm_w4's GELU epilogues produced); counted waits retire the oldest reads."""
+    import isa_lds_hazard as H
+
+    spill = [(0, "ds_read_b128 v[0:3], v112"), (8, "scratch_store_dwordx4 off, v[0:3], off")]
+    assert [h[0] for h in H.check_kernel(0, spill)] == [8]
+    counted = [(0, "ds_read_b128 v[0:3], v9"), (8, "ds_read_b128 v[4:7], v9 offset:2048"),
+               (16, "s_waitcnt lgkmcnt(1)"), (24, "v_mfma_f32_16x16x32_bf16 a[0:3], v[0:3], v[0:3], a[0:3]"),
+               (32, "v_mfma_f32_16x16x32_bf16 a[0:3], v[4:7], v[0:3], a[0:3]")]
+    assert [h[0] for h in H.check_kernel(0, counted)] == [32]
+    # loop back edge: reads issued at the bottom are pending at the top until the wait there
+    loop = [(0, "v_mfma_f32_16x16x32_bf16 a[0:3], v[0:3], v[0:3], a[0:3]"), (8, "ds_read_b128 v[0:3], v9"),
+            (16, "s_cbranch_scc1 -3 <k+0x0>")]
+    assert [h[0] for h in H.check_kernel(0, loop)] == [0]
+    waited = [(0, "s_waitcnt lgkmcnt(0)")] + [(a + 8, i) for a, i in loop]
+    assert H.check_kernel(0, waited) == []
+
+
+def test_isa_lds_hazard_kernels_clean():
+    """Every built kernel object passes the checker (the hand-placed waits of gemm_w4 included)."""
+    import glob
+
+    import isa_lds_hazard as H
+
+    objs = sorted(glob.glob(os.path.join(ROOT, "build", "obj", "*.hip.o")))
+    if not objs or not os.path.exists(os.path.join(H.LLVM, "llvm-objdump")):
+        pytest.skip("kernel objects not built here")
+    for obj in objs:
+        assert H.check_object(obj) == [], obj

@@ -13,7 +13,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from rag_llm_k8s_amd.ops import native as N  # noqa: E402
 
 SHAPES = [(6144, 4096, "none"), (4096, 4096, "resid"), (14336, 4096, "silu_mul"), (4096, 14336, "resid"),
-          (4096, 4096, "none"), (4096, 14336, "none")]
+          (4096, 4096, "none"), (4096, 14336, "none"),
+          # K scaling (fixed per-tile cost = prologue + epilogue): 6-7 vs 0, 8-9 vs 1
+          (6144, 2048, "none"), (6144, 8192, "none"), (4096, 2048, "resid"), (4096, 8192, "resid")]
 
 
 def main():
@@ -35,7 +37,11 @@ def main():
                 fns[p] = lambda: torch.matmul(x, w.t())  # noqa: E731
             elif p == "blas":  # the library route of ops.native (resid: in-place addmm, beta = 1)
                 h = r.clone() if r is not None else None
-                fns[p] = lambda h=h: N._gemm_blas(x, w, h, h if h is not None else out, epi)  # noqa: E731
+                if epi == "silu_mul":  # no library epilogue: the plain GEMM of both halves
+                    o2 = torch.empty(M, wn, device="cuda").bfloat16()
+                    fns[p] = lambda o2=o2: N._gemm_blas(x, w, None, o2, "none")  # noqa: E731
+                else:
+                    fns[p] = lambda h=h: N._gemm_blas(x, w, h, h if h is not None else out, epi)  # noqa: E731
             elif "@" in p:  # "6@0": gemm_w4 with the persistent grid set to 0 (one block per tile)
                 path, grid = (int(v) for v in p.split("@"))
 

@@ -9,8 +9,8 @@ import sys
 
 
 def short(name):
-    for key in ("gemm_w4c_kernel", "gemm_w4_kernel", "gemm_pp_kernel", "gemm_pp4_kernel", "attn_prefill_kernel", "attn_decode_kernel",
-                "Cijk"):
+    for key in ("gemm_w4_kernel", "gemm_pp_kernel", "attn_prefill_v3_kernel", "attn_prefill_kernel",
+                "attn_decode_kernel", "Cijk"):
         if key in name:
             i = name.find("<")
             return key + (name[i:i + 12] if i >= 0 and key != "Cijk" else "")
@@ -48,6 +48,10 @@ def main():
                         out.append("%s=%.1f%%" % (lab, 100 * c[k] / wc))
             if "SQ_LDS_IDX_ACTIVE" in c:
                 out.append("ldsconf=%.3f" % (c.get("SQ_LDS_BANK_CONFLICT", 0) / max(1, c["SQ_LDS_IDX_ACTIVE"])))
+            waves = max(1, d["grid"] // 64)
+            ins = ["%s=%.0f" % (k[9:].lower(), c[k] / waves) for k in sorted(c) if k.startswith("SQ_INSTS_")]
+            if ins:
+                out.append("per-wave " + " ".join(ins))
             if "TCC_HIT_sum" in c:
                 out.append("l2hit=%.1f%%" % (100 * c["TCC_HIT_sum"] / max(1, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])))
             print("  ".join(out))
