@@ -23,9 +23,12 @@ from __future__ import annotations
 
 import logging
 import os
+import time
 
 import torch
 import torch.distributed as dist
+
+from ..utils import faults
 
 log = logging.getLogger(__name__)
 
@@ -79,6 +82,10 @@ class TPComm:
     def _guard(self):
         if self.broken is not None:
             raise CommError(self.broken)
+        skew = faults.value("comm_skew_ms")
+        if skew:  # fault injection: this rank reaches the collective late by a per-call, per-rank amount
+            self._calls = getattr(self, "_calls", 0) + 1
+            time.sleep(float(skew) * ((self._calls * 7 + self.rank * 3) % 5) / 4e3)
 
     # ------------------------------------------------------------------ collectives
     def all_reduce(self, x: torch.Tensor):

@@ -14,6 +14,7 @@ real server) can switch on without code changes:
   embed_error            the embedder raises (retrieval failure -> HTTP 500)
   comm_hang_s=X          a TP follower stalls X s before stepping (collective watchdog)
   bench_tp_hang_s=X      bench.py's TP=N C=1 phase stalls X s (its watchdog must exit non-zero)
+  comm_skew_ms=X         every TP collective starts late on each rank by 0..X ms (per call and rank)
 
 `set_faults()` overrides the environment in-process (tests).
 """

@@ -236,3 +236,14 @@ def test_dp_ingest_and_sharded_search_layouts(world):
         D, I = ref.search(out[r]["q"], 5)
         assert torch.equal(out[r]["I"], I)
         assert torch.allclose(out[r]["D"], D, atol=1e-5)
+
+
+def test_tp8_skewed_ranks_same_results(monkeypatch):
+    """The 8-rank TP collective sequence (prefill, split-K decode with the fused row-parallel reduction,
+    vocab-parallel sampling, control channel) with every rank reaching every collective late by a
+    different 0..20 ms (RAGK_FAULTS comm_skew_ms): the same tokens and texts as without skew. A rank
+    that is merely late is never an error; only a bounded wait that expires is (tests/test_faults_cpu.py)."""
+    ref = _run(8, _batch_worker, 8, 5)
+    monkeypatch.setenv("RAGK_FAULTS", "comm_skew_ms=20")
+    out = _run(8, _batch_worker, 8, 5)
+    assert all(out[r] == ref[0] for r in range(8))
