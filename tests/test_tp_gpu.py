@@ -235,8 +235,12 @@ def _spawn(target, timeout=600, world=WORLD):
     procs = [ctx.Process(target=target, args=(r, port, d) + extra) for r in range(world)]
     for p in procs:
         p.start()
-    for p in procs:
-        p.join(timeout=timeout)
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline and any(p.is_alive() for p in procs):
+        procs[[p.is_alive() for p in procs].index(True)].join(timeout=30)
+        alive = [r for r, p in enumerate(procs) if p.is_alive()]
+        if alive:  # the parent's view every 30 s: which ranks are still running
+            _log(-1, world, "ranks still running: %s" % alive)
     for p in procs:
         if p.is_alive():
             p.kill()
@@ -245,11 +249,10 @@ def _spawn(target, timeout=600, world=WORLD):
     return [torch.load(os.path.join(d, "r%d.pt" % r), weights_only=False) for r in range(world)]
 
 
-# 8 ranks as 8 processes on ONE GPU is opt-in (RAGK_TEST_TP8=1): of five round-4 runs one passed and four
-# stalled or timed out in a peer wait, at a different point each time (first prefill, graph replay, eager
-# decode) -- eight time-sliced GPU contexts whose collectives each need all eight running at once. The
-# 8-rank peer-mapped collectives themselves are covered by tests/test_ipc_allreduce_gpu.py (WORLD 8).
-TP_WORLDS = [2, 4] + ([8] if os.environ.get("RAGK_TEST_TP8") == "1" else [])
+# 8 ranks as 8 processes on ONE GPU: with HIP's default 4 hardware queues per process (32 queues) a rank's
+# collective kernel could start tens of seconds after its peers' (queue co-scheduling; kernel trace in
+# profiles/tp8_trace_report_r5.txt), so the workers run one queue each (_tp_worker).
+TP_WORLDS = [2, 4, 8]
 
 
 @pytest.mark.parametrize("world", TP_WORLDS)
@@ -259,7 +262,7 @@ def test_tp_llama8b_widths_on_one_gpu(native, world):
     logits vs TP=1, graph + async decode == eager (2 / 4 ranks), the same samples on every rank, and the
     micro-batched overlap prefill (the 1100-token prompt)."""
     WORLD = world
-    out = _spawn(_tp_worker, world=world)
+    out = _spawn(_tp_worker, world=world, timeout=420 if world >= 8 else 600)
     assert all(o["ipc"] for o in out), "peer-mapped collectives must pass their self-test"
     ref = out[0]["ref_logits"]
     for r in range(WORLD):

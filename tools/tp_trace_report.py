@@ -25,7 +25,8 @@ def load(root):
             name = r.get("Kernel_Name", "")
             if any(k in name for k in KEYS):
                 pid = r.get("Process_Id") or os.path.basename(f).split("_")[0]
-                per[pid].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name.split("(")[0][-40:]))
+                per[pid].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                                 next(k for k in KEYS if k in name)))
     for v in per.values():
         v.sort()
     return per
