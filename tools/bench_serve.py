@@ -77,9 +77,11 @@ def main():
     ap.add_argument("--max-batch", type=int, default=64)
     ap.add_argument("--max-prefill-tokens", type=int, default=8192,
                     help="prefill budget per (mixed) engine step: bounds how long a step can stall decoding requests")
-    ap.add_argument("--mixed-prefill-tokens", default="2048",
-                    help="prompt tokens a step carrying decode rows may take (engine mixed_prefill_tokens); a "
-                         "comma list runs the Poisson phase once per value (same server)")
+    ap.add_argument("--mixed-prefill-tokens", type=int, default=2048,
+                    help="prompt tokens a step carrying decode rows may take (engine mixed_prefill_tokens; 0 = off)")
+    ap.add_argument("--poisson-configs", default=None,
+                    help="comma list of mixed:max prefill budgets (e.g. 0:8192,2048:32768): the Poisson phase once "
+                         "per pair on the same server (default: the two flags above)")
     ap.add_argument("--c1", type=int, default=20, help="sequential single requests (0 = skip)")
     ap.add_argument("--rate", type=float, default=8.0, help="Poisson arrival rate, requests/s (0 = skip)")
     ap.add_argument("--duration", type=float, default=30.0, help="seconds of Poisson arrivals")
@@ -98,13 +100,15 @@ def main():
     from rag_llm_k8s_amd.utils.workload import build_workload, make_queries
 
     _build.build_all()
-    budgets = [int(b) for b in str(a.mixed_prefill_tokens).split(",")]
+    configs = ([tuple(int(v) for v in c.split(":")) for c in a.poisson_configs.split(",")] if a.poisson_configs
+               else [(a.mixed_prefill_tokens, a.max_prefill_tokens)])
     dev = "cuda:0" if torch.cuda.is_available() else "cpu"
     t0 = time.time()
     wl = build_workload(model=a.model, embedder=a.embedder, n_chunks=a.chunks, retrieve_k=4, context_k=4,
-                        max_new_tokens=a.max_new_tokens, max_batch=a.max_batch, max_prefill_tokens=a.max_prefill_tokens,
+                        max_new_tokens=a.max_new_tokens, max_batch=a.max_batch,
+                        max_prefill_tokens=max(c[1] for c in configs),
                         device=dev, seed=0, use_graphs=dev.startswith("cuda"), start_threads=True, ignore_eos=True,
-                        mixed_prefill_tokens=budgets[0],
+                        mixed_prefill_tokens=configs[0][0],
                         **({"word_vocab": 20000, "chunk_words": 120} if a.model == "tiny" else {}))
     svc = wl.svc
     svc.engine.warmup_graphs() if dev.startswith("cuda") else None
@@ -121,14 +125,15 @@ def main():
            "config": {"model": "Llama-3.1-8B-Instruct" if a.model == "8b" else "llama-tiny",
                       "embedder": "all-MiniLM-L6-v2", "index": "FlatL2 %d vectors" % a.chunks, "retrieve_k": 4,
                       "context_k": 4, "max_new_tokens": a.max_new_tokens, "max_prefill_tokens": a.max_prefill_tokens,
-                      "mixed_prefill_tokens": budgets, "max_batch": a.max_batch, "dtype": "bf16"},
+                      "poisson_configs": ["%d:%d" % c for c in configs], "max_batch": a.max_batch, "dtype": "bf16"},
            "data": "synthetic (random-init weights; Zipfian pseudo-English corpus)", "setup_s": round(setup_s, 1)}
     if a.c1:
         rs = [post(port, next(qi)) for _ in range(a.c1)]
         res["c1"] = summarize(rs)
         print("C=1: %s" % json.dumps(res["c1"]), flush=True)
-    for bi, budget in enumerate(budgets if a.rate > 0 else []):
-        svc.engine.mixed_prefill_tokens = budget  # between runs: the engine is idle
+    for bi, (budget, maxp) in enumerate(configs if a.rate > 0 else []):
+        # between runs the engine is idle; both are read per step (LLMEngine._admit)
+        svc.engine.mixed_prefill_tokens, svc.engine.max_prefill_tokens = budget, maxp
         rng = random.Random(11)
         out, lock, threads = [], threading.Lock(), []
 
@@ -156,9 +161,10 @@ def main():
         ok = [r for r in out if "error" not in r]
         s = summarize(ok, wall)
         s.update(rate_rps=a.rate, duration_s=a.duration, errors=len(out) - len(ok),
-                 offered_tokens_per_s=round(a.rate * a.max_new_tokens, 1), mixed_prefill_tokens=budget)
-        res["poisson" if bi == 0 else "poisson_mixed_%d" % budget] = s
-        print("Poisson %.1f/s, mixed budget %d: %s" % (a.rate, budget, json.dumps(s)), flush=True)
+                 offered_tokens_per_s=round(a.rate * a.max_new_tokens, 1), mixed_prefill_tokens=budget,
+                 max_prefill_tokens=maxp)
+        res["poisson" if bi == 0 else "poisson_%d_%d" % (budget, maxp)] = s
+        print("Poisson %.1f/s, mixed %d max %d: %s" % (a.rate, budget, maxp, json.dumps(s)), flush=True)
     res["engine"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in svc.engine.stats.items()}
     line = json.dumps(res)
     print(line, flush=True)
