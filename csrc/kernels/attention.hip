@@ -703,6 +703,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void attn_prefill_v3_kernel(Prefil
     const int soff_k = tile_soff(st_k ? t + 3 : 0);
     const int soff_v = tile_soff(st_v ? t + 2 : 0);
     float alpha = 1.f, mx = -INFINITY, mref = 0.f, ls = 0.f, pend = 0.f;
+    float pv[32];  // the probabilities of this tile (P is packed from here, S_cur is not rewritten)
     pp_static_for<32>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       // MFMA slot i
@@ -725,14 +726,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void attn_prefill_v3_kernel(Prefil
       // softmax chunk: max in slots 0..3, row statistics in 4, one element per slot from 5 on
       if constexpr (DIAG == 1) {
       } else if constexpr (i < 4) {
-        float v[8];
+        // no input pins: a pinned copy of each element cost a v_mov (the sched barrier keeps the slot)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          v[e] = S_cur[i / 2][8 * (i % 2) + e];
-          pin(v[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) mx = fmaxf(mx, v[e]);
+        for (int e = 0; e < 8; ++e) mx = fmaxf(mx, S_cur[i / 2][8 * (i % 2) + e]);
         pin(mx);
       } else if constexpr (i == 4) {
         mx = max_xor32(mx);
@@ -745,23 +741,23 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void attn_prefill_v3_kernel(Prefil
         pin(m_i);
         pin(mref);
       } else {
-        // elements x with 5 + (27 x) / 32 == i; each exp result is added to the row sum one element
-        // later (no exp -> add dependency inside a slot: that was a wait state per element)
+        // elements x with 5 + (27 x) / 32 == i: the probability straight from the accumulator, pinned
+        // (results only: a pinned copy of an input element cost a v_mov); each is added to the row sum
+        // one element later (no exp -> add dependency inside a slot)
         pp_static_for<32>([&](auto xc) {
           constexpr int x = decltype(xc)::value;
           if constexpr (5 + (27 * x) / 32 == i) {
-            float sv = S_cur[x >> 4][x & 15];
-            pin(sv);
-            ls += pend;
-            const float pe = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -mref));
-            S_cur[x >> 4][x & 15] = pe;
+            float pe = __builtin_amdgcn_exp2f(__builtin_fmaf(S_cur[x >> 4][x & 15], c, -mref));
+            pin(pe);
+            ls += pend;  // the previous element's value: no exp -> add dependency inside a slot
             pend = pe;
+            pv[x] = pe;
             if constexpr (x % 8 == 7) {
-              P[x / 8] = pack_p32(S_cur[x / 16], 8 * ((x / 8) & 1));
+              P[x / 8] = (bf16x8){f2bf_s(pv[x - 7]), f2bf_s(pv[x - 6]), f2bf_s(pv[x - 5]), f2bf_s(pv[x - 4]),
+                                  f2bf_s(pv[x - 3]), f2bf_s(pv[x - 2]), f2bf_s(pv[x - 1]), f2bf_s(pv[x])};
               pin(P[x / 8]);
             }
             pin(ls);
-            pin(pend);
           }
         });
       }

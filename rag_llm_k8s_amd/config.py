@@ -54,8 +54,10 @@ class RagConfig:
     max_batch: int = 64  # concurrent sequences in one decode step
     max_model_len: int = 16384
     max_prefill_tokens: int = 32768  # tokens per prefill step (chunked prefill budget)
-    # prompt tokens per step while sequences are decoding (decode-aware budget, TPOT bound; 0 = off)
-    mixed_prefill_tokens: int = 2048
+    # prompt tokens per step while sequences are decoding (decode-aware cap; 0 = off). Off by default:
+    # at Poisson 8 req/s caps of 2048 / 1024 / 512 made TPOT p50 15-27 ms and TTFT p50 0.2-10 s against
+    # 10.6 ms / 82 ms uncapped -- every small chunk re-reads the weights (profiles/serve_r5b.json)
+    mixed_prefill_tokens: int = 0
     kv_cache_fraction: float = 0.80  # of free HBM after weights
     kv_cache_blocks: int = 0  # explicit override (64-token blocks)
     embed_batch_tokens: int = 65536

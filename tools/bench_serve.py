@@ -75,9 +75,9 @@ def main():
     ap.add_argument("--chunks", type=int, default=10000)
     ap.add_argument("--max-new-tokens", type=int, default=150)
     ap.add_argument("--max-batch", type=int, default=64)
-    ap.add_argument("--max-prefill-tokens", type=int, default=8192,
+    ap.add_argument("--max-prefill-tokens", type=int, default=32768,
                     help="prefill budget per (mixed) engine step: bounds how long a step can stall decoding requests")
-    ap.add_argument("--mixed-prefill-tokens", type=int, default=2048,
+    ap.add_argument("--mixed-prefill-tokens", type=int, default=0,
                     help="prompt tokens a step carrying decode rows may take (engine mixed_prefill_tokens; 0 = off)")
     ap.add_argument("--poisson-configs", default=None,
                     help="comma list of mixed:max prefill budgets (e.g. 0:8192,2048:32768): the Poisson phase once "

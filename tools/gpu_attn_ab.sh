@@ -4,10 +4,10 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-V=${AP_VARIANTS:-0,1}
-{ AP_VARIANTS=$V timeout -k 10 120 python3 -u tools/attn_pp_ab.py &&
-  AP_VARIANTS=$V AP_LENS=5200 timeout -k 10 120 python3 -u tools/attn_pp_ab.py &&
-  AP_VARIANTS=$V AP_LENS=2048 AP_CTX=3072 timeout -k 10 120 python3 -u tools/attn_pp_ab.py; } > gpurun_out/attn_ab.log 2>&1
+
+{ timeout -k 10 120 python3 -u tools/attn_pp_ab.py &&
+  AP_LENS=5200 timeout -k 10 120 python3 -u tools/attn_pp_ab.py &&
+  AP_LENS=2048 AP_CTX=3072 timeout -k 10 120 python3 -u tools/attn_pp_ab.py; } > gpurun_out/attn_ab.log 2>&1
 rc=$?
 cat gpurun_out/attn_ab.log | grep -v amdgpu.ids
 exit $rc
