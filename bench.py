@@ -150,13 +150,19 @@ def main():
     dev = ctx.device
     comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, dev, ctx.tp_cpu_group) if ctx.tp > 1 else None
     t_setup = time.time()
+
+    def progress(msg):  # rank 0, stderr (the JSON line is the only stdout)
+        if ctx.rank == 0:
+            print("bench: " + msg, file=sys.stderr, flush=True)
+
     wl = build_workload(model=a.model, embedder=a.embedder, n_chunks=a.chunks, chunk_words=a.chunk_words,
                         retrieve_k=a.retrieve_k, context_k=a.context_k, max_new_tokens=a.max_new_tokens,
                         max_batch=a.concurrency,
                         device=dev, ctx=ctx, tp_comm=comm, seed=0, use_graphs=not a.no_graphs, index_type=a.index,
-                        dtype=a.dtype, index_vectors=a.index_vectors)
+                        dtype=a.dtype, index_vectors=a.index_vectors, progress=progress)
     svc = wl.svc
     svc.engine.warmup_graphs()
+    progress("graphs captured, setup %.1f s" % (time.time() - t_setup))
     params = SamplingParams(max_new_tokens=a.max_new_tokens, temperature=0.7, top_p=0.9, top_k=50, do_sample=True,
                             ignore_eos=True)
     setup_s = time.time() - t_setup
@@ -173,6 +179,7 @@ def main():
 
     for w in range(a.warmup):
         run_step(-1 - w)
+        progress("warmup step %d done" % w)
     D.barrier(ctx)
     sync()
     t0 = time.perf_counter()

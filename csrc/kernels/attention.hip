@@ -1234,7 +1234,7 @@ hipError_t launch_prefill(PrefillArgs a, int n_tiles, hipStream_t st) {
   const dim3 grid(n_tiles * n_hg);
   if constexpr (D == 128 && GB == 4 && CAUSAL && PAGED) {
     if (a.kv_bytes) {
-      hipLaunchKernelGGL((attn_prefill_v3_kernel<8, false, 0, 0, true>), grid, dim3(512), 0, st, a);
+      hipLaunchKernelGGL((attn_prefill_v3_kernel<8, false, 0, 1, true>), grid, dim3(512), 0, st, a);
       return hipGetLastError();
     }
   }

@@ -143,7 +143,9 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
                    max_new_tokens=150, max_batch=32, max_model_len=8192, max_prefill_tokens=32768, device="cuda",
                    ctx=None, tp_comm=None, seed=0, use_graphs=True, index_type="flat", kv_blocks=None,
                    word_vocab=400000, dtype="bf16", index_vectors=0, start_threads=False, ignore_eos=False,
-                   mixed_prefill_tokens=0):
+                   mixed_prefill_tokens=0, progress=None):
+    """`progress(msg)`: called after each setup stage (bench.py prints it: a 70B / 1M-vector setup runs
+    for minutes)."""
     from ..engine.encoder_engine import EmbeddingEngine
     from ..engine.llm_engine import LLMEngine
     from ..index.store import DocumentStore
@@ -165,6 +167,8 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     enc_vocab = min(16000, ecfg.vocab_size) if xlmr else ecfg.vocab_size
     llm_tok, enc_tok = make_tokenizers(wm, lcfg.vocab_size, enc_vocab, ctx, "unigram" if xlmr else "wordpiece")
     t["tokenizers_s"] = time.time() - t0
+    say = progress or (lambda msg: None)
+    say("tokenizers %.1f s" % t["tokenizers_s"])
 
     t0 = time.time()
     tp_rank = ctx.tp_rank if ctx is not None else 0
@@ -183,6 +187,7 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     ew = E.EncoderWeights.random(ecfg, device, seed=seed + 1)
     emb = EmbeddingEngine(E.EncoderModel(ecfg, ew, device), enc_tok)
     t["weights_s"] = time.time() - t0
+    say("weights %.1f s" % t["weights_s"])
 
     t0 = time.time()
     chunks = make_chunks(wm, n_chunks, chunk_words, seed)
@@ -199,6 +204,7 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     if device.startswith("cuda"):
         torch.cuda.synchronize()
     t["embed_s"] = time.time() - t0  # tokenize + encode of the n_chunks corpus (ingest throughput)
+    say("corpus %.1f s, embed %.1f s" % (t["corpus_s"], t["embed_s"]))
     meta = [{"filename": "synthetic_%05d.pdf" % (i // 20), "chunk_id": i % 20, "text": c}
             for i, c in enumerate(chunks)]
     # BASELINE config 4 scale (1M-chunk index): the rest of the index is a second corpus of
@@ -216,6 +222,7 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
                                              "chunk_id": (done + i) % 1000, "text": x}
                                             for i, x in enumerate(texts)]))
             done += nb
+            say("index corpus %d / %d chunks embedded" % (done, index_vectors))
     if index_type == "ivf":  # train the coarse quantizer on the whole corpus (faiss subsample rule)
         store.index.train(torch.cat([vecs] + [v for v, _ in pads]))
     store.add(vecs, meta, dedupe=False, persist=False)
@@ -224,6 +231,7 @@ def build_workload(model="8b", embedder="minilm", n_chunks=10000, chunk_words=10
     if device.startswith("cuda"):
         torch.cuda.synchronize()
     t["ingest_s"] = time.time() - t0
+    say("ingest %.1f s" % t["ingest_s"])
     svc = RagService(cfg, engine, llm_tok, emb, store, gen_config={"do_sample": True,
                                                                    "eos_token_id": lcfg.eos_token_id},
                      start_threads=start_threads)

@@ -29,6 +29,8 @@ B70="--model 70b --index ivf --index-vectors 1000000"
 case "${WHICH:-all}" in
   fp8) run fp8 600 $FP8 --steps 5 --warmup 2 && prof fp8 600 $FP8 --steps 2 --warmup 1 --c1 1 --c1-tp 0 ;;
   70b) run 70b_ivf 900 $B70 --steps 2 --warmup 1 --c1 1 && prof 70b_ivf 900 $B70 --steps 1 --warmup 1 --c1 0 --c1-tp 0 ;;
+  70b_run) run 70b_ivf 1000 $B70 --steps 2 --warmup 1 --c1 1 ;;
+  70b_prof) prof 70b_ivf 1000 $B70 --steps 1 --warmup 1 --c1 0 --c1-tp 0 ;;
   all) run fp8 600 $FP8 --steps 5 --warmup 2 && prof fp8 600 $FP8 --steps 2 --warmup 1 --c1 1 --c1-tp 0 &&
        run 70b_ivf 900 $B70 --steps 2 --warmup 1 --c1 1 && prof 70b_ivf 900 $B70 --steps 1 --warmup 1 --c1 0 --c1-tp 0 ;;
 esac
