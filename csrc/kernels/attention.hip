@@ -695,10 +695,18 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void attn_prefill_v3_kernel(Prefil
   // d-step (i-16) / 2). Slot i reads the fragment of slot i + V3_PF; the last V3_PF slots read the
   // first PV(t) fragments of the next iteration. Softmax(t) of S_cur -> P in chunks. DMA: K(t+3) (slots 6..18),
   // V(t+2) (22..28). Then O *= alpha(t) (rare), vmcnt (this iteration's DMAs stay in flight), barrier.
-  auto fast = [&](int t, f32x16 (&S_cur)[2], f32x16 (&S_next)[2]) {
+  // PH = t & 3, a compile-time constant (the loop below is unrolled by the ring's 4 slots): with the slot
+  // offsets constant every fragment read folds its tile offset into the ds_read immediate (one v_add per
+  // fragment read with runtime offsets; unrolled: 6 x 5.4k 1328 -> 1279 us, one 5.2k prompt 250 -> 229,
+  // profiles/attn_prefill_unroll4_ab_r5.log)
+  auto fast = [&](auto ph_tag, int t, f32x16 (&S_cur)[2], f32x16 (&S_next)[2]) {
+    constexpr int PH = decltype(ph_tag)::value;
     unsigned long long t0 = 0;
     if constexpr (STAMP) t0 = __builtin_amdgcn_s_memtime();
-    const int vo = vslot_off(t - 1), ko = kslot_off(t + 1), vno = vslot_off(t);
+    static_assert(V3_NS == 4 && PH >= 0 && PH < 4, "slot phase");
+    constexpr int vo = (V3_NS + ((PH + 3) & 3)) * C::TILEB;  // V(t - 1)
+    constexpr int ko = ((PH + 1) & 3) * C::TILEB;            // K(t + 1)
+    constexpr int vno = (V3_NS + PH) * C::TILEB;             // V(t)
     const bool st_k = t + 3 < n_kt, st_v = t + 2 < n_kt;
     const int soff_k = tile_soff(st_k ? t + 3 : 0);
     const int soff_v = tile_soff(st_v ? t + 2 : 0);
@@ -812,12 +820,26 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void attn_prefill_v3_kernel(Prefil
     for (int j = 0; j < V3_PF; ++j) ring[j] = vfrag(vslot_off(0), j % 4, j / 4);
     barrier();  // (O is zero: no rescale; the prologue DMAs were drained)
     t = 1;
-    for (; t + 1 < t_end; t += 2) {
-      fast(t, S1, S0);
-      fast(t + 1, S0, S1);
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    using P2 = std::integral_constant<int, 2>;
+    using P3 = std::integral_constant<int, 3>;
+    for (; t + 3 < t_end; t += 4) {  // t = 1 (mod 4) at every trip
+      fast(P1{}, t, S1, S0);
+      fast(P2{}, t + 1, S0, S1);
+      fast(P3{}, t + 2, S1, S0);
+      fast(P0{}, t + 3, S0, S1);
     }
     if (t < t_end) {
-      fast(t, S1, S0);
+      fast(P1{}, t, S1, S0);
+      ++t;
+    }
+    if (t < t_end) {
+      fast(P2{}, t, S0, S1);
+      ++t;
+    }
+    if (t < t_end) {
+      fast(P3{}, t, S1, S0);
       ++t;
     }
     if (t & 1) {
