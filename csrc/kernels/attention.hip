@@ -1104,13 +1104,15 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_i, mx);
     const float m_use = m_new == -INFINITY ? 0.f : m_new;
-    const float alpha = exp2f(m_i - m_use);
+    // raw v_exp_f32 (the libm exp2f adds a denormal-range fixup per call: ~4 VALU; softmax terms below
+    // 2^-126 do not change any fp32 sum here)
+    const float alpha = __builtin_amdgcn_exp2f(m_i - m_use);
     float ls = 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(s4[t][r] - m_use);
+        const float p = __builtin_amdgcn_exp2f(s4[t][r] - m_use);
         s4[t][r] = p;
         ls += p;
       }

@@ -201,6 +201,9 @@ __device__ __forceinline__ void w4_epilogue_full_bf16(const f32x4 (&acc)[8][8], 
           o[4 + k] = silu(acc[i][2 * p + 1][k]) * acc[i][2 * p + 5][k];
         }
         *reinterpret_cast<u32x4*>(Cb + (size_t)(row0 + 16 * i) * ldc + colw + 32 * p) = pack8(o);
+        // one 8-column group at a time: interleaving all 16 groups' VALU raised the register peak past
+        // the budget (spills, and a vmcnt(0) drain per tile for the reload)
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   } else {

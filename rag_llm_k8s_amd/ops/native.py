@@ -90,15 +90,14 @@ def use_pp(M, N, K, epi):
     return N % 128 == 0 if epi == "silu_mul" else N % 8 == 0
 
 
-# Large-M GEMMs through hipBLASLt (torch) instead of gemm_w4, by epilogue. "resid" (default): the
-# residual-add projections (o_proj, down: h += x @ W^T, one in-place addmm with beta = 1 -- a plain
-# BLAS GEMM, one fp32 -> bf16 rounding as in gemm_w4's epilogue). In the bench they ran 8.5 % faster
-# than gemm_w4's residual epilogue kernels (prefill 49.3-49.5 -> 48.2 s over 25 steps, 1586 -> 1613
-# tok/s, same box alternating; profiles/bench_prefill_blas_ab_r4.log), while the qkv projection on
-# hipBLASLt ("plain") was no faster than gemm_w4 (1587 vs 1586) and the fused SiLU*up GEMM has no
-# library form. "none": every large-M GEMM on gemm_w4 (0 library kernels); "plain": no-epilogue GEMMs
-# only; "all": both.
-PREFILL_BLAS = os.environ.get("RAGK_PREFILL_BLAS", "resid")
+# Large-M GEMMs through hipBLASLt (torch) instead of gemm_w4, by epilogue (A/B only). "none" (default):
+# every large-M GEMM on the hand-written gemm_w4, no library kernel on the prefill path. "resid": the
+# residual-add projections (o_proj, down: h += x @ W^T as one in-place addmm, beta = 1) on hipBLASLt --
+# its K-loop is 4-6 % faster on those two shapes, worth 0.85 % of the headline bench (1644 / 1648 vs
+# 1660 / 1661 tok/s, same box alternating, profiles/bench_prefill_blas_ab_r5.log); "plain": no-epilogue
+# GEMMs only; "all": both. The fused SiLU*up gate/up GEMM has no library form (gemm_w4 is 2.8 % faster
+# than hipBLASLt's plain GEMM of the same shape, profiles/gemm_silu_rcp_r5.log).
+PREFILL_BLAS = os.environ.get("RAGK_PREFILL_BLAS", "none")
 
 
 def _gemm_blas(x, w, resid, out, epi):

@@ -80,30 +80,31 @@ def test_gemm_w4_grid_independent(native):
 
 
 def test_gemm_large_m_routing(native, monkeypatch):
-    """Large-M prefill GEMMs: no-epilogue and fused-epilogue GEMMs run on the hand-written gemm_w4 (the
-    default route equals an explicit path-6 call bit for bit); the residual-add projections go to an
-    in-place hipBLASLt addmm by default (PREFILL_BLAS = "resid": measured faster in the bench), within
-    bf16 rounding of gemm_w4 and of fp32, and back on gemm_w4 bit for bit with PREFILL_BLAS = "none"."""
+    """Large-M prefill GEMMs: every epilogue runs on the hand-written gemm_w4 by default (PREFILL_BLAS =
+    "none": the default route equals an explicit path-6 call bit for bit, residual add in place included);
+    the A/B route PREFILL_BLAS = "resid" (in-place hipBLASLt addmm) agrees within bf16 rounding of gemm_w4
+    and of fp32."""
     torch.manual_seed(21)
     M, N, K = 8192 + 17, 1024, 512
     x = torch.randn(M, K, device=DEV).bfloat16()
     w = (torch.randn(N, K, device=DEV) / math.sqrt(K)).bfloat16()
     r = torch.randn(M, N, device=DEV).bfloat16()
-    assert native.PREFILL_BLAS == "resid"
+    assert native.PREFILL_BLAS == "none"
     assert torch.equal(native.gemm(x, w), native.gemm(x, w, path=6))
+    w4 = native.gemm(x, w, resid=r, epi="resid", path=6)
+    h2 = r.clone()
+    native.gemm(x, w, resid=h2, epi="resid", out=h2)  # default route, in place
+    assert torch.equal(h2, w4)
+    ref = x.float() @ w.float().t() + r.float()
+    assert rel_err(w4, ref) < 1e-2
+    monkeypatch.setattr(native, "PREFILL_BLAS", "resid")
     h = r.clone()
     native.gemm(x, w, resid=h, epi="resid", out=h)
-    ref = x.float() @ w.float().t() + r.float()
     assert rel_err(h, ref) < 1e-2
-    w4 = native.gemm(x, w, resid=r, epi="resid", path=6)
     assert (h.float() - w4.float()).abs().max().item() <= 2 * (ref.abs().max().item() * 2 ** -8)
     y = torch.empty_like(r)
     native.gemm(x, w, resid=r, epi="resid", out=y)  # out-of-place form
     assert torch.equal(y, h)
-    monkeypatch.setattr(native, "PREFILL_BLAS", "none")
-    h2 = r.clone()
-    native.gemm(x, w, resid=h2, epi="resid", out=h2)
-    assert torch.equal(h2, w4)
 
 
 def _check_pingpong(native, M, N, K, path=2):
