@@ -288,20 +288,27 @@ __device__ __forceinline__ void w4_epilogue_reg(const f32x4 (&acc)[8][8], int wr
         bv[j] = *reinterpret_cast<const uint2*>(bias + (FULL ? gc : min(gc, Nout - 4)));
       }
     }
-    uint2 rv[RES ? 64 : 1];
-    if constexpr (RES) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int gr = FULL ? row0 + 16 * i : min(row0 + 16 * i, M - 1);
-          const int gc = colw + w4_perm(16 * j + 4 * fh);
-          rv[8 * i + j] = *reinterpret_cast<const uint2*>(resid + (size_t)gr * ldr + (FULL ? gc : min(gc, Nout - 4)));
-        }
-    }
+    // residual row groups in flight: the whole tile (RD = 8, 128 registers) for the residual-only form;
+    // one 16-row group at a time with a bias too (the whole tile there made this rarely taken path the
+    // loop body's register peak: 22 -> 8 spilled values bf16, 38 -> 0 fp32; the residual-only form
+    // spills more, 2 -> 4, when grouped)
+    constexpr int RD = BIAS ? 1 : 8;
+    uint2 rv[RES ? 8 * RD : 1];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int gr = row0 + 16 * i;
+      if constexpr (RES) {
+        if (i % RD == 0) {
+#pragma unroll
+          for (int g = 0; g < RD; ++g)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const int grc = FULL ? gr + 16 * g : min(gr + 16 * g, M - 1);
+              const int gc = colw + w4_perm(16 * j + 4 * fh);
+              rv[8 * g + j] = *reinterpret_cast<const uint2*>(resid + (size_t)grc * ldr + (FULL ? gc : min(gc, Nout - 4)));
+            }
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int gc = colw + w4_perm(16 * j + 4 * fh);
@@ -317,7 +324,7 @@ __device__ __forceinline__ void w4_epilogue_reg(const f32x4 (&acc)[8][8], int wr
           }
           if constexpr (RES) {
             float r[4];
-            unpack4(rv[8 * i + j], r);
+            unpack4(rv[8 * (i % RD) + j], r);
 #pragma unroll
             for (int k = 0; k < 4; ++k) o[k] += r[k];
           }
