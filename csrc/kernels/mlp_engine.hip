@@ -1,0 +1,391 @@
+// Persistent decode MLP for batch 1 on gfx950 (the loader-ring engine):
+//     h += W_down . (silu(W_gate . x) * (W_up . x)),    x = rmsnorm(h) (given, bf16 [H])
+// as ONE launch of one workgroup per CU, instead of the SiLU*up stream GEMM + the down GEMM
+// (two launches, each with its own grid fill and drain around a 235 / 117 MB weight stream).
+//
+// Why: at batch 1 the decode layer is a weight stream, and each launch boundary costs the stream a
+// fill (the first loads of every block start cold) and a drain (the tail of the slowest blocks).
+// Here the weights of BOTH projections go through one LDS ring per CU without a break: the ring's
+// loader does not depend on the activations, so while the consumers wait for the chip-wide
+// hand-off between the two projections (every CU needs all I activations before it can start the
+// down projection), the loader is already filling the ring with down-projection weights.
+//
+// Workgroup = 4 waves: wave 0 = loader, waves 1..3 = consumers.
+//   * work split: workgroup w owns 8-wide groups of activations [a0, a1) (gate rows and up rows of
+//     those activations from the packed [64 gate | 64 up] weight tiles) and 16-row groups of output
+//     rows [d0, d1) of the down projection; a ring slot = 16 weight rows x 512 K columns (16 KiB):
+//     phase A slots (8 gate + 8 up rows, chunk fastest), then phase B slots (16 down rows);
+//   * loader: LDS-DMA (global_load_lds, 16 B per lane, one instruction per 1 KiB row piece), up to
+//     ME_INFLIGHT slots in flight, a slot published (LDS word FULL = seq + 1) behind a counted vmcnt;
+//     a slot is refilled only after its consumer wrote FREE = seq + 1 (after its fragment reads);
+//   * consumers: slot s goes to consumer s % 3; its 16 rows are one MFMA 16x16x32 column tile
+//     (x broadcast in the A operand: row m = 0 of the product is the result), 16 K-steps per slot;
+//     the 16 per-slot sums go to an LDS partial array (summed in a fixed order later: deterministic);
+//   * end of phase A (the last consumer to arrive, LDS counter): act = bf16(silu(gate) * up) for the
+//     workgroup's activations, stored write-through (sc1, 8-B agent stores) to the act workspace,
+//     vmcnt(0), then ONE agent-scope atomic add on this workgroup's counter shard (8 shards, one per
+//     XCD in dispatch order; a shard's last arriver adds to a top counter); one lane polls the top
+//     counter (sc1 loads) until every workgroup of this launch arrived, then the wave loads all I
+//     activations with sc1 buffer loads into LDS and sets an LDS word the other consumers wait on;
+//   * end of phase B (last consumer): h[row] = bf16(h[row] + sum of the row's partials).
+// Counters are monotonic (never re-zeroed between launches, so a hipGraph replay needs no memset
+// node): a workgroup's own add returns the count before it, which names the launch generation; the
+// wait is for (generation + 1) x members on every shard. Every wait is bounded: on a timeout the
+// error word is set (ragk_mlp_engine_error) and the host resets the counters.
+// Deadlock freedom: one workgroup per CU (the LDS footprint admits one), grid = CU count, all
+// resident; the only cross-workgroup wait is the act hand-off.
+#include "common.h"
+using namespace ragk;
+
+namespace {
+
+constexpr int ME_THREADS = 256;
+constexpr int ME_ROWS = 16;                        // weight rows per slot
+constexpr int ME_KC = 512;                         // K columns per slot
+constexpr int ME_PITCH = ME_KC * 2 + 16;           // LDS row pitch: 16-B skew between consecutive rows
+constexpr int ME_SLOT = ME_ROWS * ME_PITCH;        // 16640 B
+constexpr int ME_RING = 7;
+constexpr int ME_INFLIGHT = 3;                     // slots in flight behind the newest issue
+constexpr int ME_NCONS = 3;
+constexpr int ME_VEC = 28672;                      // x (phase A) / act (phase B) bytes: max(2H, 2I)
+constexpr int ME_MAXA = 64, ME_MAXB = 56;          // slots per workgroup and phase
+constexpr int ME_SHARDS = 8;
+constexpr int ME_CTR_STRIDE = 16;                  // u64 per shard: one 128-B line each
+constexpr unsigned ME_SPIN_LIMIT = 1u << 21;       // x s_sleep 2: ~0.1-0.2 s
+
+struct MlpArgs {
+  const bf16_t* xn;        // [H] normalised input row
+  const bf16_t* wgu;       // [2I][H] packed [64 gate | 64 up] per 128 rows
+  const bf16_t* wd;        // [H][I]
+  bf16_t* h;               // [H] residual, updated in place
+  bf16_t* act;             // [I] hand-off workspace
+  unsigned long long* ctr; // [ME_SHARDS][ME_CTR_STRIDE] arrival counters
+  unsigned* err;           // timeout word
+  unsigned long long* stamps;  // optional [G][8] s_memrealtime stamps (tools/mlp_engine_bench.py ME_STAMPS=1)
+  int H, I;
+};
+
+__device__ __forceinline__ void me_stamp(const MlpArgs& a, int i) {
+  if (a.stamps) a.stamps[blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
+}
+
+struct MlpSmem {
+  char ring[ME_RING * ME_SLOT];
+  char vec[ME_VEC];
+  float part[(ME_MAXA + ME_MAXB) * ME_ROWS];
+  bf16_t actl[64];
+  unsigned full[8], freew[8];
+  unsigned doneA, doneB, actReady, pad;
+};
+
+template <int N>
+__device__ __forceinline__ void me_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (((N >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
+}
+__device__ __forceinline__ void me_wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// LDS flag words: explicit address-space-3 volatile accesses (a generic volatile pointer compiles to
+// flat_load / flat_store, which also count in vmcnt and would break the loader's counted waits)
+typedef __attribute__((address_space(3))) volatile unsigned lds_u32;
+__device__ __forceinline__ unsigned lds_ld(const unsigned* p) { return *(const lds_u32*)(p); }
+__device__ __forceinline__ void lds_st(unsigned* p, unsigned v) { *(lds_u32*)(p) = v; }
+
+// bounded spin on an LDS word (same workgroup): true when *p == want
+__device__ __forceinline__ bool me_spin_lds(const unsigned* p, unsigned want, unsigned* err) {
+  for (unsigned it = 0; lds_ld(p) != want; ++it) {
+    if (it > ME_SPIN_LIMIT) {
+      __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return true;
+}
+
+struct SlotMap {
+  int a0, nA, d0, KA, KB;
+  __device__ __forceinline__ int chunk(int s) const { return s < nA ? s % KA : (s - nA) % KB; }
+};
+
+// The loader's wave-uniform cursor over its slots (no divisions in the issue loop): slot s, group g
+// (activation group in phase A, down row group in phase B), K chunk kc; the slot's 16 rows are
+// base + r * stride (+ jump for the up rows: packed row of up j = packed row of gate j + 64).
+struct LoadCursor {
+  int s = 0, g = 0, kc = 0;
+  __device__ __forceinline__ void next(const SlotMap& m) {
+    ++s;
+    ++kc;
+    if (s == m.nA) {
+      g = 0;
+      kc = 0;
+    } else if (kc == (s < m.nA ? m.KA : m.KB)) {
+      kc = 0;
+      ++g;
+    }
+  }
+};
+
+template <bool NT>
+__device__ __forceinline__ void me_issue_slot(const MlpArgs& a, const SlotMap& m, const LoadCursor& cu, MlpSmem& sm,
+                                              int lane) {
+  char* dst = sm.ring + (cu.s % ME_RING) * ME_SLOT;
+  const char* base;
+  long long stride, jump;
+  if (cu.s < m.nA) {
+    const int j0 = 8 * (m.a0 + cu.g);
+    const int prow0 = (j0 >> 6) * 128 + (j0 & 63);
+    base = reinterpret_cast<const char*>(a.wgu) + (long long)prow0 * a.H * 2 + cu.kc * (ME_KC * 2);
+    stride = 2ll * a.H;
+    jump = 112ll * a.H;
+  } else {
+    base = reinterpret_cast<const char*>(a.wd) + (long long)(16 * (m.d0 + cu.g)) * a.I * 2 + cu.kc * (ME_KC * 2);
+    stride = 2ll * a.I;
+    jump = 0;
+  }
+#pragma unroll
+  for (int r = 0; r < ME_ROWS; ++r) {
+    const char* src = base + r * stride + (r >= 8 ? jump : 0) + lane * 16;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(dst + r * ME_PITCH), 16, 0,
+                                     NT ? 2 : 0);
+  }
+}
+
+template <bool NT>
+__global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
+  __shared__ __attribute__((aligned(16))) MlpSmem sm;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int G = gridDim.x, w = blockIdx.x;
+  const int NA = a.I / 8, ND = a.H / 16;
+  SlotMap m;
+  m.KA = a.H / ME_KC;
+  m.KB = a.I / ME_KC;
+  m.a0 = (int)((long long)w * NA / G);
+  const int a1 = (int)((long long)(w + 1) * NA / G);
+  m.d0 = (int)((long long)w * ND / G);
+  const int d1 = (int)((long long)(w + 1) * ND / G);
+  m.nA = (a1 - m.a0) * m.KA;
+  const int nB = (d1 - m.d0) * m.KB;
+  const int nS = m.nA + nB;
+
+  if (wid == 0) {
+    if (lane == 0) me_stamp(a, 0);
+    if (lane < 8) {
+      sm.full[lane] = 0u;
+      sm.freew[lane] = 0u;
+    }
+    if (lane == 0) {
+      sm.doneA = 0u;
+      sm.doneB = 0u;
+      sm.actReady = 0u;
+    }
+    LoadCursor cu;
+    const int pre = nS < ME_INFLIGHT ? nS : ME_INFLIGHT;
+    for (int s = 0; s < pre; ++s, cu.next(m)) me_issue_slot<NT>(a, m, cu, sm, lane);
+  } else {
+    // x -> LDS (written by the previous launch: plain loads)
+    const int t = threadIdx.x - 64;
+    for (int i = t; i < a.H / 8; i += 192)
+      *reinterpret_cast<u32x4*>(sm.vec + 16 * i) = *reinterpret_cast<const u32x4*>(a.xn + 8 * i);
+  }
+  me_wait_lgkm0();
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  if (wid == 0) {
+    // ---------------- loader ----------------
+    int pub = 0;
+    LoadCursor cu;
+    const int s0 = nS < ME_INFLIGHT ? nS : ME_INFLIGHT;
+    for (int s = 0; s < s0; ++s) cu.next(m);
+    for (int s = s0; s < nS; ++s, cu.next(m)) {
+      const int r = s % ME_RING;
+      if (s >= ME_RING) {
+        const unsigned need = (unsigned)(s - ME_RING + 1);
+        if (lds_ld(&sm.freew[r]) != need) {
+          // the ring is full: publish what has landed before blocking on the consumers
+          me_wait_vm<0>();
+          for (; pub < s; ++pub) lds_st(&sm.full[pub % ME_RING], (unsigned)pub + 1u);
+          if (!me_spin_lds(&sm.freew[r], need, a.err)) break;
+        }
+      }
+      me_issue_slot<NT>(a, m, cu, sm, lane);
+      if (s - pub + 1 > ME_INFLIGHT) {
+        me_wait_vm<16 * ME_INFLIGHT>();
+        lds_st(&sm.full[pub % ME_RING], (unsigned)pub + 1u);
+        ++pub;
+      }
+    }
+    if (lane == 0) me_stamp(a, 1);
+    me_wait_vm<0>();
+    for (; pub < nS; ++pub) lds_st(&sm.full[pub % ME_RING], (unsigned)pub + 1u);
+    return;
+  }
+
+  // ---------------- consumers ----------------
+  const int c = wid - 1;
+  const int n = lane & 15, kg = lane >> 4;
+  bool arrivedA = false;
+  auto finish_A = [&]() {
+    // called once per consumer, after its last phase-A slot (its partial stores retired)
+    me_wait_lgkm0();
+    unsigned prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add(&sm.doneA, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    prev = __shfl(prev, 0, 64);
+    if (prev != ME_NCONS - 1) return;
+    // last consumer of phase A: this workgroup's activations
+    if (lane == 0) me_stamp(a, 2);
+    const int nact = m.nA / m.KA * 8;  // <= 64
+    if (lane < nact) {
+      const int g = lane >> 3, jj = lane & 7;
+      float gs = 0.f, us = 0.f;
+      for (int kc = 0; kc < m.KA; ++kc) {
+        const float* p = sm.part + (g * m.KA + kc) * ME_ROWS;
+        gs += p[jj];
+        us += p[8 + jj];
+      }
+      sm.actl[lane] = f2bf(silu(gs) * us);
+    }
+    me_wait_lgkm0();
+    if (lane < nact / 4) {
+      const unsigned long long v = *reinterpret_cast<const unsigned long long*>(sm.actl + 4 * lane);
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.act + 8 * m.a0 + 4 * lane), v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // arrive on this workgroup's shard; the count before the add names this launch's generation. The
+    // last arriver of a shard adds to the top counter; the waiters poll only the top counter (one
+    // load per poll: 256 workgroups polling 8 shard lines was ~38 G polls/s of fabric traffic beside
+    // the other CUs' weight streams)
+    const int shard = w & (ME_SHARDS - 1);
+    const int nsh = G < ME_SHARDS ? G : ME_SHARDS;
+    unsigned long long* top = a.ctr + ME_SHARDS * ME_CTR_STRIDE;
+    unsigned long long want = 0;
+    if (lane == 0) {
+      const unsigned long long mine = (unsigned long long)((G - shard + ME_SHARDS - 1) / ME_SHARDS);
+      const unsigned long long old =
+          __hip_atomic_fetch_add(a.ctr + shard * ME_CTR_STRIDE, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long gen = old / mine;
+      if (old + 1 == (gen + 1) * mine) __hip_atomic_fetch_add(top, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      want = (gen + 1) * (unsigned long long)nsh;
+      for (unsigned it = 0; __hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want; ++it) {
+        if (it > ME_SPIN_LIMIT) {
+          __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
+    // all I activations -> LDS, every load sc1 (the producers stored them sc1)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.act, 0, a.I * 2, 0x00020000);
+    const int nv = a.I / 8;
+    for (int i0 = 0; i0 < nv; i0 += 64 * 4) {
+      u32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 64 * u + lane;
+        v[u] = i < nv ? __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * i, 0, 16))
+                      : (u32x4){0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 64 * u + lane;
+        if (i < nv) *reinterpret_cast<u32x4*>(sm.vec + 16 * i) = v[u];
+      }
+    }
+    me_wait_lgkm0();
+    if (lane == 0) lds_st(&sm.actReady, 1u);
+    if (lane == 0) me_stamp(a, 3);
+  };
+
+  bool actOk = false;
+  for (int s = c; s < nS; s += ME_NCONS) {
+    if (s >= m.nA && !arrivedA) {
+      finish_A();
+      arrivedA = true;
+    }
+    if (s >= m.nA && !actOk) {
+      if (!me_spin_lds(&sm.actReady, 1u, a.err)) break;
+      actOk = true;
+    }
+    const int r = s % ME_RING;
+    if (!me_spin_lds(&sm.full[r], (unsigned)s + 1u, a.err)) break;
+    const char* slot = sm.ring + r * ME_SLOT;
+    const char* xv = sm.vec + m.chunk(s) * (ME_KC * 2);
+    bf16x8 wf[16], xf[16];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      wf[ks] = *reinterpret_cast<const bf16x8*>(slot + n * ME_PITCH + (ks * 32 + kg * 8) * 2);
+      xf[ks] = *reinterpret_cast<const bf16x8*>(xv + (ks * 32 + kg * 8) * 2);
+    }
+    me_wait_lgkm0();
+    if (lane == 0) lds_st(&sm.freew[r], (unsigned)s + 1u);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[ks], wf[ks], acc, 0, 0, 0);
+    // C[m][n]: lane (n, kg) holds rows 4kg..4kg+3 of column n; row 0 (x) sits in lanes 0..15
+    if (lane < 16) sm.part[s * ME_ROWS + n] = acc[0];
+  }
+  if (!arrivedA) finish_A();
+
+  // ---------------- phase B tail: the last consumer finishes the rows ----------------
+  me_wait_lgkm0();
+  unsigned prev = 0;
+  if (lane == 0) prev = __hip_atomic_fetch_add(&sm.doneB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  prev = __shfl(prev, 0, 64);
+  if (prev != ME_NCONS - 1) return;
+  const int nd = d1 - m.d0;
+  if (lane < 16 * nd) {
+    const int g = lane >> 4, rr = lane & 15;
+    float acc = 0.f;
+    for (int kc = 0; kc < m.KB; ++kc) acc += sm.part[(m.nA + g * m.KB + kc) * ME_ROWS + rr];
+    const int row = 16 * (m.d0 + g) + rr;
+    a.h[row] = f2bf(acc + bf2f(a.h[row]));
+  }
+  if (lane == 0) me_stamp(a, 4);
+}
+
+int g_me_nt = 1;
+unsigned long long* g_me_stamps = nullptr;
+
+}  // namespace
+
+// Whether the engine takes this shape on a grid of G workgroups (G = CU count).
+RAGK_API int ragk_mlp_engine_ok(int M, int H, int I, int G) {
+  if (M != 1 || G < 1 || H <= 0 || I <= 0) return 0;
+  if (H % ME_KC || I % ME_KC || I % 64 || H % 16) return 0;
+  if (2 * H > ME_VEC || 2 * I > ME_VEC) return 0;
+  const int NA = I / 8, ND = H / 16;
+  const int maxA = (NA + G - 1) / G, maxB = (ND + G - 1) / G;
+  if (maxA * (H / ME_KC) > ME_MAXA || maxB * (I / ME_KC) > ME_MAXB || maxA * 8 > 64 || maxB * 16 > 64) return 0;
+  return 1;
+}
+
+RAGK_API int ragk_mlp_engine_set_nt(int nt) {
+  g_me_nt = nt ? 1 : 0;
+  return 0;
+}
+
+// stage stamps of every workgroup into a [G][8] u64 buffer (nullptr = off; A/B tooling only)
+RAGK_API int ragk_mlp_engine_set_stamps(void* p) {
+  g_me_stamps = (unsigned long long*)p;
+  return 0;
+}
+
+RAGK_API int ragk_mlp_engine(const void* xn, const void* wgu, const void* wd, void* h, void* act, void* ctr, void* err,
+                             int M, int H, int I, int G, hipStream_t st) {
+  if (!ragk_mlp_engine_ok(M, H, I, G)) return (int)hipErrorInvalidValue;
+  if (!xn || !wgu || !wd || !h || !act || !ctr || !err) return (int)hipErrorInvalidValue;
+  MlpArgs a{(const bf16_t*)xn, (const bf16_t*)wgu, (const bf16_t*)wd, (bf16_t*)h, (bf16_t*)act,
+            (unsigned long long*)ctr, (unsigned*)err, g_me_stamps, H, I};
+  if (g_me_nt)
+    hipLaunchKernelGGL(mlp_engine_kernel<true>, dim3(G), dim3(ME_THREADS), 0, st, a);
+  else
+    hipLaunchKernelGGL(mlp_engine_kernel<false>, dim3(G), dim3(ME_THREADS), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// bytes of the workspace words (counters + error word) the host allocates zeroed and resets on error
+RAGK_API int ragk_mlp_engine_ctr_bytes() { return (ME_SHARDS + 1) * ME_CTR_STRIDE * 8; }

@@ -345,6 +345,8 @@ class LlamaModel:
         silu_fused = tp and be.part_silu_ok(M, layers[0]["wgu"], layers[0]["wdown"])
         xn = None if fuse_norm else be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
         merge = M <= DECODE_OPROJ_MERGE_MAX_M and be.part_merge_ok(M, inp.meta, layers[0]["wo"], Hq, D)
+        # batch 1: gate/up + SiLU + down + residual as ONE persistent launch (csrc/kernels/mlp_engine.hip)
+        mlp_eng = M == 1 and not tp and be.mlp_engine_ok(M, layers[0]["wgu"], layers[0]["wdown"])
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
             P = be.gemm_part_norm(h, L["ln_in"], c.rms_norm_eps, L["wqkv"]) if fuse_norm else be.gemm_part(xn, L["wqkv"])
@@ -357,6 +359,11 @@ class LlamaModel:
             if silu_fused:
                 P = be.gemm_part_silu(be.gemm_part_gu(xn, L["wgu"]), L["wdown"])
                 xn = reduce_norm(P, nxt)
+                continue
+            if mlp_eng:
+                be.mlp_engine(xn, L["wgu"], L["wdown"], h)
+                if not fuse_norm or li + 1 == len(layers):
+                    xn = be.rmsnorm(h, nxt, c.rms_norm_eps)
                 continue
             a = be.gemm(xn, L["wgu"], epi="silu_mul")
             if M <= DECODE_DOWN_SKINNY_MAX_M and not tp:

@@ -39,6 +39,11 @@ _SIGS = {
     "ragk_gemm_stream_part": [P, I, P, I, P, I, I, I, I, I, S],
     "ragk_gemm_part_silu": [P, I, P, I, P, I, I, I, I, S],
     "ragk_gemm_part_silu_ok": [I, I, I, I],
+    "ragk_mlp_engine_ok": [I, I, I, I],
+    "ragk_mlp_engine_set_nt": [I],
+    "ragk_mlp_engine_set_stamps": [P],
+    "ragk_mlp_engine": [P, P, P, P, P, P, P, I, I, I, I, S],
+    "ragk_mlp_engine_ctr_bytes": [],
     "ragk_gemm_part_ksteps": [I, I, I],
     "ragk_gemm_part_set_min_blocks": [I],
     "ragk_add_partials_rmsnorm": [P, I, I, P, I, P, P, I, I, F, S],

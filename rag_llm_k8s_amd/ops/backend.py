@@ -141,6 +141,17 @@ class TorchBackend:
     def gemm_part_norm(self, h, gamma, eps, w):
         return self.gemm_part(R.rmsnorm(h, gamma, eps), w)
 
+    def mlp_engine_ok(self, M, w_gu, w_down):
+        return (self.enable_part and M == 1 and not isinstance(w_gu, Fp8Weight) and not isinstance(w_down, Fp8Weight)
+                and w_down.shape[1] % 64 == 0)
+
+    def mlp_engine(self, xn, w_gu, w_down, h):
+        """h += W_down (silu(gate) * up) for one row: bf16 activations, one rounding of the residual add."""
+        t = (xn.float() @ w_gu.float().t()).view(xn.shape[0], -1, 2, 64)  # packed [64 gate | 64 up] tiles
+        a = (torch.nn.functional.silu(t[:, :, 0, :]) * t[:, :, 1, :]).reshape(xn.shape[0], -1).to(torch.bfloat16)
+        h.copy_((h.float() + a.float() @ w_down.float().t()).to(h.dtype))
+        return h
+
     def add_partials_rmsnorm(self, P, h, w, eps):
         h.copy_((h.float() + P.sum(0).to(h.dtype).float()).to(h.dtype))
         return R.rmsnorm(h, w, eps)
@@ -282,6 +293,12 @@ class NativeBackend(TorchBackend):
 
     def add_partials_rmsnorm(self, P, h, w, eps):
         return self.n.add_partials_rmsnorm(P, h, w, eps)
+
+    def mlp_engine_ok(self, M, w_gu, w_down):
+        return self.n.mlp_engine_ok(M, w_gu, w_down)
+
+    def mlp_engine(self, xn, w_gu, w_down, h):
+        return self.n.mlp_engine(xn, w_gu, w_down, h)
 
     def rope_kv_partials(self, P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D):
         self.n.rope_kv_partials(P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)

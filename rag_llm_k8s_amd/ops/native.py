@@ -454,6 +454,66 @@ def gemm_part_silu(pgu, w, out=None):
     return out
 
 
+# ----------------------------------------------------------------------------- persistent decode MLP
+# Batch-1 decode MLP as one persistent launch (csrc/kernels/mlp_engine.hip): h += W_down (silu(W_gate x) *
+# (W_up x)) with both weight streams going through one LDS ring per CU (RAGK_MLP_ENGINE=1 turns it on; off by default until it beats the two launches).
+MLP_ENGINE = os.environ.get("RAGK_MLP_ENGINE", "0") == "1"
+_me_ws = {}
+
+
+def _me_workspace(dev, I):
+    """(act [I] bf16, counters + error word) per device; the counters are monotonic across launches and
+    zeroed only here and after a timeout (mlp_engine_check)."""
+    key = (str(dev), I)
+    ws = _me_ws.get(key)
+    if ws is None:
+        nb = int(_lib.lib().ragk_mlp_engine_ctr_bytes())
+        words = torch.zeros(nb // 8 + 2, dtype=torch.int64, device=dev)
+        ws = (torch.zeros(I, dtype=torch.bfloat16, device=dev), words, nb)
+        _me_ws[key] = ws
+    return ws
+
+
+def mlp_engine_ok(M, w_gu, w_down):
+    if not MLP_ENGINE or not (isinstance(w_gu, torch.Tensor) and isinstance(w_down, torch.Tensor)):
+        return False
+    if w_gu.dtype != torch.bfloat16 or w_down.dtype != torch.bfloat16 or not w_gu.is_cuda:
+        return False
+    H, I = w_down.shape
+    if w_gu.shape != (2 * I, H) or not (w_gu.is_contiguous() and w_down.is_contiguous()):
+        return False
+    return bool(_lib.lib().ragk_mlp_engine_ok(M, H, I, _cu_count()))
+
+
+def mlp_engine(xn, w_gu, w_down, h):
+    """h += W_down . (silu(gate) * up) for ONE row (xn = the post-attention RMSNorm of h, bf16 [1, H])."""
+    _bf16_2d(xn, "xn")
+    _bf16_2d(h, "h")
+    H, I = w_down.shape
+    _req(xn.shape == (1, H) and h.shape == (1, H) and xn.is_contiguous() and h.is_contiguous(), "xn / h [1, H]")
+    _req(mlp_engine_ok(1, w_gu, w_down), "mlp_engine shape")
+    act, words, nb = _me_workspace(xn.device, I)
+    err = words.data_ptr() + nb
+    check(_lib.lib().ragk_mlp_engine(xn.data_ptr(), w_gu.data_ptr(), w_down.data_ptr(), h.data_ptr(), act.data_ptr(),
+                                     words.data_ptr(), err, 1, H, I, _cu_count(), stream_ptr()), "ragk_mlp_engine")
+    return h
+
+
+def mlp_engine_check(dev=None):
+    """Raise if a persistent MLP launch on `dev` timed out in a wait (then re-arm its counters). Syncs."""
+    for key, (_, words, nb) in list(_me_ws.items()):
+        if dev is not None and key[0] != str(dev):
+            continue
+        e = int(words[nb // 8].item())
+        if e:
+            words.zero_()
+            raise RuntimeError("persistent decode MLP: wait timed out (code %d); counters reset" % e)
+
+
+def set_mlp_engine_nt(nt):
+    check(_lib.lib().ragk_mlp_engine_set_nt(int(nt)), "ragk_mlp_engine_set_nt")
+
+
 STREAM_S_OVERRIDE = 0  # tuning hook (tools/tune_stream.py)
 
 

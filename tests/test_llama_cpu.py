@@ -158,6 +158,28 @@ def test_split_k_decode_path_matches_plain_decode(tiny):
     assert outs[0] == outs[1]
 
 
+def test_batch1_decode_mlp_engine_path_matches_plain_decode(tiny):
+    """Batch-1 split-K decode with the persistent MLP launch (gate/up + SiLU + down + residual in one op,
+    csrc/kernels/mlp_engine.hip on the GPU; its torch oracle here) generates the same greedy tokens as the
+    plain decode path, and the op runs once per layer per decode step."""
+    cfg, hf, sd = tiny
+    w = LlamaWeights.from_state_dict(cfg, sd, "cpu")
+    torch.manual_seed(6)
+    prompt = [torch.randint(3, cfg.vocab_size, (31,)).tolist()]
+    params = SamplingParams(max_new_tokens=8, do_sample=False, ignore_eos=True)
+    outs = []
+    for part in (False, True):
+        model = LlamaModel(cfg, w, "cpu", max_positions=512)
+        model.be.enable_part = part
+        calls = []
+        orig = model.be.mlp_engine
+        model.be.mlp_engine = lambda *a: (calls.append(1), orig(*a))[1]
+        eng = LLMEngine(model, num_blocks=32, max_batch=4, max_model_len=512, use_graphs=False)
+        outs.append(eng.generate(prompt, params))
+        assert len(calls) == (7 * cfg.num_hidden_layers if part else 0)
+    assert outs[0] == outs[1]
+
+
 def test_mixed_prefill_decode_steps_match_separate_steps(tiny):
     """Mixed steps (decoding sequences ride along in a prefill step as 1-token chunks) produce the same
     tokens as separate prefill / decode steps, for requests that arrive while others decode; a mixed
