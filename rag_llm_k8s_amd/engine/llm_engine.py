@@ -765,6 +765,9 @@ class LLMEngine:
             self.bm.free(sid)
         self._free_after = []
         tok = step["host_out"][:step["n"]].tolist()
+        self._n_collect = getattr(self, "_n_collect", 0) + 1
+        if self._n_collect % 64 == 0:
+            self._check_kernel_errors()
         finished = []
         for s, t in zip(step["seqs"], tok):
             if s.status == FINISHED:  # stopped (or aborted) before this step's token was read
@@ -775,6 +778,13 @@ class LLMEngine:
                 self._finish(s, r, defer_free=id(s) in in_flight)
                 finished.append(s)
         return finished
+
+    def _check_kernel_errors(self):
+        """Bounded in-kernel waits report timeouts through error words instead of hanging: surface them
+        (the persistent decode MLP's hand-off; its counters are re-armed by the check)."""
+        if torch.device(self.device).type == "cuda":
+            from ..ops import native
+            native.mlp_engine_check(self.device)
 
     def _drain(self):
         """Complete the in-flight decode step (before a prefill, an abort, or when nothing is left)."""

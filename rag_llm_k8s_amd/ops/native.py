@@ -456,8 +456,8 @@ def gemm_part_silu(pgu, w, out=None):
 
 # ----------------------------------------------------------------------------- persistent decode MLP
 # Batch-1 decode MLP as one persistent launch (csrc/kernels/mlp_engine.hip): h += W_down (silu(W_gate x) *
-# (W_up x)) with both weight streams going through one LDS ring per CU (RAGK_MLP_ENGINE=1 turns it on; off by default until it beats the two launches).
-MLP_ENGINE = os.environ.get("RAGK_MLP_ENGINE", "0") == "1"
+# (W_up x)) with both weight streams going through one LDS ring per CU (RAGK_MLP_ENGINE=0 turns it off). Batch-1 decode step 3.47 -> 3.34 ms (profiles/mlp_engine_r5.log).
+MLP_ENGINE = os.environ.get("RAGK_MLP_ENGINE", "1") != "0"
 _me_ws = {}
 
 
@@ -502,7 +502,8 @@ def mlp_engine(xn, w_gu, w_down, h):
 def mlp_engine_check(dev=None):
     """Raise if a persistent MLP launch on `dev` timed out in a wait (then re-arm its counters). Syncs."""
     for key, (_, words, nb) in list(_me_ws.items()):
-        if dev is not None and key[0] != str(dev):
+        d = torch.device(dev) if dev is not None else None
+        if d is not None and d.index is not None and torch.device(key[0]) != d:
             continue
         e = int(words[nb // 8].item())
         if e:
