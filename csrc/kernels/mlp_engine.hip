@@ -1,7 +1,10 @@
-// Persistent decode MLP for batch 1 on gfx950 (the loader-ring engine):
-//     h += W_down . (silu(W_gate . x) * (W_up . x)),    x = rmsnorm(h) (given, bf16 [H])
-// as ONE launch of one workgroup per CU, instead of the SiLU*up stream GEMM + the down GEMM
-// (two launches, each with its own grid fill and drain around a 235 / 117 MB weight stream).
+// Persistent decode post-attention tail for batch 1 on gfx950 (the loader-ring engine):
+//     h += bf16(sum_s P[s]);  x = rmsnorm(h) * gamma        (P: the o_proj split-K slabs; or x given)
+//     h += W_down . (silu(W_gate . x) * (W_up . x))
+// as ONE launch of one workgroup per CU, instead of add_partials_rmsnorm + the SiLU*up stream GEMM +
+// the down GEMM (three launches, two of them with their own grid fill and drain around a 235 / 117 MB
+// weight stream). Measured (Llama-3.1-8B shapes, hipGraph replay, profiles/mlp_engine_r5.log): 64 vs
+// 70 us per layer; batch-1 decode step 3.44-3.47 -> 3.33 ms.
 //
 // Why: at batch 1 the decode layer is a weight stream, and each launch boundary costs the stream a
 // fill (the first loads of every block start cold) and a drain (the tail of the slowest blocks).
@@ -10,7 +13,8 @@
 // hand-off between the two projections (every CU needs all I activations before it can start the
 // down projection), the loader is already filling the ring with down-projection weights.
 //
-// Workgroup = 4 waves: wave 0 = loader, waves 1..3 = consumers.
+// Workgroup = 4 waves: wave 0 = loader, waves 1..3 = consumers (ME_NLOAD / ME_THREADS: one loader wave
+// measured the same as two -- the HBM stream, not the in-flight depth, is the limit).
 //   * work split: workgroup w owns 8-wide groups of activations [a0, a1) (gate rows and up rows of
 //     those activations from the packed [64 gate | 64 up] weight tiles) and 16-row groups of output
 //     rows [d0, d1) of the down projection; a ring slot = 16 weight rows x 512 K columns (16 KiB):
@@ -27,6 +31,9 @@
 //     XCD in dispatch order; a shard's last arriver adds to a top counter); one lane polls the top
 //     counter (sc1 loads) until every workgroup of this launch arrived, then the wave loads all I
 //     activations with sc1 buffer loads into LDS and sets an LDS word the other consumers wait on;
+//   * fused tail (P given): before phase A every workgroup forms the whole row h + bf16(sum P) and its
+//     norm (add_partials_rmsnorm's math) from the slabs while the loader's first slots are in flight;
+//     it keeps its own down rows of that residual and writes h only at its end;
 //   * end of phase B (last consumer): h[row] = bf16(h[row] + sum of the row's partials).
 // Counters are monotonic (never re-zeroed between launches, so a hipGraph replay needs no memset
 // node): a workgroup's own add returns the count before it, which names the launch generation; the
@@ -46,7 +53,8 @@ constexpr int ME_PITCH = ME_KC * 2 + 16;           // LDS row pitch: 16-B skew b
 constexpr int ME_SLOT = ME_ROWS * ME_PITCH;        // 16640 B
 constexpr int ME_RING = 7;
 constexpr int ME_INFLIGHT = 3;                     // slots in flight behind the newest issue
-constexpr int ME_NCONS = 3;
+constexpr int ME_NLOAD = 1;                       // loader waves (slot s: loader s % ME_NLOAD)
+constexpr int ME_NCONS = ME_THREADS / 64 - ME_NLOAD;  // consumer waves
 constexpr int ME_VEC = 28672;                      // x (phase A) / act (phase B) bytes: max(2H, 2I)
 constexpr int ME_MAXA = 64, ME_MAXB = 56;          // slots per workgroup and phase
 constexpr int ME_SHARDS = 8;
@@ -54,7 +62,11 @@ constexpr int ME_CTR_STRIDE = 16;                  // u64 per shard: one 128-B l
 constexpr unsigned ME_SPIN_LIMIT = 1u << 21;       // x s_sleep 2: ~0.1-0.2 s
 
 struct MlpArgs {
-  const bf16_t* xn;        // [H] normalised input row
+  const bf16_t* xn;        // [H] normalised input row (P == nullptr)
+  const float* P;          // [S][H] o_proj split-K slabs: h += bf16(sum P), x = rmsnorm(h) * gamma in-launch
+  const bf16_t* gamma;     // [H] post-attention norm weight (with P)
+  float eps;
+  int S;
   const bf16_t* wgu;       // [2I][H] packed [64 gate | 64 up] per 128 rows
   const bf16_t* wd;        // [H][I]
   bf16_t* h;               // [H] residual, updated in place
@@ -74,9 +86,18 @@ struct MlpSmem {
   char vec[ME_VEC];
   float part[(ME_MAXA + ME_MAXB) * ME_ROWS];
   bf16_t actl[64];
+  float hres[64];          // this workgroup's rows of h after the o_proj residual (fused tail)
+  float red[8];
   unsigned full[8], freew[8];
   unsigned doneA, doneB, actReady, pad;
 };
+
+__device__ __forceinline__ void unpack4(uint2 v, float (&f)[4]) {
+  f[0] = __uint_as_float(v.x << 16);
+  f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16);
+  f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
 
 template <int N>
 __device__ __forceinline__ void me_wait_vm() {
@@ -168,63 +189,136 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
   const int nB = (d1 - m.d0) * m.KB;
   const int nS = m.nA + nB;
 
-  if (wid == 0) {
-    if (lane == 0) me_stamp(a, 0);
-    if (lane < 8) {
-      sm.full[lane] = 0u;
-      sm.freew[lane] = 0u;
+  if (wid < ME_NLOAD) {
+    if (wid == 0) {
+      if (lane == 0) me_stamp(a, 0);
+      if (lane < 8) {
+        sm.full[lane] = 0u;
+        sm.freew[lane] = 0u;
+      }
+      if (lane == 0) {
+        sm.doneA = 0u;
+        sm.doneB = 0u;
+        sm.actReady = 0u;
+        }
     }
-    if (lane == 0) {
-      sm.doneA = 0u;
-      sm.doneB = 0u;
-      sm.actReady = 0u;
-    }
+    // each loader's first ME_INFLIGHT slots (ME_NLOAD x ME_INFLIGHT < ME_RING: no slot is reused yet)
     LoadCursor cu;
-    const int pre = nS < ME_INFLIGHT ? nS : ME_INFLIGHT;
-    for (int s = 0; s < pre; ++s, cu.next(m)) me_issue_slot<NT>(a, m, cu, sm, lane);
-  } else {
+    for (int k = 0; k < wid; ++k) cu.next(m);
+    for (int k = 0; k < ME_INFLIGHT && cu.s < nS; ++k) {
+      me_issue_slot<NT>(a, m, cu, sm, lane);
+      for (int q = 0; q < ME_NLOAD; ++q) cu.next(m);
+    }
+  } else if (!a.P) {
     // x -> LDS (written by the previous launch: plain loads)
-    const int t = threadIdx.x - 64;
-    for (int i = t; i < a.H / 8; i += 192)
+    const int t = threadIdx.x - 64 * ME_NLOAD;
+    for (int i = t; i < a.H / 8; i += ME_THREADS - 64 * ME_NLOAD)
       *reinterpret_cast<u32x4*>(sm.vec + 16 * i) = *reinterpret_cast<const u32x4*>(a.xn + 8 * i);
+  }
+  if (a.P) {
+    // fused post-attention tail (all waves; the loader has its first slots in flight), pass 1:
+    // hn = bf16(h + bf16(sum_s P[s])) -> LDS, sum of squares (add_partials_rmsnorm's math). Every
+    // workgroup forms the whole row (the norm needs all of it); it keeps its own down rows of hn for
+    // the final residual and writes h only at its end (every reader of h is past its phase A by then).
+    const int t = threadIdx.x;
+    float ss = 0.f;
+    const int n4 = a.H / 4;
+    constexpr int U = 2;
+    constexpr int CT = ME_THREADS;
+    for (int i0 = 0; i0 < n4; i0 += U * CT) {
+      f32x4 pv[U][8];
+      uint2 hv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = min(i0 + u * CT + t, n4 - 1);
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+          if (s < a.S) pv[u][s] = *reinterpret_cast<const f32x4*>(a.P + (size_t)s * a.H + 4 * i);
+        hv[u] = *reinterpret_cast<const uint2*>(a.h + 4 * i);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * CT + t;
+        if (i >= n4) continue;
+        f32x4 acc = pv[u][0];
+#pragma unroll
+        for (int s = 1; s < 8; ++s)
+          if (s < a.S) acc += pv[u][s];
+        for (int s = 8; s < a.S; ++s) acc += *reinterpret_cast<const f32x4*>(a.P + (size_t)s * a.H + 4 * i);
+        float hf[4];
+        unpack4(hv[u], hf);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = bf2f(f2bf(hf[e] + bf2f(f2bf(acc[e]))));
+          ss += v[e] * v[e];
+        }
+        *reinterpret_cast<uint2*>(sm.vec + 8 * i) = make_uint2(pk2bf(v[0], v[1]), pk2bf(v[2], v[3]));
+        const int r0 = 4 * i - 16 * m.d0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (r0 + e >= 0 && r0 + e < 16 * (d1 - m.d0)) sm.hres[r0 + e] = v[e];
+      }
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) sm.red[wid] = ss;
+    me_wait_lgkm0();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // pass 2, in place: x = bf16(gamma * bf16(hn * inv))
+    float ssum = 0.f;
+#pragma unroll
+    for (int w2 = 0; w2 < ME_THREADS / 64; ++w2) ssum += sm.red[w2];
+    const float inv = rsqrtf(ssum / (float)a.H + a.eps);
+    for (int i = t; i < n4; i += CT) {
+      float hf[4], g[4], o[4];
+      unpack4(*reinterpret_cast<const uint2*>(sm.vec + 8 * i), hf);
+      unpack4(*reinterpret_cast<const uint2*>(a.gamma + 4 * i), g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = g[e] * bf2f(f2bf(hf[e] * inv));
+      *reinterpret_cast<uint2*>(sm.vec + 8 * i) = make_uint2(pk2bf(o[0], o[1]), pk2bf(o[2], o[3]));
+    }
   }
   me_wait_lgkm0();
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 
-  if (wid == 0) {
-    // ---------------- loader ----------------
-    int pub = 0;
+  if (wid < ME_NLOAD) {
+    // ---------------- loaders: slots wid, wid + ME_NLOAD, ... ----------------
+    static_assert(ME_NLOAD * ME_INFLIGHT < ME_RING, "pre-issued slots must not wrap the ring");
+    int pub = wid;  // oldest issued, unpublished slot of this loader
     LoadCursor cu;
-    const int s0 = nS < ME_INFLIGHT ? nS : ME_INFLIGHT;
-    for (int s = 0; s < s0; ++s) cu.next(m);
-    for (int s = s0; s < nS; ++s, cu.next(m)) {
+    for (int k = 0; k < wid + ME_NLOAD * ME_INFLIGHT; ++k) cu.next(m);
+    for (; cu.s < nS;) {
+      const int s = cu.s;
       const int r = s % ME_RING;
       if (s >= ME_RING) {
         const unsigned need = (unsigned)(s - ME_RING + 1);
         if (lds_ld(&sm.freew[r]) != need) {
           // the ring is full: publish what has landed before blocking on the consumers
           me_wait_vm<0>();
-          for (; pub < s; ++pub) lds_st(&sm.full[pub % ME_RING], (unsigned)pub + 1u);
+          for (; pub < s; pub += ME_NLOAD) lds_st(&sm.full[pub % ME_RING], (unsigned)pub + 1u);
           if (!me_spin_lds(&sm.freew[r], need, a.err)) break;
         }
       }
       me_issue_slot<NT>(a, m, cu, sm, lane);
-      if (s - pub + 1 > ME_INFLIGHT) {
+      if ((s - pub) / ME_NLOAD + 1 > ME_INFLIGHT) {
         me_wait_vm<16 * ME_INFLIGHT>();
         lds_st(&sm.full[pub % ME_RING], (unsigned)pub + 1u);
-        ++pub;
+        pub += ME_NLOAD;
       }
+      for (int q = 0; q < ME_NLOAD; ++q) cu.next(m);
     }
-    if (lane == 0) me_stamp(a, 1);
+    if (lane == 0 && wid == 0) me_stamp(a, 1);
     me_wait_vm<0>();
-    for (; pub < nS; ++pub) lds_st(&sm.full[pub % ME_RING], (unsigned)pub + 1u);
+    for (; pub < nS; pub += ME_NLOAD) lds_st(&sm.full[pub % ME_RING], (unsigned)pub + 1u);
     return;
   }
 
   // ---------------- consumers ----------------
-  const int c = wid - 1;
+  const int c = wid - ME_NLOAD;
   const int n = lane & 15, kg = lane >> 4;
   bool arrivedA = false;
   auto finish_A = [&]() {
@@ -322,9 +416,15 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
     }
     me_wait_lgkm0();
     if (lane == 0) lds_st(&sm.freew[r], (unsigned)s + 1u);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // four independent accumulation chains (one dependent chain of 16 MFMAs made the consumers, not
+    // the weight stream, the pace of the ring)
+    f32x4 acc4[4];
 #pragma unroll
-    for (int ks = 0; ks < 16; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[ks], wf[ks], acc, 0, 0, 0);
+    for (int q = 0; q < 4; ++q) acc4[q] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks)
+      acc4[ks & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[ks], wf[ks], acc4[ks & 3], 0, 0, 0);
+    const f32x4 acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
     // C[m][n]: lane (n, kg) holds rows 4kg..4kg+3 of column n; row 0 (x) sits in lanes 0..15
     if (lane < 16) sm.part[s * ME_ROWS + n] = acc[0];
   }
@@ -342,7 +442,7 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
     float acc = 0.f;
     for (int kc = 0; kc < m.KB; ++kc) acc += sm.part[(m.nA + g * m.KB + kc) * ME_ROWS + rr];
     const int row = 16 * (m.d0 + g) + rr;
-    a.h[row] = f2bf(acc + bf2f(a.h[row]));
+    a.h[row] = f2bf(acc + (a.P ? sm.hres[16 * g + rr] : bf2f(a.h[row])));
   }
   if (lane == 0) me_stamp(a, 4);
 }
@@ -374,12 +474,15 @@ RAGK_API int ragk_mlp_engine_set_stamps(void* p) {
   return 0;
 }
 
-RAGK_API int ragk_mlp_engine(const void* xn, const void* wgu, const void* wd, void* h, void* act, void* ctr, void* err,
-                             int M, int H, int I, int G, hipStream_t st) {
+// xn != nullptr: x given. Otherwise the fused post-attention tail: P [S][H] fp32 o_proj slabs, gamma, eps
+// (h += bf16(sum P); x = rmsnorm(h) * gamma, add_partials_rmsnorm's math, inside the launch).
+RAGK_API int ragk_mlp_engine(const void* xn, const float* P, int S, const void* gamma, float eps, const void* wgu,
+                             const void* wd, void* h, void* act, void* ctr, void* err, int M, int H, int I, int G,
+                             hipStream_t st) {
   if (!ragk_mlp_engine_ok(M, H, I, G)) return (int)hipErrorInvalidValue;
-  if (!xn || !wgu || !wd || !h || !act || !ctr || !err) return (int)hipErrorInvalidValue;
-  MlpArgs a{(const bf16_t*)xn, (const bf16_t*)wgu, (const bf16_t*)wd, (bf16_t*)h, (bf16_t*)act,
-            (unsigned long long*)ctr, (unsigned*)err, g_me_stamps, H, I};
+  if (!wgu || !wd || !h || !act || !ctr || !err || (!xn && (!P || !gamma || S < 1 || H % 4))) return (int)hipErrorInvalidValue;
+  MlpArgs a{(const bf16_t*)xn, xn ? nullptr : P, (const bf16_t*)gamma, eps, S, (const bf16_t*)wgu,
+            (const bf16_t*)wd, (bf16_t*)h, (bf16_t*)act, (unsigned long long*)ctr, (unsigned*)err, g_me_stamps, H, I};
   if (g_me_nt)
     hipLaunchKernelGGL(mlp_engine_kernel<true>, dim3(G), dim3(ME_THREADS), 0, st, a);
   else

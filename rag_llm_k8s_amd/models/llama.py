@@ -354,16 +354,17 @@ class LlamaModel:
             be.attn_decode_rope(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, attn, Hq, Hkv, D,
                                 defer_merge=merge)
             P = be.gemm_part_merge(attn, inp.meta, L["wo"], Hq) if merge else be.gemm_part(attn, L["wo"])
-            xn = reduce_norm(P, L["ln_post"])
             nxt = layers[li + 1]["ln_in"] if li + 1 < len(layers) else w.norm
+            if mlp_eng:
+                # o_proj slabs + residual + post-attention norm + gate/up + SiLU + down + residual: one launch
+                be.mlp_engine_tail(P, h, L["ln_post"], c.rms_norm_eps, L["wgu"], L["wdown"])
+                if not fuse_norm or li + 1 == len(layers):
+                    xn = be.rmsnorm(h, nxt, c.rms_norm_eps)
+                continue
+            xn = reduce_norm(P, L["ln_post"])
             if silu_fused:
                 P = be.gemm_part_silu(be.gemm_part_gu(xn, L["wgu"]), L["wdown"])
                 xn = reduce_norm(P, nxt)
-                continue
-            if mlp_eng:
-                be.mlp_engine(xn, L["wgu"], L["wdown"], h)
-                if not fuse_norm or li + 1 == len(layers):
-                    xn = be.rmsnorm(h, nxt, c.rms_norm_eps)
                 continue
             a = be.gemm(xn, L["wgu"], epi="silu_mul")
             if M <= DECODE_DOWN_SKINNY_MAX_M and not tp:

@@ -152,6 +152,10 @@ class TorchBackend:
         h.copy_((h.float() + a.float() @ w_down.float().t()).to(h.dtype))
         return h
 
+    def mlp_engine_tail(self, P, h, gamma, eps, w_gu, w_down):
+        """add_partials_rmsnorm (o_proj slabs + residual + post-attention norm) then mlp_engine, one op."""
+        return self.mlp_engine(self.add_partials_rmsnorm(P, h, gamma, eps), w_gu, w_down, h)
+
     def add_partials_rmsnorm(self, P, h, w, eps):
         h.copy_((h.float() + P.sum(0).to(h.dtype).float()).to(h.dtype))
         return R.rmsnorm(h, w, eps)
@@ -299,6 +303,9 @@ class NativeBackend(TorchBackend):
 
     def mlp_engine(self, xn, w_gu, w_down, h):
         return self.n.mlp_engine(xn, w_gu, w_down, h)
+
+    def mlp_engine_tail(self, P, h, gamma, eps, w_gu, w_down):
+        return self.n.mlp_engine_tail(P, h, gamma, eps, w_gu, w_down)
 
     def rope_kv_partials(self, P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D):
         self.n.rope_kv_partials(P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)

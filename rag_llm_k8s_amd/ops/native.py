@@ -488,14 +488,30 @@ def mlp_engine_ok(M, w_gu, w_down):
 def mlp_engine(xn, w_gu, w_down, h):
     """h += W_down . (silu(gate) * up) for ONE row (xn = the post-attention RMSNorm of h, bf16 [1, H])."""
     _bf16_2d(xn, "xn")
+    _req(xn.shape == (1, w_down.shape[0]) and xn.is_contiguous(), "xn [1, H]")
+    return _mlp_engine_launch(xn.data_ptr(), None, 0, None, 0.0, w_gu, w_down, h)
+
+
+def mlp_engine_tail(P, h, gamma, eps, w_gu, w_down):
+    """The batch-1 post-attention tail in one launch: h += bf16(sum of the o_proj slabs P [S, 1, H]);
+    x = rmsnorm(h) * gamma (add_partials_rmsnorm's math); h += W_down . (silu(gate) * up)."""
+    H = w_down.shape[0]
+    _req(P.dtype == torch.float32 and P.is_cuda and P.is_contiguous() and P.dim() == 3 and P.shape[1:] == (1, H),
+         "P [S, 1, H] fp32")
+    _req(gamma.dtype == torch.bfloat16 and gamma.is_contiguous() and gamma.numel() == H, "gamma [H] bf16")
+    return _mlp_engine_launch(None, P.data_ptr(), P.shape[0], gamma.data_ptr(), float(eps), w_gu, w_down, h)
+
+
+def _mlp_engine_launch(xn_ptr, P_ptr, S, g_ptr, eps, w_gu, w_down, h):
     _bf16_2d(h, "h")
     H, I = w_down.shape
-    _req(xn.shape == (1, H) and h.shape == (1, H) and xn.is_contiguous() and h.is_contiguous(), "xn / h [1, H]")
+    _req(h.shape == (1, H) and h.is_contiguous(), "h [1, H]")
     _req(mlp_engine_ok(1, w_gu, w_down), "mlp_engine shape")
-    act, words, nb = _me_workspace(xn.device, I)
+    act, words, nb = _me_workspace(h.device, I)
     err = words.data_ptr() + nb
-    check(_lib.lib().ragk_mlp_engine(xn.data_ptr(), w_gu.data_ptr(), w_down.data_ptr(), h.data_ptr(), act.data_ptr(),
-                                     words.data_ptr(), err, 1, H, I, _cu_count(), stream_ptr()), "ragk_mlp_engine")
+    check(_lib.lib().ragk_mlp_engine(xn_ptr, P_ptr, S, g_ptr, eps, w_gu.data_ptr(), w_down.data_ptr(), h.data_ptr(),
+                                     act.data_ptr(), words.data_ptr(), err, 1, H, I, _cu_count(), stream_ptr()),
+          "ragk_mlp_engine")
     return h
 
 

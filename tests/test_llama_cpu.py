@@ -159,7 +159,8 @@ def test_split_k_decode_path_matches_plain_decode(tiny):
 
 
 def test_batch1_decode_mlp_engine_path_matches_plain_decode(tiny):
-    """Batch-1 split-K decode with the persistent MLP launch (gate/up + SiLU + down + residual in one op,
+    """Batch-1 split-K decode with the persistent post-attention launch (o_proj slabs + residual + norm +
+    gate/up + SiLU + down + residual in one op,
     csrc/kernels/mlp_engine.hip on the GPU; its torch oracle here) generates the same greedy tokens as the
     plain decode path, and the op runs once per layer per decode step."""
     cfg, hf, sd = tiny
@@ -172,8 +173,8 @@ def test_batch1_decode_mlp_engine_path_matches_plain_decode(tiny):
         model = LlamaModel(cfg, w, "cpu", max_positions=512)
         model.be.enable_part = part
         calls = []
-        orig = model.be.mlp_engine
-        model.be.mlp_engine = lambda *a: (calls.append(1), orig(*a))[1]
+        orig = model.be.mlp_engine_tail
+        model.be.mlp_engine_tail = lambda *a: (calls.append(1), orig(*a))[1]
         eng = LLMEngine(model, num_blocks=32, max_batch=4, max_model_len=512, use_graphs=False)
         outs.append(eng.generate(prompt, params))
         assert len(calls) == (7 * cfg.num_hidden_layers if part else 0)

@@ -1,5 +1,6 @@
-"""Batch-1 decode MLP per layer: the persistent engine (csrc/kernels/mlp_engine.hip) vs the separate
-SiLU*up + down kernels it replaces, Llama-3.1-8B shapes, L layers of distinct random weights (1.4 GB per 4
+"""Batch-1 post-attention tail per layer: the persistent engine (csrc/kernels/mlp_engine.hip: o_proj slabs
++ residual + RMSNorm + gate/up + SiLU + down + residual) vs the separate add_partials_rmsnorm + SiLU*up +
+down kernels it replaces, Llama-3.1-8B shapes, L layers of distinct random weights (1.4 GB per 4
 layers, so the weights stream from HBM as in a decode step), each form captured in a hipGraph and
 replayed back to back; GPU time per layer.
 
@@ -37,14 +38,18 @@ def main():
     x = torch.randn(1, H, device=dev).bfloat16()
     h = torch.randn(1, H, device=dev).bfloat16()
 
+    P = torch.randn(8, 1, H, device=dev) * 0.01
+    gamma = torch.ones(H, device=dev).bfloat16()
+
     def separate():
         for wgu, wd in layers:
-            a = native.gemm(x, wgu, epi="silu_mul")
+            xn = native.add_partials_rmsnorm(P, h, gamma, 1e-5)
+            a = native.gemm(xn, wgu, epi="silu_mul")
             native.gemm(a, wd, resid=h, epi="resid", out=h)
 
     def engine():
         for wgu, wd in layers:
-            native.mlp_engine(x, wgu, wd, h)
+            native.mlp_engine_tail(P, h, gamma, 1e-5, wgu, wd)
 
     def graph_of(fn):
         s = torch.cuda.Stream()
@@ -88,7 +93,7 @@ def main():
         _lib.lib().ragk_mlp_engine_set_stamps(st.data_ptr())
         for _ in range(3):
             st.zero_()
-            native.mlp_engine(x, layers[0][0], layers[0][1], h)
+            native.mlp_engine_tail(P, h, gamma, 1e-5, layers[0][0], layers[0][1])
             torch.cuda.synchronize()
         _lib.lib().ragk_mlp_engine_set_stamps(None)
         s = st.cpu().double()
