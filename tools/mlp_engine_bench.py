@@ -91,12 +91,23 @@ def main():
         G = native._cu_count()
         st = torch.zeros(G, 8, dtype=torch.int64, device=dev)
         _lib.lib().ragk_mlp_engine_set_stamps(st.data_ptr())
-        for _ in range(3):
+        runs = []
+        for li in range(4):
             st.zero_()
-            native.mlp_engine_tail(P, h, gamma, 1e-5, layers[0][0], layers[0][1])
+            native.mlp_engine_tail(P, h, gamma, 1e-5, layers[li][0], layers[li][1])
             torch.cuda.synchronize()
+            runs.append(st.cpu().double().clone())
+        # skew structure: phase-A finish per XCD (dispatch order w % 8) and its repeatability across launches
+        for k, r in enumerate(runs):
+            us_r = (r[:, 2] - r[:, 0].min()) / 100.0
+            per = [us_r[x::8].median().item() for x in range(8)]
+            print("launch %d phase A done per XCD p50: %s" % (k, " ".join("%.1f" % v for v in per)), flush=True)
+        a0 = (runs[-1][:, 2] - runs[-1][:, 0].min()) / 100.0
+        a1 = (runs[-2][:, 2] - runs[-2][:, 0].min()) / 100.0
+        c = torch.corrcoef(torch.stack([a0, a1]))[0, 1].item()
+        print("per-workgroup phase A finish, correlation between two launches: %.2f" % c, flush=True)
         _lib.lib().ragk_mlp_engine_set_stamps(None)
-        s = st.cpu().double()
+        s = runs[-1]
         t0 = s[:, 0].min()
         us = (s[:, :5] - t0) / 100.0  # 100 MHz -> us
         names = ["start", "loader done", "phase A done", "act ready", "end"]
