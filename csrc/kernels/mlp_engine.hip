@@ -75,7 +75,13 @@ struct MlpArgs {
   unsigned* err;           // timeout word
   unsigned long long* stamps;  // optional [G][8] s_memrealtime stamps (tools/mlp_engine_bench.py ME_STAMPS=1)
   int H, I;
+  int w_even, w_odd;       // phase-A work weights of workgroups on even / odd XCDs
 };
+
+// prefix weight of workgroups [0, w): even w weigh we, odd wo
+__host__ __device__ __forceinline__ long long me_cum(int w, int we, int wo) {
+  return (long long)(w / 2) * (we + wo) + (long long)(w & 1) * we;
+}
 
 __device__ __forceinline__ void me_stamp(const MlpArgs& a, int i) {
   if (a.stamps) a.stamps[blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
@@ -181,8 +187,11 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
   SlotMap m;
   m.KA = a.H / ME_KC;
   m.KB = a.I / ME_KC;
-  m.a0 = (int)((long long)w * NA / G);
-  const int a1 = (int)((long long)(w + 1) * NA / G);
+  // activation groups split in proportion to per-XCD stream rate (dispatch order w % 8 = XCD): the
+  // workgroups on even XCDs streamed the same phase-A work ~15 % slower, repeatably (correlation 0.97
+  // launch to launch, profiles/mlp_engine_skew_r5.log), and the hand-off waits for the slowest
+  m.a0 = (int)((long long)NA * me_cum(w, a.w_even, a.w_odd) / me_cum(G, a.w_even, a.w_odd));
+  const int a1 = (int)((long long)NA * me_cum(w + 1, a.w_even, a.w_odd) / me_cum(G, a.w_even, a.w_odd));
   m.d0 = (int)((long long)w * ND / G);
   const int d1 = (int)((long long)(w + 1) * ND / G);
   m.nA = (a1 - m.a0) * m.KA;
@@ -448,6 +457,7 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
 }
 
 int g_me_nt = 1;
+int g_me_w_even = 27, g_me_w_odd = 32;  // measured per-XCD rate ratio ~0.84
 unsigned long long* g_me_stamps = nullptr;
 
 }  // namespace
@@ -458,9 +468,19 @@ RAGK_API int ragk_mlp_engine_ok(int M, int H, int I, int G) {
   if (H % ME_KC || I % ME_KC || I % 64 || H % 16) return 0;
   if (2 * H > ME_VEC || 2 * I > ME_VEC) return 0;
   const int NA = I / 8, ND = H / 16;
-  const int maxA = (NA + G - 1) / G, maxB = (ND + G - 1) / G;
+  const long long T = me_cum(G, g_me_w_even, g_me_w_odd);
+  const int wmax = g_me_w_even > g_me_w_odd ? g_me_w_even : g_me_w_odd;
+  const int maxA = (int)(((long long)NA * wmax + T - 1) / T), maxB = (ND + G - 1) / G;  // floor-difference bound
   if (maxA * (H / ME_KC) > ME_MAXA || maxB * (I / ME_KC) > ME_MAXB || maxA * 8 > 64 || maxB * 16 > 64) return 0;
   return 1;
+}
+
+// phase-A weights of workgroups on even / odd XCDs (A/B tooling: 1, 1 = the even split)
+RAGK_API int ragk_mlp_engine_set_xcd_weights(int we, int wo) {
+  if (we < 1 || wo < 1 || we > 1000 || wo > 1000) return (int)hipErrorInvalidValue;
+  g_me_w_even = we;
+  g_me_w_odd = wo;
+  return 0;
 }
 
 RAGK_API int ragk_mlp_engine_set_nt(int nt) {
@@ -482,7 +502,8 @@ RAGK_API int ragk_mlp_engine(const void* xn, const float* P, int S, const void* 
   if (!ragk_mlp_engine_ok(M, H, I, G)) return (int)hipErrorInvalidValue;
   if (!wgu || !wd || !h || !act || !ctr || !err || (!xn && (!P || !gamma || S < 1 || H % 4))) return (int)hipErrorInvalidValue;
   MlpArgs a{(const bf16_t*)xn, xn ? nullptr : P, (const bf16_t*)gamma, eps, S, (const bf16_t*)wgu,
-            (const bf16_t*)wd, (bf16_t*)h, (bf16_t*)act, (unsigned long long*)ctr, (unsigned*)err, g_me_stamps, H, I};
+            (const bf16_t*)wd, (bf16_t*)h, (bf16_t*)act, (unsigned long long*)ctr, (unsigned*)err, g_me_stamps, H, I,
+            g_me_w_even, g_me_w_odd};
   if (g_me_nt)
     hipLaunchKernelGGL(mlp_engine_kernel<true>, dim3(G), dim3(ME_THREADS), 0, st, a);
   else

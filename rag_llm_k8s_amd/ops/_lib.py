@@ -42,6 +42,7 @@ _SIGS = {
     "ragk_mlp_engine_ok": [I, I, I, I],
     "ragk_mlp_engine_set_nt": [I],
     "ragk_mlp_engine_set_stamps": [P],
+    "ragk_mlp_engine_set_xcd_weights": [I, I],
     "ragk_mlp_engine": [P, P, I, P, F, P, P, P, P, P, P, I, I, I, I, S],
     "ragk_mlp_engine_ctr_bytes": [],
     "ragk_gemm_part_ksteps": [I, I, I],

@@ -73,17 +73,23 @@ def main():
         return (time.perf_counter() - t0) / reps / L * 1e6
 
     nts = [int(t) for t in os.environ.get("ME_NT", "1").split(",") if t]
+    # ME_XW="27:32,1:1": alternate the per-XCD phase-A weights (even:odd) -- engine runs per setting
+    xws = [tuple(int(v) for v in s.split(":")) for s in os.environ.get("ME_XW", "").split(",") if s] or [None]
     g_sep = graph_of(separate)
     for rnd in range(2):
         print("round %d: separate kernels %.2f us/layer" % (rnd, timed(g_sep)), flush=True)
         for nt in nts:
-            native.set_mlp_engine_nt(nt)
-            g_eng = graph_of(engine)
-            t = timed(g_eng)
-            native.mlp_engine_check()
-            print("round %d: engine nt=%d %.2f us/layer (%.2f TB/s of weights)" % (
-                rnd, nt, t, (3 * H * I * 2) / t / 1e6), flush=True)
-            del g_eng
+            for xw in xws:
+                from rag_llm_k8s_amd.ops import _lib
+                if xw is not None:
+                    _lib.lib().ragk_mlp_engine_set_xcd_weights(*xw)
+                native.set_mlp_engine_nt(nt)
+                g_eng = graph_of(engine)
+                t = timed(g_eng)
+                native.mlp_engine_check()
+                print("round %d: engine nt=%d xcd weights %s %.2f us/layer (%.2f TB/s of weights)" % (
+                    rnd, nt, xw, t, (3 * H * I * 2) / t / 1e6), flush=True)
+                del g_eng
     native.set_mlp_engine_nt(1)
     if os.environ.get("ME_STAMPS") == "1":
         # one launch with stage stamps (s_memrealtime, 100 MHz): per-workgroup times from the earliest start
