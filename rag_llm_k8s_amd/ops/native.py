@@ -467,6 +467,9 @@ def _me_workspace(dev, I):
     key = (str(dev), I)
     ws = _me_ws.get(key)
     if ws is None:
+        # allocated by an eager call, never inside a hipGraph capture: a graph-pool allocation (with its
+        # zero-fill captured) would be handed to later eager launches after the graph is gone
+        _req(not torch.cuda.is_current_stream_capturing(), "mlp_engine workspace: run one eager step before capture")
         nb = int(_lib.lib().ragk_mlp_engine_ctr_bytes())
         words = torch.zeros(nb // 8 + 2, dtype=torch.int64, device=dev)
         ws = (torch.zeros(I, dtype=torch.bfloat16, device=dev), words, nb)
