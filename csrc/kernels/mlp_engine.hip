@@ -83,6 +83,15 @@ __host__ __device__ __forceinline__ long long me_cum(int w, int we, int wo) {
   return (long long)(w / 2) * (we + wo) + (long long)(w & 1) * we;
 }
 
+// Workgroup w's share: activation groups [r[0], r[1]) (weighted by XCD parity), down row groups [r[2], r[3])
+__host__ __device__ __forceinline__ void me_split(int G, int w, int NA, int ND, int we, int wo, int (&r)[4]) {
+  const long long T = me_cum(G, we, wo);
+  r[0] = (int)((long long)NA * me_cum(w, we, wo) / T);
+  r[1] = (int)((long long)NA * me_cum(w + 1, we, wo) / T);
+  r[2] = (int)((long long)w * ND / G);
+  r[3] = (int)((long long)(w + 1) * ND / G);
+}
+
 __device__ __forceinline__ void me_stamp(const MlpArgs& a, int i) {
   if (a.stamps) a.stamps[blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
 }
@@ -190,10 +199,12 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
   // activation groups split in proportion to per-XCD stream rate (dispatch order w % 8 = XCD): the
   // workgroups on even XCDs streamed the same phase-A work ~15 % slower, repeatably (correlation 0.97
   // launch to launch, profiles/mlp_engine_skew_r5.log), and the hand-off waits for the slowest
-  m.a0 = (int)((long long)NA * me_cum(w, a.w_even, a.w_odd) / me_cum(G, a.w_even, a.w_odd));
-  const int a1 = (int)((long long)NA * me_cum(w + 1, a.w_even, a.w_odd) / me_cum(G, a.w_even, a.w_odd));
-  m.d0 = (int)((long long)w * ND / G);
-  const int d1 = (int)((long long)(w + 1) * ND / G);
+  int rng[4];
+  me_split(G, w, NA, ND, a.w_even, a.w_odd, rng);
+  m.a0 = rng[0];
+  const int a1 = rng[1];
+  m.d0 = rng[2];
+  const int d1 = rng[3];
   m.nA = (a1 - m.a0) * m.KA;
   const int nB = (d1 - m.d0) * m.KB;
   const int nS = m.nA + nB;
@@ -457,7 +468,9 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
 }
 
 int g_me_nt = 1;
-int g_me_w_even = 27, g_me_w_odd = 32;  // measured per-XCD rate ratio ~0.84
+// measured per-XCD rate ratio ~0.84; for Llama-3.1-8B on 256 CUs (7 groups per workgroup on average)
+// 27 : 32 and 3 : 4 give the same integer split, 6 : 8 groups (profiles/mlp_engine_xcd_weights_r5.log)
+int g_me_w_even = 3, g_me_w_odd = 4;
 unsigned long long* g_me_stamps = nullptr;
 
 }  // namespace
@@ -473,6 +486,16 @@ RAGK_API int ragk_mlp_engine_ok(int M, int H, int I, int G) {
   const int maxA = (int)(((long long)NA * wmax + T - 1) / T), maxB = (ND + G - 1) / G;  // floor-difference bound
   if (maxA * (H / ME_KC) > ME_MAXA || maxB * (I / ME_KC) > ME_MAXB || maxA * 8 > 64 || maxB * 16 > 64) return 0;
   return 1;
+}
+
+// The kernel's work split for workgroup w of G (CPU-tested: every activation group and down row group
+// owned exactly once, per-workgroup slot counts within the LDS partial capacity).
+RAGK_API int ragk_mlp_engine_split(int G, int w, int H, int I, int* out4) {
+  if (G < 1 || w < 0 || w >= G || !out4) return (int)hipErrorInvalidValue;
+  int r[4];
+  me_split(G, w, I / 8, H / 16, g_me_w_even, g_me_w_odd, r);
+  for (int i = 0; i < 4; ++i) out4[i] = r[i];
+  return 0;
 }
 
 // phase-A weights of workgroups on even / odd XCDs (A/B tooling: 1, 1 = the even split)

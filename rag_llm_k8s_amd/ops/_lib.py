@@ -45,6 +45,7 @@ _SIGS = {
     "ragk_mlp_engine_set_xcd_weights": [I, I],
     "ragk_mlp_engine": [P, P, I, P, F, P, P, P, P, P, P, I, I, I, I, S],
     "ragk_mlp_engine_ctr_bytes": [],
+    "ragk_mlp_engine_split": [I, I, I, I, P],
     "ragk_gemm_part_ksteps": [I, I, I],
     "ragk_gemm_part_set_min_blocks": [I],
     "ragk_add_partials_rmsnorm": [P, I, I, P, I, P, P, I, I, F, S],
