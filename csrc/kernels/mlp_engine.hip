@@ -37,10 +37,13 @@
 //   * end of phase B (last consumer): h[row] = bf16(h[row] + sum of the row's partials).
 // Counters are monotonic (never re-zeroed between launches, so a hipGraph replay needs no memset
 // node): a workgroup's own add returns the count before it, which names the launch generation; the
-// wait is for (generation + 1) x members on every shard. Every wait is bounded: on a timeout the
-// error word is set (ragk_mlp_engine_error) and the host resets the counters.
+// shard's last arriver adds to the top counter, which the waiters poll for (generation + 1) x shards.
+// Every wait is bounded: on a timeout the error word is set, and the host (ops/native.py
+// mlp_engine_check, called by the engine every 64 decode steps) raises and re-arms the counters.
 // Deadlock freedom: one workgroup per CU (the LDS footprint admits one), grid = CU count, all
-// resident; the only cross-workgroup wait is the act hand-off.
+// resident; the only cross-workgroup wait is the act hand-off. (A GPU shared with another process's
+// long-running kernels can keep a workgroup from being dispatched: the bounded wait then reports a
+// timeout instead of hanging; the model uses the engine only at TP = 1.)
 #include "common.h"
 using namespace ragk;
 
