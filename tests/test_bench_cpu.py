@@ -26,9 +26,11 @@ def _bench(n, *extra, env_extra=None, rc=0):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py"] + args
     env = dict(os.environ, OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", **(env_extra or {}))
-    r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
+    # stdout and stderr apart: a rank's stderr message written while rank 0 prints its JSON line could
+    # otherwise land inside that line (seen with the injected TP-phase hang)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=600)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert r.returncode == rc and len(lines) == 1, (r.returncode, r.stdout[-3000:])
+    assert r.returncode == rc and len(lines) == 1, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
     return json.loads(lines[0])
 
 
