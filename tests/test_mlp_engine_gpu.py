@@ -125,6 +125,35 @@ def test_mlp_engine_tail_matches_separate_kernels(native, S):
     assert rel_err(h - hmid, _ref(xr, hmid, gate, up, down) - hmid) < 2e-2
 
 
+def test_mlp_engine_under_concurrent_load(native):
+    """Hand-off under uneven load: a memory-bound kernel on another stream holds CUs while the engine
+    launches, so its workgroups are dispatched late and unevenly and stream at uneven rates; every launch
+    must still complete (no timeout) and match the unloaded result bit for bit."""
+    H, I = 4096, 14336
+    _, _, wgu, down = _weights(H, I, 41)
+    torch.manual_seed(42)
+    P = torch.randn(8, 1, H, device=DEV) * 0.2
+    gamma = (1 + 0.1 * torch.randn(H, device=DEV)).bfloat16()
+    h0 = torch.randn(1, H, device=DEV).bfloat16()
+    ref = h0.clone()
+    native.mlp_engine_tail(P, ref, gamma, 1e-5, wgu, down)
+    torch.cuda.synchronize()
+    big = torch.ones(256 * 1024 * 1024 // 4, device=DEV)  # 1 GiB
+    side = torch.cuda.Stream()
+    outs = []
+    for k in range(6):
+        with torch.cuda.stream(side):
+            for _ in range(2 + k % 3):
+                big.mul_(1.0000001)
+        h = h0.clone()
+        native.mlp_engine_tail(P, h, gamma, 1e-5, wgu, down)
+        outs.append(h)
+    torch.cuda.synchronize()
+    native.mlp_engine_check()
+    for h in outs:
+        assert torch.equal(h, ref)
+
+
 def test_mlp_engine_shape_gate(native):
     """Shapes the engine does not take are refused up front (the model keeps the separate kernels)."""
     _, _, wgu, down = _weights(1024, 2048, 3)
