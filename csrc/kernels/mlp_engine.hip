@@ -38,13 +38,22 @@
 // Counters are monotonic (never re-zeroed between launches, so a hipGraph replay needs no memset
 // node): a workgroup's own add returns the count before it, which names the launch generation; the
 // shard's last arriver adds to the top counter, which the waiters poll for (generation + 1) x shards.
-// Every wait is bounded: on a timeout the error word is set, and the host (ops/native.py
-// mlp_engine_check, called by the engine every 64 decode steps) raises and re-arms the counters.
+// Every wait is bounded by ONE deadline per workgroup (s_memrealtime at entry + the timeout word, 100 ms by
+// default): a wait that gives up writes the error code to the device error word AND to a host-mapped
+// pinned word, raises this workgroup's LDS abort flag (every other wave of the workgroup leaves its own
+// wait at its next check), and the workgroup then writes NOTHING: no h rows, no activations past the
+// failure, no slots published that were never loaded. A launch that finds the device error word already
+// set (an earlier launch of the same step failed) exits before touching any state, so the step's later
+// layers cannot mis-synchronise on counters the failed launch left off their generation. The engine reads
+// the host word after every decode step's existing event sync (no extra device sync), discards that step
+// and the one in flight behind it, re-arms the counters and recomputes them on the separate kernels
+// (engine/llm_engine.py _recover_engine_fault).
 // Deadlock freedom: one workgroup per CU (the LDS footprint admits one), grid = CU count, all
 // resident; the only cross-workgroup wait is the act hand-off. (A GPU shared with another process's
 // long-running kernels can keep a workgroup from being dispatched: the bounded wait then reports a
 // timeout instead of hanging; the model uses the engine only at TP = 1.)
 #include "common.h"
+#include <cstring>
 using namespace ragk;
 
 namespace {
@@ -62,7 +71,9 @@ constexpr int ME_VEC = 28672;                      // x (phase A) / act (phase B
 constexpr int ME_MAXA = 64, ME_MAXB = 56;          // slots per workgroup and phase
 constexpr int ME_SHARDS = 8;
 constexpr int ME_CTR_STRIDE = 16;                  // u64 per shard: one 128-B line each
-constexpr unsigned ME_SPIN_LIMIT = 1u << 21;       // x s_sleep 2: ~0.1-0.2 s
+constexpr unsigned ME_TIMEOUT_TICKS = 10000000u;   // default deadline: 100 ms of s_memrealtime (100 MHz)
+// error codes (device word, host word): which wait gave up
+constexpr unsigned ME_ERR_HANDOFF = 1u, ME_ERR_SLOT = 2u, ME_ERR_FREE = 3u, ME_ERR_ACT = 4u;
 
 struct MlpArgs {
   const bf16_t* xn;        // [H] normalised input row (P == nullptr)
@@ -75,7 +86,9 @@ struct MlpArgs {
   bf16_t* h;               // [H] residual, updated in place
   bf16_t* act;             // [I] hand-off workspace
   unsigned long long* ctr; // [ME_SHARDS][ME_CTR_STRIDE] arrival counters
-  unsigned* err;           // timeout word
+  unsigned* err;           // device error word (0 = healthy); a set word makes later launches exit at entry
+  unsigned* err_host;      // device address of a host-mapped pinned word (the engine polls it per step)
+  const unsigned* tmo;     // deadline in s_memrealtime ticks (0 = ME_TIMEOUT_TICKS); a test hook forces timeouts
   unsigned long long* stamps;  // optional [G][8] s_memrealtime stamps (tools/mlp_engine_bench.py ME_STAMPS=1)
   int H, I;
   int w_even, w_odd;       // phase-A work weights of workgroups on even / odd XCDs
@@ -107,7 +120,7 @@ struct MlpSmem {
   float hres[64];          // this workgroup's rows of h after the o_proj residual (fused tail)
   float red[8];
   unsigned full[8], freew[8];
-  unsigned doneA, doneB, actReady, pad;
+  unsigned doneA, doneB, actReady, abort;
 };
 
 __device__ __forceinline__ void unpack4(uint2 v, float (&f)[4]) {
@@ -129,12 +142,27 @@ typedef __attribute__((address_space(3))) volatile unsigned lds_u32;
 __device__ __forceinline__ unsigned lds_ld(const unsigned* p) { return *(const lds_u32*)(p); }
 __device__ __forceinline__ void lds_st(unsigned* p, unsigned v) { *(lds_u32*)(p) = v; }
 
-// bounded spin on an LDS word (same workgroup): true when *p == want
-__device__ __forceinline__ bool me_spin_lds(const unsigned* p, unsigned want, unsigned* err) {
+__device__ __forceinline__ unsigned long long me_now() { return __builtin_amdgcn_s_memrealtime(); }
+
+// A wait gave up: report (device word for the launches behind this one, host word for the engine) and
+// raise the workgroup's abort flag.
+__device__ __forceinline__ void me_fail(const MlpArgs& a, MlpSmem& sm, unsigned code) {
+  __hip_atomic_store(a.err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.err_host) __hip_atomic_store(a.err_host, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  lds_st(&sm.abort, 1u);
+}
+
+// bounded spin on an LDS word (same workgroup): true when *p == want; false when this workgroup aborted
+// (another wave gave up) or the deadline passed (this wave gives up)
+__device__ __forceinline__ bool me_spin_lds(const unsigned* p, unsigned want, const MlpArgs& a, MlpSmem& sm,
+                                            unsigned long long deadline, unsigned code) {
   for (unsigned it = 0; lds_ld(p) != want; ++it) {
-    if (it > ME_SPIN_LIMIT) {
-      __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
+    if ((it & 31) == 31) {
+      if (lds_ld(&sm.abort)) return false;
+      if (me_now() > deadline) {
+        me_fail(a, sm, code);
+        return false;
+      }
     }
     __builtin_amdgcn_s_sleep(1);
   }
@@ -211,6 +239,9 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
   m.nA = (a1 - m.a0) * m.KA;
   const int nB = (d1 - m.d0) * m.KB;
   const int nS = m.nA + nB;
+  // this workgroup's deadline for every wait below (one clock, one bound)
+  const unsigned tk = *a.tmo;
+  const unsigned long long deadline = me_now() + (tk ? tk : ME_TIMEOUT_TICKS);
 
   if (wid < ME_NLOAD) {
     if (wid == 0) {
@@ -223,7 +254,9 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
         sm.doneA = 0u;
         sm.doneB = 0u;
         sm.actReady = 0u;
-        }
+        // an earlier launch failed (its workgroups left the counters off their generation): skip
+        sm.abort = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
+      }
     }
     // each loader's first ME_INFLIGHT slots (ME_NLOAD x ME_INFLIGHT < ME_RING: no slot is reused yet)
     LoadCursor cu;
@@ -307,11 +340,16 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
+  if (lds_ld(&sm.abort)) {  // skipped launch: touch nothing (drain the loader's first slots first)
+    if (wid < ME_NLOAD) me_wait_vm<0>();
+    return;
+  }
 
   if (wid < ME_NLOAD) {
     // ---------------- loaders: slots wid, wid + ME_NLOAD, ... ----------------
     static_assert(ME_NLOAD * ME_INFLIGHT < ME_RING, "pre-issued slots must not wrap the ring");
     int pub = wid;  // oldest issued, unpublished slot of this loader
+    bool ok = true;
     LoadCursor cu;
     for (int k = 0; k < wid + ME_NLOAD * ME_INFLIGHT; ++k) cu.next(m);
     for (; cu.s < nS;) {
@@ -323,7 +361,10 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
           // the ring is full: publish what has landed before blocking on the consumers
           me_wait_vm<0>();
           for (; pub < s; pub += ME_NLOAD) lds_st(&sm.full[pub % ME_RING], (unsigned)pub + 1u);
-          if (!me_spin_lds(&sm.freew[r], need, a.err)) break;
+          if (!me_spin_lds(&sm.freew[r], need, a, sm, deadline, ME_ERR_FREE)) {
+            ok = false;  // aborted: issued slots past `pub` are never published
+            break;
+          }
         }
       }
       me_issue_slot<NT>(a, m, cu, sm, lane);
@@ -336,7 +377,8 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
     }
     if (lane == 0 && wid == 0) me_stamp(a, 1);
     me_wait_vm<0>();
-    for (; pub < nS; pub += ME_NLOAD) lds_st(&sm.full[pub % ME_RING], (unsigned)pub + 1u);
+    if (ok)
+      for (; pub < nS; pub += ME_NLOAD) lds_st(&sm.full[pub % ME_RING], (unsigned)pub + 1u);
     return;
   }
 
@@ -344,13 +386,15 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
   const int c = wid - ME_NLOAD;
   const int n = lane & 15, kg = lane >> 4;
   bool arrivedA = false;
-  auto finish_A = [&]() {
+  // false: this workgroup aborted (or the hand-off timed out): the caller leaves without writing anything
+  auto finish_A = [&]() -> bool {
     // called once per consumer, after its last phase-A slot (its partial stores retired)
     me_wait_lgkm0();
+    if (lds_ld(&sm.abort)) return false;
     unsigned prev = 0;
     if (lane == 0) prev = __hip_atomic_fetch_add(&sm.doneA, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     prev = __shfl(prev, 0, 64);
-    if (prev != ME_NCONS - 1) return;
+    if (prev != ME_NCONS - 1) return true;
     // last consumer of phase A: this workgroup's activations
     if (lane == 0) me_stamp(a, 2);
     const int nact = m.nA / m.KA * 8;  // <= 64
@@ -379,6 +423,7 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
     const int nsh = G < ME_SHARDS ? G : ME_SHARDS;
     unsigned long long* top = a.ctr + ME_SHARDS * ME_CTR_STRIDE;
     unsigned long long want = 0;
+    int failed = 0;
     if (lane == 0) {
       const unsigned long long mine = (unsigned long long)((G - shard + ME_SHARDS - 1) / ME_SHARDS);
       const unsigned long long old =
@@ -386,14 +431,16 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
       const unsigned long long gen = old / mine;
       if (old + 1 == (gen + 1) * mine) __hip_atomic_fetch_add(top, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       want = (gen + 1) * (unsigned long long)nsh;
-      for (unsigned it = 0; __hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want; ++it) {
-        if (it > ME_SPIN_LIMIT) {
-          __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        if (me_now() > deadline) {  // another workgroup never arrived: no activations are read
+          me_fail(a, sm, ME_ERR_HANDOFF);
+          failed = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(4);
       }
     }
+    if (__shfl(failed, 0, 64)) return false;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
     // all I activations -> LDS, every load sc1 (the producers stored them sc1)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.act, 0, a.I * 2, 0x00020000);
@@ -415,20 +462,21 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
     me_wait_lgkm0();
     if (lane == 0) lds_st(&sm.actReady, 1u);
     if (lane == 0) me_stamp(a, 3);
+    return true;
   };
 
   bool actOk = false;
   for (int s = c; s < nS; s += ME_NCONS) {
     if (s >= m.nA && !arrivedA) {
-      finish_A();
       arrivedA = true;
+      if (!finish_A()) return;
     }
     if (s >= m.nA && !actOk) {
-      if (!me_spin_lds(&sm.actReady, 1u, a.err)) break;
+      if (!me_spin_lds(&sm.actReady, 1u, a, sm, deadline, ME_ERR_ACT)) return;
       actOk = true;
     }
     const int r = s % ME_RING;
-    if (!me_spin_lds(&sm.full[r], (unsigned)s + 1u, a.err)) break;
+    if (!me_spin_lds(&sm.full[r], (unsigned)s + 1u, a, sm, deadline, ME_ERR_SLOT)) return;
     const char* slot = sm.ring + r * ME_SLOT;
     const char* xv = sm.vec + m.chunk(s) * (ME_KC * 2);
     bf16x8 wf[16], xf[16];
@@ -451,14 +499,16 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
     // C[m][n]: lane (n, kg) holds rows 4kg..4kg+3 of column n; row 0 (x) sits in lanes 0..15
     if (lane < 16) sm.part[s * ME_ROWS + n] = acc[0];
   }
-  if (!arrivedA) finish_A();
+  if (!arrivedA && !finish_A()) return;
 
   // ---------------- phase B tail: the last consumer finishes the rows ----------------
   me_wait_lgkm0();
+  if (lds_ld(&sm.abort)) return;  // a wave of this workgroup gave up: h stays unwritten
   unsigned prev = 0;
   if (lane == 0) prev = __hip_atomic_fetch_add(&sm.doneB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   prev = __shfl(prev, 0, 64);
   if (prev != ME_NCONS - 1) return;
+  if (lds_ld(&sm.abort)) return;
   const int nd = d1 - m.d0;
   if (lane < 16 * nd) {
     const int g = lane >> 4, rr = lane & 15;
@@ -522,14 +572,17 @@ RAGK_API int ragk_mlp_engine_set_stamps(void* p) {
 
 // xn != nullptr: x given. Otherwise the fused post-attention tail: P [S][H] fp32 o_proj slabs, gamma, eps
 // (h += bf16(sum P); x = rmsnorm(h) * gamma, add_partials_rmsnorm's math, inside the launch).
+// err: device error word; err_host: device address of a host-mapped word (may be null); tmo: device word
+// holding the deadline in s_memrealtime ticks (0 = default).
 RAGK_API int ragk_mlp_engine(const void* xn, const float* P, int S, const void* gamma, float eps, const void* wgu,
-                             const void* wd, void* h, void* act, void* ctr, void* err, int M, int H, int I, int G,
-                             hipStream_t st) {
+                             const void* wd, void* h, void* act, void* ctr, void* err, void* err_host, const void* tmo,
+                             int M, int H, int I, int G, hipStream_t st) {
   if (!ragk_mlp_engine_ok(M, H, I, G)) return (int)hipErrorInvalidValue;
-  if (!wgu || !wd || !h || !act || !ctr || !err || (!xn && (!P || !gamma || S < 1 || H % 4))) return (int)hipErrorInvalidValue;
+  if (!wgu || !wd || !h || !act || !ctr || !err || !tmo || (!xn && (!P || !gamma || S < 1 || H % 4)))
+    return (int)hipErrorInvalidValue;
   MlpArgs a{(const bf16_t*)xn, xn ? nullptr : P, (const bf16_t*)gamma, eps, S, (const bf16_t*)wgu,
-            (const bf16_t*)wd, (bf16_t*)h, (bf16_t*)act, (unsigned long long*)ctr, (unsigned*)err, g_me_stamps, H, I,
-            g_me_w_even, g_me_w_odd};
+            (const bf16_t*)wd, (bf16_t*)h, (bf16_t*)act, (unsigned long long*)ctr, (unsigned*)err,
+            (unsigned*)err_host, (const unsigned*)tmo, g_me_stamps, H, I, g_me_w_even, g_me_w_odd};
   if (g_me_nt)
     hipLaunchKernelGGL(mlp_engine_kernel<true>, dim3(G), dim3(ME_THREADS), 0, st, a);
   else
@@ -537,5 +590,21 @@ RAGK_API int ragk_mlp_engine(const void* xn, const float* P, int S, const void* 
   return (int)hipGetLastError();
 }
 
-// bytes of the workspace words (counters + error word) the host allocates zeroed and resets on error
+// bytes of the workspace counters the host allocates zeroed and re-arms after an error (the error word and
+// the timeout word follow them: ops/native.py _me_workspace)
 RAGK_API int ragk_mlp_engine_ctr_bytes() { return (ME_SHARDS + 1) * ME_CTR_STRIDE * 8; }
+
+// Host-mapped, coherent pinned words (64 B): the kernels' error reports the engine reads after every step
+// without a device sync. Returns the host pointer (null on failure); ragk_host_word_dev gives the device one.
+RAGK_API void* ragk_host_word_alloc() {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+  memset(p, 0, 64);
+  return p;
+}
+RAGK_API void* ragk_host_word_dev(void* host) {
+  void* d = nullptr;
+  if (!host || hipHostGetDevicePointer(&d, host, 0) != hipSuccess) return nullptr;
+  return d;
+}
+RAGK_API int ragk_host_word_free(void* host) { return host ? (int)hipHostFree(host) : 0; }

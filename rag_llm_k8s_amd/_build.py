@@ -74,6 +74,29 @@ def _run(cmd):
     return r.stdout
 
 
+def check_lds_waits(objs, jobs=4):
+    """Build step: every freshly compiled kernel object passes tools/isa_lds_hazard.py (no instruction touches
+    an LDS read's registers before the lgkmcnt that retires it -- the hand-placed asm waits of gemm_w4 and
+    the attention kernels). A hazard fails the build; a tree without the tool or llvm-objdump skips it."""
+    tool = os.path.join(ROOT, "tools", "isa_lds_hazard.py")
+    if not os.path.exists(tool):
+        return
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("isa_lds_hazard", tool)
+    H = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(H)
+    if not os.path.exists(os.path.join(H.LLVM, "llvm-objdump")):
+        return
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        bad = [(o, b) for o, b in zip(objs, ex.map(H.check_object, objs)) if b]
+    if bad:
+        for o in {o for o, _ in bad}:
+            os.remove(o)  # recompiled (and re-checked) by the next build
+        raise RuntimeError("LDS-wait hazards in %s" % "; ".join(
+            "%s: %s at %#x" % (os.path.basename(o), k, h[0][0]) for o, b in bad for k, h in b[:2]))
+
+
 def build_hip(verbose=False, jobs=None):
     os.makedirs(OBJ_DIR, exist_ok=True)
     os.makedirs(LIB_DIR, exist_ok=True)
@@ -105,6 +128,8 @@ def build_hip(verbose=False, jobs=None):
             out = f.result()
             if verbose and out.strip():
                 print(out)
+    if todo:
+        check_lds_waits([o for _, o in todo], jobs)
     if todo or prev != stamp or _newer(objs, HIP_LIB):
         _run([HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", HIP_LIB])
         with open(stamp_txt, "w") as f:

@@ -659,7 +659,9 @@ class LLMEngine:
                     run()
             torch.cuda.current_stream(dev).wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # captured on the warm-up stream: stream-keyed native state (the persistent decode MLP's
+            # arrival counters, ops/native.py _me_workspace) was allocated by the warm-up runs above
+            with torch.cuda.graph(g, stream=s):
                 run()
             self._tok_out.copy_(saved)
             entry["graph"] = g
@@ -727,6 +729,7 @@ class LLMEngine:
         carry[:n] = [prev_row[id(s)] if c else -1 for s, c in zip(seqs, carried)]
         host = np.concatenate([self._decode_inputs_async(seqs, B, carried), samp, carry])
         e["packed"].copy_(self._h2d_i32(host), non_blocking=True)
+        forced = self._engine_fault_hook()
         if self._timing is not None:
             ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ea.record()
@@ -735,6 +738,8 @@ class LLMEngine:
             self._timing.append((ea, eb))
         else:
             e["graph"].replay()
+        if forced:
+            self._engine_fault_hook(release=True)
         self._out_idx ^= 1
         host_out = self._out_pins[self._out_idx]
         host_out[:n].copy_(e["out"][:n], non_blocking=True)
@@ -744,6 +749,10 @@ class LLMEngine:
             s.computed = s.length + (1 if id(s) in prev_row else 0)
         cur = dict(seqs=seqs, out=e["out"], event=ev, host_out=host_out, n=n)
         fin = self._collect(prev, in_flight=set(id(s) for s in seqs))
+        if fin is None:  # prev failed in-kernel; cur consumed its tokens on the device
+            self._recover_engine_fault([prev, cur])
+            self.stats["decode_s"] += time.perf_counter() - t0
+            return []
         self._inflight = cur
         self.stats["decode_steps"] += 1
         self._count_batch(n)
@@ -764,10 +773,9 @@ class LLMEngine:
         for sid in self._free_after:  # rows of the step before `step`: done with those blocks now
             self.bm.free(sid)
         self._free_after = []
+        if self._kernel_fault():
+            return None  # the caller discards this step (and the one in flight behind it)
         tok = step["host_out"][:step["n"]].tolist()
-        self._n_collect = getattr(self, "_n_collect", 0) + 1
-        if self._n_collect % 64 == 0:
-            self._check_kernel_errors()
         finished = []
         for s, t in zip(step["seqs"], tok):
             if s.status == FINISHED:  # stopped (or aborted) before this step's token was read
@@ -779,12 +787,56 @@ class LLMEngine:
                 finished.append(s)
         return finished
 
-    def _check_kernel_errors(self):
-        """Bounded in-kernel waits report timeouts through error words instead of hanging: surface them
-        (the persistent decode MLP's hand-off; its counters are re-armed by the check)."""
-        if torch.device(self.device).type == "cuda":
+    def _kernel_fault(self) -> int:
+        """Error code a bounded in-kernel wait reported during the steps synchronised so far (the persistent
+        decode MLP's hand-off, ops/native.py mlp_engine_fault): host-mapped words, read after the step's
+        event sync at no extra cost. 0 = healthy."""
+        if not self.is_cuda:
+            return 0
+        from ..ops import native
+        return native.mlp_engine_fault(self.device)
+
+    def _engine_fault_hook(self, release=False):
+        """RAGK_FAULTS=mlp_engine_timeout_at_step=N: the N-th decode step's persistent MLP launches get a
+        one-tick deadline (every wait gives up) -- the recovery path's test."""
+        from ..ops import native
+        if release:
+            native.mlp_engine_force_timeout(0, self.device)
+            return False
+        at = faults.value("mlp_engine_timeout_at_step")
+        if at is None or not self.is_cuda or faults.tick("mlp_engine_timeout_at_step") != int(at):
+            return False
+        native.mlp_engine_force_timeout(1, self.device)
+        return True
+
+    def _recover_engine_fault(self, steps):
+        """A persistent decode MLP launch gave up a wait: its step's rows (and those of the step in flight
+        behind it, which consumed its tokens) are garbage and are NOT accepted. Wait for the device, re-arm
+        the counters, turn the engine off for this process (its graphs are recaptured on the separate
+        kernels on demand) and rewind every affected sequence to its last accepted token, so the next decode
+        step recomputes those rows; the KV rows they wrote are rewritten by the recomputation."""
+        code = self._kernel_fault()
+        if self.is_cuda:
             from ..ops import native
-            native.mlp_engine_check(self.device)
+            torch.cuda.synchronize(self.device)
+            native.mlp_engine_rearm(self.device)
+            native.MLP_ENGINE = False
+        self.graphs.clear()
+        self._inflight = None
+        for sid in self._free_after:
+            self.bm.free(sid)
+        self._free_after = []
+        n = 0
+        for step in steps:
+            if step is None:
+                continue
+            for s in step["seqs"]:
+                if s.status != FINISHED:
+                    s.computed = s.length - 1
+                    n += 1
+        self.stats["engine_faults"] = self.stats.get("engine_faults", 0) + 1
+        log.error("persistent decode MLP: a wait gave up (code %d); %d rows of the last decode steps discarded "
+                  "and recomputed on the separate kernels (engine off for this process)", code, n)
 
     def _drain(self):
         """Complete the in-flight decode step (before a prefill, an abort, or when nothing is left)."""
@@ -793,6 +845,10 @@ class LLMEngine:
         t0 = time.perf_counter()
         step, self._inflight = self._inflight, None
         fin = self._collect(step)
+        if fin is None:
+            self._recover_engine_fault([step])
+            self.stats["decode_s"] += time.perf_counter() - t0
+            return []
         for sid in self._free_after:
             self.bm.free(sid)
         self._free_after = []
@@ -813,12 +869,19 @@ class LLMEngine:
             e["packed"].copy_(self._h2d_i32(host), non_blocking=True)
             if full_vocab:  # eager forward, exact sampler over the whole vocabulary
                 tok = self._sample_full_vocab(self.model.forward(e["inp"])[:n], seqs)
-            elif e["graph"] is not None:
-                e["graph"].replay()
-                tok = e["out"][:n].cpu().tolist()
             else:
-                e["run"]()
+                forced = self._engine_fault_hook()
+                if e["graph"] is not None:
+                    e["graph"].replay()
+                else:
+                    e["run"]()
+                if forced:
+                    self._engine_fault_hook(release=True)
                 tok = e["out"][:n].cpu().tolist()
+            if self._kernel_fault():  # synchronised by the token read-back above
+                self._recover_engine_fault([dict(seqs=seqs)])
+                self.stats["decode_s"] += time.perf_counter() - t0
+                return finished
         else:
             host = self._decode_inputs_host(seqs, n)
             mb = self.max_blocks
@@ -831,6 +894,10 @@ class LLMEngine:
                 tok = self._sample_full_vocab(logits, seqs)
             else:
                 tok = self._sample_rows(logits, *self._sampling_tensors(seqs)).tolist()
+            if self._kernel_fault():
+                self._recover_engine_fault([dict(seqs=seqs)])
+                self.stats["decode_s"] += time.perf_counter() - t0
+                return finished
         for s in seqs:
             s.computed = s.length
         for s, t in zip(seqs, tok):

@@ -43,7 +43,10 @@ _SIGS = {
     "ragk_mlp_engine_set_nt": [I],
     "ragk_mlp_engine_set_stamps": [P],
     "ragk_mlp_engine_set_xcd_weights": [I, I],
-    "ragk_mlp_engine": [P, P, I, P, F, P, P, P, P, P, P, I, I, I, I, S],
+    "ragk_mlp_engine": [P, P, I, P, F, P, P, P, P, P, P, P, P, I, I, I, I, S],
+    "ragk_host_word_alloc": [],
+    "ragk_host_word_dev": [P],
+    "ragk_host_word_free": [P],
     "ragk_mlp_engine_ctr_bytes": [],
     "ragk_mlp_engine_split": [I, I, I, I, P],
     "ragk_gemm_part_ksteps": [I, I, I],
@@ -98,7 +101,8 @@ _SIGS = {
     "ragk_ar_set_fences": [P, I],
     "ragk_ar_get_fences": [P],
 }
-_RESTYPES = {"ragk_ar_create": ctypes.c_void_p, "ragk_ar_error_host_ptr": ctypes.c_void_p, "ragk_ar_max_bytes": ctypes.c_long, "ragk_ar_destroy": None}
+_RESTYPES = {"ragk_host_word_alloc": ctypes.c_void_p, "ragk_host_word_dev": ctypes.c_void_p,
+             "ragk_ar_create": ctypes.c_void_p, "ragk_ar_error_host_ptr": ctypes.c_void_p, "ragk_ar_max_bytes": ctypes.c_long, "ragk_ar_destroy": None}
 
 _lib = None
 _lock = threading.Lock()

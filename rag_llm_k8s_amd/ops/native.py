@@ -461,19 +461,62 @@ MLP_ENGINE = os.environ.get("RAGK_MLP_ENGINE", "1") != "0"
 _me_ws = {}
 
 
+class _MeWorkspace:
+    """One launch stream's engine state: act [I] bf16 (the hand-off), the monotonic arrival counters, the
+    device error word (a set word makes later launches exit at entry), the deadline word (test hook) and a
+    host-mapped pinned error word the engine reads after every step without a device sync."""
+
+    def __init__(self, dev, I):
+        L = _lib.lib()
+        self.nb = int(L.ragk_mlp_engine_ctr_bytes())
+        # int64 words: counters | error (u32 at byte nb) | deadline ticks (u32 at byte nb + 8)
+        self.words = torch.zeros(self.nb // 8 + 2, dtype=torch.int64, device=dev)
+        self.act = torch.zeros(I, dtype=torch.bfloat16, device=dev)
+        self.host = L.ragk_host_word_alloc()
+        _req(bool(self.host), "mlp_engine: hipHostMalloc of the host error word failed")
+        self.host_dev = L.ragk_host_word_dev(self.host)
+        _req(bool(self.host_dev), "mlp_engine: no device address for the host error word")
+        import ctypes
+
+        self._host_word = ctypes.c_uint.from_address(self.host)
+
+    @property
+    def err_ptr(self):
+        return self.words.data_ptr() + self.nb
+
+    @property
+    def tmo_ptr(self):
+        return self.words.data_ptr() + self.nb + 8
+
+    def fault(self) -> int:
+        return int(self._host_word.value)
+
+    def rearm(self):
+        """Zero the counters and both error words (the device must be idle: no launch of this workspace in
+        flight)."""
+        self.words[: self.nb // 8 + 1].zero_()
+        self._host_word.value = 0
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            if self.host:
+                _lib.lib().ragk_host_word_free(self.host)
+                self.host = None
+        except Exception:
+            pass
+
+
 def _me_workspace(dev, I):
-    """(act [I] bf16, counters + error word) per device; the counters are monotonic across launches and
-    zeroed only here and after a timeout (mlp_engine_check)."""
-    key = (str(dev), I)
+    """The workspace of the launching stream: two streams (two engines, or two captured graphs of one
+    process) never share arrival counters. Allocated by an eager launch, never inside a hipGraph capture
+    (a graph-pool allocation, with its zero-fill captured, would be handed to later eager launches after
+    the graph is gone): warm up on the stream the graph is then captured on."""
+    key = (str(dev), stream_ptr(), I)
     ws = _me_ws.get(key)
     if ws is None:
-        # allocated by an eager call, never inside a hipGraph capture: a graph-pool allocation (with its
-        # zero-fill captured) would be handed to later eager launches after the graph is gone
-        _req(not torch.cuda.is_current_stream_capturing(), "mlp_engine workspace: run one eager step before capture")
-        nb = int(_lib.lib().ragk_mlp_engine_ctr_bytes())
-        words = torch.zeros(nb // 8 + 2, dtype=torch.int64, device=dev)
-        ws = (torch.zeros(I, dtype=torch.bfloat16, device=dev), words, nb)
-        _me_ws[key] = ws
+        _req(not torch.cuda.is_current_stream_capturing(),
+             "mlp_engine workspace: run one eager step on the capture stream before capture")
+        ws = _me_ws[key] = _MeWorkspace(dev, I)
     return ws
 
 
@@ -510,24 +553,53 @@ def _mlp_engine_launch(xn_ptr, P_ptr, S, g_ptr, eps, w_gu, w_down, h):
     H, I = w_down.shape
     _req(h.shape == (1, H) and h.is_contiguous(), "h [1, H]")
     _req(mlp_engine_ok(1, w_gu, w_down), "mlp_engine shape")
-    act, words, nb = _me_workspace(h.device, I)
-    err = words.data_ptr() + nb
+    ws = _me_workspace(h.device, I)
     check(_lib.lib().ragk_mlp_engine(xn_ptr, P_ptr, S, g_ptr, eps, w_gu.data_ptr(), w_down.data_ptr(), h.data_ptr(),
-                                     act.data_ptr(), words.data_ptr(), err, 1, H, I, _cu_count(), stream_ptr()),
+                                     ws.act.data_ptr(), ws.words.data_ptr(), ws.err_ptr, ws.host_dev, ws.tmo_ptr, 1,
+                                     H, I, _cu_count(), stream_ptr()),
           "ragk_mlp_engine")
     return h
 
 
-def mlp_engine_check(dev=None):
-    """Raise if a persistent MLP launch on `dev` timed out in a wait (then re-arm its counters). Syncs."""
-    for key, (_, words, nb) in list(_me_ws.items()):
-        d = torch.device(dev) if dev is not None else None
+def mlp_engine_fault(dev=None) -> int:
+    """Error code of a persistent MLP launch on `dev` that gave up a wait (0 = healthy). Reads the
+    host-mapped words only: no device sync, so the engine checks it after every step's event sync."""
+    d = torch.device(dev) if dev is not None else None
+    for key, ws in list(_me_ws.items()):
         if d is not None and d.index is not None and torch.device(key[0]) != d:
             continue
-        e = int(words[nb // 8].item())
+        e = ws.fault()
         if e:
-            words.zero_()
-            raise RuntimeError("persistent decode MLP: wait timed out (code %d); counters reset" % e)
+            return e
+    return 0
+
+
+def mlp_engine_rearm(dev=None):
+    """Re-arm every workspace on `dev` after a fault (call with the device idle)."""
+    d = torch.device(dev) if dev is not None else None
+    for key, ws in list(_me_ws.items()):
+        if d is None or d.index is None or torch.device(key[0]) == d:
+            ws.rearm()
+
+
+def mlp_engine_check(dev=None):
+    """Raise if a persistent MLP launch on `dev` timed out in a wait (then re-arm its counters). Syncs."""
+    if not _me_ws:
+        return
+    torch.cuda.synchronize(dev)
+    e = mlp_engine_fault(dev)
+    if e:
+        mlp_engine_rearm(dev)
+        raise RuntimeError("persistent decode MLP: wait timed out (code %d); counters reset" % e)
+
+
+def mlp_engine_force_timeout(ticks, dev=None):
+    """Test hook: deadline of the following launches in s_memrealtime ticks (0 = the kernel's default). A
+    device-side word written on the current stream, so launches captured in a hipGraph see it too."""
+    d = torch.device(dev) if dev is not None else None
+    for key, ws in list(_me_ws.items()):
+        if d is None or d.index is None or torch.device(key[0]) == d:
+            ws.words[ws.nb // 8 + 1].fill_(int(ticks))
 
 
 def set_mlp_engine_nt(nt):

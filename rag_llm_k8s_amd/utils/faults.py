@@ -15,6 +15,8 @@ real server) can switch on without code changes:
   comm_hang_s=X          a TP follower stalls X s before stepping (collective watchdog)
   bench_tp_hang_s=X      bench.py's TP=N C=1 phase stalls X s (its watchdog must exit non-zero)
   comm_skew_ms=X         every TP collective starts late on each rank by 0..X ms (per call and rank)
+  mlp_engine_timeout_at_step=N  the N-th decode step's persistent MLP launches get a one-tick deadline
+                         (every in-kernel wait gives up: the engine must discard and recompute the step)
 
 `set_faults()` overrides the environment in-process (tests).
 """

@@ -181,6 +181,37 @@ def test_batch1_decode_mlp_engine_path_matches_plain_decode(tiny):
     assert outs[0] == outs[1]
 
 
+def test_engine_fault_step_discarded_and_recomputed(tiny):
+    """An in-kernel wait that gave up (the persistent decode MLP's error word, engine._kernel_fault) makes the
+    engine discard that decode step instead of accepting its tokens, rewind the sequences to their last
+    accepted token and recompute the step; the loop keeps going (nothing raises) and the generated tokens
+    equal an unfaulted run's, for sampled and greedy requests in one batch. The GPU form (a forced one-tick
+    deadline inside the real kernel, async decode + hipGraphs) is tests/test_mlp_engine_gpu.py."""
+    cfg, hf, sd = tiny
+    w = LlamaWeights.from_state_dict(cfg, sd, "cpu")
+    torch.manual_seed(11)
+    prompts = [torch.randint(3, cfg.vocab_size, (n,)).tolist() for n in (17, 29)]
+    params = SamplingParams(max_new_tokens=9, temperature=0.8, top_p=0.9, top_k=20, ignore_eos=True)
+    outs = []
+    for fault_at in (None, 3, 1):
+        model = LlamaModel(cfg, w, "cpu", max_positions=512)
+        eng = LLMEngine(model, num_blocks=32, max_batch=4, max_model_len=512, use_graphs=False)
+        if fault_at is not None:
+            seen = []
+
+            def fault(eng=eng, seen=seen, at=fault_at):
+                if eng.stats["decode_steps"] + 1 == at and not seen:
+                    seen.append(1)
+                    return 2
+                return 0
+
+            eng._kernel_fault = fault
+        outs.append(eng.generate(prompts, params, seeds=[5, 6]))
+        assert all(len(o) == 9 for o in outs[-1])
+        assert eng.stats.get("engine_faults", 0) == (0 if fault_at is None else 1)
+    assert outs[1] == outs[0] and outs[2] == outs[0]
+
+
 def test_mixed_prefill_decode_steps_match_separate_steps(tiny):
     """Mixed steps (decoding sequences ride along in a prefill step as 1-token chunks) produce the same
     tokens as separate prefill / decode steps, for requests that arrive while others decode; a mixed

@@ -89,7 +89,7 @@ def test_mlp_engine_repeated_and_graph(native):
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, stream=s):  # the warm-up stream: its engine workspace exists
         run(hg)
     for _ in range(5):
         hg.copy_(h0)
@@ -160,3 +160,57 @@ def test_mlp_engine_shape_gate(native):
     assert not native.mlp_engine_ok(2, wgu, down)  # batch 1 only
     _, _, wgu70, down70 = _weights(8192, 1024, 4)   # H = 8192: x does not fit next to the ring
     assert native.mlp_engine_ok(1, wgu70, down70) == (2 * 8192 <= 28672)
+
+
+def _engine_run(native, model, cfg, prompt, fault_at=None, switch_at=None):
+    """Greedy batch-1 generation through the engine (hipGraph + async decode). fault_at: the persistent MLP
+    launches of that decode step get a one-tick deadline (every wait gives up). switch_at: the engine is
+    turned off (as the recovery does) before that decode step, without any fault."""
+    from rag_llm_k8s_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from rag_llm_k8s_amd.utils import faults
+
+    native.MLP_ENGINE = True
+    faults.set_faults("mlp_engine_timeout_at_step=%d" % fault_at if fault_at else "")
+    try:
+        eng = LLMEngine(model, num_blocks=64, max_batch=1, max_prefill_tokens=4096, max_model_len=1024,
+                        eos_ids=cfg.eos_token_id, graph_buckets=[1])
+        eng.warmup_graphs([1])
+        s = eng.add_request(prompt, SamplingParams(max_new_tokens=16, do_sample=False, ignore_eos=True), seed=1)
+        while eng.has_work():
+            if switch_at is not None and native.MLP_ENGINE and eng.stats["decode_steps"] == switch_at - 1:
+                torch.cuda.synchronize()
+                native.MLP_ENGINE = False
+                eng.graphs.clear()
+            eng.step()
+        torch.cuda.synchronize()
+        return list(s.out), dict(eng.stats)
+    finally:
+        faults.set_faults(None)
+
+
+def test_engine_fault_is_discarded_and_recomputed(native):
+    """A persistent MLP launch whose waits give up (forced one-tick deadline at decode step 5, inside the
+    captured graph) writes no h rows, the launches behind it in the same step exit at entry, and the engine
+    sees the host-mapped error word at that step's collection: the step and the one in flight behind it are
+    discarded, the counters re-armed, the engine turned off and the rows recomputed on the separate kernels.
+    No token of a failed step is accepted (the output equals a run that switched to the separate kernels at
+    the same step without a fault), the loop finishes every request, nothing raises."""
+    from rag_llm_k8s_amd.models import llama as L
+
+    cfg = L.llama_tiny(vocab=512, layers=2, hidden=1024, heads=8, kv_heads=2, inter=2048)
+    w = L.LlamaWeights.random(cfg, DEV, seed=3)
+    model = L.LlamaModel(cfg, w, DEV, max_positions=2048)
+    assert native.mlp_engine_ok(1, w.layers[0]["wgu"], w.layers[0]["wdown"])
+    prompt = torch.randint(3, cfg.vocab_size, (40,), generator=torch.Generator().manual_seed(4)).tolist()
+    n_ws = len(native._me_ws)
+    ref, st_ref = _engine_run(native, model, cfg, prompt, switch_at=5)
+    assert st_ref.get("engine_faults", 0) == 0 and len(ref) == 16
+    assert len(native._me_ws) > n_ws  # the engine ran (a workspace for this engine's capture stream)
+    got, st = _engine_run(native, model, cfg, prompt, fault_at=5)
+    assert st.get("engine_faults", 0) == 1
+    assert native.mlp_engine_fault() == 0  # re-armed
+    assert got == ref
+    # and the engine itself is healthy again after a re-arm: a clean run reproduces an all-engine run
+    on1, st1 = _engine_run(native, model, cfg, prompt)
+    on2, st2 = _engine_run(native, model, cfg, prompt)
+    assert on1 == on2 and st1.get("engine_faults", 0) == 0 and len(on1) == 16

@@ -90,6 +90,12 @@ def test_isa_lds_hazard_model():
     loop = [(0, "v_mfma_f32_16x16x32_bf16 a[0:3], v[0:3], v[0:3], a[0:3]"), (8, "ds_read_b128 v[0:3], v9"),
             (16, "s_cbranch_scc1 -3 <k+0x0>")]
     assert [h[0] for h in H.check_kernel(0, loop)] == [0]
+    # forward branch: the taken path reaches its target with the read pending, the fall-through waits first
+    fwd = [(0, "ds_read_b128 v[0:3], v9"), (8, "s_cbranch_scc1 2 <k+0x18>"), (16, "s_waitcnt lgkmcnt(0)"),
+           (24, "v_add_f32 v4, v0, v5")]
+    assert [h[0] for h in H.check_kernel(0, fwd)] == [24]
+    fwd_ok = fwd[:1] + [(4, "s_waitcnt lgkmcnt(0)")] + fwd[1:]
+    assert H.check_kernel(0, fwd_ok) == []
     waited = [(0, "s_waitcnt lgkmcnt(0)")] + [(a + 8, i) for a, i in loop]
     assert H.check_kernel(0, waited) == []
 

@@ -149,11 +149,7 @@ def _init(rank, port, world=WORLD):
 
 def _tp_worker(rank, port, d, world):
     WORLD = world
-    if world >= 8:
-        # 8 processes on one GPU: one hardware queue each, so every rank's queue is mapped at once (a
-        # collective spinning on a mapped queue while a peer's queue waits unmapped never completes)
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")
-    ctx = _init(rank, port, world)
+    ctx = _init(rank, port, world)  # 8 ranks: 2 hardware queues per process (see _init)
     _log(rank, world, "process group up")
     from rag_llm_k8s_amd.engine.llm_engine import LLMEngine, SamplingParams
     from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights

@@ -67,6 +67,10 @@ def main():
         while any(s.computed < len(s.prompt) for s in eng.running) or eng.waiting:
             eng.step()
         torch.cuda.synchronize()
+        # DA_SLEEP=s: idle this long between the prefill and the decode steps (does the decode rate depend on
+        # how recently the GPU ran the MFMA-bound prefill? power / clock state)
+        if float(os.environ.get("DA_SLEEP", "0")) > 0:
+            time.sleep(float(os.environ["DA_SLEEP"]))
         d0, n0 = eng.stats["decode_s"], eng.stats["decode_steps"]
         t0 = time.perf_counter()
         eng.run_until_done()
@@ -76,9 +80,14 @@ def main():
         print("B=%d ctx=%d: %d decode steps, %.3f ms/step (engine decode_s %.3f ms/step), %.0f tok/s" % (
             B, plen, n, dt / n * 1e3, (eng.stats["decode_s"] - d0) / n * 1e3, B * n / dt), flush=True)
         if eng._timing:  # RAGK_DECODE_TIMING=1: GPU time of each captured step, in situ
-            ts = sorted(a.elapsed_time(b) for a, b in eng._timing[-n:])
+            seq = [a.elapsed_time(b) for a, b in eng._timing[-n:]]
+            ts = sorted(seq)
             print("B=%d in-situ graph time: median %.3f ms, min %.3f, max %.3f" % (
                 B, ts[len(ts) // 2], ts[0], ts[-1]), flush=True)
+            w = max(1, len(seq) // 8)  # in order: does the step time drift after the prefill?
+            print("B=%d in-situ graph time by window of %d steps: %s" % (B, w, " ".join(
+                "%.3f" % (sum(seq[i:i + w]) / len(seq[i:i + w])) for i in range(0, len(seq), w))), flush=True)
+            eng._timing.clear()
         # pure GPU time of the captured decode step: back-to-back replays of the B-bucket graph
         # (stale inputs are fine: same shapes and context lengths), no host work in between
         e = eng.graphs.get(B)

@@ -10,9 +10,9 @@ the bias / GELU epilogue instantiations of gemm_w4), the copy takes stale bytes.
 Model: LDS operations complete in order (ds_* only; scalar loads also count in lgkmcnt, which makes
 `lgkmcnt(N)` retire at least the reads this model retires, so the check stays conservative).
 `lgkmcnt(N)` leaves the N youngest ds operations pending. Any other instruction that names a pending
-read's register (source or destination) is a hazard. The scan walks each kernel in address order
-(nothing pending after an unconditional branch) and again from every backward-branch target with the
-state at the branch (the loop back edge).
+read's register (source or destination) is a hazard. The pending state flows over the kernel's control-flow
+graph (fall-through, forward and backward branch targets; a join takes the union of its predecessors'
+pending reads) to a fixed point, so a hazard on a taken forward branch or around a loop back edge is seen.
 
   python tools/isa_lds_hazard.py build/obj/gemm_w4.hip.o [kernel-substring]
 """
@@ -73,63 +73,73 @@ def kernels(text):
     return out
 
 
-def scan(insns, start, state, stop=None):
-    """Walk from index `start` with pending list `state`; returns (hazards, {index: state} at backward
-    branches)."""
-    pending = list(state)
-    hazards, back = [], {}
-    addr_index = {a: i for i, (a, _) in enumerate(insns)}
-    for i in range(start, len(insns)):
-        if stop is not None and i == stop:
-            break
-        addr, ins = insns[i]
-        op = ins.split()[0] if ins else ""
-        if op == "s_waitcnt":
-            m = LGKM.search(ins)
-            if m:
-                n = int(m.group(1))
-                pending = pending[len(pending) - n:] if n < len(pending) else pending
-                if n == 0:
-                    pending = []
-            continue
-        touched = regs(ins)
-        live = set().union(*pending) if pending else set()
-        if op.startswith("ds_"):
-            operands = ins[len(op):]
-            dst = regs(operands.split(",")[0]) if op.startswith("ds_read") else set()
-            srcs = touched - dst if op.startswith("ds_read") else touched
-            if srcs & live:  # a pending destination may be re-read into (LDS returns in order)
-                hazards.append((addr, ins, sorted(srcs & live)))
-            pending.append(frozenset(dst))
-            continue
-        if touched & live:
-            hazards.append((addr, ins, sorted(touched & live)))
-        if op.startswith("s_cbranch") or op == "s_branch":
-            t = TARGET.search(ins)
-            if t:
-                tgt = t.group(2)
-                back[i] = (tgt, list(pending))
-            if op == "s_branch":  # the next instruction is reached from elsewhere: state unknown
-                pending = []
-        elif op in ("s_endpgm", "s_setpc_b64"):
-            pending = []
-    return hazards, back, addr_index
+MAX_PENDING = 16  # the lgkm counter saturates: the wave stalls rather than keep more LDS operations in flight
+
+
+def merge(a, b):
+    """Join of two pending lists (oldest first) at a control-flow merge: aligned from the youngest entry, each
+    position holds the union of both paths' registers (conservative for any later lgkmcnt(N))."""
+    if a is None:
+        return b
+    n = max(len(a), len(b))
+    a = (frozenset(),) * (n - len(a)) + a
+    b = (frozenset(),) * (n - len(b)) + b
+    return tuple(x | y for x, y in zip(a, b))
+
+
+def step(ins, pending):
+    """Transfer one instruction: (new pending tuple, registers it touched while pending, or empty)."""
+    op = ins.split()[0] if ins else ""
+    if op == "s_waitcnt":
+        m = LGKM.search(ins)
+        if m:
+            n = int(m.group(1))
+            pending = pending[len(pending) - n:] if 0 < n < len(pending) else (() if n == 0 else pending)
+        return pending, set()
+    touched = regs(ins)
+    live = set().union(*pending) if pending else set()
+    if op.startswith("ds_"):
+        dst = regs(ins[len(op):].split(",")[0]) if op.startswith("ds_read") else set()
+        srcs = touched - dst if op.startswith("ds_read") else touched
+        return (pending + (frozenset(dst),))[-MAX_PENDING:], srcs & live  # a pending dst may be re-read into
+    return pending, touched & live
+
+
+def successors(i, ins, base, addr_index, n):
+    op = ins.split()[0] if ins else ""
+    out = []
+    if op.startswith("s_cbranch") or op == "s_branch":
+        t = TARGET.search(ins)
+        if t:
+            j = addr_index.get(base + int(t.group(2), 16))
+            if j is not None:
+                out.append(j)
+    if op not in ("s_branch", "s_endpgm", "s_setpc_b64") and i + 1 < n:
+        out.append(i + 1)
+    return out
 
 
 def check_kernel(base, insns):
-    hazards, back, addr_index = scan(insns, 0, [])
-    for i, (off, st) in back.items():
-        tgt = base + int(off, 16)
-        j = addr_index.get(tgt)
-        if j is not None and j <= i and st:
-            h2, _, _ = scan(insns, j, st, stop=i + 1)
-            hazards += h2
-    seen, out = set(), []
-    for h in hazards:
-        if h[0] not in seen:
-            seen.add(h[0])
-            out.append(h)
-    return out
+    """Hazards of one kernel: a worklist dataflow over the control-flow graph (fall-through, forward and
+    backward branch targets), the pending list at a join being the merge of its predecessors'."""
+    n = len(insns)
+    if not n:
+        return []
+    addr_index = {a - 0: i for i, (a, _) in enumerate(insns)}
+    state = [None] * n
+    state[0] = ()
+    work, hz = [0], {}
+    while work:
+        i = work.pop()
+        out, bad = step(insns[i][1], state[i])
+        if bad:
+            hz[insns[i][0]] = (insns[i][0], insns[i][1], sorted(bad))
+        for j in successors(i, insns[i][1], base, addr_index, n):
+            m = merge(state[j], out)
+            if m != state[j]:
+                state[j] = m
+                work.append(j)
+    return [hz[a] for a in sorted(hz)]
 
 
 def check_object(obj, name_filter=""):

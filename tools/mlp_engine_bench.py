@@ -59,7 +59,7 @@ def main():
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr):
+        with torch.cuda.graph(gr, stream=s):  # the warm-up stream (stream-keyed engine workspace)
             fn()
         return gr
 
