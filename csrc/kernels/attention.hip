@@ -962,7 +962,9 @@ constexpr int decode_lds_bytes() { return NW * Cfg<D>::TILEB + G * D * 2; }
 // CU keeps the same KV bytes in flight as two 4-wave blocks and needs no merge launch). A multi-partition
 // sequence writes its partition records; attn_decode_reduce_kernel (or, deferred, the o_proj GEMM's
 // gemm_part_merge) merges them.
-template <int D, int G, bool NT = false, int NW = 4>
+// DG = 1 (diagnostic build, tools/attn_decode_probe.py): the same K / V loads and waits, no QK^T / softmax / PV
+// -- how much of the kernel's time the KV access pattern alone takes.
+template <int D, int G, bool NT = false, int NW = 4, int DG = 0>
 __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part, int kvh, int b, char* smem) {
   constexpr int NTH = NW * 64;
   using C = Cfg<D>;
@@ -1058,6 +1060,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
 #pragma unroll
   for (int dt = 0; dt < C::DT; ++dt) o[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float m_i = -INFINITY, l_i = 0.f;
+  unsigned dsink = 0;
 
   for (int kt = kt0 + wid_u; kt < kt1; kt += NW) {
     bf16x8 kf[4][C::KS];
@@ -1081,6 +1084,15 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
           kf[t][s] = NT ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D +
                                                                                     32 * s + 8 * fh))
                         : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
+    }
+    if constexpr (DG == 1) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int s = 0; s < C::KS; ++s) dsink ^= __builtin_bit_cast(u32x4, kf[t][s])[0];
+      wait_vmcnt0();
+      dsink ^= *reinterpret_cast<const unsigned*>(sV + 4 * lane);
+      continue;
     }
     f32x4 s4[4];
 #pragma unroll
@@ -1130,6 +1142,10 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     }
   }
 
+  if constexpr (DG == 1) {
+    if (dsink == 0x9e3779b9u) a.out[(size_t)b * a.out_stride + lane] = 0;  // keeps the loads alive
+    return;
+  }
   // ---- combine the 4 waves in LDS ----
   __syncthreads();
   float* sm = reinterpret_cast<float*>(smem);    // [4][16] max
@@ -1170,10 +1186,10 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
   }
 }
 
-template <int D, int G, bool NT = false, int NW = 4>
+template <int D, int G, bool NT = false, int NW = 4, int DG = 0>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attn_decode_kernel(DecodeArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[decode_lds_bytes<D, G, NW>()];
-  attn_decode_block<D, G, NT, NW>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+  attn_decode_block<D, G, NT, NW, DG>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 // merge split-K partitions: grid (Hq, B), block D threads. The partition statistics are loaded by
@@ -1314,6 +1330,12 @@ RAGK_API int ragk_attn_prefill(const void* q, int q_stride, const void* k, const
 static int g_decode_nt = 0;
 // 8-wave single-partition decode attention once batch x KV heads reaches this (0 = never)
 static int g_decode_nw8_min = 0;
+// diagnostic instantiation of the 8-wave kernel (DG above; A/B tooling only, 0 = off)
+static int g_decode_diag = 0;
+RAGK_API int ragk_attn_decode_set_diag(int dg) {
+  g_decode_diag = dg == 1 ? 1 : 0;
+  return 0;
+}
 RAGK_API int ragk_attn_decode_set_nw8(int min_pairs) {
   g_decode_nw8_min = min_pairs > 0 ? min_pairs : 0;
   return 0;
@@ -1370,7 +1392,9 @@ static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, hipStre
   dim3 grid(max_parts, Hkv, B);
   if (D == 128 && G == 4 && max_parts == 1 && g_decode_nw8_min > 0 && B * Hkv >= g_decode_nw8_min) {
     // one partition per sequence over >= 1 block per CU: 8-wave blocks, no merge launch
-    if (g_decode_nt)
+    if (g_decode_diag)
+      hipLaunchKernelGGL((attn_decode_kernel<128, 4, true, 8, 1>), grid, dim3(512), 0, st, a);
+    else if (g_decode_nt)
       hipLaunchKernelGGL((attn_decode_kernel<128, 4, true, 8>), grid, dim3(512), 0, st, a);
     else
       hipLaunchKernelGGL((attn_decode_kernel<128, 4, false, 8>), grid, dim3(512), 0, st, a);

@@ -4,6 +4,9 @@ decode) and, under `rocprofv3 --kernel-trace --stats`, the per-kernel split.
 
   python tools/decode_anatomy.py 1 32          # batch sizes
   DA_PROMPT=5200 DA_STEPS=64 ...
+
+"graph replay only" replays the step's graph back to back from the engine's metadata at mid-run (DA_MID,
+default DA_STEPS / 2), so every row is live.
 """
 import os
 import sys
@@ -12,6 +15,61 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def replay_probe(eng, B, mid):
+    """Back-to-back replays of the B-bucket graph from the engine's current (mid-run) metadata: the GPU time
+    of one decode step with no host work in between; DA_REPLAY_MODES=h2d,d2h,both,adv,sync,pipe,pipe_copy add
+    the engine's per-step copies / waits around the replays."""
+    e = eng.graphs.get(B)
+    if e is None or e["graph"] is None:
+        return
+    pk = e["packed"]
+    live = int((pk[3 * B:4 * B] > 1).sum())
+    e["graph"].replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(20):
+        e["graph"].replay()
+    torch.cuda.synchronize()
+    print("B=%d graph replay only (after %d steps, %d live rows): %.3f ms/step" % (
+        B, mid, live, (time.perf_counter() - t0) / 20 * 1e3), flush=True)
+    pin = torch.empty(pk.numel(), dtype=torch.int32, pin_memory=True)
+    pin.copy_(pk.cpu())
+    tok_host = torch.empty(e["out"].numel(), dtype=torch.int32, pin_memory=True)
+    # adv: every replay advances each row by one token (positions, KV-append slots, kv_lens), as the
+    # engine's steps do; sync: the host waits for every replay before launching the next
+    base = pin.clone()
+    prev_ev = None
+    for mode in [m for m in os.environ.get("DA_REPLAY_MODES", "").split(",") if m]:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for it in range(20):
+            if mode in ("h2d", "both", "pipe_copy"):
+                pk.copy_(pin.to(pk.device, non_blocking=True), non_blocking=True)
+            if mode == "adv":
+                stg = torch.empty_like(pin).pin_memory()
+                stg.copy_(base)
+                stg[B:4 * B] += it + 1  # pos, slots, kv_lens (the rows stay inside their last block)
+                pk.copy_(stg.to(pk.device, non_blocking=True), non_blocking=True)
+            e["graph"].replay()
+            if mode in ("d2h", "both"):
+                tok_host.copy_(e["out"], non_blocking=True)
+                torch.cuda.Event().record()
+            if mode == "sync":
+                torch.cuda.current_stream().synchronize()
+            if mode in ("pipe", "pipe_copy"):  # the engine's pipeline: wait for the PREVIOUS replay
+                if mode == "pipe_copy":
+                    tok_host.copy_(e["out"], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                if it:
+                    prev_ev.synchronize()
+                prev_ev = ev
+        torch.cuda.synchronize()
+        print("B=%d graph replay + %s: %.3f ms/step" % (B, mode, (time.perf_counter() - t0) / 20 * 1e3), flush=True)
+    pk.copy_(base.to(pk.device))  # the engine continues from its own metadata
+    torch.cuda.synchronize()
 
 
 def main():
@@ -72,6 +130,15 @@ def main():
         if float(os.environ.get("DA_SLEEP", "0")) > 0:
             time.sleep(float(os.environ["DA_SLEEP"]))
         d0, n0 = eng.stats["decode_s"], eng.stats["decode_steps"]
+        # the graph is replayed from a MID-RUN state: at the end of a run the packed metadata is the last step's,
+        # whose batch has shrunk (sequences prefilled in earlier chunks rode along in the mixed prefill steps
+        # and finish first), so an end-of-run replay streams only those rows' KV (a round-6 finding: the
+        # "graph replay only" number of earlier rounds was a 7-row step at B = 32)
+        mid = int(os.environ.get("DA_MID", str(max(1, steps // 2))))
+        for _ in range(mid):
+            eng.step()
+        torch.cuda.synchronize()
+        replay_probe(eng, B, mid)
         t0 = time.perf_counter()
         eng.run_until_done()
         torch.cuda.synchronize()
@@ -88,17 +155,6 @@ def main():
             print("B=%d in-situ graph time by window of %d steps: %s" % (B, w, " ".join(
                 "%.3f" % (sum(seq[i:i + w]) / len(seq[i:i + w])) for i in range(0, len(seq), w))), flush=True)
             eng._timing.clear()
-        # pure GPU time of the captured decode step: back-to-back replays of the B-bucket graph
-        # (stale inputs are fine: same shapes and context lengths), no host work in between
-        e = eng.graphs.get(B)
-        if e is not None and e["graph"] is not None:
-            e["graph"].replay()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(20):
-                e["graph"].replay()
-            torch.cuda.synchronize()
-            print("B=%d graph replay only: %.3f ms/step" % (B, (time.perf_counter() - t0) / 20 * 1e3), flush=True)
         del eng
         torch.cuda.empty_cache()
 

@@ -62,14 +62,32 @@ def main():
         dt = time.perf_counter() - t0
         n = eng.stats["decode_steps"] - n0
         print("B=%d ctx=%d: %d decode steps, %.3f ms/step wall" % (B, plen, n, dt / n * 1e3), flush=True)
+        del eng
+        torch.cuda.empty_cache()
+        # graph replay from a MID-RUN state (every row live; an end-of-run replay would stream only the rows
+        # of the shrunken last batch): a fresh engine, half the decode steps, then back-to-back replays
+        eng = LLMEngine(m, num_blocks=B * 128 + 16, max_batch=B, max_prefill_tokens=32768, max_model_len=8192,
+                        eos_ids=cfg.eos_token_id, graph_buckets=[B])
+        eng.warmup_graphs([B])
+        gen = torch.Generator().manual_seed(B)
+        for i in range(B):
+            eng.add_request(torch.randint(3, cfg.vocab_size, (plen,), generator=gen).tolist(), p, seed=i)
+        while any(s.computed < len(s.prompt) for s in eng.running) or eng.waiting:
+            eng.step()
+        for _ in range(max(1, steps // 2)):
+            eng.step()
+        torch.cuda.synchronize()
         e = eng.graphs.get(B)
+        live = int((e["packed"][3 * B:4 * B] > 1).sum())
         e["graph"].replay()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(20):
             e["graph"].replay()
         torch.cuda.synchronize()
-        print("B=%d graph replay only: %.3f ms/step" % (B, (time.perf_counter() - t0) / 20 * 1e3), flush=True)
+        print("B=%d graph replay only (mid-run, %d live rows): %.3f ms/step" % (
+            B, live, (time.perf_counter() - t0) / 20 * 1e3), flush=True)
+        eng.run_until_done()
         del eng
         torch.cuda.empty_cache()
     T = int(os.environ.get("TPP_PREFILL", "0"))
