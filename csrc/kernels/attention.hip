@@ -953,9 +953,10 @@ __device__ __forceinline__ int decode_part_tiles(int n_kt, const DecodeArgs& a) 
   return max(a.part_tiles, (n_kt + a.max_parts - 1) / a.max_parts);
 }
 
-// LDS of one decode-attention block: one V tile per wave, then the block's rotated q (G x D bf16).
-template <int D, int G, int NW = 4>
-constexpr int decode_lds_bytes() { return NW * Cfg<D>::TILEB + G * D * 2; }
+// LDS of one decode-attention block: one V tile per wave (KL: and one K tile per wave after them), then the
+// block's rotated q (G x D bf16).
+template <int D, int G, int NW = 4, bool KL = false>
+constexpr int decode_lds_bytes() { return NW * Cfg<D>::TILEB * (KL ? 2 : 1) + G * D * 2; }
 
 // One split-K partition block of decode attention: partition `part` of KV head `kvh` of sequence `b`.
 // NW: waves per block (4; 8 for the batch-32 grid with one partition per sequence: one 8-wave block per
@@ -963,8 +964,12 @@ constexpr int decode_lds_bytes() { return NW * Cfg<D>::TILEB + G * D * 2; }
 // sequence writes its partition records; attn_decode_reduce_kernel (or, deferred, the o_proj GEMM's
 // gemm_part_merge) merges them.
 // DG = 1 (diagnostic build, tools/attn_decode_probe.py): the same K / V loads and waits, no QK^T / softmax / PV
-// -- how much of the kernel's time the KV access pattern alone takes.
-template <int D, int G, bool NT = false, int NW = 4, int DG = 0>
+// -- how much of the kernel's time the KV access pattern alone takes. DG = 2: as 1, but K also arrives by
+// LDS-DMA (1 KiB per instruction, into the V buffer: results meaningless) instead of 64-B row pieces.
+// KL: K tiles arrive by LDS-DMA too (whole 1 KiB pieces instead of 64-B row pieces per lane: the pure access
+// pattern streams 4-5 % faster, tools/attn_decode_probe.py) and the QK^T fragments are read from LDS; a
+// wave then holds 32 KB of LDS, so the single-partition grid uses 4-wave blocks (one per CU).
+template <int D, int G, bool NT = false, int NW = 4, int DG = 0, bool KL = false>
 __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part, int kvh, int b, char* smem) {
   constexpr int NTH = NW * 64;
   using C = Cfg<D>;
@@ -987,27 +992,30 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
   // of following them -- at batch 1 a wave handles a single tile and the two latencies were in series.
   // Not for the sequence's last tile: the new token's k / v is appended into it during the prologue.
   char* sV = smem + wid * C::TILEB;
+  char* sK = smem + (NW + wid) * C::TILEB;  // KL only
   const bool pre = a.qkv_p != nullptr && kt0 + wid_u < kt1 && kt0 + wid_u != n_kt - 1;  // wave-uniform
   bf16x8 kf0[4][C::KS];
   if (pre) {
     const size_t base = ((size_t)bt[kt0 + wid_u] * a.Hkv + kvh) * KT * D;
     const bf16_t* kb = a.kc + base;
     const bf16_t* vb = a.vc + base;
+    if constexpr (KL) stage_kv<D, false, NT, 1>(sK, 0, 1, lane, [&](int r) { return kb + (size_t)r * D; });
     stage_kv<D, true, NT, 1>(sV, 0, 1, lane, [&](int r) { return vb + (size_t)r * D; });
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int s = 0; s < C::KS; ++s)
-        kf0[t][s] = NT ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D +
-                                                                                   32 * s + 8 * fh))
-                       : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
+        if constexpr (!KL)
+          kf0[t][s] = NT ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D +
+                                                                                     32 * s + 8 * fh))
+                         : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
   }
   if (a.qkv_p != nullptr) {
     // q = RoPE(bf16(sum_s P[s][b])) for this KV head's G query heads, one (d, d + D/2) rotate_half
     // pair of 8-vectors per thread (G * D/16 threads, all slab loads of a thread in flight together),
     // staged through LDS; in the block owning the last KV tile, other threads append the new
     // token's k (rotated) and v meanwhile. One barrier covers both.
-    bf16_t* s_q = reinterpret_cast<bf16_t*>(smem + NW * C::TILEB);
+    bf16_t* s_q = reinterpret_cast<bf16_t*>(smem + NW * C::TILEB * (KL ? 2 : 1));
     constexpr int NV = D / 16;  // pairs per head
     const int pos = a.positions[b];
     const float* prow = a.qkv_p + (size_t)b * a.ldp;
@@ -1064,11 +1072,39 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
 
   for (int kt = kt0 + wid_u; kt < kt1; kt += NW) {
     bf16x8 kf[4][C::KS];
-    if (pre && kt == kt0 + wid_u) {  // requested before the prologue
+    if constexpr (KL) {
+      if (!(pre && kt == kt0 + wid_u)) {  // else staged before the prologue
+        const size_t base = ((size_t)bt[kt] * a.Hkv + kvh) * KT * D;
+        const bf16_t* kb = a.kc + base;
+        const bf16_t* vb = a.vc + base;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // previous tile's K / V reads retired
+        stage_kv<D, false, NT, 1>(sK, 0, 1, lane, [&](int r) { return kb + (size_t)r * D; });
+        stage_kv<D, true, NT, 1>(sV, 0, 1, lane, [&](int r) { return vb + (size_t)r * D; });
+      }
+      // K first: QK^T and the softmax run while the V tile (the 16 youngest LDS-DMAs) is still landing. The
+      // builtin wait (not inline asm) updates the compiler's own counter model, so it adds no vmcnt(0) of its own.
+      static_assert(Cfg<D>::PIECES < 64, "vmcnt range");
+      __builtin_amdgcn_s_waitcnt((Cfg<D>::PIECES & 15) | (((Cfg<D>::PIECES >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int s = 0; s < C::KS; ++s) kf[t][s] = load_k<D>(sK, t, s, lane);
+    } else if (pre && kt == kt0 + wid_u) {  // requested before the prologue
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int s = 0; s < C::KS; ++s) kf[t][s] = kf0[t][s];
+    } else if (DG == 2) {
+      const size_t base = ((size_t)bt[kt] * a.Hkv + kvh) * KT * D;
+      const bf16_t* kb = a.kc + base;
+      const bf16_t* vb = a.vc + base;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      stage_kv<D, true, NT, 1>(sV, 0, 1, lane, [&](int r) { return vb + (size_t)r * D; });
+      stage_kv<D, false, NT, 1>(sV, 0, 1, lane, [&](int r) { return kb + (size_t)r * D; });
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int s = 0; s < C::KS; ++s) kf[t][s] = (bf16x8){0, 0, 0, 0, 0, 0, 0, 0};
     } else {
       const size_t base = ((size_t)bt[kt] * a.Hkv + kvh) * KT * D;
       const bf16_t* kb = a.kc + base;
@@ -1085,7 +1121,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
                                                                                     32 * s + 8 * fh))
                         : *reinterpret_cast<const bf16x8*>(kb + (size_t)(16 * t + fr) * D + 32 * s + 8 * fh);
     }
-    if constexpr (DG == 1) {
+    if constexpr (DG != 0) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -1134,7 +1170,10 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     for (int dt = 0; dt < C::DT; ++dt) o[dt] *= alpha;
     const bf16x8 pb0 = pack_p(s4[0], s4[1]);
     const bf16x8 pb1 = pack_p(s4[2], s4[3]);
-    wait_vmcnt0();  // V tile landed in this wave's LDS
+    if constexpr (KL)
+      __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));  // V tile landed (vmcnt(0), seen by the compiler)
+    else
+      wait_vmcnt0();  // V tile landed in this wave's LDS
 #pragma unroll
     for (int dt = 0; dt < C::DT; ++dt) {
       o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(load_vt<D>(sV, dt, 0, lane), pb0, o[dt], 0, 0, 0);
@@ -1142,7 +1181,7 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
     }
   }
 
-  if constexpr (DG == 1) {
+  if constexpr (DG != 0) {
     if (dsink == 0x9e3779b9u) a.out[(size_t)b * a.out_stride + lane] = 0;  // keeps the loads alive
     return;
   }
@@ -1186,10 +1225,10 @@ __device__ __forceinline__ void attn_decode_block(const DecodeArgs& a, int part,
   }
 }
 
-template <int D, int G, bool NT = false, int NW = 4, int DG = 0>
-__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attn_decode_kernel(DecodeArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[decode_lds_bytes<D, G, NW>()];
-  attn_decode_block<D, G, NT, NW, DG>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+template <int D, int G, bool NT = false, int NW = 4, int DG = 0, bool KL = false>
+__global__ __launch_bounds__(NW * 64, (NW == 4 && !KL) ? 2 : 1) void attn_decode_kernel(DecodeArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[decode_lds_bytes<D, G, NW, KL>()];
+  attn_decode_block<D, G, NT, NW, DG, KL>(a, blockIdx.x, blockIdx.y, blockIdx.z, smem);
 }
 
 // merge split-K partitions: grid (Hq, B), block D threads. The partition statistics are loaded by
@@ -1332,8 +1371,14 @@ static int g_decode_nt = 0;
 static int g_decode_nw8_min = 0;
 // diagnostic instantiation of the 8-wave kernel (DG above; A/B tooling only, 0 = off)
 static int g_decode_diag = 0;
+// single-partition grid on 4-wave blocks with K tiles by LDS-DMA (KL above; 0 = the 8-wave kernel)
+static int g_decode_kl = 0;
+RAGK_API int ragk_attn_decode_set_kl(int on) {
+  g_decode_kl = on ? 1 : 0;
+  return 0;
+}
 RAGK_API int ragk_attn_decode_set_diag(int dg) {
-  g_decode_diag = dg == 1 ? 1 : 0;
+  g_decode_diag = (dg == 1 || dg == 2) ? dg : 0;
   return 0;
 }
 RAGK_API int ragk_attn_decode_set_nw8(int min_pairs) {
@@ -1392,8 +1437,12 @@ static int launch_attn_decode(DecodeArgs a, int B, int D, int max_parts, hipStre
   dim3 grid(max_parts, Hkv, B);
   if (D == 128 && G == 4 && max_parts == 1 && g_decode_nw8_min > 0 && B * Hkv >= g_decode_nw8_min) {
     // one partition per sequence over >= 1 block per CU: 8-wave blocks, no merge launch
-    if (g_decode_diag)
+    if (g_decode_kl && !g_decode_diag)
+      hipLaunchKernelGGL((attn_decode_kernel<128, 4, true, 4, 0, true>), grid, dim3(256), 0, st, a);
+    else if (g_decode_diag == 1)
       hipLaunchKernelGGL((attn_decode_kernel<128, 4, true, 8, 1>), grid, dim3(512), 0, st, a);
+    else if (g_decode_diag == 2)
+      hipLaunchKernelGGL((attn_decode_kernel<128, 4, true, 8, 2>), grid, dim3(512), 0, st, a);
     else if (g_decode_nt)
       hipLaunchKernelGGL((attn_decode_kernel<128, 4, true, 8>), grid, dim3(512), 0, st, a);
     else

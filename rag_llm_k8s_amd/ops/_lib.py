@@ -35,6 +35,7 @@ _SIGS = {
     "ragk_attn_decode_set_nw8": [I],
     "ragk_attn_decode_set_defer": [I],
     "ragk_attn_decode_set_diag": [I],
+    "ragk_attn_decode_set_kl": [I],
     "ragk_gemm_part_merge": [P, P, P, I, P, I, I, I, P, I, P, P, I, I, I, I, S],
     "ragk_gemm_part_merge_ok": [I, I, I, I, I],
     "ragk_gemm_stream_part": [P, I, P, I, P, I, I, I, I, I, S],

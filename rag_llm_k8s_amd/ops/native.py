@@ -895,10 +895,19 @@ DECODE_NW8_MIN_PAIRS = 256
 DECODE_NT_MIN_BH = 64
 
 
+# The single-partition grid (DECODE_NW8_MIN_PAIRS) on 4-wave blocks whose K tiles arrive by LDS-DMA in 1 KiB
+# pieces like the V tiles (attention.hip KL), instead of 8-wave blocks loading K as 64-B row pieces into
+# registers: batch-32 decode attention over 5.2k-token contexts 114.2-116.8 -> 109.5-110.1 us per layer
+# (5.9-6.0 -> 6.3 TB/s of KV; with +-150-token context jitter 116-118 -> 110-111 us),
+# tools/attn_decode_probe.py, profiles/attn_decode_probe_r6.log.
+DECODE_KL = os.environ.get("RAGK_DECODE_KL", "1") != "0"
+
+
 def _set_decode_nt(B, Hkv):
     L = _lib.lib()
     check(L.ragk_attn_decode_set_nt(1 if B * Hkv >= DECODE_NT_MIN_BH else 0), "ragk_attn_decode_set_nt")
     check(L.ragk_attn_decode_set_nw8(DECODE_NW8_MIN_PAIRS), "ragk_attn_decode_set_nw8")
+    check(L.ragk_attn_decode_set_kl(1 if DECODE_KL else 0), "ragk_attn_decode_set_kl")
 
 
 def attn_decode(q, k_cache, v_cache, block_tables, kv_lens, out, Hq, Hkv, D, part_tiles, max_parts, ws_o=None,

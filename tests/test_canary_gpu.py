@@ -161,7 +161,11 @@ def test_prefill_attention_and_kv_writes_in_bounds(native):
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (4, 1)])
-def test_decode_attention_in_bounds(native, Hq, Hkv):
+@pytest.mark.parametrize("single", [False, True])
+def test_decode_attention_in_bounds(native, Hq, Hkv, single, monkeypatch):
+    """single: the single-partition grid (the batch-32 path: K tiles by LDS-DMA in 4-wave blocks)."""
+    if single:
+        monkeypatch.setattr(native, "DECODE_NW8_MIN_PAIRS", 1)
     torch.manual_seed(10)
     D = 128
     lens = [65, 3000, 1]

@@ -404,9 +404,12 @@ def test_attn_decode(native, kv_lens, Hq, Hkv, target):
 @pytest.mark.parametrize("kv_lens,Hq,Hkv", [([5200, 1, 64, 4100], 32, 8), ([65, 3000, 700], 4, 1), ([1], 32, 8),
                                              ([8100] * 3 + [5], 32, 8)])
 @pytest.mark.parametrize("nt", [0, 1])
-def test_attn_decode_nw8_single_partition(native, kv_lens, Hq, Hkv, nt, monkeypatch):
-    """Single-partition decode attention in 8-wave blocks (attention.hip NW = 8, the batch-32 grid): no merge
-    launch; vs the fp32 oracle and within rounding of the 4-wave split-K kernel, nt loads or not."""
+@pytest.mark.parametrize("kl", [0, 1])
+def test_attn_decode_nw8_single_partition(native, kv_lens, Hq, Hkv, nt, kl, monkeypatch):
+    """Single-partition decode attention (the batch-32 grid: one block per sequence and KV head, no merge
+    launch), as 8-wave blocks with K in registers (kl = 0) and as 4-wave blocks with K tiles by LDS-DMA (kl = 1,
+    attention.hip KL, the default): vs the fp32 oracle and within rounding of the split-K kernel, nt loads or not."""
+    monkeypatch.setattr(native, "DECODE_KL", bool(kl))
     D = 128
     torch.manual_seed(17)
     kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=5)
@@ -430,6 +433,50 @@ def test_attn_decode_nw8_single_partition(native, kv_lens, Hq, Hkv, nt, monkeypa
                              v_full=lambda s: R.paged_kv_view(vc, bt[s], kv_lens[s], 64))
     assert rel_err(out.cpu().reshape(B, Hq, D), ref) < 2e-2
     assert rel_err(out.cpu(), ref4.cpu()) < 1e-2
+
+
+@pytest.mark.parametrize("kl", [0, 1])
+def test_attn_decode_rope_single_partition_kl(native, kl, monkeypatch):
+    """The engine's batch-32 decode attention (fused RoPE + KV append from the qkv slabs, single partition,
+    nt): same cache contents as rope_kv_partials (bit for bit) and the same attention output within rounding
+    for the 8-wave and the K-by-LDS-DMA 4-wave kernels; new tokens at a block end, a block start, alone."""
+    monkeypatch.setattr(native, "DECODE_NW8_MIN_PAIRS", 1)
+    monkeypatch.setattr(native, "DECODE_NT_MIN_BH", 1)
+    D, S, Hq, Hkv = 128, 4, 32, 8
+    kv_lens = [5200, 64, 65, 1, 3001, 4160]
+    torch.manual_seed(15)
+    kc, vc, bt = _paged_setup(kv_lens, Hkv, D, seed=6)
+    B = len(kv_lens)
+    kc, vc, bt = kc.to(DEV), vc.to(DEV), bt.to(DEV)
+    kvl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    pos = kvl - 1
+    slots = (bt[torch.arange(B, device=DEV), (pos // 64).long()] * 64 + pos % 64).int()
+    P = torch.randn(S, B, (Hq + 2 * Hkv) * D, device=DEV)
+    cos, sin = R.rope_tables(D, 8192, theta=500000.0, scaling=None)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pt, mp = native.decode_partitions(max(kv_lens), B, Hkv)
+    assert mp == 1
+    kc2, vc2 = kc.clone(), vc.clone()
+    q = torch.empty(B, Hq * D, device=DEV).bfloat16()
+    native.rope_kv_partials(P, q, pos, cos, sin, slots, kc2, vc2, Hq, Hkv, D)
+    monkeypatch.setattr(native, "DECODE_KL", False)
+    ref = torch.empty(B, Hq * D, device=DEV).bfloat16()
+    native.attn_decode(q, kc2, vc2, bt, kvl, ref, Hq, Hkv, D, pt, mp)
+    monkeypatch.setattr(native, "DECODE_KL", bool(kl))
+    out = torch.full((B, Hq * D), float("nan"), device=DEV).bfloat16()
+    native.attn_decode_rope(P, pos, cos, sin, slots, kc, vc, bt, kvl, out, Hq, Hkv, D, pt, mp)
+    torch.cuda.synchronize()
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    if kl:
+        assert rel_err(out, ref) < 1e-2
+    else:
+        assert torch.equal(out, ref)
+    cu = torch.arange(B + 1, dtype=torch.int32)
+    qh = q.cpu().reshape(B, Hq, D)
+    oracle = R.attention_varlen(qh, None, None, cu, kvl.cpu(), True, 1 / math.sqrt(D),
+                                k_full=lambda s: R.paged_kv_view(kc.cpu(), bt.cpu()[s], kv_lens[s], 64),
+                                v_full=lambda s: R.paged_kv_view(vc.cpu(), bt.cpu()[s], kv_lens[s], 64))
+    assert rel_err(out.cpu().reshape(B, Hq, D), oracle) < 2e-2
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (4, 1), (8, 1)])

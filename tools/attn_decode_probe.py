@@ -6,8 +6,9 @@ Infinity Cache). Prints us per launch and TB/s of KV for each variant:
   python tools/attn_decode_probe.py                 # AP_B=32 AP_CTX=5264 AP_NL=6 AP_JITTER=0
   AP_VARIANTS=base,diag,base python tools/attn_decode_probe.py
 
-variants: base | diag (loads + waits only, no QK^T / softmax / PV: attention.hip DG = 1) | nt0 (default
-cache policy). AP_JITTER=n: context lengths uniform in [ctx - n, ctx + n] (the bench's RAG prompts vary).
+variants: base | diag (loads + waits only, no QK^T / softmax / PV: attention.hip DG = 1) | diag_dma (as diag,
+K by 1 KiB LDS-DMA pieces too: DG = 2) | kl (4-wave blocks, K tiles by LDS-DMA: attention.hip KL) | nt0
+(default cache policy). AP_CHECK=1: every variant's output vs the base kernel's. AP_JITTER=n: context lengths uniform in [ctx - n, ctx + n] (the bench's RAG prompts vary).
 """
 import math
 import os
@@ -29,7 +30,10 @@ def main():
     NL = int(os.environ.get("AP_NL", "6"))
     jit = int(os.environ.get("AP_JITTER", "0"))
     reps = int(os.environ.get("AP_REPS", "20"))
-    Hq, Hkv, D = 32, 8, 128
+    # AP_HKV=1 with AP_B=256: the same 256 (sequence, KV head) streams and bytes, each stream's tiles in
+    # consecutive cache blocks -- the access pattern of a head-major cache layout ([Hkv][blocks][64][D])
+    Hkv = int(os.environ.get("AP_HKV", "8"))
+    Hq, D = 4 * Hkv, 128
     dev = "cuda"
     g = torch.Generator().manual_seed(1)
     lens = [ctx + (int(torch.randint(-jit, jit + 1, (1,), generator=g)) if jit else 0) for _ in range(B)]
@@ -62,11 +66,26 @@ def main():
             native.attn_decode_rope(P, pos, cos, sin, slots, kc, vc, bt, kvl, out, Hq, Hkv, D, pt, mp)
 
     variants = [v for v in os.environ.get("AP_VARIANTS", "base,diag,base,diag").split(",") if v]
+    if os.environ.get("AP_CHECK") == "1":
+        outs = {}
+        kl_default = native.DECODE_KL
+        for v in ("base", "kl"):
+            native.DECODE_KL = v == "kl"
+            kc, vc = caches[0]
+            native.attn_decode_rope(P, pos, cos, sin, slots, kc, vc, bt, kvl, out, Hq, Hkv, D, pt, mp)
+            torch.cuda.synchronize()
+            outs[v] = out.clone()
+        native.DECODE_KL = kl_default
+        print("kl vs base: bit-identical %s, max abs diff %.3g" % (
+            torch.equal(outs["kl"], outs["base"]), (outs["kl"].float() - outs["base"].float()).abs().max().item()),
+            flush=True)
     graphs = {}
     for v in variants:
         key = v
         if key not in graphs:
-            L.ragk_attn_decode_set_diag(1 if v == "diag" else 0)
+            L.ragk_attn_decode_set_diag({"diag": 1, "diag_dma": 2}.get(v, 0))
+            kl_default = native.DECODE_KL
+            native.DECODE_KL = v == "kl"  # base: the 8-wave kernel with K in registers
             nt_min = native.DECODE_NT_MIN_BH
             native.DECODE_NT_MIN_BH = 1 << 30 if v == "nt0" else nt_min
             s = torch.cuda.Stream()
@@ -81,6 +100,7 @@ def main():
             graphs[key] = gr
             native.DECODE_NT_MIN_BH = nt_min
             L.ragk_attn_decode_set_diag(0)
+            native.DECODE_KL = kl_default
         gr = graphs[key]
         gr.replay()
         torch.cuda.synchronize()
