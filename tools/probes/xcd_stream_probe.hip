@@ -11,6 +11,9 @@ typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 // MODE 0: sequential (each wave 8 KB contiguous per step, the 4 waves adjacent: 32 KB per step);
 // MODE 1: the decode engine's slot order: 16 rows of ROWB bytes (a weight matrix row), 1 KiB from each
 // row per slot (K-chunk kc of all 16 rows), then the next K chunk; 16-row groups one after another.
+// MODE 2: the stream GEMM's stage order (gemm_stream.hip, 64-row tiles): each 1 KiB LDS-DMA piece is 8 rows
+// x 128 B, a stage = 64 rows x 128 B (one 64-element K-step), consecutive stages advance 128 B along the rows;
+// per wave 4 stages (8 pieces) in flight. MODE 3: as 2 with 256 B per row per stage (4 rows x 256 B per piece).
 template <bool DMA, int MODE>
 __global__ __launch_bounds__(256) void stream_kernel(const u32x4* __restrict__ src, size_t per_wg, unsigned long long* t,
                                                      unsigned* sink, int rowb) {
@@ -33,6 +36,31 @@ __global__ __launch_bounds__(256) void stream_kernel(const u32x4* __restrict__ s
                                              (__attribute__((address_space(3))) void*)&lds[wid][64 * u], 16, 0, 2);
           else
             acc ^= __builtin_nontemporal_load(p + off);
+        }
+        if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+  }
+  if constexpr (MODE == 2 || MODE == 3) {
+    // rows of rowb bytes, 64-row tiles, stage = 64 rows x SEG bytes; piece q of a stage = 64 lanes x 16 B
+    constexpr int SEG = MODE == 2 ? 128 : 256;        // bytes per row per stage
+    constexpr int RPP = 1024 / SEG;                   // rows per 1 KiB piece
+    constexpr int LPR = SEG / 16;                     // lanes per row
+    const size_t rowv = rowb / 16, tiles = per_wg / (64 * rowv), steps = rowb / SEG;
+    for (size_t tl = 0; tl < tiles; ++tl)
+      for (size_t k = 0; k < steps; k += 8 / (64 / RPP / 4)) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {  // 8 pieces per wave: (64 / RPP) / 4 pieces per wave per stage
+          constexpr int PPW = 64 / RPP / 4;
+          const int st = u / PPW, q = wid * PPW + (u % PPW);
+          const int r = q * RPP + lane / LPR;
+          const size_t off = (tl * 64 + r) * rowv + (k + st) * (SEG / 16) + (lane % LPR);
+          if (k + st < steps) {
+            if constexpr (DMA)
+              __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p + off),
+                                               (__attribute__((address_space(3))) void*)&lds[wid][64 * u], 16, 0, 2);
+            else
+              acc ^= __builtin_nontemporal_load(p + off);
+          }
         }
         if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -69,13 +97,19 @@ int main() {
   if (hipMalloc(&src, per_wg_bytes * G) || hipMalloc(&t, 16 * G) || hipMalloc(&sink, 4)) return 1;
   hipMemset(src, 1, per_wg_bytes * G);
   std::vector<unsigned long long> h(2 * G);
-  const int rowbs[3] = {0, 8192, 28672};
-  for (int pat = 0; pat < 3; ++pat)
+  const int rowbs[5] = {0, 8192, 28672, 8192, 8192};
+  for (int pat = 0; pat < 5; ++pat)
     for (int mode = 0; mode < 2; ++mode) {
       for (int rep = 0; rep < 3; ++rep) {
         const int rb = rowbs[pat];
         if (pat == 0)
           hipLaunchKernelGGL((mode ? stream_kernel<true, 0> : stream_kernel<false, 0>), dim3(G), dim3(256), 0, 0, src,
+                             per_wg, t, sink, rb);
+        else if (pat == 3)
+          hipLaunchKernelGGL((mode ? stream_kernel<true, 2> : stream_kernel<false, 2>), dim3(G), dim3(256), 0, 0, src,
+                             per_wg, t, sink, rb);
+        else if (pat == 4)
+          hipLaunchKernelGGL((mode ? stream_kernel<true, 3> : stream_kernel<false, 3>), dim3(G), dim3(256), 0, 0, src,
                              per_wg, t, sink, rb);
         else
           hipLaunchKernelGGL((mode ? stream_kernel<true, 1> : stream_kernel<false, 1>), dim3(G), dim3(256), 0, 0, src,
@@ -89,10 +123,11 @@ int main() {
         }
         // bytes actually read in the slot pattern: whole 16-row groups
         const size_t rowv = rb / 16;
-        const size_t bytes = pat == 0 ? per_wg_bytes : (per_wg / (16 * rowv)) * 16 * rowv * 16;
-        printf("%s %s rep %d: total %.1f us (%.2f TB/s); per-XCD median us:", pat == 0 ? "sequential   " :
-               (pat == 1 ? "slots row 8K " : "slots row 28K"), mode ? "lds-dma" : "plain  ", rep, (t1 - t0) / 100.0,
-               bytes * G / ((t1 - t0) / 100.0) / 1e6);
+        const size_t bytes = pat == 0 ? per_wg_bytes
+                             : (pat >= 3 ? (per_wg / (64 * rowv)) * 64 * rowv * 16 : (per_wg / (16 * rowv)) * 16 * rowv * 16);
+        const char* names[5] = {"sequential   ", "slots row 8K ", "slots row 28K", "stages 128 B ", "stages 256 B "};
+        printf("%s %s rep %d: total %.1f us (%.2f TB/s); per-XCD median us:", names[pat], mode ? "lds-dma" : "plain  ",
+               rep, (t1 - t0) / 100.0, bytes * G / ((t1 - t0) / 100.0) / 1e6);
         for (int x = 0; x < 8; ++x) {
           std::vector<double> d;
           for (int w = x; w < G; w += 8) d.push_back((h[2 * w + 1] - h[2 * w]) / 100.0);
