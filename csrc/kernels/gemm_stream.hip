@@ -97,7 +97,7 @@ __device__ __forceinline__ void glds16_nt(const void* gsrc, void* lds_wave_base)
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 2);
 }
 
-template <int MT, bool FP8, bool NT, int ROWS, bool PAIR>
+template <int MT, bool FP8, bool NT, int ROWS, bool PAIR, bool NOX = false>
 __device__ __forceinline__ void stage_load(const bf16_t* __restrict__ X, int ldx, int M,
                                            const unsigned char* __restrict__ Wb, int ldw_bytes, int Nrows, int tile,
                                            int kel, char* st, int wid, int lane) {
@@ -114,6 +114,7 @@ __device__ __forceinline__ void stage_load(const bf16_t* __restrict__ X, int ldx
     else glds16(Wb + (size_t)gr * ldw_bytes + kbyte + c * 16, st + q * 1024);
   }
   // activations: XROWS rows x XROW bytes, as 128-B half-rows for the fp8 (256-B) case
+  if constexpr (NOX) return;
   char* xs = st + G::WBYTES;
 #pragma unroll
   for (int i = 0; i < G::XP; ++i) {
@@ -140,7 +141,10 @@ __device__ __forceinline__ void stage_load(const bf16_t* __restrict__ X, int ldx
 // ([S][M][N], gemm_part's layout) and exits -- no ticket, no in-kernel reduction (the release / acquire
 // of the last-arriver form made the 8-way split down projection 56 us at batch 32; gemm_part's
 // register-streaming blocks need 114 KB of LDS for its activation slice there and run in two rounds).
-template <int MT, int EPI, bool OUT_F32, bool FP8, bool NT = false, int ROWS = WROWS, bool SLAB = false>
+// DG = 1 (diagnostic, tools/stream_gemm_probe.py): the ring, its waits and barriers, no fragment reads or MFMA
+// (results meaningless) -- how fast the weight stream itself runs in this kernel's structure. DG = 2: also
+// no activation staging (weights only); DG = 3: as 2 without the per-stage barrier.
+template <int MT, int EPI, bool OUT_F32, bool FP8, bool NT = false, int ROWS = WROWS, bool SLAB = false, int DG = 0>
 __global__ __launch_bounds__(ST_THREADS, ROWS == 64 ? 2 : 1) void gemm_stream_kernel(
     const bf16_t* __restrict__ X, int ldx, const void* __restrict__ Wv, int ldw, const float* __restrict__ wscale,
     void* C, int ldc, const bf16_t* __restrict__ bias, const bf16_t* resid, int ldr, int M, int N, int K, int S,
@@ -172,22 +176,25 @@ __global__ __launch_bounds__(ST_THREADS, ROWS == 64 ? 2 : 1) void gemm_stream_ke
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
     if (p < nst)
-      stage_load<MT, FP8, NT, ROWS, PAIR>(X, ldx, M, Wb, ldw_bytes, Nrows, ntile, k0 + p * G::KSTEP,
+      stage_load<MT, FP8, NT, ROWS, PAIR, (DG >= 2)>(X, ldx, M, Wb, ldw_bytes, Nrows, ntile, k0 + p * G::KSTEP,
                                           smem + p * G::STAGE, wid_u, lane);
 
   for (int t = 0; t < nst; ++t) {
     // stage t landed (this wave's part): at most the later stages' loads still outstanding
     const int ahead = min(nst - 1 - t, NS - 2);
-    if (ahead >= NS - 2) wait_vm<(NS - 2) * G::LOADS>();
+    constexpr int LD = DG >= 2 ? G::WPW : G::LOADS;  // LDS-DMAs per wave per stage
+    if (ahead >= NS - 2) wait_vm<(NS - 2) * LD>();
     else wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier_raw();  // every wave's part of stage t landed; every wave finished reading stage t-1
+    if constexpr (DG != 3) barrier_raw();  // every wave's part of stage t landed; every wave finished reading stage t-1
     if (t + NS - 1 < nst)
-      stage_load<MT, FP8, NT, ROWS, PAIR>(X, ldx, M, Wb, ldw_bytes, Nrows, ntile, k0 + (t + NS - 1) * G::KSTEP,
+      stage_load<MT, FP8, NT, ROWS, PAIR, (DG >= 2)>(X, ldx, M, Wb, ldw_bytes, Nrows, ntile, k0 + (t + NS - 1) * G::KSTEP,
                                           smem + ((t + NS - 1) % NS) * G::STAGE, wid_u, lane);
     const char* wt = smem + (t % NS) * G::STAGE;
     const char* xt = wt + G::WBYTES;
-    if constexpr (!FP8) {
+    if constexpr (DG == 1) {
+      continue;
+    } else if constexpr (!FP8) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int c = 4 * s + fh;
@@ -338,6 +345,8 @@ __global__ __launch_bounds__(ST_THREADS, ROWS == 64 ? 2 : 1) void gemm_stream_ke
 
 // Weight-stream cache policy for the SiLU*up (gate/up) instantiations: 1 = non-temporal.
 int g_stream_nt = 1;
+// diagnostic build of the SiLU*up 64-row kernel (DG above; A/B tooling only)
+int g_stream_diag = 0;
 // Tile rows for the SiLU*up GEMM: 64 = two blocks per CU over 64-row (32 gate + 32 up) tiles, so the
 // 28672-row Llama gate/up grid (448 tiles) occupies all 256 CUs; 128 = one block per CU, 224 tiles.
 int g_stream_pair_rows = 64;
@@ -354,7 +363,16 @@ int launch_stream(const void* X, int ldx, const void* W, int ldw, const float* w
   hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI, F32, FP8, NTV, R>), dim3((Nrows + R - 1) / R, S), dim3(ST_THREADS), \
                      0, st, (const bf16_t*)X, ldx, W, ldw, wscale, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid,  \
                      ldr, M, N, K, S, ws, cnt)
-    if (g_stream_pair_rows == 64) {
+    if (g_stream_pair_rows == 64 && g_stream_diag && !FP8) {
+#define RAGK_ST_DG(DGV)                                                                                              \
+  hipLaunchKernelGGL((gemm_stream_kernel<MT, EPI, F32, FP8, true, 64, false, DGV>), dim3((Nrows + 63) / 64, S),       \
+                     dim3(ST_THREADS), 0, st, (const bf16_t*)X, ldx, W, ldw, wscale, C, ldc, (const bf16_t*)bias,     \
+                     (const bf16_t*)resid, ldr, M, N, K, S, ws, cnt)
+      if (g_stream_diag == 1) RAGK_ST_DG(1);
+      else if (g_stream_diag == 2) RAGK_ST_DG(2);
+      else RAGK_ST_DG(3);
+#undef RAGK_ST_DG
+    } else if (g_stream_pair_rows == 64) {
       if (g_stream_nt) RAGK_ST_PAIR(true, 64);
       else RAGK_ST_PAIR(false, 64);
     } else {
@@ -406,6 +424,11 @@ int dispatch_stream(const void* X, int ldx, const void* W, int ldw, const float*
 
 // Split count for the stream decode GEMM: enough blocks for 256 CUs (one block per CU), at least
 // 8 K-steps per block, S | K-steps.
+RAGK_API int ragk_gemm_stream_set_diag(int dg) {
+  g_stream_diag = (dg >= 1 && dg <= 3) ? dg : 0;
+  return 0;
+}
+
 RAGK_API int ragk_gemm_stream_set_nt(int nt) {
   g_stream_nt = nt ? 1 : 0;
   return 0;

@@ -25,6 +25,7 @@ _SIGS = {
     "ragk_gemm_pp": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_w4_set_grid": [I],
     "ragk_gemm_stream_set_nt": [I],
+    "ragk_gemm_stream_set_diag": [I],
     "ragk_gemm_stream_set_pair_rows": [I],
     "ragk_gemm_w4": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
     "ragk_gemm_w4_splitk": [P, I, P, I, P, I, I, I, I, S],
