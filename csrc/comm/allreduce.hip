@@ -79,7 +79,7 @@ struct ArPeers {
   size_t row_stage_bytes;    // one fp32 staging half: max_rows * max_h * 4
   size_t row_result_bytes;   // one bf16 result half: max_rows * max_h * 2
   unsigned* host_err;        // host-mapped pinned word: the engine polls it after every step, no sync
-  unsigned spin_limit;       // bound of one peer wait, in s_memrealtime ticks (100 MHz)
+  unsigned long long spin_limit;  // bound of one peer wait, in s_memrealtime ticks (100 MHz; 64-bit: > 43 s)
 };
 
 // Which wait gave up: the error record names the collective (call site), the peer that never arrived,
@@ -492,11 +492,9 @@ RAGK_API long ragk_ar_max_bytes(void* hp) { return (long)((ArHandle*)hp)->data_b
 
 // Bound of each peer wait in microseconds (default 5 s); tests shorten it.
 RAGK_API int ragk_ar_set_spin_limit(void* hp, unsigned limit_us) {
-  const unsigned long long ticks = (unsigned long long)limit_us * 100ull;  // 100 MHz
-  const unsigned limit = ticks > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (unsigned)ticks;
   ArHandle* h = (ArHandle*)hp;
   if (!h || limit_us == 0) return (int)hipErrorInvalidValue;
-  h->peers.spin_limit = limit;
+  h->peers.spin_limit = (unsigned long long)limit_us * 100ull;  // 100 MHz ticks (a 32-bit bound capped at 43 s)
   return 0;
 }
 

@@ -136,12 +136,14 @@ def _prefill_decode_logits(model, ids, nxt):
 
 def _init(rank, port, world=WORLD):
     # every rank on cuda:0 on purpose: the distinctness self-test must be told so. Eight processes with
-    # HIP's default 4 hardware queues each over-subscribe the device's mapped queues; 2 queues per process
-    # keeps every queue mapped (set before HIP init) so no peer-waiting kernel waits on an unmapped queue.
+    # HIP's default 4 hardware queues each over-subscribe the device's mapped queues (a rank's collective
+    # kernel started ~43 s after its peers', profiles/tp8_trace_report_r5.txt); 2 queues per process still
+    # stalled a round-6 suite run (215 s to the first logits, then a timed-out collective). One queue per
+    # process (set before HIP init): 8 queues, every one mapped, no peer-waiting kernel on an unmapped queue.
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", RAGK_TP_CONTROL="gloo", RAGK_ALLOW_SHARED_DEVICE="1")
     if world >= 8:
-        os.environ["GPU_MAX_HW_QUEUES"] = "2"
+        os.environ["GPU_MAX_HW_QUEUES"] = "1"
     from rag_llm_k8s_amd.parallel.dist import init_distributed
 
     return init_distributed(tp=world, backend="gloo")
@@ -149,7 +151,7 @@ def _init(rank, port, world=WORLD):
 
 def _tp_worker(rank, port, d, world):
     WORLD = world
-    ctx = _init(rank, port, world)  # 8 ranks: 2 hardware queues per process (see _init)
+    ctx = _init(rank, port, world)  # 8 ranks: 1 hardware queue per process (see _init)
     _log(rank, world, "process group up")
     from rag_llm_k8s_amd.engine.llm_engine import LLMEngine, SamplingParams
     from rag_llm_k8s_amd.models.llama import LlamaModel, LlamaWeights
@@ -160,19 +162,28 @@ def _tp_worker(rank, port, d, world):
     try:
         cfg = _cfg()
         sd = _state_dict(cfg)
-        # 8 processes time-slicing one GPU (and 16 host CPUs): a rank can trail the others by seconds, so
-        # the rehearsal's peer waits get a 60 s bound instead of the serving default (5 s)
+        # 8 processes time-slicing one GPU (and 16 host CPUs): a rank can trail the others by a long time.
+        # On a FRESH box the first 8-rank run stalled 29 s and then > 60 s inside its first two prefills
+        # (call 5-10 peer waits) while a second run in the same pytest process, and the 2 / 4-rank runs before
+        # it, finished in seconds: per-process cold start (first launches of each kernel while the image's
+        # pages come in), not the protocol. The rehearsal's peer waits get a 240 s bound instead of the
+        # serving default (5 s); the 2 / 4-rank cases keep the default. (Until round 6 the kernels held the
+        # bound as 32-bit 100 MHz ticks, capped at 43 s: the "60 s" asked for here was 43 s.)
         comm = TPComm(ctx.tp_group, ctx.tp, ctx.tp_rank, ctx.device, ctx.tp_cpu_group, ipc_max_bytes=16 << 20,
-                      ipc_spin_limit=60_000_000 if world >= 8 else None)
+                      ipc_spin_limit=240_000_000 if world >= 8 else None)
         res["ipc"] = comm.ipc is not None
         _log(rank, world, "comm up (peer-mapped: %s)" % res["ipc"])
         w = LlamaWeights.from_state_dict(cfg, sd, ctx.device, ctx.tp_rank, ctx.tp)
         m = LlamaModel(cfg, w, ctx.device, comm=comm, max_positions=4096)
+        _log(rank, world, "model up")
         gen = torch.Generator().manual_seed(7)
         ids = torch.randint(3, cfg.vocab_size, (300,), generator=gen).tolist()
         local = _prefill_logits(m, ids)  # [1, V/2] this rank's vocab shard
+        torch.cuda.synchronize()
+        _log(rank, world, "prefill logits")
         full = comm.ipc.all_gather(local.contiguous()).view(WORLD, 1, -1)
         res["tp_logits"] = torch.cat([full[r] for r in range(WORLD)], 1)[:, :cfg.vocab_size].cpu()
+        _log(rank, world, "prefill logits gathered")
         local = _prefill_decode_logits(m, ids, 77)  # decode: fused row-parallel reduction
         full = comm.ipc.all_gather(local.contiguous()).view(WORLD, 1, -1)
         res["tp_dec_logits"] = torch.cat([full[r] for r in range(WORLD)], 1)[:, :cfg.vocab_size].cpu()
@@ -208,6 +219,7 @@ def _tp_worker(rank, port, d, world):
                 eng.warmup_graphs()
                 _log(rank, world, "graphs captured")
             res[("sampled", graphs)] = eng.generate(prompts, sampled, seeds=[11, 12, 13])
+            _log(rank, world, "sampled generate done (graphs=%s)" % graphs)
             res[("greedy", graphs)] = eng.generate(prompts, greedy)
             res[("async", graphs)] = eng.async_decode
             _log(rank, world, "engine graphs=%s" % graphs)
@@ -248,9 +260,10 @@ def _spawn(target, timeout=600, world=WORLD):
 # 8 ranks as 8 processes on ONE GPU: with HIP's default 4 hardware queues per process (32 queues) a rank's
 # collective kernel could start tens of seconds after its peers' (queue co-scheduling; kernel trace in
 # profiles/tp8_trace_report_r5.txt), so the workers run one queue each (_tp_worker).
-TP_WORLDS = [2, 4, 8]
+TP_WORLDS = [int(w) for w in os.environ.get("RAGK_TP_WORLDS", "2,4,8").split(",")]
 
 
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("world", TP_WORLDS)
 def test_tp_llama8b_widths_on_one_gpu(native, world):
     """TP=2/4/8 shards of Llama-3.1-8B widths (TP=8: 4 query heads, 1 KV head, 1792 FFN rows, a 16k-row
@@ -258,7 +271,7 @@ def test_tp_llama8b_widths_on_one_gpu(native, world):
     logits vs TP=1, graph + async decode == eager (2 / 4 ranks), the same samples on every rank, and the
     micro-batched overlap prefill (the 1100-token prompt)."""
     WORLD = world
-    out = _spawn(_tp_worker, world=world, timeout=420 if world >= 8 else 600)
+    out = _spawn(_tp_worker, world=world, timeout=840 if world >= 8 else 600)
     assert all(o["ipc"] for o in out), "peer-mapped collectives must pass their self-test"
     ref = out[0]["ref_logits"]
     for r in range(WORLD):
