@@ -73,8 +73,7 @@ constexpr int ME_SHARDS = 8;
 constexpr int ME_CTR_STRIDE = 16;                  // u64 per shard: one 128-B line each
 constexpr unsigned ME_TIMEOUT_TICKS = 10000000u;   // default deadline: 100 ms of s_memrealtime (100 MHz)
 // error codes (device word, host word): which wait gave up
-constexpr unsigned ME_ERR_HANDOFF = 1u, ME_ERR_SLOT = 2u, ME_ERR_FREE = 3u, ME_ERR_ACT = 4u, ME_ERR_HANDOFF2 = 5u,
-                   ME_ERR_X = 6u;
+constexpr unsigned ME_ERR_HANDOFF = 1u, ME_ERR_SLOT = 2u, ME_ERR_FREE = 3u, ME_ERR_ACT = 4u;
 
 struct MlpArgs {
   const bf16_t* xn;        // [H] normalised input row (P == nullptr)
@@ -91,12 +90,7 @@ struct MlpArgs {
   unsigned* err_host;      // device address of a host-mapped pinned word (the engine polls it per step)
   const unsigned* tmo;     // deadline in s_memrealtime ticks (0 = ME_TIMEOUT_TICKS); a test hook forces timeouts
   unsigned long long* stamps;  // optional [G][8] s_memrealtime stamps (tools/mlp_engine_bench.py ME_STAMPS=1)
-  // phase C (next layer's input norm + qkv GEMM, N2 > 0): x2 = rmsnorm(h_out) * gamma2 after a second
-  // chip-wide hand-off on h, then P2[kc][n] = sum over K chunk kc of x2 . wqkv[n] (H / ME_KC split-K slabs)
-  const bf16_t* wqkv;      // [N2][H]
-  const bf16_t* gamma2;    // [H]
-  float* P2;               // [H / ME_KC][N2]
-  int H, I, N2;
+  int H, I;
   int w_even, w_odd;       // phase-A work weights of workgroups on even / odd XCDs
 };
 
@@ -126,8 +120,7 @@ struct MlpSmem {
   float hres[64];          // this workgroup's rows of h after the o_proj residual (fused tail)
   float red[8];
   unsigned full[8], freew[8];
-  unsigned doneA, doneB, actReady, abort, xReady;
-  bf16_t hloc[64];         // this workgroup's h rows after the down residual (phase C publishes them)
+  unsigned doneA, doneB, actReady, abort;
 };
 
 __device__ __forceinline__ void unpack4(uint2 v, float (&f)[4]) {
@@ -176,45 +169,9 @@ __device__ __forceinline__ bool me_spin_lds(const unsigned* p, unsigned want, co
   return true;
 }
 
-// One chip-wide hand-off (called by one wave of each workgroup after its stores retired): arrive on this
-// workgroup's shard of the counter set at `set` (8 shard lines, then the top counter's line); the count
-// before the add names this launch's generation. The last arriver of a shard adds to the top counter; the
-// waiters poll only the top counter (one load per poll: 256 workgroups polling 8 shard lines was ~38 G
-// polls/s of fabric traffic beside the other CUs' weight streams). false (wave-uniform): the deadline
-// passed first (reported with `code`); nothing past the hand-off may be read then.
-__device__ __forceinline__ bool me_handoff(const MlpArgs& a, MlpSmem& sm, unsigned long long* set, int w, int G,
-                                           int lane, unsigned long long deadline, unsigned code) {
-  const int shard = w & (ME_SHARDS - 1);
-  const int nsh = G < ME_SHARDS ? G : ME_SHARDS;
-  unsigned long long* top = set + ME_SHARDS * ME_CTR_STRIDE;
-  int failed = 0;
-  if (lane == 0) {
-    const unsigned long long mine = (unsigned long long)((G - shard + ME_SHARDS - 1) / ME_SHARDS);
-    const unsigned long long old =
-        __hip_atomic_fetch_add(set + shard * ME_CTR_STRIDE, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long gen = old / mine;
-    if (old + 1 == (gen + 1) * mine) __hip_atomic_fetch_add(top, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long want = (gen + 1) * (unsigned long long)nsh;
-    while (__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-      if (me_now() > deadline) {  // another workgroup never arrived
-        me_fail(a, sm, code);
-        failed = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(4);
-    }
-  }
-  if (__shfl(failed, 0, 64)) return false;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the caller's loads below the poll
-  return true;
-}
-
 struct SlotMap {
   int a0, nA, d0, KA, KB;
-  int nB, c0;  // phase C: first slot nA + nB, first unit c0 (unit u = row group u / KA, K chunk u % KA)
-  __device__ __forceinline__ int chunk(int s) const {
-    return s < nA ? s % KA : s < nA + nB ? (s - nA) % KB : (c0 + s - nA - nB) % KA;
-  }
+  __device__ __forceinline__ int chunk(int s) const { return s < nA ? s % KA : (s - nA) % KB; }
 };
 
 // The loader's wave-uniform cursor over its slots (no divisions in the issue loop): slot s, group g
@@ -225,13 +182,10 @@ struct LoadCursor {
   __device__ __forceinline__ void next(const SlotMap& m) {
     ++s;
     ++kc;
-    if (s == m.nA + m.nB) {  // phase C starts at unit c0 (checked first: nB may be 0)
-      g = m.c0 / m.KA;
-      kc = m.c0 % m.KA;
-    } else if (s == m.nA) {
+    if (s == m.nA) {
       g = 0;
       kc = 0;
-    } else if (kc == (s < m.nA || s >= m.nA + m.nB ? m.KA : m.KB)) {
+    } else if (kc == (s < m.nA ? m.KA : m.KB)) {
       kc = 0;
       ++g;
     }
@@ -250,13 +204,9 @@ __device__ __forceinline__ void me_issue_slot(const MlpArgs& a, const SlotMap& m
     base = reinterpret_cast<const char*>(a.wgu) + (long long)prow0 * a.H * 2 + cu.kc * (ME_KC * 2);
     stride = 2ll * a.H;
     jump = 112ll * a.H;
-  } else if (cu.s < m.nA + m.nB) {
+  } else {
     base = reinterpret_cast<const char*>(a.wd) + (long long)(16 * (m.d0 + cu.g)) * a.I * 2 + cu.kc * (ME_KC * 2);
     stride = 2ll * a.I;
-    jump = 0;
-  } else {  // phase C: row group g of the next layer's qkv weight
-    base = reinterpret_cast<const char*>(a.wqkv) + (long long)(16 * cu.g) * a.H * 2 + cu.kc * (ME_KC * 2);
-    stride = 2ll * a.H;
     jump = 0;
   }
 #pragma unroll
@@ -288,12 +238,7 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
   const int d1 = rng[3];
   m.nA = (a1 - m.a0) * m.KA;
   const int nB = (d1 - m.d0) * m.KB;
-  m.nB = nB;
-  // phase C units (row group x K chunk of the next qkv GEMM), contiguous per workgroup
-  const int NC = (a.N2 / 16) * m.KA;
-  m.c0 = (int)((long long)w * NC / G);
-  const int nC = (int)((long long)(w + 1) * NC / G) - m.c0;
-  const int nS = m.nA + nB + nC;
+  const int nS = m.nA + nB;
   // this workgroup's deadline for every wait below (one clock, one bound)
   const unsigned tk = *a.tmo;
   const unsigned long long deadline = me_now() + (tk ? tk : ME_TIMEOUT_TICKS);
@@ -309,7 +254,6 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
         sm.doneA = 0u;
         sm.doneB = 0u;
         sm.actReady = 0u;
-        sm.xReady = 0u;
         // an earlier launch failed (its workgroups left the counters off their generation): skip
         sm.abort = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
       }
@@ -471,7 +415,33 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
                          __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!me_handoff(a, sm, a.ctr, w, G, lane, deadline, ME_ERR_HANDOFF)) return false;
+    // arrive on this workgroup's shard; the count before the add names this launch's generation. The
+    // last arriver of a shard adds to the top counter; the waiters poll only the top counter (one
+    // load per poll: 256 workgroups polling 8 shard lines was ~38 G polls/s of fabric traffic beside
+    // the other CUs' weight streams)
+    const int shard = w & (ME_SHARDS - 1);
+    const int nsh = G < ME_SHARDS ? G : ME_SHARDS;
+    unsigned long long* top = a.ctr + ME_SHARDS * ME_CTR_STRIDE;
+    unsigned long long want = 0;
+    int failed = 0;
+    if (lane == 0) {
+      const unsigned long long mine = (unsigned long long)((G - shard + ME_SHARDS - 1) / ME_SHARDS);
+      const unsigned long long old =
+          __hip_atomic_fetch_add(a.ctr + shard * ME_CTR_STRIDE, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long gen = old / mine;
+      if (old + 1 == (gen + 1) * mine) __hip_atomic_fetch_add(top, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      want = (gen + 1) * (unsigned long long)nsh;
+      while (__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+        if (me_now() > deadline) {  // another workgroup never arrived: no activations are read
+          me_fail(a, sm, ME_ERR_HANDOFF);
+          failed = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+    }
+    if (__shfl(failed, 0, 64)) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
     // all I activations -> LDS, every load sc1 (the producers stored them sc1)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.act, 0, a.I * 2, 0x00020000);
     // every load in flight at once (one round trip; 7 dependent groups of 4 cost ~5 us here)
@@ -495,97 +465,7 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
     return true;
   };
 
-  // end of phase B (every consumer once, after its last phase-B slot): the last consumer finishes this
-  // workgroup's h rows. Phase C (N2 > 0): it publishes them, waits for every workgroup's rows (second
-  // hand-off), and forms x2 = rmsnorm(h) * gamma2 in LDS (the P pass's math) for the qkv slots.
-  auto finish_B = [&]() -> bool {
-    me_wait_lgkm0();
-    if (lds_ld(&sm.abort)) return false;  // a wave of this workgroup gave up: h stays unwritten
-    unsigned prev = 0;
-    if (lane == 0) prev = __hip_atomic_fetch_add(&sm.doneB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    prev = __shfl(prev, 0, 64);
-    if (prev != ME_NCONS - 1) return true;
-    if (lds_ld(&sm.abort)) return false;
-    const int nd = d1 - m.d0;
-    if (lane < 16 * nd) {
-      const int g = lane >> 4, rr = lane & 15;
-      float acc = 0.f;
-      for (int kc = 0; kc < m.KB; ++kc) acc += sm.part[(m.nA + g * m.KB + kc) * ME_ROWS + rr];
-      const int row = 16 * (m.d0 + g) + rr;
-      const bf16_t hv = f2bf(acc + (a.P ? sm.hres[16 * g + rr] : bf2f(a.h[row])));
-      if (a.N2)
-        sm.hloc[lane] = hv;
-      else
-        a.h[row] = hv;
-    }
-    if (lane == 0) me_stamp(a, 4);
-    if (!a.N2) return true;
-    // gamma2 into registers now (it does not depend on the hand-off: its loads overlap the wait below)
-    constexpr int NG = 32;  // H <= 8192 (ragk_mlp_engine_ok)
-    uint2 gv[NG];
-#pragma unroll
-    for (int t = 0; t < NG; ++t) {
-      const int i = lane + 64 * t;
-      gv[t] = i < a.H / 4 ? *reinterpret_cast<const uint2*>(a.gamma2 + 4 * i) : make_uint2(0u, 0u);
-    }
-    me_wait_lgkm0();
-    if (lane < 4 * nd) {  // this workgroup's rows are contiguous: 8-B agent-scope stores, as the activations
-      const unsigned long long v = *reinterpret_cast<const unsigned long long*>(sm.hloc + 4 * lane);
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.h + 16 * m.d0 + 4 * lane), v, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (!me_handoff(a, sm, a.ctr + (ME_SHARDS + 1) * ME_CTR_STRIDE, w, G, lane, deadline, ME_ERR_HANDOFF2))
-      return false;
-    // every row of h (sc1 loads, all in flight) -> LDS as bf16, sum of squares
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.h, 0, a.H * 2, 0x00020000);
-    constexpr int NV = ME_VEC / 1024;
-    const int nv = a.H / 8;
-    u32x4 v[NV];
-#pragma unroll
-    for (int u = 0; u < NV; ++u) {
-      const int i = 64 * u + lane;
-      v[u] = i < nv ? __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * i, 0, 16))
-                    : (u32x4){0u, 0u, 0u, 0u};
-    }
-    float ss = 0.f;
-#pragma unroll
-    for (int u = 0; u < NV; ++u) {
-      const int i = 64 * u + lane;
-      if (i < nv) {
-        *reinterpret_cast<u32x4*>(sm.vec + 16 * i) = v[u];
-        float f[4];
-        unpack4(make_uint2(v[u][0], v[u][1]), f);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) ss += f[e] * f[e];
-        unpack4(make_uint2(v[u][2], v[u][3]), f);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) ss += f[e] * f[e];
-      }
-    }
-    ss = wave_sum(ss);
-    const float inv = rsqrtf(ss / (float)a.H + a.eps);
-    me_wait_lgkm0();
-#pragma unroll
-    for (int t = 0; t < NG; ++t) {  // in place: x2 = bf16(gamma2 * bf16(h * inv))
-      const int i = lane + 64 * t;
-      if (i < a.H / 4) {
-        float hf[4], g[4], o[4];
-        unpack4(*reinterpret_cast<const uint2*>(sm.vec + 8 * i), hf);
-        unpack4(gv[t], g);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = g[e] * bf2f(f2bf(hf[e] * inv));
-        *reinterpret_cast<uint2*>(sm.vec + 8 * i) = make_uint2(pk2bf(o[0], o[1]), pk2bf(o[2], o[3]));
-      }
-    }
-    me_wait_lgkm0();
-    if (lane == 0) lds_st(&sm.xReady, 1u);
-    if (lane == 0) me_stamp(a, 5);
-    return true;
-  };
-
-  bool actOk = false, arrivedB = false, xOk = false;
-  const int c1 = m.nA + nB;  // first phase-C slot
+  bool actOk = false;
   for (int s = c; s < nS; s += ME_NCONS) {
     if (s >= m.nA && !arrivedA) {
       arrivedA = true;
@@ -594,14 +474,6 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
     if (s >= m.nA && !actOk) {
       if (!me_spin_lds(&sm.actReady, 1u, a, sm, deadline, ME_ERR_ACT)) return;
       actOk = true;
-    }
-    if (s >= c1 && !arrivedB) {
-      arrivedB = true;
-      if (!finish_B()) return;
-    }
-    if (s >= c1 && !xOk) {
-      if (!me_spin_lds(&sm.xReady, 1u, a, sm, deadline, ME_ERR_X)) return;
-      xOk = true;
     }
     const int r = s % ME_RING;
     if (!me_spin_lds(&sm.full[r], (unsigned)s + 1u, a, sm, deadline, ME_ERR_SLOT)) return;
@@ -625,16 +497,27 @@ __global__ __launch_bounds__(ME_THREADS, 1) void mlp_engine_kernel(MlpArgs a) {
       acc4[ks & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[ks], wf[ks], acc4[ks & 3], 0, 0, 0);
     const f32x4 acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
     // C[m][n]: lane (n, kg) holds rows 4kg..4kg+3 of column n; row 0 (x) sits in lanes 0..15
-    if (s < c1) {
-      if (lane < 16) sm.part[s * ME_ROWS + n] = acc[0];
-    } else if (lane < 16) {  // phase C: the unit's 16 sums go straight to its split-K slab
-      const int u = m.c0 + s - c1;
-      a.P2[(size_t)(u % m.KA) * a.N2 + 16 * (u / m.KA) + n] = acc[0];
-    }
+    if (lane < 16) sm.part[s * ME_ROWS + n] = acc[0];
   }
   if (!arrivedA && !finish_A()) return;
-  if (!arrivedB && !finish_B()) return;
-  if (lane == 0 && a.N2) me_stamp(a, 6);  // (the consumer that stores last: about the workgroup's end)
+
+  // ---------------- phase B tail: the last consumer finishes the rows ----------------
+  me_wait_lgkm0();
+  if (lds_ld(&sm.abort)) return;  // a wave of this workgroup gave up: h stays unwritten
+  unsigned prev = 0;
+  if (lane == 0) prev = __hip_atomic_fetch_add(&sm.doneB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  prev = __shfl(prev, 0, 64);
+  if (prev != ME_NCONS - 1) return;
+  if (lds_ld(&sm.abort)) return;
+  const int nd = d1 - m.d0;
+  if (lane < 16 * nd) {
+    const int g = lane >> 4, rr = lane & 15;
+    float acc = 0.f;
+    for (int kc = 0; kc < m.KB; ++kc) acc += sm.part[(m.nA + g * m.KB + kc) * ME_ROWS + rr];
+    const int row = 16 * (m.d0 + g) + rr;
+    a.h[row] = f2bf(acc + (a.P ? sm.hres[16 * g + rr] : bf2f(a.h[row])));
+  }
+  if (lane == 0) me_stamp(a, 4);
 }
 
 int g_me_nt = 1;
@@ -649,7 +532,7 @@ unsigned long long* g_me_stamps = nullptr;
 RAGK_API int ragk_mlp_engine_ok(int M, int H, int I, int G) {
   if (M != 1 || G < 1 || H <= 0 || I <= 0) return 0;
   if (H % ME_KC || I % ME_KC || I % 64 || H % 16) return 0;
-  if (2 * H > ME_VEC || 2 * I > ME_VEC || H > 8192) return 0;
+  if (2 * H > ME_VEC || 2 * I > ME_VEC) return 0;
   const int NA = I / 8, ND = H / 16;
   const long long T = me_cum(G, g_me_w_even, g_me_w_odd);
   const int wmax = g_me_w_even > g_me_w_odd ? g_me_w_even : g_me_w_odd;
@@ -691,20 +574,15 @@ RAGK_API int ragk_mlp_engine_set_stamps(void* p) {
 // (h += bf16(sum P); x = rmsnorm(h) * gamma, add_partials_rmsnorm's math, inside the launch).
 // err: device error word; err_host: device address of a host-mapped word (may be null); tmo: device word
 // holding the deadline in s_memrealtime ticks (0 = default).
-// N2 > 0: phase C, the NEXT layer's input norm and qkv GEMM in the same launch: P2 [H / 512][N2] fp32 split-K
-// slabs of rmsnorm(h_out) * gamma2 . wqkv^T (wqkv [N2][H]); the decode attention reduces them.
 RAGK_API int ragk_mlp_engine(const void* xn, const float* P, int S, const void* gamma, float eps, const void* wgu,
                              const void* wd, void* h, void* act, void* ctr, void* err, void* err_host, const void* tmo,
-                             const void* wqkv, const void* gamma2, float* P2, int N2, int M, int H, int I, int G,
-                             hipStream_t st) {
+                             int M, int H, int I, int G, hipStream_t st) {
   if (!ragk_mlp_engine_ok(M, H, I, G)) return (int)hipErrorInvalidValue;
   if (!wgu || !wd || !h || !act || !ctr || !err || !tmo || (!xn && (!P || !gamma || S < 1 || H % 4)))
     return (int)hipErrorInvalidValue;
-  if (N2 < 0 || N2 % 16 || (N2 && (!wqkv || !gamma2 || !P2))) return (int)hipErrorInvalidValue;
   MlpArgs a{(const bf16_t*)xn, xn ? nullptr : P, (const bf16_t*)gamma, eps, S, (const bf16_t*)wgu,
             (const bf16_t*)wd, (bf16_t*)h, (bf16_t*)act, (unsigned long long*)ctr, (unsigned*)err,
-            (unsigned*)err_host, (const unsigned*)tmo, g_me_stamps, (const bf16_t*)wqkv, (const bf16_t*)gamma2,
-            P2, H, I, N2, g_me_w_even, g_me_w_odd};
+            (unsigned*)err_host, (const unsigned*)tmo, g_me_stamps, H, I, g_me_w_even, g_me_w_odd};
   if (g_me_nt)
     hipLaunchKernelGGL(mlp_engine_kernel<true>, dim3(G), dim3(ME_THREADS), 0, st, a);
   else
@@ -712,10 +590,9 @@ RAGK_API int ragk_mlp_engine(const void* xn, const float* P, int S, const void* 
   return (int)hipGetLastError();
 }
 
-// bytes of the workspace counters the host allocates zeroed and re-arms after an error: two hand-off counter
-// sets (8 shard lines + the top counter's line each; the error word and the timeout word follow them:
-// ops/native.py _me_workspace)
-RAGK_API int ragk_mlp_engine_ctr_bytes() { return 2 * (ME_SHARDS + 1) * ME_CTR_STRIDE * 8; }
+// bytes of the workspace counters the host allocates zeroed and re-arms after an error (the error word and
+// the timeout word follow them: ops/native.py _me_workspace)
+RAGK_API int ragk_mlp_engine_ctr_bytes() { return (ME_SHARDS + 1) * ME_CTR_STRIDE * 8; }
 
 // Host-mapped, coherent pinned words (64 B): the kernels' error reports the engine reads after every step
 // without a device sync. Returns the host pointer (null on failure); ragk_host_word_dev gives the device one.

@@ -347,17 +347,9 @@ class LlamaModel:
         merge = M <= DECODE_OPROJ_MERGE_MAX_M and be.part_merge_ok(M, inp.meta, layers[0]["wo"], Hq, D)
         # batch 1: gate/up + SiLU + down + residual as ONE persistent launch (csrc/kernels/mlp_engine.hip)
         mlp_eng = M == 1 and not tp and be.mlp_engine_ok(M, layers[0]["wgu"], layers[0]["wdown"])
-        # ... and the next layer's input norm + qkv GEMM in the same launch (a second hand-off on h)
-        eng_next = (mlp_eng and fuse_norm and len(layers) > 1
-                    and be.mlp_engine_next_ok(layers[0]["wgu"], layers[0]["wdown"], layers[1]["wqkv"]))
-        Pq = None  # the next layer's qkv slabs when the previous engine launch produced them
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
-            if Pq is not None:
-                P, Pq = Pq, None
-            else:
-                P = (be.gemm_part_norm(h, L["ln_in"], c.rms_norm_eps, L["wqkv"]) if fuse_norm
-                     else be.gemm_part(xn, L["wqkv"]))
+            P = be.gemm_part_norm(h, L["ln_in"], c.rms_norm_eps, L["wqkv"]) if fuse_norm else be.gemm_part(xn, L["wqkv"])
             # RoPE + KV append inside the attention kernel; at batch <= 2 its split-K merge inside the o_proj GEMM
             be.attn_decode_rope(P, inp.positions, self.cos, self.sin, inp.slots, kc, vc, inp.meta, attn, Hq, Hkv, D,
                                 defer_merge=merge)
@@ -365,10 +357,6 @@ class LlamaModel:
             nxt = layers[li + 1]["ln_in"] if li + 1 < len(layers) else w.norm
             if mlp_eng:
                 # o_proj slabs + residual + post-attention norm + gate/up + SiLU + down + residual: one launch
-                if eng_next and li + 1 < len(layers):  # + the next layer's input norm and qkv partials
-                    Pq = be.mlp_engine_tail(P, h, L["ln_post"], c.rms_norm_eps, L["wgu"], L["wdown"],
-                                            layers[li + 1]["wqkv"], nxt)
-                    continue
                 be.mlp_engine_tail(P, h, L["ln_post"], c.rms_norm_eps, L["wgu"], L["wdown"])
                 if not fuse_norm or li + 1 == len(layers):
                     xn = be.rmsnorm(h, nxt, c.rms_norm_eps)

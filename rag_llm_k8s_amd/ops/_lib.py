@@ -46,7 +46,7 @@ _SIGS = {
     "ragk_mlp_engine_set_nt": [I],
     "ragk_mlp_engine_set_stamps": [P],
     "ragk_mlp_engine_set_xcd_weights": [I, I],
-    "ragk_mlp_engine": [P, P, I, P, F, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, S],
+    "ragk_mlp_engine": [P, P, I, P, F, P, P, P, P, P, P, P, P, I, I, I, I, S],
     "ragk_host_word_alloc": [],
     "ragk_host_word_dev": [P],
     "ragk_host_word_free": [P],

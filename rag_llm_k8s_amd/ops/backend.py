@@ -152,16 +152,9 @@ class TorchBackend:
         h.copy_((h.float() + a.float() @ w_down.float().t()).to(h.dtype))
         return h
 
-    def mlp_engine_tail(self, P, h, gamma, eps, w_gu, w_down, next_wqkv=None, next_gamma=None):
-        """add_partials_rmsnorm (o_proj slabs + residual + post-attention norm) then mlp_engine, one op;
-        with next_wqkv / next_gamma also the next layer's input norm + qkv partials (gemm_part_norm)."""
-        self.mlp_engine(self.add_partials_rmsnorm(P, h, gamma, eps), w_gu, w_down, h)
-        if next_wqkv is None:
-            return h
-        return self.gemm_part_norm(h, next_gamma, eps, next_wqkv)
-
-    def mlp_engine_next_ok(self, w_gu, w_down, next_wqkv):
-        return self.mlp_engine_ok(1, w_gu, w_down) and not isinstance(next_wqkv, Fp8Weight)
+    def mlp_engine_tail(self, P, h, gamma, eps, w_gu, w_down):
+        """add_partials_rmsnorm (o_proj slabs + residual + post-attention norm) then mlp_engine, one op."""
+        return self.mlp_engine(self.add_partials_rmsnorm(P, h, gamma, eps), w_gu, w_down, h)
 
     def add_partials_rmsnorm(self, P, h, w, eps):
         h.copy_((h.float() + P.sum(0).to(h.dtype).float()).to(h.dtype))
@@ -311,12 +304,8 @@ class NativeBackend(TorchBackend):
     def mlp_engine(self, xn, w_gu, w_down, h):
         return self.n.mlp_engine(xn, w_gu, w_down, h)
 
-    def mlp_engine_tail(self, P, h, gamma, eps, w_gu, w_down, next_wqkv=None, next_gamma=None):
-        return self.n.mlp_engine_tail(P, h, gamma, eps, w_gu, w_down, next_wqkv, next_gamma)
-
-    def mlp_engine_next_ok(self, w_gu, w_down, next_wqkv):
-        return (not isinstance(next_wqkv, Fp8Weight) and self.n.MLP_ENGINE_NEXT_QKV
-                and self.n.mlp_engine_next_ok(w_gu, w_down, next_wqkv))
+    def mlp_engine_tail(self, P, h, gamma, eps, w_gu, w_down):
+        return self.n.mlp_engine_tail(P, h, gamma, eps, w_gu, w_down)
 
     def rope_kv_partials(self, P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D):
         self.n.rope_kv_partials(P, q_out, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)

@@ -458,9 +458,6 @@ def gemm_part_silu(pgu, w, out=None):
 # Batch-1 decode MLP as one persistent launch (csrc/kernels/mlp_engine.hip): h += W_down (silu(W_gate x) *
 # (W_up x)) with both weight streams going through one LDS ring per CU (RAGK_MLP_ENGINE=0 turns it off). Batch-1 decode step 3.47 -> 3.34 ms (profiles/mlp_engine_r5.log).
 MLP_ENGINE = os.environ.get("RAGK_MLP_ENGINE", "1") != "0"
-# The engine also runs the NEXT layer's input norm + qkv GEMM (phase C, a second hand-off on h at the end of
-# the launch; models/llama.py hidden_states_decode_part) instead of a separate gemm_part_norm launch.
-MLP_ENGINE_NEXT_QKV = False  # measured slower (docs/PERF_NOTES.md "Round 6")
 _me_ws = {}
 
 
@@ -541,49 +538,27 @@ def mlp_engine(xn, w_gu, w_down, h):
     return _mlp_engine_launch(xn.data_ptr(), None, 0, None, 0.0, w_gu, w_down, h)
 
 
-def mlp_engine_tail(P, h, gamma, eps, w_gu, w_down, next_wqkv=None, next_gamma=None):
+def mlp_engine_tail(P, h, gamma, eps, w_gu, w_down):
     """The batch-1 post-attention tail in one launch: h += bf16(sum of the o_proj slabs P [S, 1, H]);
-    x = rmsnorm(h) * gamma (add_partials_rmsnorm's math); h += W_down . (silu(gate) * up).
-    With next_wqkv [N2, H] / next_gamma [H] (the next layer's qkv weight and input-norm weight) the same
-    launch also forms rmsnorm(h) * next_gamma after a second chip-wide hand-off and streams the next qkv
-    GEMM; returns its split-K slabs [H / 512, 1, N2] fp32 (attn_decode_rope's input, gemm_part_norm's
-    layout). Otherwise returns h."""
+    x = rmsnorm(h) * gamma (add_partials_rmsnorm's math); h += W_down . (silu(gate) * up)."""
     H = w_down.shape[0]
     _req(P.dtype == torch.float32 and P.is_cuda and P.is_contiguous() and P.dim() == 3 and P.shape[1:] == (1, H),
          "P [S, 1, H] fp32")
     _req(gamma.dtype == torch.bfloat16 and gamma.is_contiguous() and gamma.numel() == H, "gamma [H] bf16")
-    return _mlp_engine_launch(None, P.data_ptr(), P.shape[0], gamma.data_ptr(), float(eps), w_gu, w_down, h,
-                              next_wqkv, next_gamma)
+    return _mlp_engine_launch(None, P.data_ptr(), P.shape[0], gamma.data_ptr(), float(eps), w_gu, w_down, h)
 
 
-def mlp_engine_next_ok(w_gu, w_down, next_wqkv):
-    """Whether the engine can also run the next layer's qkv GEMM (phase C) for these weights."""
-    H = w_down.shape[0]
-    return (mlp_engine_ok(1, w_gu, w_down) and next_wqkv.dtype == torch.bfloat16 and next_wqkv.dim() == 2
-            and next_wqkv.shape[1] == H and next_wqkv.shape[0] % 16 == 0 and next_wqkv.stride(0) == H
-            and next_wqkv.stride(1) == 1)
-
-
-def _mlp_engine_launch(xn_ptr, P_ptr, S, g_ptr, eps, w_gu, w_down, h, next_wqkv=None, next_gamma=None):
+def _mlp_engine_launch(xn_ptr, P_ptr, S, g_ptr, eps, w_gu, w_down, h):
     _bf16_2d(h, "h")
     H, I = w_down.shape
     _req(h.shape == (1, H) and h.is_contiguous(), "h [1, H]")
     _req(mlp_engine_ok(1, w_gu, w_down), "mlp_engine shape")
     ws = _me_workspace(h.device, I)
-    P2, N2, wq, g2 = None, 0, 0, 0
-    if next_wqkv is not None:
-        _req(mlp_engine_next_ok(w_gu, w_down, next_wqkv), "mlp_engine next qkv shape")
-        _req(next_gamma is not None and next_gamma.dtype == torch.bfloat16 and next_gamma.is_contiguous()
-             and next_gamma.numel() == H, "next_gamma [H] bf16")
-        N2 = next_wqkv.shape[0]
-        P2 = torch.empty((H // 512, 1, N2), dtype=torch.float32, device=h.device)
-        wq, g2 = next_wqkv.data_ptr(), next_gamma.data_ptr()
     check(_lib.lib().ragk_mlp_engine(xn_ptr, P_ptr, S, g_ptr, eps, w_gu.data_ptr(), w_down.data_ptr(), h.data_ptr(),
-                                     ws.act.data_ptr(), ws.words.data_ptr(), ws.err_ptr, ws.host_dev, ws.tmo_ptr, wq,
-                                     g2, P2.data_ptr() if P2 is not None else None, N2, 1, H, I, _cu_count(),
-                                     stream_ptr()),
+                                     ws.act.data_ptr(), ws.words.data_ptr(), ws.err_ptr, ws.host_dev, ws.tmo_ptr, 1,
+                                     H, I, _cu_count(), stream_ptr()),
           "ragk_mlp_engine")
-    return P2 if P2 is not None else h
+    return h
 
 
 def mlp_engine_fault(dev=None) -> int:

@@ -51,21 +51,6 @@ def main():
         for wgu, wd in layers:
             native.mlp_engine_tail(P, h, gamma, 1e-5, wgu, wd)
 
-    # ME_NEXT=1: also the next layer's input norm + qkv GEMM (8B: 6144 x 4096): the engine's phase C against
-    # the engine followed by the separate gemm_part_norm launch, each per layer; stage stamps of phase C
-    wqkvs = []
-    if os.environ.get("ME_NEXT") == "1":
-        wqkvs = [(torch.randn(6144, H, device=dev) / math.sqrt(H)).bfloat16() for _ in range(L)]
-
-    def engine_then_qkv():
-        for (wgu, wd), wq in zip(layers, wqkvs):
-            native.mlp_engine_tail(P, h, gamma, 1e-5, wgu, wd)
-            native.gemm_part_norm(h, gamma, 1e-5, wq)
-
-    def engine_next():
-        for (wgu, wd), wq in zip(layers, wqkvs):
-            native.mlp_engine_tail(P, h, gamma, 1e-5, wgu, wd, wq, gamma)
-
     def graph_of(fn):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -90,29 +75,6 @@ def main():
     nts = [int(t) for t in os.environ.get("ME_NT", "1").split(",") if t]
     # ME_XW="27:32,1:1": alternate the per-XCD phase-A weights (even:odd) -- engine runs per setting
     xws = [tuple(int(v) for v in s.split(":")) for s in os.environ.get("ME_XW", "").split(",") if s] or [None]
-    if wqkvs:
-        g_a, g_b = graph_of(engine_then_qkv), graph_of(engine_next)
-        for rnd in range(3):
-            ta, tb = timed(g_a), timed(g_b)
-            native.mlp_engine_check()
-            print("round %d: engine + gemm_part_norm %.2f us/layer, engine with phase C %.2f us/layer" % (rnd, ta, tb),
-                  flush=True)
-        del g_a, g_b
-        from rag_llm_k8s_amd.ops import _lib
-        G = native._cu_count()
-        st = torch.zeros(G, 8, dtype=torch.int64, device=dev)
-        _lib.lib().ragk_mlp_engine_set_stamps(st.data_ptr())
-        for li in range(4):
-            st.zero_()
-            native.mlp_engine_tail(P, h, gamma, 1e-5, layers[li][0], layers[li][1], wqkvs[li], gamma)
-            torch.cuda.synchronize()
-        _lib.lib().ragk_mlp_engine_set_stamps(None)
-        us = (st.cpu().double() - st[:, 0].min().item()) / 100.0
-        names = ["start", "loader done", "phase A done", "act ready", "B rows done", "x2 ready", "end"]
-        for i, n in enumerate(names):
-            col = us[:, i]
-            print("stamp %-13s min %7.2f  p50 %7.2f  max %7.2f us" % (n, col.min(), col.median(), col.max()), flush=True)
-        return
     g_sep = graph_of(separate)
     for rnd in range(2):
         print("round %d: separate kernels %.2f us/layer" % (rnd, timed(g_sep)), flush=True)
