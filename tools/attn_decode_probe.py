@@ -49,8 +49,20 @@ def main():
     slots = torch.tensor([int(bt[i, p // 64]) * 64 + p % 64 for i, p in enumerate(pos.tolist())], dtype=torch.int32)
     kvl = torch.tensor(lens, dtype=torch.int32)
     bt, pos, slots, kvl = bt.to(dev), pos.to(dev), slots.to(dev), kvl.to(dev)
-    caches = [(torch.randn(nblocks, Hkv, 64, D, device=dev).bfloat16(), torch.randn(nblocks, Hkv, 64, D, device=dev).bfloat16())
-              for _ in range(NL)]
+    # AP_VOFF=bytes: K and V of a layer in ONE allocation, V starting that many bytes past the end of K (a
+    # tile's K and V pieces then sit at different offsets modulo the memory interleave); default: two
+    # separate allocations
+    voff = int(os.environ.get("AP_VOFF", "-1"))
+
+    def kv_pair():
+        n = nblocks * Hkv * 64 * D
+        if voff < 0:
+            return (torch.randn(nblocks, Hkv, 64, D, device=dev).bfloat16(),
+                    torch.randn(nblocks, Hkv, 64, D, device=dev).bfloat16())
+        buf = torch.randn(2 * n + voff // 2, device=dev).bfloat16()
+        return buf[:n].view(nblocks, Hkv, 64, D), buf[n + voff // 2:2 * n + voff // 2].view(nblocks, Hkv, 64, D)
+
+    caches = [kv_pair() for _ in range(NL)]
     cos, sin = rope_tables(D, 8192, 500000.0, None)
     cos, sin = cos.to(dev), sin.to(dev)
     P = torch.randn(4, B, (Hq + 2 * Hkv) * D, device=dev) * 0.1
