@@ -344,4 +344,5 @@ enum RagkEpilogue : int {
   EPI_SILU_MUL = 5,  // paired columns: C[:, j] = silu(gate_j) * up_j
   EPI_GELU = 6,      // C = gelu_erf(acc)
   EPI_BIAS_GELU_TANH = 7,  // GPT-2 MLP
+  EPI_ROPE_KV = 8,   // qkv projection (D = 128 heads): RoPE on q / k, k and v rows also into the paged KV cache
 };

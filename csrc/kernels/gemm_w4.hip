@@ -160,6 +160,7 @@ constexpr bool epi_bias(int e) {
 
 template <int EPI, bool OUT_F32>
 constexpr int w4_epi_vmem() {
+  if constexpr (EPI == EPI_ROPE_KV) return 63;    // loads + stores over the counter's range: the bound clamps
   if constexpr (EPI == EPI_SILU_MUL) return 16;  // 8 rows x 2 pairs of 16-B stores
   if constexpr (OUT_F32) return 64 + (epi_res(EPI) ? 64 : 0) + (epi_bias(EPI) ? 8 : 0);
   return 32 + (epi_res(EPI) ? 32 : 0) + (epi_bias(EPI) ? 4 : 0);
@@ -247,6 +248,90 @@ __device__ __forceinline__ void w4_epilogue_full_bf16(const f32x4 (&acc)[8][8], 
 #pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = w4_act<EPI>(o[k]);
         *reinterpret_cast<u32x4*>(Cb + (size_t)(row0 + 16 * i) * ldc + colw + 32 * p) = pack8(o);
+      }
+    }
+  }
+}
+
+// EPI_ROPE_KV: the qkv projection's epilogue does rope_kv's work (norm.hip rope_kv_kernel, the same bf16
+// rounding of every op, the same cos / sin tables: bit-identical): a wave's 128 columns are one head; lane
+// (fr, fh) holds, per row, columns 8fh + 32p + 0..7 (p = 0..3), so the rotate_half pairs d / d + 64 are
+// p / p + 2 of the same lane. q heads: rotated into C; k heads: rotated into C and the paged cache at the
+// row's slot; v heads: C and the cache. Rows two at a time (cos / sin in registers: 64 values), loads
+// never predicated (rows past M clamp; only the stores are guarded).
+struct RopeKV {
+  const int* pos;
+  const int* slot;
+  const float* cos_t;  // [positions][64]
+  const float* sin_t;
+  bf16_t* kc;          // [blocks][Hkv][BS][128]
+  bf16_t* vc;
+  int Hq, Hkv, BS;
+};
+
+template <bool FULL>
+__device__ __forceinline__ void w4_epilogue_rope(const f32x4 (&acc)[8][8], int wr, int wc, int fr, int fh, int m0,
+                                                 int n0, bf16_t* C, int ldc, const RopeKV& rk, int M) {
+  const int row0 = m0 + wr * 128 + fr;
+  const int hd = (n0 + wc * 128) >> 7;
+  const int d0 = 8 * fh;
+  const bool isq = hd < rk.Hq, isk = !isq && hd < rk.Hq + rk.Hkv, rot = hd < rk.Hq + rk.Hkv;
+  const int kvh = isk ? hd - rk.Hq : hd - rk.Hq - rk.Hkv;
+  bf16_t* cache = isk ? rk.kc : rk.vc;
+  int pos[8], slot[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = FULL ? row0 + 16 * i : min(row0 + 16 * i, M - 1);
+    pos[i] = rk.pos[r];
+    slot[i] = rk.slot[r];
+  }
+#pragma unroll
+  for (int i2 = 0; i2 < 8; i2 += 2) {
+    u32x4 cv[2][2][2], sv[2][2][2];  // [row][p][half]
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const float* ct = rk.cos_t + (size_t)pos[i2 + u] * 64 + d0 + 32 * p;
+        const float* st = rk.sin_t + (size_t)pos[i2 + u] * 64 + d0 + 32 * p;
+        cv[u][p][0] = *reinterpret_cast<const u32x4*>(ct);
+        cv[u][p][1] = *reinterpret_cast<const u32x4*>(ct + 4);
+        sv[u][p][0] = *reinterpret_cast<const u32x4*>(st);
+        sv[u][p][1] = *reinterpret_cast<const u32x4*>(st + 4);
+      }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = i2 + u;
+      const int gr = row0 + 16 * i;
+      float o[4][8];
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          o[p][k] = bf2f(f2bf(acc[i][2 * p][k]));
+          o[p][4 + k] = bf2f(f2bf(acc[i][2 * p + 1][k]));
+        }
+      if (rot) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float c = __uint_as_float(cv[u][p][k >> 2][k & 3]), sn = __uint_as_float(sv[u][p][k >> 2][k & 3]);
+            const float x1 = o[p][k], x2 = o[p + 2][k];
+            o[p][k] = bf2f(f2bf(bf2f(f2bf(x1 * c)) + bf2f(f2bf(-x2 * sn))));
+            o[p + 2][k] = bf2f(f2bf(bf2f(f2bf(x2 * c)) + bf2f(f2bf(x1 * sn))));
+          }
+      }
+      if (FULL || gr < M) {
+        bf16_t* crow = C + (size_t)gr * ldc + n0 + wc * 128 + d0;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) *reinterpret_cast<u32x4*>(crow + 32 * p) = pack8(o[p]);
+        const int sl = slot[i];
+        if (!isq && sl >= 0) {
+          bf16_t* dst = cache + (((size_t)(sl / rk.BS) * rk.Hkv + kvh) * rk.BS + (sl % rk.BS)) * 128 + d0;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) *reinterpret_cast<u32x4*>(dst + 32 * p) = pack8(o[p]);
+        }
       }
     }
   }
@@ -471,7 +556,7 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
                                                                 const bf16_t* __restrict__ B, int ldb, void* C,
                                                                 int ldc, const bf16_t* __restrict__ bias,
                                                                 const bf16_t* resid, int ldr, int M, int N, int K,
-                                                                int nsplit) {
+                                                                int nsplit, RopeKV rk) {
   __shared__ __attribute__((aligned(16))) char smem[W4_LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -495,6 +580,7 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
   // before the data landed (tools/isa_lds_hazard.py checks every instantiation for that). Those read
   // them after the epilogue instead.
   constexpr bool LATE_F0 = !(EPI == EPI_NONE || EPI == EPI_SILU_MUL || (EPI == EPI_RESID && !OUT_F32));
+  static_assert(EPI != EPI_ROPE_KV || (!OUT_F32 && !KSPLIT), "rope epilogue: bf16 output, no split-K");
 
   int tile = blockIdx.x;
   int z = KSPLIT ? tile / nwg : 0;
@@ -572,7 +658,14 @@ __global__ __launch_bounds__(W4_THREADS, 1) void gemm_w4_kernel(const bf16_t* __
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     w4_pin_acc(acc);
     void* Cz = KSPLIT ? (void*)(reinterpret_cast<float*>(C) + (size_t)z * M * ldc) : C;
-    if (m0 + WBM <= M && n0 + WBN <= N) {
+    if constexpr (EPI == EPI_ROPE_KV) {
+      if (m0 + WBM <= M) {
+        w4_epilogue_rope<true>(acc, wr, wc, fr, fh, m0, n0, reinterpret_cast<bf16_t*>(Cz), ldc, rk, M);
+      } else {
+        w4_epilogue_rope<false>(acc, wr, wc, fr, fh, m0, n0, reinterpret_cast<bf16_t*>(Cz), ldc, rk, M);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // guarded: count unknown, drain (the next K-tile 1 lands too)
+      }
+    } else if (m0 + WBM <= M && n0 + WBN <= N) {
       if constexpr (OUT_F32)
         w4_epilogue_reg<EPI, true, true>(acc, wr, wc, fr, fh, m0, n0, Cz, ldc, bias, resid, ldr, M, Nout);
       else
@@ -616,7 +709,8 @@ int launch_w4(const void* A, int lda, const void* B, int ldb, void* C, int ldc, 
               int ldr, int M, int N, int K, hipStream_t st) {
   const int nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
   hipLaunchKernelGGL((gemm_w4_kernel<EPI, F32>), dim3(w4_grid(nwg)), dim3(W4_THREADS), 0, st, (const bf16_t*)A, lda,
-                     (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K, 1);
+                     (const bf16_t*)B, ldb, C, ldc, (const bf16_t*)bias, (const bf16_t*)resid, ldr, M, N, K, 1,
+                     RopeKV{});
   return (int)hipGetLastError();
 }
 
@@ -672,6 +766,24 @@ RAGK_API int ragk_gemm_w4_splitk(const void* A, int lda, const void* B, int ldb,
   const int nwg = ((M + WBM - 1) / WBM) * ((N + WBN - 1) / WBN);
   hipLaunchKernelGGL((gemm_w4_kernel<EPI_NONE, true, true>), dim3(w4_grid(nwg * nsplit)), dim3(W4_THREADS), 0, st,
                      (const bf16_t*)A, lda, (const bf16_t*)B, ldb, (void*)P, N, nullptr, nullptr, 0, M, N, K / nsplit,
-                     nsplit);
+                     nsplit, RopeKV{});
+  return (int)hipGetLastError();
+}
+
+// qkv = A . B^T (B = [(Hq + 2 Hkv) * 128][K]) with rope_kv's work in the epilogue (EPI_ROPE_KV above): q and
+// k rotated (positions pos[M], tables cos_t / sin_t [positions][64]), k and v rows also into the paged caches
+// kc / vc [blocks][Hkv][BS][128] at slot[M] (slot < 0: not cached). Same conditions as ragk_gemm_w4.
+RAGK_API int ragk_gemm_w4_rope_kv(const void* A, int lda, const void* B, int ldb, void* C, int ldc, int M, int K,
+                                  const int* pos, const int* slot, const float* cos_t, const float* sin_t, void* kc,
+                                  void* vc, int Hq, int Hkv, int BS, hipStream_t st) {
+  if (M <= 0) return 0;
+  const int N = (Hq + 2 * Hkv) * 128;
+  if (K % WBK != 0 || K / WBK < W4_MIN_KT || Hq < 1 || Hkv < 1 || BS < 1 || N % WBN != 0) return (int)hipErrorInvalidValue;
+  if (!pos || !slot || !cos_t || !sin_t || !kc || !vc || ldc % 8 != 0) return (int)hipErrorInvalidValue;
+  if ((long long)M * lda * 2 >= (1LL << 31) || (long long)N * ldb * 2 >= (1LL << 31)) return (int)hipErrorInvalidValue;
+  const int nwg = ((M + WBM - 1) / WBM) * (N / WBN);
+  const RopeKV rk{pos, slot, cos_t, sin_t, (bf16_t*)kc, (bf16_t*)vc, Hq, Hkv, BS};
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI_ROPE_KV, false>), dim3(w4_grid(nwg)), dim3(W4_THREADS), 0, st,
+                     (const bf16_t*)A, lda, (const bf16_t*)B, ldb, C, ldc, nullptr, nullptr, 0, M, N, K, 1, rk);
   return (int)hipGetLastError();
 }

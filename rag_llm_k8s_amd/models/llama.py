@@ -273,8 +273,7 @@ class LlamaModel:
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
         kc, vc = self.kv_cache[li]
         xn = be.rmsnorm(h, L["ln_in"], c.rms_norm_eps)
-        qkv = be.gemm(xn, L["wqkv"])
-        be.rope_kv(qkv, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
+        qkv = be.gemm_rope_kv(xn, L["wqkv"], inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
         if inp.meta.kind == "decode":
             be.attn_decode(qkv, kc, vc, inp.meta, attn, Hq, Hkv, D)
         else:
@@ -411,8 +410,7 @@ class LlamaModel:
         xn = be.rmsnorm(h, layers[0]["ln_in"], c.rms_norm_eps)
         for li, L in enumerate(layers):
             kc, vc = self.kv_cache[li]
-            qkv = be.gemm(xn, L["wqkv"])
-            be.rope_kv(qkv, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
+            qkv = be.gemm_rope_kv(xn, L["wqkv"], inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
             be.attn_prefill(qkv, kc, vc, inp.meta, attn, Hq, Hkv, D)
             if ns_o > 1:
                 xn = be.add_partials_rmsnorm(be.gemm_splitk(attn, L["wo"], ns_o), h, L["ln_post"], c.rms_norm_eps)
@@ -459,8 +457,7 @@ class LlamaModel:
         for li, L in enumerate(w.layers):
             kc, vc = self.kv_cache[li]
             comm.all_gather_into(xg, be.rmsnorm(h, L["ln_in"], c.rms_norm_eps))
-            qkv = be.gemm(xg[:T], L["wqkv"])
-            be.rope_kv(qkv, inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
+            qkv = be.gemm_rope_kv(xg[:T], L["wqkv"], inp.positions, self.cos, self.sin, inp.slots, kc, vc, Hq, Hkv, D)
             be.attn_prefill(qkv, kc, vc, inp.meta, attn, Hq, Hkv, D)
             be.gemm(attn, L["wo"], out=part[:T])
             h += comm.reduce_scatter(part, rs)

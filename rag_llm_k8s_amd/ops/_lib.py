@@ -28,6 +28,7 @@ _SIGS = {
     "ragk_gemm_stream_set_diag": [I],
     "ragk_gemm_stream_set_pair_rows": [I],
     "ragk_gemm_w4": [P, I, P, I, P, I, P, P, I, I, I, I, I, I, S],
+    "ragk_gemm_w4_rope_kv": [P, I, P, I, P, I, I, I, P, P, P, P, P, P, I, I, I, S],
     "ragk_gemm_w4_splitk": [P, I, P, I, P, I, I, I, I, S],
     "ragk_gemm_part": [P, I, P, I, P, I, I, I, I, S],
     "ragk_gemm_part_norm": [P, I, P, F, P, I, P, I, I, I, I, S],

@@ -111,6 +111,13 @@ class TorchBackend:
             kc[s // KV_BLOCK, :, s % KV_BLOCK] = k[ok]
             vc[s // KV_BLOCK, :, s % KV_BLOCK] = v[ok]
 
+    def gemm_rope_kv(self, x, w, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D):
+        """qkv projection + rope_kv (the GPU backend fuses them into the GEMM epilogue)."""
+        qkv = self.gemm(x, w)
+        self.rope_kv(qkv, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)
+        return qkv
+
+
     # split-K decode path (GPU: gemm_part.hip + the consumers in norm.hip) ----------------
     enable_part = False  # the torch oracle runs the same dataflow when a test switches it on
 
@@ -269,6 +276,13 @@ class NativeBackend(TorchBackend):
 
     def rope_kv(self, qkv, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D, apply_rope=True):
         self.n.rope_kv(qkv, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D, apply_rope=apply_rope)
+
+    def gemm_rope_kv(self, x, w, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D):
+        if self.n.gemm_rope_kv_ok(x, w, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D):
+            return self.n.gemm_rope_kv(x, w, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)
+        qkv = self.gemm(x, w)
+        self.rope_kv(qkv, positions, cos_t, sin_t, slots, kc, vc, Hq, Hkv, D)
+        return qkv
 
     enable_part = __import__("os").environ.get("RAGK_DECODE_PART", "1") == "1"
 

@@ -100,6 +100,53 @@ def use_pp(M, N, K, epi):
 PREFILL_BLAS = os.environ.get("RAGK_PREFILL_BLAS", "none")
 
 
+# The prefill qkv projection with rope_kv's work in the gemm_w4 epilogue (RoPE on q / k, k and v rows into
+# the paged cache; bit-identical to gemm + rope_kv): one pass over the 32k-token chunk's qkv fewer.
+PREFILL_ROPE_FUSED = os.environ.get("RAGK_PREFILL_ROPE", "1") != "0"
+
+
+def gemm_rope_kv_ok(x, w, positions, cos_t, sin_t, slots, k_cache, v_cache, Hq, Hkv, D):
+    """Whether gemm_rope_kv takes these operands (else: gemm + rope_kv)."""
+    if not PREFILL_ROPE_FUSED or D != 128 or slots is None or k_cache is None or v_cache is None:
+        return False
+    if not (isinstance(x, torch.Tensor) and isinstance(w, torch.Tensor) and x.is_cuda and w.dim() == 2):
+        return False
+    M, K = x.shape
+    N = w.shape[0]
+    if N != (Hq + 2 * Hkv) * D or N % 256 or w.shape[1] != K or not use_pp(M, N, K, "none"):
+        return False
+    if PREFILL_BLAS in ("plain", "all"):
+        return False
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or x.stride(1) != 1 or w.stride(1) != 1:
+        return False
+    if x.stride(0) * M * 2 >= 2 ** 31 or w.stride(0) * N * 2 >= 2 ** 31:
+        return False
+    if not (k_cache.is_contiguous() and v_cache.is_contiguous() and k_cache.dim() == 4 and k_cache.shape[1] == Hkv
+            and k_cache.shape[3] == D and v_cache.shape == k_cache.shape and k_cache.dtype == torch.bfloat16):
+        return False
+    if not (cos_t.dtype == torch.float32 and sin_t.dtype == torch.float32 and cos_t.is_contiguous()
+            and sin_t.is_contiguous() and cos_t.shape[-1] == D // 2):
+        return False
+    return (positions.dtype == torch.int32 and slots.dtype == torch.int32 and positions.is_contiguous()
+            and slots.is_contiguous() and positions.numel() == M and slots.numel() == M)
+
+
+def gemm_rope_kv(x, w, positions, cos_t, sin_t, slots, k_cache, v_cache, Hq, Hkv, D, out=None):
+    """qkv = x @ w^T with RoPE applied to q and k and the k / v rows written to the paged cache at `slots`
+    (gemm + rope_kv in one launch; callers check gemm_rope_kv_ok first)."""
+    _req(gemm_rope_kv_ok(x, w, positions, cos_t, sin_t, slots, k_cache, v_cache, Hq, Hkv, D), "gemm_rope_kv operands")
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    _req(out.shape == (M, N) and out.stride(1) == 1 and out.stride(0) % 8 == 0, "gemm_rope_kv out")
+    check(_lib.lib().ragk_gemm_w4_rope_kv(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(),
+                                          out.stride(0), M, K, positions.data_ptr(), slots.data_ptr(),
+                                          cos_t.data_ptr(), sin_t.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                                          Hq, Hkv, k_cache.shape[2], stream_ptr()), "ragk_gemm_w4_rope_kv")
+    return out
+
+
 def _gemm_blas(x, w, resid, out, epi):
     if epi == "resid":
         if out.data_ptr() == resid.data_ptr() and out.stride() == resid.stride():

@@ -296,6 +296,38 @@ def test_rope_kv_write(native):
         assert torch.equal(vc_c[s // BS, :, s % BS], v[t])
 
 
+@pytest.mark.parametrize("M,Hq,Hkv", [(2300, 32, 8), (4096, 32, 8), (1111, 4, 1)])
+def test_gemm_rope_kv_bit_identical_to_gemm_then_rope_kv(native, M, Hq, Hkv):
+    """The qkv projection with rope_kv's work in the gemm_w4 epilogue (EPI_ROPE_KV) vs gemm_w4 followed by
+    rope_kv: the qkv rows (rotated q / k, plain v) and both paged caches bit-identical, ragged M tails
+    (guarded edge tiles), rows without a cache slot (slot -1), llama3-scaled RoPE tables, positions out of
+    order; TP=8-shard widths (4 q heads, 1 KV head)."""
+    D, BS, K = 128, 64, 4096
+    N = (Hq + 2 * Hkv) * D
+    g = torch.Generator(device=DEV).manual_seed(M + Hq)
+    x = (torch.randn(M, K, device=DEV, generator=g) * 0.5).bfloat16()
+    w = (torch.randn(N, K, device=DEV, generator=g) / math.sqrt(K)).bfloat16()
+    cos, sin = R.rope_tables(D, 16384, theta=500000.0,
+                             scaling={"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                      "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pos = torch.randint(0, 16384, (M,), device=DEV, generator=g).int()
+    nb = M // BS + 4
+    slots = torch.randperm(nb * BS, device=DEV, generator=g)[:M].int()
+    slots[::7] = -1
+    kc = torch.zeros(nb, Hkv, BS, D, device=DEV).bfloat16()
+    vc = torch.zeros_like(kc)
+    assert native.gemm_rope_kv_ok(x, w, pos, cos, sin, slots, kc, vc, Hq, Hkv, D)
+    got = native.gemm_rope_kv(x, w, pos, cos, sin, slots, kc, vc, Hq, Hkv, D)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    ref = native.gemm(x, w)
+    native.rope_kv(ref, pos, cos, sin, slots, kc2, vc2, Hq, Hkv, D)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    assert int((kc != 0).sum().item()) > 0
+
+
 def _paged_setup(lens, Hkv, D, seed=0):
     g = torch.Generator().manual_seed(seed)
     nb_per = [(L + 63) // 64 for L in lens]
